@@ -1,0 +1,117 @@
+"""ctypes binding of the C ABI in include/otslam.h (libotslam_hip.so, built in-tree for gfx950).
+
+This is the only way the facade reaches the hot path.  There is no CPU fallback: if the library is missing or
+no HIP device is present, every compute call raises RuntimeError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libotslam_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "otslam.h")
+
+OT_OK = 0
+OT_ERR_INVALID_ARGUMENT = 1
+OT_ERR_UNSUPPORTED_FORMAT = 2
+OT_ERR_CAPACITY = 3
+OT_ERR_HIP = 4
+
+OT_COLOR_NONE = 0
+OT_COLOR_RGB8 = 1
+
+
+class ot_intrinsics(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("fx", C.c_double), ("fy", C.c_double),
+                ("cx", C.c_double), ("cy", C.c_double)]
+
+
+_p = C.c_void_p
+_d = C.c_double
+_i32 = C.c_int32
+_i64 = C.c_int64
+_pi64 = C.POINTER(C.c_int64)
+_pint = C.POINTER(ot_intrinsics)
+
+# name -> argtypes (restype is int32 status unless listed in _RESTYPES)
+SIGNATURES = {
+    "ot_last_error": [],
+    "ot_version": [],
+    "ot_abi_version": [],
+    "ot_depth_to_float": [_p, _p, _i64, _d, _d, _p],
+    "ot_depth_multiplier": [_pint, _p, _p],
+    "ot_unproject": [_p, _p, _pint, _p, _i32, _p, _p, _i64, _pi64, _p],
+    "ot_voxel_down_sample": [_p, _p, _p, _i64, _d, _p, _p, _p, _p, _pi64, _p],
+    "ot_remove_statistical_outlier": [_p, _i64, _i32, _d, _p, _p, _pi64, _p],
+    "ot_remove_radius_outlier": [_p, _i64, _i32, _d, _p, _pi64, _p],
+    "ot_filter_min_z": [_p, _p, _i64, _d, _p, _p, _pi64, _p],
+    "ot_gather_rows3": [_p, _p, _i64, _p, _p],
+    "ot_tsdf_create": [_d, _d, _i32, _i32, _i32, _i64, C.POINTER(_p)],
+    "ot_tsdf_destroy": [_p],
+    "ot_tsdf_reset": [_p],
+    "ot_tsdf_integrate": [_p, _p, _p, _pint, _p, _p],
+    "ot_tsdf_integrate_u16": [_p, _p, _p, _pint, _p, _d, _d, _p],
+    "ot_tsdf_flush": [_p, _p],
+    "ot_tsdf_set_batch": [_p, _i32],
+    "ot_tsdf_num_units": [_p, _pi64],
+    "ot_tsdf_counters": [_p, _pi64, _pi64],
+    "ot_tsdf_set_profiling": [_p, _i32],
+    "ot_tsdf_kernel_time": [_p, C.POINTER(C.c_double), _pi64],
+    "ot_tsdf_export_units": [_p, _p, _p, _p, _p, _p],
+    "ot_tsdf_extract_triangle_mesh": [_p, _pi64, _pi64, _p],
+    "ot_tsdf_fetch_triangle_mesh": [_p, _p, _p, _p, _p],
+    "ot_mesh_compute_vertex_normals": [_p, _i64, _p, _i64, _p, _p],
+    "ot_mesh_sample_points_uniformly": [_p, _p, _p, _i64, _p, _i64, _i64, C.c_uint64, _p, _p, _p, _p],
+    "ot_occupancy_to_points": [_p, _i32, _i32, _i32, _d, _d, _d, _p, _pi64, _p],
+}
+_RESTYPES = {"ot_last_error": C.c_char_p, "ot_version": C.c_char_p, "ot_abi_version": C.c_int32}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class OTError(RuntimeError):
+    """Raised for any non-OK status; message mirrors Open3D's utility::LogError text."""
+
+
+def load():
+    """Load libotslam_hip.so (raises RuntimeError, never falls back)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"HIP extension missing: {LIB_PATH} (run __graft_entry__.build())")
+        lib = C.CDLL(LIB_PATH)
+        missing = []
+        for name, argtypes in SIGNATURES.items():
+            try:
+                f = getattr(lib, name)
+            except AttributeError:
+                missing.append(name)
+                continue
+            f.argtypes = argtypes
+            f.restype = _RESTYPES.get(name, C.c_int32)
+        lib._ot_missing = set(missing)
+        _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    lib = load()
+    if name in lib._ot_missing:
+        raise RuntimeError(f"{LIB_PATH} does not export {name} (stale build?)")
+    st = getattr(lib, name)(*args)
+    if st != OT_OK:
+        msg = lib.ot_last_error().decode(errors="replace")
+        raise OTError(msg or f"{name} failed with status {st}")
+    return st
+
+
+def intrinsics_struct(intr) -> ot_intrinsics:
+    return ot_intrinsics(int(intr.width), int(intr.height), float(intr.fx), float(intr.fy), float(intr.cx),
+                         float(intr.cy))

@@ -1,0 +1,96 @@
+// common.h — shared helpers of the MI355X-native hot path (HIP, gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/otslam.h"
+
+namespace ot {
+
+// ------------------------------------------------------------------------------------------ errors
+void set_error(const std::string& msg);
+ot_status fail(ot_status code, const std::string& msg);
+
+#define OT_HIP_TRY(expr)                                                                                   \
+    do {                                                                                                   \
+        hipError_t e__ = (expr);                                                                           \
+        if (e__ != hipSuccess)                                                                             \
+            return ::ot::fail(OT_ERR_HIP, std::string("HIP error ") + hipGetErrorString(e__) + " at " +     \
+                                              __FILE__ + ":" + std::to_string(__LINE__) + " (" #expr ")"); \
+    } while (0)
+
+#define OT_LAUNCH_CHECK() OT_HIP_TRY(hipGetLastError())
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ----------------------------------------------------------------------------- per-device scratch
+// Grow-only scratch arena (one per device).  Not thread-safe: the facade is single-threaded per process
+// (Open3D's calls are synchronous from one Python thread, SURVEY.md §8(b) Threading).
+void* scratch(size_t bytes, int slot);
+
+// --------------------------------------------------------------------------------- math helpers
+struct Mat4d {
+    double m[16];
+};
+struct Mat4f {
+    float m[16];
+};
+
+// Eigen generic 4x4 inverse (compute_inverse_size4 + cofactor_4x4), host side.
+void inverse4(const double* m, double* r);
+
+// ordered encoding of doubles so that unsigned integer order == numeric order (for atomicMin/Max)
+__host__ __device__ inline unsigned long long dbl_to_ordered(double d) {
+    unsigned long long u = __double_as_longlong(d);
+    return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__host__ __device__ inline double ordered_to_dbl(unsigned long long u) {
+    u = (u & 0x8000000000000000ull) ? (u & 0x7FFFFFFFFFFFFFFFull) : ~u;
+    return __longlong_as_double((long long)u);
+}
+
+// packed int3 key: 21 bits per axis, biased by 2^20, x-major => numeric order == (x, y, z) lexicographic
+constexpr int KEY_BITS = 21;
+constexpr int KEY_BIAS = 1 << 20;
+constexpr unsigned long long KEY_EMPTY = ~0ull;
+__host__ __device__ inline bool key_in_range(int x, int y, int z) {
+    return x >= -KEY_BIAS && x < KEY_BIAS && y >= -KEY_BIAS && y < KEY_BIAS && z >= -KEY_BIAS && z < KEY_BIAS;
+}
+__host__ __device__ inline unsigned long long pack_key(int x, int y, int z) {
+    return ((unsigned long long)(x + KEY_BIAS) << 42) | ((unsigned long long)(y + KEY_BIAS) << 21) |
+           (unsigned long long)(z + KEY_BIAS);
+}
+__host__ __device__ inline void unpack_key(unsigned long long k, int& x, int& y, int& z) {
+    x = (int)((k >> 42) & 0x1FFFFF) - KEY_BIAS;
+    y = (int)((k >> 21) & 0x1FFFFF) - KEY_BIAS;
+    z = (int)(k & 0x1FFFFF) - KEY_BIAS;
+}
+__host__ __device__ inline unsigned long long mix64(unsigned long long z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// ------------------------------------------------------------------------ wave / block primitives
+__device__ inline unsigned lane_id() { return __lane_id(); }
+
+// exclusive prefix of a predicate within the wave (64 lanes) and the wave total
+__device__ inline int wave_excl_count(bool pred, int& total) {
+    unsigned long long m = __ballot(pred);
+    total = __popcll(m);
+    unsigned long long lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
+    return __popcll(m & lt);
+}
+
+template <typename T>
+__device__ inline T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace ot

@@ -1,0 +1,145 @@
+// compact.h — order-preserving (stable) stream compaction for gfx950.
+//
+// Three launches: (1) each 256-thread workgroup counts the items its predicate keeps (4 consecutive items
+// per lane, wave ballot + popcount, no atomics); (2) one workgroup scans the per-workgroup counts;
+// (3) each workgroup re-evaluates the predicate and writes the kept items at
+// workgroup-offset + wave-offset + lane prefix (ballot/mbcnt).  Output order == input index order, which is
+// the row-major order Open3D produces for unprojection and the order numpy boolean masks keep.
+#pragma once
+
+#include "common.h"
+
+namespace ot {
+
+constexpr int CMP_THREADS = 256;
+constexpr int CMP_ITEMS = 4;
+constexpr int CMP_TILE = CMP_THREADS * CMP_ITEMS;
+
+// inclusive scan within a wave (64 lanes)
+__device__ inline int wave_incl_scan(int v) {
+    const int lane = (int)lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// exclusive scan over a 256-thread workgroup; returns the exclusive prefix and the block total
+__device__ inline int block_excl_scan_256(int v, int& total) {
+    __shared__ int wsum[CMP_THREADS / 64];
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+    int inc = wave_incl_scan(v);
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < CMP_THREADS / 64; ++w) {
+        int s = wsum[w];
+        if (w < wid) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return off + inc - v;
+}
+
+template <class Pred>
+__global__ __launch_bounds__(CMP_THREADS) void k_compact_count(int64_t n, Pred pred, int* block_counts) {
+    const int64_t base = (int64_t)blockIdx.x * CMP_TILE + (int64_t)threadIdx.x * CMP_ITEMS;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < CMP_ITEMS; ++k) {
+        int64_t i = base + k;
+        if (i < n && pred(i)) ++c;
+    }
+    c = wave_sum(c);
+    __shared__ int ws[CMP_THREADS / 64];
+    if (lane_id() == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < CMP_THREADS / 64; ++w) t += ws[w];
+        block_counts[blockIdx.x] = t;
+    }
+}
+
+// single workgroup (1024 threads) exclusive scan of `n` ints in place; writes the grand total to *total
+// (internal linkage: every translation unit gets its own copy)
+namespace {
+__global__ __launch_bounds__(1024) void k_scan_inplace(int* v, int n, int64_t* total) {
+    __shared__ int wsum[16];
+    __shared__ long long carry_s;
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) carry_s = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + threadIdx.x;
+        const int x = (i < n) ? v[i] : 0;
+        int inc = wave_incl_scan(x);
+        if (lane == 63) wsum[wid] = inc;
+        __syncthreads();
+        int off = 0, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            int s = wsum[w];
+            if (w < wid) off += s;
+            tot += s;
+        }
+        const long long carry = carry_s;
+        if (i < n) v[i] = (int)(carry + off + inc - x);
+        __syncthreads();
+        if (threadIdx.x == 0) carry_s = carry + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry_s;
+}
+}  // namespace
+
+
+template <class Pred, class Emit>
+__global__ __launch_bounds__(CMP_THREADS) void k_compact_emit(int64_t n, Pred pred, Emit emit,
+                                                              const int* block_offsets) {
+    const int64_t base = (int64_t)blockIdx.x * CMP_TILE + (int64_t)threadIdx.x * CMP_ITEMS;
+    bool keep[CMP_ITEMS];
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < CMP_ITEMS; ++k) {
+        int64_t i = base + k;
+        keep[k] = (i < n) && pred(i);
+        c += keep[k] ? 1 : 0;
+    }
+    int total;
+    int pos = block_excl_scan_256(c, total) + block_offsets[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < CMP_ITEMS; ++k)
+        if (keep[k]) emit(base + k, (int64_t)pos++);
+}
+
+// Host driver: runs the three launches on `stream` and returns the kept count on the host (synchronises).
+template <class Pred, class Emit>
+ot_status compact(int64_t n, Pred pred, Emit emit, hipStream_t stream, int64_t* n_out_host, int scratch_slot) {
+    const int64_t nblocks = (n + CMP_TILE - 1) / CMP_TILE;
+    if (n <= 0) {
+        *n_out_host = 0;
+        return OT_OK;
+    }
+    if (nblocks > (int64_t)0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "compaction input too large");
+    char* ws = (char*)scratch(sizeof(int) * (size_t)nblocks + 64, scratch_slot);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    int64_t* d_total = (int64_t*)ws;
+    int* d_counts = (int*)(ws + 64);
+    hipLaunchKernelGGL((k_compact_count<Pred>), dim3((unsigned)nblocks), dim3(CMP_THREADS), 0, stream, n, pred,
+                       d_counts);
+    hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(1024), 0, stream, d_counts, (int)nblocks, d_total);
+    hipLaunchKernelGGL((k_compact_emit<Pred, Emit>), dim3((unsigned)nblocks), dim3(CMP_THREADS), 0, stream, n,
+                       pred, emit, (const int*)d_counts);
+    OT_LAUNCH_CHECK();
+    int64_t tot = 0;
+    OT_HIP_TRY(hipMemcpyAsync(&tot, d_total, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    *n_out_host = tot;
+    return OT_OK;
+}
+
+}  // namespace ot

@@ -1,0 +1,17 @@
+// sort.h — host entry points of sort.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/otslam.h"
+
+namespace ot {
+
+// Stable LSD radix sort of n (key, value) pairs over key bits [0, end_bit).  Scratch slot for temp storage.
+ot_status sort_pairs_u64_u32(const unsigned long long* kin, unsigned long long* kout, const unsigned* vin,
+                             unsigned* vout, size_t n, int end_bit, hipStream_t stream, int scratch_slot);
+
+// Device-wide exclusive prefix sum of int64.
+ot_status exclusive_scan_i64(const long long* in, long long* out, size_t n, hipStream_t stream, int scratch_slot);
+
+}  // namespace ot

@@ -1,0 +1,106 @@
+// tsdf.h — device layout of the scalable TSDF volume (pipelines.integration.ScalableTSDFVolume).
+//
+// HBM layout (one allocation per field group, sized at create time):
+//   hash table  : open addressing, linear probing, capacity = pow2 >= 4 * max_units
+//                 hkeys u64 (packed int3 unit key, KEY_EMPTY = ~0), hvals i32 (unit id, -1 = not allocated),
+//                 stamp i32 (last frame that touched the slot)
+//   unit pool   : max_units blocks of 16^3 voxels, field-planar inside a block:
+//                 vox[id][field][z][x*16 + y], field = {tsdf, weight, r, g, b} (f32).  One 256-lane
+//                 workgroup owns a block; lane (x, y) walks z, so every z step is one coalesced 1-KiB row
+//                 per field (the per-column z walk is what reproduces Open3D's incremental float math).
+//   unit_keys   : int32 [max_units][3]
+//   touched     : per-frame list of unit ids (bit 31 = freshly allocated this frame => state starts at 0)
+#pragma once
+
+#include <vector>
+
+#include "common.h"
+
+namespace ot {
+
+constexpr int UNIT_RES = 16;
+constexpr int UNIT_VOX = UNIT_RES * UNIT_RES * UNIT_RES;  // 4096
+constexpr int UNIT_FIELDS = 5;
+constexpr int UNIT_FLOATS = UNIT_FIELDS * UNIT_VOX;  // 20480 floats = 80 KiB
+
+// counters[] slots
+constexpr int C_TOUCHED = 0;   // units touched by the current frame
+constexpr int C_UNITS = 1;     // units allocated
+constexpr int C_OVERFLOW = 2;  // pool exhausted (units dropped)
+constexpr int C_HASHERR = 3;   // hash full or key out of range
+constexpr int C_BATCH_PAIRS = 4;  // (frame, unit) pairs in the current batch
+constexpr int N_COUNTERS = 8;
+
+// stats[] slots (u64)
+constexpr int S_UPDATES = 0;
+constexpr int S_UNIT_INTEGRATIONS = 1;
+
+struct TsdfDev {
+    unsigned long long* hkeys;
+    int* hvals;
+    int* stamp;
+    int* touched;
+    int* counters;
+    unsigned long long* stats;
+    int* unit_keys;
+    float* vox;
+    int hash_mask;
+    int max_units;
+};
+
+struct PendingFrame {
+    const uint16_t* depth;
+    const uint8_t* color;
+    ot_intrinsics intr;
+    double extrinsic[16];
+    double depth_scale, depth_trunc;
+};
+
+struct MeshBuffers {
+    double* v = nullptr;
+    double* c = nullptr;
+    int32_t* t = nullptr;
+    int64_t nv = 0, nt = 0;
+    int64_t cap_v = 0, cap_t = 0;
+};
+
+}  // namespace ot
+
+struct ot_tsdf {
+    int device = 0;
+    double voxel_length = 0.0, sdf_trunc = 0.0, unit_length = 0.0;
+    int color_type = 1, stride = 4;
+    int64_t max_units = 0;
+    int64_t hash_cap = 0;
+    ot::TsdfDev dev{};
+    int frame_id = 0;
+    // multiplier image cache
+    float* mult = nullptr;
+    ot_intrinsics mult_intr{};
+    bool mult_valid = false;
+    // float depth staging for the u16 path
+    float* depth_f = nullptr;
+    int64_t depth_f_cap = 0;
+    // batching of integrate_u16
+    int batch_max = 1;
+    std::vector<ot::PendingFrame> pending;
+    void* batch_ws = nullptr;
+    size_t batch_ws_bytes = 0;
+    // sorted-unit cache (rank -> id), valid for `sorted_units` units
+    unsigned* sorted_ids = nullptr;
+    int64_t sorted_units = -1;
+    int sorted_frame = -1;
+    // extracted mesh
+    ot::MeshBuffers mesh;
+    // kernel timing (events around the dominant integration kernel)
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
+    double prof_ms = 0.0;
+    int64_t prof_launches = 0;
+};
+
+namespace ot {
+// shared between tsdf.hip and mc.hip
+ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units);
+ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream);
+}  // namespace ot

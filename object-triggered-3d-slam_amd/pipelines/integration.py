@@ -1,0 +1,133 @@
+"""open3d.pipelines.integration counterparts: ScalableTSDFVolume on the GPU block hash (tsdf.hip).
+
+Call surface = reconstruct_rgbd_filter.py:81-85 (constructor), :105 (integrate), :112 (extract_triangle_mesh).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+
+import numpy as np
+
+from .. import _device as D
+from .. import _lib as L
+from ..geometry import RGBDImage, TriangleMesh, _Arr
+
+
+class TSDFVolumeColorType(enum.IntEnum):
+    NoColor = 0
+    RGB8 = 1
+    Gray32 = 2
+
+
+class ScalableTSDFVolume:
+    """pipelines.integration.ScalableTSDFVolume(voxel_length, sdf_trunc, color_type=NoColor,
+    volume_unit_resolution=16, depth_sampling_stride=4).
+
+    Extra keyword arguments (not in Open3D): `max_units` (block-pool capacity in HBM) and `batch_frames`
+    (frames queued per fused integration launch; results are identical for any value)."""
+
+    def __init__(self, voxel_length, sdf_trunc, color_type=TSDFVolumeColorType.NoColor, volume_unit_resolution=16,
+                 depth_sampling_stride=4, max_units=0, batch_frames=1):
+        D.require_gpu()
+        ct = int(color_type)
+        if ct == TSDFVolumeColorType.Gray32:
+            raise RuntimeError("[ScalableTSDFVolume] Gray32 color type is not supported by this build")
+        self.voxel_length = float(voxel_length)
+        self.sdf_trunc = float(sdf_trunc)
+        self.color_type = TSDFVolumeColorType(ct)
+        self.volume_unit_resolution = int(volume_unit_resolution)
+        self.depth_sampling_stride = int(depth_sampling_stride)
+        h = C.c_void_p()
+        L.call("ot_tsdf_create", self.voxel_length, self.sdf_trunc, ct, self.volume_unit_resolution,
+               self.depth_sampling_stride, int(max_units), C.byref(h))
+        self._h = h
+        self._keep = []  # frames queued for a batched launch stay referenced until the flush
+        if batch_frames != 1:
+            self.set_batch(batch_frames)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                L.load().ot_tsdf_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def set_batch(self, frames):
+        L.call("ot_tsdf_set_batch", self._h, int(frames))
+
+    def reset(self):
+        L.call("ot_tsdf_reset", self._h)
+        self._keep.clear()
+
+    def integrate(self, image: RGBDImage, intrinsic, extrinsic):
+        """ScalableTSDFVolume::Integrate.  Raw-uint16 RGBD images take the fused path."""
+        ext = np.ascontiguousarray(np.asarray(extrinsic, dtype=np.float64).reshape(4, 4))
+        rgb8 = self.color_type == TSDFVolumeColorType.RGB8
+        color = image.color
+        if rgb8 and (color.num_of_channels != 3 or color.dtype != np.uint8):
+            raise RuntimeError("[ScalableTSDFVolume::Integrate] Unsupported image format.")
+        depth = image.depth
+        if depth.dtype != np.float32 or depth.width != intrinsic.width or depth.height != intrinsic.height:
+            raise RuntimeError("[ScalableTSDFVolume::Integrate] Unsupported image format.")
+        if rgb8 and (color.width != intrinsic.width or color.height != intrinsic.height):
+            raise RuntimeError("[ScalableTSDFVolume::Integrate] Unsupported image format.")
+        intr = L.intrinsics_struct(intrinsic)
+        cdev = color.dev() if rgb8 else None
+        raw = getattr(image, "_raw_depth", None)
+        if raw is not None:
+            d16, scale, trunc = raw
+            self._keep.append((d16, cdev))
+            L.call("ot_tsdf_integrate_u16", self._h, D.ptr(d16), D.ptr(cdev), C.byref(intr),
+                   ext.ctypes.data_as(C.c_void_p), scale, trunc, D.stream_ptr())
+        else:
+            L.call("ot_tsdf_integrate", self._h, D.ptr(depth.dev()), D.ptr(cdev), C.byref(intr),
+                   ext.ctypes.data_as(C.c_void_p), D.stream_ptr())
+
+    def flush(self):
+        L.call("ot_tsdf_flush", self._h, D.stream_ptr())
+        self._keep.clear()
+
+    # ---- readers (each flushes queued frames first) ----
+    def num_units(self):
+        n = C.c_int64(0)
+        L.call("ot_tsdf_num_units", self._h, C.byref(n))
+        self._keep.clear()
+        return n.value
+
+    def counters(self):
+        """(voxel_updates, unit_integrations) since create/reset."""
+        u, k = C.c_int64(0), C.c_int64(0)
+        L.call("ot_tsdf_counters", self._h, C.byref(u), C.byref(k))
+        self._keep.clear()
+        return u.value, k.value
+
+    def export_units(self):
+        """All units sorted by key: keys (U,3) int32, tsdf/weight (U,4096) f32, color (U,4096,3) f32
+        (voxels in Open3D IndexOf order x*256 + y*16 + z)."""
+        n = self.num_units()
+        keys = D.empty((n, 3), "int32")
+        tsdf = D.empty((n, 4096), "float32")
+        weight = D.empty((n, 4096), "float32")
+        color = D.empty((n, 4096, 3), "float32")
+        L.call("ot_tsdf_export_units", self._h, D.ptr(keys), D.ptr(tsdf), D.ptr(weight), D.ptr(color),
+               D.stream_ptr())
+        return keys, tsdf, weight, color
+
+    def extract_triangle_mesh(self):
+        """ScalableTSDFVolume::ExtractTriangleMesh — GPU marching cubes (mc.hip)."""
+        nv, nt = C.c_int64(0), C.c_int64(0)
+        L.call("ot_tsdf_extract_triangle_mesh", self._h, C.byref(nv), C.byref(nt), D.stream_ptr())
+        self._keep.clear()
+        V = D.empty((nv.value, 3), "float64")
+        VC = D.empty((nv.value, 3), "float64")
+        T = D.empty((nt.value, 3), "int32")
+        L.call("ot_tsdf_fetch_triangle_mesh", self._h, D.ptr(V), D.ptr(VC), D.ptr(T), D.stream_ptr())
+        mesh = TriangleMesh()
+        mesh._v = _Arr(dev=V)
+        mesh._t = _Arr(dev=T)
+        if self.color_type == TSDFVolumeColorType.RGB8:
+            mesh._vc = _Arr(dev=VC)
+        return mesh

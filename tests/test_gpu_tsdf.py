@@ -1,0 +1,167 @@
+"""GPU parity: depth conversion, multiplier, unprojection and ScalableTSDFVolume integration vs the CPU oracle.
+
+Bit-exact: depth float image, multiplier image, unprojected point count/order/xyz (identity and posed
+extrinsic), TSDF unit key set, per-voxel weight and tsdf.  Colour (f32 running mean on the GPU vs f64 in
+Open3D/oracle): |rel| <= 1e-4 (SURVEY.md §8(c) parity contract).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_bitwise, ref_intr
+
+pytestmark = pytest.mark.gpu
+
+
+def _integration(pkg):
+    return pkg.pipelines.integration
+
+
+def test_depth_to_float_bitexact(pkg, O, gpu, seq16):
+    depth = seq16[0][0]
+    for trunc in (3.0, 5.0):
+        img = pkg.geometry.Image(depth)
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(seq16[1][0]), img, depth_scale=1000.0, depth_trunc=trunc,
+            convert_rgb_to_intensity=False)
+        assert_bitwise(np.asarray(rgbd.depth), O.depth_to_float(depth, 1000.0, trunc), "depth float")
+
+
+def test_depth_to_float_edge_values(pkg, O, gpu):
+    d = np.array([[0, 1, 2999, 3000, 3001, 65535, 4999, 5000, 7, 13, 2, 3]], np.uint16)
+    img = pkg.geometry.Image(d)
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(np.zeros((1, 12, 3), np.uint8)), img, depth_scale=1000.0, depth_trunc=3.0,
+        convert_rgb_to_intensity=False)
+    assert_bitwise(np.asarray(rgbd.depth), O.depth_to_float(d, 1000.0, 3.0), "depth edge values")
+
+
+def test_multiplier_bitexact(pkg, O, gpu, synth):
+    L = pkg._lib
+    for intr_t in (synth.REF_INTRINSICS_640, synth.REF_INTRINSICS_1280):
+        w, h = intr_t[0], intr_t[1]
+        out = torch.empty((h, w), dtype=torch.float32, device="cuda")
+        intr = L.ot_intrinsics(*intr_t)
+        L.call("ot_depth_multiplier", C.byref(intr), C.c_void_p(out.data_ptr()), None)
+        torch.cuda.synchronize()
+        assert_bitwise(out.cpu().numpy(), O.depth_multiplier(*intr_t), "multiplier")
+
+
+@pytest.mark.parametrize("posed", [False, True])
+def test_unproject_bitexact(pkg, O, gpu, synth, seq16, posed):
+    depth, color, ext = seq16
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[1]), pkg.geometry.Image(depth[1]), depth_scale=1000.0, depth_trunc=5.0,
+        convert_rgb_to_intensity=False)
+    e = ext[1] if posed else None
+    pcd = pkg.geometry.PointCloud.create_from_rgbd_image(rgbd, intr, *( [e] if posed else []))
+    rx, rc = O.unproject(O.depth_to_float(depth[1], 1000.0, 5.0), color[1], intr_t, e)
+    assert len(pcd.points) == rx.shape[0] > 100000
+    assert_bitwise(np.asarray(pcd.points), rx, "unprojected xyz")
+    assert_bitwise(np.asarray(pcd.colors), rc, "unprojected rgb")
+
+
+def test_unproject_stride_and_empty(pkg, O, gpu, synth, seq16):
+    depth = seq16[0][2]
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    pcd = pkg.geometry.PointCloud.create_from_depth_image(pkg.geometry.Image(depth), intr, seq16[2][2],
+                                                          depth_scale=1000.0, depth_trunc=3.0, stride=4)
+    rx, _ = O.unproject(O.depth_to_float(depth, 1000.0, 3.0), None, intr_t, seq16[2][2], stride=4)
+    assert_bitwise(np.asarray(pcd.points), rx, "stride-4 xyz")
+    empty = pkg.geometry.PointCloud.create_from_depth_image(pkg.geometry.Image(np.zeros_like(depth)), intr)
+    assert len(empty.points) == 0
+
+
+def _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=1, trunc=3.0):
+    integ = _integration(pkg)
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    vol = integ.ScalableTSDFVolume(voxel_length=voxel, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                   batch_frames=batch)
+    ref = O.TSDF(voxel, 0.04, 1, 4)
+    for k in range(depth.shape[0]):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=trunc,
+            convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, trunc), color[k], intr_t, ext[k])
+    return vol, ref
+
+
+def _compare_volumes(vol, ref):
+    keys, tsdf, weight, col = (t.cpu().numpy() for t in vol.export_units())
+    rk, rt, rw, rc = ref.export()
+    assert_bitwise(keys, rk, "unit keys")
+    assert_bitwise(weight, rw, "voxel weights")
+    assert_bitwise(tsdf, rt, "voxel tsdf")
+    np.testing.assert_allclose(col, rc, rtol=1e-4, atol=1e-4 * 255)
+    upd, units = vol.counters()
+    assert upd == ref.total_updates()
+    assert units == ref.unit_integrations()
+    return keys.shape[0]
+
+
+@pytest.mark.parametrize("voxel", [0.01, 0.005])
+def test_tsdf_integrate_bitexact(pkg, O, gpu, synth, seq16, voxel):
+    depth, color, ext = seq16
+    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, voxel)
+    n = _compare_volumes(vol, ref)
+    assert n > 300
+
+
+def test_tsdf_lexical_order_matters(pkg, O, gpu, synth, seq16):
+    """Running averages depend on frame order: the GPU must apply frames in call order."""
+    depth, color, ext = seq16
+    vol, ref = _run_pair(pkg, O, synth, depth[::-1].copy(), color[::-1].copy(), ext[::-1].copy(), 0.01)
+    _compare_volumes(vol, ref)
+
+
+def test_tsdf_reset_and_empty_frame(pkg, O, gpu, synth, seq16):
+    depth, color, ext = seq16
+    integ = _integration(pkg)
+    intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth))
+    vol = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
+    zero = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[0]), pkg.geometry.Image(np.zeros_like(depth[0])), convert_rgb_to_intensity=False)
+    vol.integrate(zero, intr, ext[0])
+    assert vol.num_units() == 0
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), convert_rgb_to_intensity=False)
+    vol.integrate(rgbd, intr, ext[0])
+    assert vol.num_units() > 0
+    vol.reset()
+    assert vol.num_units() == 0
+
+
+def test_tsdf_unsupported_format(pkg, gpu, synth, seq16):
+    depth, color, ext = seq16
+    integ = _integration(pkg)
+    intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth))
+    vol = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
+    gray = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), convert_rgb_to_intensity=True)
+    with pytest.raises(RuntimeError, match="Unsupported image format"):
+        vol.integrate(gray, intr, ext[0])
+    small = pkg.camera.PinholeCameraIntrinsic(320, 240, 300.0, 300.0, 160.0, 120.0)
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), convert_rgb_to_intensity=False)
+    with pytest.raises(RuntimeError, match="Unsupported image format"):
+        vol.integrate(rgbd, small, ext[0])
+
+
+def test_tsdf_capacity_error(pkg, gpu, synth, seq16):
+    depth, color, ext = seq16
+    integ = _integration(pkg)
+    intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth))
+    vol = integ.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                   max_units=64)
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), convert_rgb_to_intensity=False)
+    vol.integrate(rgbd, intr, ext[0])
+    with pytest.raises(RuntimeError, match="pool exhausted"):
+        vol.export_units()
