@@ -45,12 +45,12 @@ void inverse4(const double* m, double* r);
 
 // ordered encoding of doubles so that unsigned integer order == numeric order (for atomicMin/Max)
 __host__ __device__ inline unsigned long long dbl_to_ordered(double d) {
-    unsigned long long u = __double_as_longlong(d);
+    unsigned long long u = __builtin_bit_cast(unsigned long long, d);
     return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 __host__ __device__ inline double ordered_to_dbl(unsigned long long u) {
     u = (u & 0x8000000000000000ull) ? (u & 0x7FFFFFFFFFFFFFFFull) : ~u;
-    return __longlong_as_double((long long)u);
+    return __builtin_bit_cast(double, u);
 }
 
 // packed int3 key: 21 bits per axis, biased by 2^20, x-major => numeric order == (x, y, z) lexicographic

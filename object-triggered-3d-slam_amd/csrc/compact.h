@@ -142,4 +142,52 @@ ot_status compact(int64_t n, Pred pred, Emit emit, hipStream_t stream, int64_t* 
     return OT_OK;
 }
 
+// segment heads of a sorted key array (i == 0 or key changes) -> their positions
+struct SegHeadPred {
+    const unsigned long long* keys;
+    __device__ bool operator()(int64_t i) const { return i == 0 || keys[i] != keys[i - 1]; }
+};
+struct SegHeadEmit {
+    int* heads;
+    __device__ void operator()(int64_t i, int64_t pos) const { heads[pos] = (int)i; }
+};
+
+// per-axis min / max of float64 [n][3] points via order-preserving u64 atomics (exact)
+struct Bounds {
+    unsigned long long mn[3];
+    unsigned long long mx[3];
+    int err;
+};
+
+namespace {
+__global__ __launch_bounds__(256) void k_bounds(const double* __restrict__ xyz, int64_t n, Bounds* b) {
+    unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0, 0, 0};
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const unsigned long long o = dbl_to_ordered(xyz[i * 3 + a]);
+            mn[a] = o < mn[a] ? o : mn[a];
+            mx[a] = o > mx[a] ? o : mx[a];
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            unsigned long long t = __shfl_xor(mn[a], off, 64);
+            mn[a] = t < mn[a] ? t : mn[a];
+            t = __shfl_xor(mx[a], off, 64);
+            mx[a] = t > mx[a] ? t : mx[a];
+        }
+    }
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            atomicMin(&b->mn[a], mn[a]);
+            atomicMax(&b->mx[a], mx[a]);
+        }
+    }
+}
+}  // namespace
+
 }  // namespace ot

@@ -1,0 +1,367 @@
+// mc.hip — ScalableTSDFVolume::ExtractTriangleMesh on MI355X (reconstruct_rgbd_filter.py:112).
+//
+// Canonical output order (Open3D's follows unordered_map iteration; parity compares canonical order):
+//   vertices  : sorted by the edge key's (owner unit key, owner-local voxel x*256+y*16+z, axis)
+//   triangles : (unit key, voxel x*256+y*16+z, tri-table order), winding (e0, e2, e1) as Open3D.
+// Pipeline (one 256-lane workgroup per unit, units in key order from the rocPRIM sort):
+//   k_mc_prepare   : neighbour table (+x/+y/+z combos via the block hash), id->rank, clear edge bitmasks
+//   k_mc_classify  : 17^3 tsdf/weight tile of the unit and its +1 neighbours staged in LDS (39 KiB); per
+//                    voxel cube index (any weight == 0 => skipped, like Open3D); cut edges marked in the
+//                    owner unit's edge bitmask (atomicOr); per-unit triangle count
+//   k_mc_count     : per-unit popcount prefix over the 384 bitmask words => vertex ids without a hash map
+//   (device scans of the per-unit counts give vertex / triangle bases)
+//   k_mc_vertices  : one lane per bitmask word, vertex = half + vl*key, += f0*vl/(f0+f1) on the edge axis,
+//                    colour (f1*c0 + f0*c1)/(f0+f1) with c = colour/255 — Open3D's float64 expressions
+//   k_mc_triangles : per-lane triangle offsets by block scan; vertex ids by popcount lookups
+#include "../../include/otslam_mc_tables.h"
+#include "compact.h"
+#include "sort.h"
+#include "tsdf.h"
+
+namespace ot {
+
+__constant__ signed char c_tri[256][16];
+__constant__ int c_eshift[12][4];
+__constant__ int c_e2v[12][2];
+__constant__ int c_shift[8][3];
+
+constexpr int EWORDS = (UNIT_VOX * 3) / 32;  // 384 bitmask words per unit
+constexpr int T17 = 17;
+
+struct McDev {
+    const unsigned* sorted_ids;  // rank -> id
+    int* rank_of;                // id -> rank
+    int* nbr;                    // [id][8] neighbour ids, index dx*4 + dy*2 + dz
+    unsigned char* cubes;        // [id][4096]
+    unsigned* eflags;            // [id][384]
+    int* wprefix;                // [id][384]
+    long long* tri_cnt;          // [rank]
+    long long* vert_cnt;         // [rank]
+    long long* tri_base;         // [rank]
+    long long* vert_base;        // [rank]
+};
+
+__device__ inline int find_unit(const TsdfDev& d, int x, int y, int z) {
+    if (!key_in_range(x, y, z)) return -1;
+    const unsigned long long key = pack_key(x, y, z);
+    unsigned slot = (unsigned)mix64(key) & (unsigned)d.hash_mask;
+    for (int probe = 0; probe <= d.hash_mask; ++probe) {
+        const unsigned long long k = d.hkeys[slot];
+        if (k == key) {
+            const int id = d.hvals[slot];
+            return id < d.max_units ? id : -1;
+        }
+        if (k == KEY_EMPTY) return -1;
+        slot = (slot + 1) & (unsigned)d.hash_mask;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(256) void k_mc_prepare(TsdfDev d, McDev m) {
+    const int r = blockIdx.x;
+    const int id = (int)m.sorted_ids[r];
+    const int t = threadIdx.x;
+    if (t < 8) {
+        const int dx = (t >> 2) & 1, dy = (t >> 1) & 1, dz = t & 1;
+        m.nbr[id * 8 + t] = t == 0 ? id
+                                   : find_unit(d, d.unit_keys[id * 3] + dx, d.unit_keys[id * 3 + 1] + dy,
+                                               d.unit_keys[id * 3 + 2] + dz);
+    }
+    if (t == 0) m.rank_of[id] = r;
+    for (int w = t; w < EWORDS; w += 256) m.eflags[(size_t)id * EWORDS + w] = 0u;
+}
+
+__global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
+    __shared__ float sF[T17 * T17 * T17];
+    __shared__ float sW[T17 * T17 * T17];
+    __shared__ int snbr[8];
+    __shared__ long long wsum[4];
+    const int r = blockIdx.x;
+    const int id = (int)m.sorted_ids[r];
+    const int t = threadIdx.x;
+    if (t < 8) snbr[t] = m.nbr[id * 8 + t];
+    __syncthreads();
+    for (int c = t; c < T17 * T17 * T17; c += 256) {
+        const int lx = c / (T17 * T17), ly = (c / T17) % T17, lz = c % T17;
+        const int nid = snbr[((lx >> 4) << 2) | ((ly >> 4) << 1) | (lz >> 4)];
+        float f = 0.0f, w = 0.0f;
+        if (nid >= 0) {
+            const float* base = d.vox + (size_t)nid * UNIT_FLOATS;
+            const int vi = (lz & 15) * 256 + (lx & 15) * 16 + (ly & 15);
+            f = base[vi];
+            w = base[UNIT_VOX + vi];
+        }
+        sF[c] = f;
+        sW[c] = w;
+    }
+    __syncthreads();
+    const int x = t >> 4, y = t & 15;
+    long long ntri = 0;
+    unsigned char* cubes = m.cubes + (size_t)id * UNIT_VOX;
+    for (int z = 0; z < UNIT_RES; ++z) {
+        int cube = 0;
+        bool valid = true;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = ((x + c_shift[i][0]) * T17 + (y + c_shift[i][1])) * T17 + (z + c_shift[i][2]);
+            if (sW[c] == 0.0f) valid = false;
+            if (sF[c] < 0.0f) cube |= (1 << i);
+        }
+        if (!valid) cube = 0;
+        if (cube == 255) cube = 0;
+        cubes[t * 16 + z] = (unsigned char)cube;
+        if (cube == 0) continue;
+        for (int k = 0; k < 15 && c_tri[cube][k] != -1; k += 3) ++ntri;
+#pragma unroll
+        for (int e = 0; e < 12; ++e) {
+            const int v0 = c_e2v[e][0], v1 = c_e2v[e][1];
+            if (((cube >> v0) & 1) == ((cube >> v1) & 1)) continue;
+            const int ox = x + c_eshift[e][0], oy = y + c_eshift[e][1], oz = z + c_eshift[e][2];
+            const int owner = snbr[((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4)];
+            const int local = (ox & 15) * 256 + (oy & 15) * 16 + (oz & 15);
+            const int bit = local * 3 + c_eshift[e][3];
+            if (owner >= 0) atomicOr(&m.eflags[(size_t)owner * EWORDS + (bit >> 5)], 1u << (bit & 31));
+        }
+    }
+    ntri = wave_sum(ntri);
+    if (lane_id() == 0) wsum[t >> 6] = ntri;
+    __syncthreads();
+    if (t == 0) m.tri_cnt[r] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// per-unit exclusive popcount prefix of the 384 bitmask words (6 waves, one word per lane)
+__global__ __launch_bounds__(EWORDS) void k_mc_count(McDev m) {
+    __shared__ int wsum[EWORDS / 64];
+    const int r = blockIdx.x;
+    const int id = (int)m.sorted_ids[r];
+    const int t = threadIdx.x;
+    const int pc = __popc(m.eflags[(size_t)id * EWORDS + t]);
+    int inc = wave_incl_scan(pc);
+    if (lane_id() == 63) wsum[t >> 6] = inc;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < EWORDS / 64; ++w) {
+        if (w < (t >> 6)) off += wsum[w];
+        tot += wsum[w];
+    }
+    m.wprefix[(size_t)id * EWORDS + t] = off + inc - pc;
+    if (t == 0) m.vert_cnt[r] = tot;
+}
+
+__device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z, float& f, float c[3]) {
+    const float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    const int vi = z * 256 + x * 16 + y;
+    f = base[vi];
+    c[0] = base[2 * UNIT_VOX + vi];
+    c[1] = base[3 * UNIT_VOX + vi];
+    c[2] = base[4 * UNIT_VOX + vi];
+}
+
+__global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, double vl, double* V, double* VC) {
+    const int r = blockIdx.x;
+    const int id = (int)m.sorted_ids[r];
+    const int w = threadIdx.x;
+    unsigned bits = m.eflags[(size_t)id * EWORDS + w];
+    if (!bits) return;
+    long long vid = m.vert_base[r] + m.wprefix[(size_t)id * EWORDS + w];
+    const int kx = d.unit_keys[id * 3], ky = d.unit_keys[id * 3 + 1], kz = d.unit_keys[id * 3 + 2];
+    const double half = vl * 0.5;
+    while (bits) {
+        const int b = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const int gbit = w * 32 + b;
+        const int local = gbit / 3, axis = gbit % 3;
+        const int x = local >> 8, y = (local >> 4) & 15, z = local & 15;
+        float f0f, f1f, c0[3], c1[3];
+        voxel_value(d, id, x, y, z, f0f, c0);
+        int x1 = x + (axis == 0), y1 = y + (axis == 1), z1 = z + (axis == 2);
+        const int nid = m.nbr[id * 8 + (((x1 >> 4) << 2) | ((y1 >> 4) << 1) | (z1 >> 4))];
+        if (nid < 0) {  // cannot happen for a valid cube (its corners have weight > 0); never read out of bounds
+            f1f = f0f;
+            c1[0] = c0[0], c1[1] = c0[1], c1[2] = c0[2];
+        } else {
+            voxel_value(d, nid, x1 & 15, y1 & 15, z1 & 15, f1f, c1);
+        }
+        const int g[3] = {kx * UNIT_RES + x, ky * UNIT_RES + y, kz * UNIT_RES + z};
+        double pt[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) pt[a] = half + vl * (double)g[a];
+        const double f0 = fabs((double)f0f), f1 = fabs((double)f1f);
+        pt[axis] += f0 * vl / (f0 + f1);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) V[vid * 3 + a] = pt[a];
+        if (VC) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double a0 = (double)c0[a] / 255.0, a1 = (double)c1[a] / 255.0;
+                VC[vid * 3 + a] = (f1 * a0 + f0 * a1) / (f0 + f1);
+            }
+        }
+        ++vid;
+    }
+}
+
+__device__ inline int edge_vid(const McDev& m, const int* snbr, int x, int y, int z, int e) {
+    const int ox = x + c_eshift[e][0], oy = y + c_eshift[e][1], oz = z + c_eshift[e][2];
+    const int owner = snbr[((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4)];
+    const int local = (ox & 15) * 256 + (oy & 15) * 16 + (oz & 15);
+    const int bit = local * 3 + c_eshift[e][3];
+    const int word = bit >> 5;
+    if (owner < 0) return 0;
+    const unsigned wbits = m.eflags[(size_t)owner * EWORDS + word];
+    const unsigned below = wbits & ((1u << (bit & 31)) - 1u);
+    return (int)(m.vert_base[m.rank_of[owner]] + m.wprefix[(size_t)owner * EWORDS + word] + __popc(below));
+}
+
+__global__ __launch_bounds__(256) void k_mc_triangles(McDev m, int32_t* T) {
+    __shared__ int snbr[8];
+    const int r = blockIdx.x;
+    const int id = (int)m.sorted_ids[r];
+    const int t = threadIdx.x;
+    if (t < 8) snbr[t] = m.nbr[id * 8 + t];
+    const unsigned char* cubes = m.cubes + (size_t)id * UNIT_VOX + t * 16;
+    int cnt = 0;
+    for (int z = 0; z < UNIT_RES; ++z) {
+        const int cube = cubes[z];
+        if (cube == 0) continue;
+        for (int k = 0; k < 15 && c_tri[cube][k] != -1; k += 3) ++cnt;
+    }
+    int total;
+    const int pre = block_excl_scan_256(cnt, total);  // contains __syncthreads (snbr visible after)
+    long long out = m.tri_base[r] + pre;
+    const int x = t >> 4, y = t & 15;
+    for (int z = 0; z < UNIT_RES; ++z) {
+        const int cube = cubes[z];
+        if (cube == 0) continue;
+        for (int k = 0; k < 15 && c_tri[cube][k] != -1; k += 3) {
+            const int a = edge_vid(m, snbr, x, y, z, c_tri[cube][k]);
+            const int b = edge_vid(m, snbr, x, y, z, c_tri[cube][k + 1]);
+            const int c = edge_vid(m, snbr, x, y, z, c_tri[cube][k + 2]);
+            T[out * 3 + 0] = a;
+            T[out * 3 + 1] = c;
+            T[out * 3 + 2] = b;
+            ++out;
+        }
+    }
+}
+
+static bool g_tables_uploaded = false;
+
+static ot_status upload_tables() {
+    if (g_tables_uploaded) return OT_OK;
+    OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_tri), OT_MC_TRI_TABLE, sizeof(OT_MC_TRI_TABLE)));
+    OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_eshift), OT_MC_EDGE_SHIFT, sizeof(OT_MC_EDGE_SHIFT)));
+    OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_e2v), OT_MC_EDGE_TO_VERT, sizeof(OT_MC_EDGE_TO_VERT)));
+    OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_shift), OT_MC_SHIFT, sizeof(OT_MC_SHIFT)));
+    g_tables_uploaded = true;
+    return OT_OK;
+}
+
+template <typename T>
+static ot_status grow(T*& p, int64_t& cap, int64_t need) {
+    if (cap >= need && p) return OT_OK;
+    if (p) OT_HIP_TRY(hipFree(p));
+    p = nullptr;
+    const int64_t n = std::max<int64_t>(need + need / 4, 1024);
+    OT_HIP_TRY(hipMalloc(&p, sizeof(T) * (size_t)n));
+    cap = n;
+    return OT_OK;
+}
+
+}  // namespace ot
+
+using namespace ot;
+
+extern "C" {
+
+ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64_t* n_triangles, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!vol || !n_vertices || !n_triangles) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    ot_status st = upload_tables();
+    if (st != OT_OK) return st;
+    int64_t U = 0;
+    st = tsdf_sorted_units(vol, stream, &U);
+    if (st != OT_OK) return st;
+    vol->mesh.nv = vol->mesh.nt = 0;
+    *n_vertices = *n_triangles = 0;
+    if (U == 0) return OT_OK;
+    // workspace: ids are dense in [0, U)
+    const size_t bytes = (size_t)U * (4 * 8 + 4 + 8 * 4 + EWORDS * 4 * 2 + UNIT_VOX) + 16 * 256;
+    char* ws = (char*)scratch(bytes, 14);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    McDev m;
+    m.sorted_ids = vol->sorted_ids;
+    char* p = ws;
+    auto take = [&](size_t n) {
+        char* q = p;
+        p += (n + 255) & ~(size_t)255;
+        return q;
+    };
+    m.tri_cnt = (long long*)take(sizeof(long long) * U);
+    m.vert_cnt = (long long*)take(sizeof(long long) * U);
+    m.tri_base = (long long*)take(sizeof(long long) * U);
+    m.vert_base = (long long*)take(sizeof(long long) * U);
+    m.rank_of = (int*)take(sizeof(int) * U);
+    m.nbr = (int*)take(sizeof(int) * 8 * U);
+    m.eflags = (unsigned*)take(sizeof(unsigned) * EWORDS * U);
+    m.wprefix = (int*)take(sizeof(int) * EWORDS * U);
+    m.cubes = (unsigned char*)take((size_t)UNIT_VOX * U);
+    if ((size_t)(p - ws) > bytes) return fail(OT_ERR_HIP, "mc workspace overflow");
+    const unsigned g = (unsigned)U;
+    hipLaunchKernelGGL(k_mc_prepare, dim3(g), dim3(256), 0, stream, vol->dev, m);
+    hipLaunchKernelGGL(k_mc_classify, dim3(g), dim3(256), 0, stream, vol->dev, m);
+    hipLaunchKernelGGL(k_mc_count, dim3(g), dim3(EWORDS), 0, stream, m);
+    OT_LAUNCH_CHECK();
+    st = exclusive_scan_i64(m.tri_cnt, m.tri_base, (size_t)U, stream, 4);
+    if (st != OT_OK) return st;
+    st = exclusive_scan_i64(m.vert_cnt, m.vert_base, (size_t)U, stream, 15);
+    if (st != OT_OK) return st;
+    long long tails[4];
+    OT_HIP_TRY(hipMemcpyAsync(&tails[0], m.tri_base + U - 1, 8, hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipMemcpyAsync(&tails[1], m.tri_cnt + U - 1, 8, hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipMemcpyAsync(&tails[2], m.vert_base + U - 1, 8, hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipMemcpyAsync(&tails[3], m.vert_cnt + U - 1, 8, hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    const int64_t nt = tails[0] + tails[1], nv = tails[2] + tails[3];
+    if (nv > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] more than 2^31 vertices");
+    MeshBuffers& mb = vol->mesh;
+    int64_t capc = mb.cap_v;
+    st = grow(mb.v, mb.cap_v, nv * 3);
+    if (st != OT_OK) return st;
+    st = grow(mb.c, capc, nv * 3);
+    if (st != OT_OK) return st;
+    st = grow(mb.t, mb.cap_t, nt * 3);
+    if (st != OT_OK) return st;
+    hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, stream, vol->dev, m, vol->voxel_length, mb.v,
+                       vol->color_type == OT_COLOR_RGB8 ? mb.c : nullptr);
+    hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, m, mb.t);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    mb.nv = nv;
+    mb.nt = nt;
+    *n_vertices = nv;
+    *n_triangles = nt;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors, int32_t* triangles,
+                                      void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    const MeshBuffers& mb = vol->mesh;
+    if (mb.nv > 0 && vertices)
+        OT_HIP_TRY(hipMemcpyAsync(vertices, mb.v, sizeof(double) * 3 * mb.nv, hipMemcpyDefault, stream));
+    if (mb.nv > 0 && vertex_colors) {
+        if (vol->color_type == OT_COLOR_RGB8)
+            OT_HIP_TRY(hipMemcpyAsync(vertex_colors, mb.c, sizeof(double) * 3 * mb.nv, hipMemcpyDefault, stream));
+        else
+            OT_HIP_TRY(hipMemsetAsync(vertex_colors, 0, sizeof(double) * 3 * mb.nv, stream));
+    }
+    if (mb.nt > 0 && triangles)
+        OT_HIP_TRY(hipMemcpyAsync(triangles, mb.t, sizeof(int32_t) * 3 * mb.nt, hipMemcpyDefault, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
+}
+
+}  // extern "C"

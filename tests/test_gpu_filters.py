@@ -1,0 +1,135 @@
+"""GPU parity: voxel_down_sample, remove_statistical_outlier, remove_radius_outlier, Z-mask, occupancy points.
+
+Bit-exact: voxel key set, per-voxel averaged xyz/colour (sums in index order), ROR kept indices, Z-mask
+compaction, occupancy points.  SOR: per-point mean kNN distance bit-exact; kept indices bit-exact (the cloud
+mean/std are float64 reductions in a different association than Open3D's sequential std::accumulate — the
+test asserts no point lies within 1e-9 relative of the threshold, where that could matter).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_bitwise, ref_intr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def frame_cloud(pkg, O, synth, seq16, gpu):
+    depth, color, ext = seq16
+    intr_t = ref_intr(synth)
+    df = O.depth_to_float(depth[0], 1000.0, 5.0)
+    xyz, rgb = O.unproject(df, color[0], intr_t, ext[0])
+    return xyz, rgb
+
+
+def _pcd(pkg, xyz, rgb=None):
+    p = pkg.geometry.PointCloud()
+    p.points = pkg.utility.Vector3dVector(xyz)
+    if rgb is not None:
+        p.colors = pkg.utility.Vector3dVector(rgb)
+    return p
+
+
+@pytest.mark.parametrize("vs", [0.005, 0.01, 0.037])
+def test_voxel_down_sample_bitexact(pkg, O, frame_cloud, vs):
+    xyz, rgb = frame_cloud
+    ds = _pcd(pkg, xyz, rgb).voxel_down_sample(vs)
+    rv, rc, rk, _ = O.voxel_down_sample(xyz, rgb, vs)
+    assert len(ds.points) == rv.shape[0]
+    assert_bitwise(np.asarray(ds.points), rv, "voxel averages")
+    assert_bitwise(np.asarray(ds.colors), rc, "voxel colours")
+
+
+def test_voxel_down_sample_keys_and_edges(pkg, O, gpu):
+    L = pkg._lib
+    rng = np.random.default_rng(5)
+    xyz = rng.uniform(-3, 3, size=(20000, 3))
+    xyz[:100] = xyz[100:200]  # duplicates
+    d = torch.from_numpy(xyz).cuda()
+    ox = torch.empty_like(d)
+    ok = torch.empty((xyz.shape[0], 3), dtype=torch.int32, device="cuda")
+    n = C.c_int64(0)
+    L.call("ot_voxel_down_sample", C.c_void_p(d.data_ptr()), None, None, xyz.shape[0], 0.05,
+           C.c_void_p(ox.data_ptr()), None, None, C.c_void_p(ok.data_ptr()), C.byref(n), None)
+    rv, _, rk, _ = O.voxel_down_sample(xyz, None, 0.05)
+    assert n.value == rv.shape[0]
+    assert_bitwise(ok[:n.value].cpu().numpy(), rk, "voxel keys")
+    assert_bitwise(ox[:n.value].cpu().numpy(), rv, "voxel averages")
+    # single point, empty, invalid size
+    one = _pcd(pkg, xyz[:1]).voxel_down_sample(0.1)
+    assert_bitwise(np.asarray(one.points), xyz[:1], "single point")
+    assert len(_pcd(pkg, np.zeros((0, 3))).voxel_down_sample(0.1).points) == 0
+    with pytest.raises(RuntimeError, match="voxel_size"):
+        _pcd(pkg, xyz).voxel_down_sample(0.0)
+
+
+def test_ror_bitexact(pkg, O, frame_cloud):
+    xyz, rgb = frame_cloud
+    ds = O.voxel_down_sample(xyz, rgb, 0.01)[0]
+    for nb, r in ((16, 0.05), (4, 0.02)):
+        out, idx = _pcd(pkg, ds).remove_radius_outlier(nb, r)
+        ridx = O.remove_radius_outlier(ds, nb, r)
+        assert_bitwise(np.asarray(idx, np.int64), ridx, f"ROR({nb},{r}) kept")
+        assert_bitwise(np.asarray(out.points), ds[ridx], "ROR points")
+
+
+@pytest.mark.parametrize("k,ratio", [(20, 2.0), (8, 1.0), (48, 0.5)])
+def test_sor_bitexact(pkg, O, frame_cloud, k, ratio):
+    xyz, rgb = frame_cloud
+    ds = O.voxel_down_sample(xyz, rgb, 0.01)[0]
+    rng = np.random.default_rng(1)
+    ds = np.concatenate([ds, rng.uniform(-2, 2, size=(50, 3))])  # isolated outliers
+    L = pkg._lib
+    d = torch.from_numpy(ds).cuda()
+    idx = torch.empty(ds.shape[0], dtype=torch.int64, device="cuda")
+    avg = torch.empty(ds.shape[0], dtype=torch.float64, device="cuda")
+    n = C.c_int64(0)
+    L.call("ot_remove_statistical_outlier", C.c_void_p(d.data_ptr()), ds.shape[0], k, ratio,
+           C.c_void_p(idx.data_ptr()), C.c_void_p(avg.data_ptr()), C.byref(n), None)
+    ridx, ravg = O.remove_statistical_outlier(ds, k, ratio)
+    assert_bitwise(avg.cpu().numpy(), ravg, "SOR mean kNN distance")
+    valid = ravg[ravg > 0]
+    mean = valid.sum() / valid.size
+    thr = mean + ratio * np.sqrt(((valid - mean) ** 2).sum() / (valid.size - 1))
+    assert np.min(np.abs(valid - thr) / thr) > 1e-9
+    assert_bitwise(idx[:n.value].cpu().numpy(), ridx, "SOR kept indices")
+    assert not set(range(ds.shape[0] - 50, ds.shape[0])) <= set(ridx.tolist())
+
+
+def test_sor_small_and_errors(pkg, O, gpu):
+    pts = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 5.0]])
+    out, idx = _pcd(pkg, pts).remove_statistical_outlier(10, 1.0)  # k > n: every point sees all 4
+    ridx, _ = O.remove_statistical_outlier(pts, 10, 1.0)
+    assert idx == ridx.tolist()
+    with pytest.raises(RuntimeError, match="Illegal input"):
+        _pcd(pkg, pts).remove_statistical_outlier(0, 1.0)
+    with pytest.raises(RuntimeError, match="Illegal input"):
+        _pcd(pkg, pts).remove_radius_outlier(2, -1.0)
+    e, ei = _pcd(pkg, np.zeros((0, 3))).remove_statistical_outlier(5, 1.0)
+    assert len(e.points) == 0 and ei == []
+
+
+def test_filter_min_z_bitexact(pkg, O, frame_cloud):
+    xyz, rgb = frame_cloud
+    out = _pcd(pkg, xyz, rgb).filter_min_z(0.03)
+    rx, rc = O.filter_min_z(xyz, rgb, 0.03)
+    assert_bitwise(np.asarray(out.points), rx, "z-mask xyz")
+    assert_bitwise(np.asarray(out.colors), rc, "z-mask rgb")
+    mask = xyz[:, 2] >= 0.03  # reconstruct_rgbd_filter.py:128
+    assert_bitwise(rx, xyz[mask], "numpy boolean mask")
+
+
+def test_occupancy_points_bitexact(pkg, O, gpu):
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, size=(333, 517), dtype=np.uint8)
+    L = pkg._lib
+    d = torch.from_numpy(img).cuda()
+    out = torch.empty((img.size, 3), dtype=torch.float64, device="cuda")
+    n = C.c_int64(0)
+    L.call("ot_occupancy_to_points", C.c_void_p(d.data_ptr()), img.shape[0], img.shape[1], 100, 0.05, -12.5, -7.25,
+           C.c_void_p(out.data_ptr()), C.byref(n), None)
+    ref = O.occupancy_to_points(img, 100, 0.05, -12.5, -7.25)
+    assert_bitwise(out[:n.value].cpu().numpy(), ref, "occupancy points")
