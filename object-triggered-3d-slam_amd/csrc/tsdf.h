@@ -44,12 +44,29 @@ struct TsdfDev {
     unsigned long long* stats;
     int* unit_keys;
     float* vox;
+    unsigned long long* fmask;  // per hash slot: frames of the current batch that touch the unit (bit f)
+    int* bslots;                // hash slots touched by the current batch (first-touch order)
     int hash_mask;
     int max_units;
 };
 
+constexpr int MAX_BATCH = 64;  // frames per fused launch (one bit each in fmask)
+
+// per-frame parameters of a batch (device resident)
+struct BatchFrame {
+    const uint16_t* depth16;  // raw depth (u16 path) or nullptr
+    const float* depthf;      // float depth read by the kernels (batch slot for u16 input, else the caller's)
+    const uint8_t* color;     // RGB8 or nullptr
+    double pose[12];          // rows 0..2 of inverse(extrinsic) (stride unprojection, float64)
+    float E[12];              // rows 0..2 of (float)extrinsic
+    float es[3];              // column 2 of (float)extrinsic * voxel_length
+    float scale;              // (float)depth_scale
+    double trunc;             // depth_trunc
+};
+
 struct PendingFrame {
-    const uint16_t* depth;
+    const uint16_t* depth;  // u16 path (nullptr for the float path)
+    const float* depthf;    // float path
     const uint8_t* color;
     ot_intrinsics intr;
     double extrinsic[16];
@@ -82,10 +99,16 @@ struct ot_tsdf {
     float* depth_f = nullptr;
     int64_t depth_f_cap = 0;
     // batching of integrate_u16
-    int batch_max = 1;
+    int batch_max = 32;
     std::vector<ot::PendingFrame> pending;
-    void* batch_ws = nullptr;
+    void* batch_ws = nullptr;       // unused (kept for ABI of the struct layout)
     size_t batch_ws_bytes = 0;
+    ot::BatchFrame* bframes = nullptr;     // device [MAX_BATCH]
+    ot::BatchFrame* hbframes = nullptr;    // pinned host staging [2][MAX_BATCH]
+    hipEvent_t hb_event[2] = {nullptr, nullptr};
+    int hb_next = 0;
+    float* bdepth = nullptr;               // device [MAX_BATCH][h][w]
+    int64_t bdepth_cap = 0;
     // sorted-unit cache (rank -> id), valid for `sorted_units` units
     unsigned* sorted_ids = nullptr;
     int64_t sorted_units = -1;

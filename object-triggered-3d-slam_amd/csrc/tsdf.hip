@@ -235,6 +235,239 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
     }
 }
 
+// ============================================================================ batched (temporal blocking)
+// One launch per batch of F <= 64 frames:
+//   k_batch_depth     : u16 -> float depth for every frame of the batch (grid.y = frame)
+//   k_batch_touch     : stride samples of every frame; a unit touched by frame f gets bit f in its slot's
+//                       fmask (64-bit atomicOr); the first bit set in a batch appends the slot to bslots
+//   k_batch_integrate : one workgroup per touched slot: allocates the unit if new, loads its 16^3 voxel state
+//                       into registers (80 VGPRs/lane), applies the batch's frames in call order (ascending
+//                       bits of fmask), writes the state back once.  Per-voxel arithmetic is the per-frame
+//                       path's, so results are bit-identical to integrating frame by frame.
+__global__ __launch_bounds__(256) void k_batch_depth(const BatchFrame* __restrict__ frames, int64_t npx) {
+    const BatchFrame& fr = frames[blockIdx.y];
+    if (!fr.depth16) return;
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    if (i0 >= npx) return;
+    const uint16_t* in = fr.depth16;
+    float* out = const_cast<float*>(fr.depthf);
+    const float scale = fr.scale;
+    const double trunc = fr.trunc;
+    if (i0 + 8 <= npx && ((reinterpret_cast<uintptr_t>(in + i0) & 15) == 0)) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(in + i0);
+        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+        float f[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f[2 * k] = (float)(w[k] & 0xFFFFu);
+            f[2 * k + 1] = (float)(w[k] >> 16);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            f[k] = f[k] / scale;
+            if ((double)f[k] >= trunc) f[k] = 0.0f;
+        }
+        *reinterpret_cast<float4*>(out + i0) = make_float4(f[0], f[1], f[2], f[3]);
+        *reinterpret_cast<float4*>(out + i0 + 4) = make_float4(f[4], f[5], f[6], f[7]);
+    } else {
+        for (int64_t i = i0; i < npx && i < i0 + 8; ++i) {
+            float f = (float)in[i];
+            f = f / scale;
+            if ((double)f >= trunc) f = 0.0f;
+            out[i] = f;
+        }
+    }
+}
+
+struct BatchTouchParams {
+    int W, stride, ws, hs;
+    double fx, fy, cx, cy;
+    double trunc, unit_len;
+    int slot_cap;
+};
+
+__device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int x, int y, int z) {
+    if (!key_in_range(x, y, z)) {
+        atomicOr(&d.counters[C_HASHERR], 2);
+        return;
+    }
+    const int slot = hash_insert(d, pack_key(x, y, z));
+    if (slot < 0) {
+        atomicOr(&d.counters[C_HASHERR], 1);
+        return;
+    }
+    const unsigned long long bit = 1ull << f;
+    if (d.fmask[slot] & bit) return;  // fast path; a stale read only costs the atomic below
+    const unsigned long long old = atomicOr(&d.fmask[slot], bit);
+    if (old == 0ull) {
+        const int pos = atomicAdd(&d.counters[C_BATCH_PAIRS], 1);
+        if (pos < slot_cap) d.bslots[pos] = slot;
+        else atomicOr(&d.counters[C_HASHERR], 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restrict__ frames, BatchTouchParams p,
+                                                     TsdfDev d) {
+    const int f = blockIdx.y;
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= p.ws * p.hs) return;
+    const BatchFrame& fr = frames[f];
+    const int r = (s / p.ws) * p.stride, c = (s % p.ws) * p.stride;
+    const float df = fr.depthf[(int64_t)r * p.W + c];
+    if (!(df > 0.0f)) return;
+    const double z = (double)df;
+    const double x = ((double)c - p.cx) * z / p.fx;
+    const double y = ((double)r - p.cy) * z / p.fy;
+    double q[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double a = fr.pose[k * 4 + 0] * x;
+        const double b = fr.pose[k * 4 + 1] * y;
+        const double cc = fr.pose[k * 4 + 2] * z;
+        q[k] = ((a + b) + cc) + fr.pose[k * 4 + 3];
+    }
+    int lo[3], hi[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = (int)floor((q[k] - p.trunc) / p.unit_len);
+        hi[k] = (int)floor((q[k] + p.trunc) / p.unit_len);
+    }
+    for (int ux = lo[0]; ux <= hi[0]; ++ux)
+        for (int uy = lo[1]; uy <= hi[1]; ++uy)
+            for (int uz = lo[2]; uz <= hi[2]; ++uz) touch_unit_batch(d, f, p.slot_cap, ux, uy, uz);
+}
+
+__global__ __launch_bounds__(256) void k_batch_integrate(const BatchFrame* __restrict__ frames, IntegrateParams p,
+                                                         TsdfDev d) {
+    __shared__ int s_id;
+    __shared__ unsigned long long s_mask;
+    const int n = d.counters[C_BATCH_PAIRS];
+    const int tid = threadIdx.x;
+    const int x = tid >> 4, y = tid & 15;
+    unsigned long long upd = 0, pairs = 0;
+    for (int t = blockIdx.x; t < n; t += gridDim.x) {
+        const int slot = d.bslots[t];
+        if (tid == 0) {
+            const unsigned long long mask = d.fmask[slot];
+            d.fmask[slot] = 0ull;  // ready for the next batch (this workgroup owns the slot)
+            int id = d.hvals[slot];
+            if (id < 0) {
+                id = atomicAdd(&d.counters[C_UNITS], 1);
+                if (id >= d.max_units) {
+                    atomicOr(&d.counters[C_OVERFLOW], 1);
+                    id = -1;
+                } else {
+                    int kx, ky, kz;
+                    unpack_key(d.hkeys[slot], kx, ky, kz);
+                    d.hvals[slot] = id;
+                    d.unit_keys[id * 3 + 0] = kx;
+                    d.unit_keys[id * 3 + 1] = ky;
+                    d.unit_keys[id * 3 + 2] = kz;
+                    id |= (int)0x80000000u;  // fresh: state starts at zero
+                }
+            }
+            s_id = id;
+            s_mask = mask;
+        }
+        __syncthreads();
+        const int ent = s_id;
+        const unsigned long long mask = s_mask;
+        __syncthreads();  // s_id / s_mask may be rewritten by the next iteration
+        if (ent == -1) continue;
+        const int id = ent & 0x7FFFFFFF;
+        const bool fresh = ent < 0;
+        int kx, ky, kz;
+        unpack_key(d.hkeys[slot], kx, ky, kz);
+        float* base = d.vox + (size_t)id * UNIT_FLOATS;
+        float ts[UNIT_RES], wt[UNIT_RES], cr[UNIT_RES], cg[UNIT_RES], cb[UNIT_RES];
+#pragma unroll
+        for (int z = 0; z < UNIT_RES; ++z) {
+            const int vi = z * 256 + tid;
+            if (fresh) {
+                ts[z] = wt[z] = cr[z] = cg[z] = cb[z] = 0.0f;
+            } else {
+                ts[z] = base[vi];
+                wt[z] = base[UNIT_VOX + vi];
+                cr[z] = base[2 * UNIT_VOX + vi];
+                cg[z] = base[3 * UNIT_VOX + vi];
+                cb[z] = base[4 * UNIT_VOX + vi];
+            }
+        }
+        const float ox = (float)((double)kx * p.unit_len);
+        const float oy = (float)((double)ky * p.unit_len);
+        const float oz = (float)((double)kz * p.unit_len);
+        const float px = (p.half + p.vl * (float)x) + ox;
+        const float py = (p.half + p.vl * (float)y) + oy;
+        const float pz = p.half + oz;
+        for (unsigned long long m = mask; m; m &= m - 1) {
+            const int f = __ffsll((long long)m) - 1;
+            const BatchFrame& fr = frames[f];
+            const float* depth = fr.depthf;
+            const uint8_t* color = fr.color;
+            float pc[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const float a = fr.E[r * 4 + 0] * px;
+                const float b = fr.E[r * 4 + 1] * py;
+                const float c = fr.E[r * 4 + 2] * pz;
+                pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
+            }
+            const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
+            ++pairs;
+#pragma unroll
+            for (int z = 0; z < UNIT_RES; ++z) {
+                if (pc[2] > 0.0f) {
+                    const float u_f = ((pc[0] * p.fx) / pc[2] + p.cx) + 0.5f;
+                    const float v_f = ((pc[1] * p.fy) / pc[2] + p.cy) + 0.5f;
+                    if (u_f >= 0.0001f && u_f < p.safe_w && v_f >= 0.0001f && v_f < p.safe_h) {
+                        const int pix = (int)v_f * p.W + (int)u_f;
+                        const float dd = depth[pix];
+                        if (dd > 0.0f) {
+                            const float sdf = (dd - pc[2]) * p.mult[pix];
+                            if (sdf > -p.trunc) {
+                                const float sv = sdf * p.trunc_inv;
+                                const float tn = (sv < 1.0f) ? sv : 1.0f;
+                                const float w = wt[z];
+                                const float w1 = w + 1.0f;
+                                ts[z] = (ts[z] * w + tn) / w1;
+                                if (color) {
+                                    const uint8_t* c = color + (int64_t)pix * 3;
+                                    cr[z] = (cr[z] * w + (float)c[0]) / w1;
+                                    cg[z] = (cg[z] * w + (float)c[1]) / w1;
+                                    cb[z] = (cb[z] * w + (float)c[2]) / w1;
+                                }
+                                wt[z] = w1;
+                                ++upd;
+                            }
+                        }
+                    }
+                }
+                pc[0] += es0;
+                pc[1] += es1;
+                pc[2] += es2;
+            }
+        }
+#pragma unroll
+        for (int z = 0; z < UNIT_RES; ++z) {
+            const int vi = z * 256 + tid;
+            base[vi] = ts[z];
+            base[UNIT_VOX + vi] = wt[z];
+            base[2 * UNIT_VOX + vi] = cr[z];
+            base[3 * UNIT_VOX + vi] = cg[z];
+            base[4 * UNIT_VOX + vi] = cb[z];
+        }
+    }
+    upd = wave_sum(upd);
+    __shared__ unsigned long long red[4];
+    if (lane_id() == 0) red[tid >> 6] = upd;
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+        if (tot) atomicAdd(&d.stats[S_UPDATES], tot);
+        if (pairs) atomicAdd(&d.stats[S_UNIT_INTEGRATIONS], pairs);
+    }
+}
+
 // export: units in sorted order, voxels transposed to Open3D IndexOf order (x*256 + y*16 + z)
 __global__ __launch_bounds__(256) void k_export(TsdfDev d, const unsigned* sorted_ids, int32_t* keys, float* tsdf,
                                                 float* weight, float* color) {
@@ -358,24 +591,115 @@ static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t
     return OT_OK;
 }
 
+static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n, hipStream_t stream) {
+    const ot_intrinsics& in = frames[0].intr;
+    ot_status st = ensure_mult(vol, &in, stream);
+    if (st != OT_OK) return st;
+    const int64_t npx = (int64_t)in.width * in.height;
+    if (vol->bdepth_cap < npx * n) {
+        if (vol->bdepth) {
+            OT_HIP_TRY(hipStreamSynchronize(stream));
+            OT_HIP_TRY(hipFree(vol->bdepth));
+            vol->bdepth = nullptr;
+        }
+        const int64_t cap = npx * std::max(n, vol->batch_max);
+        OT_HIP_TRY(hipMalloc(&vol->bdepth, sizeof(float) * cap));
+        vol->bdepth_cap = cap;
+    }
+    // per-frame parameters: pinned host staging (double-buffered, event-guarded) -> device
+    const int hb = vol->hb_next;
+    vol->hb_next ^= 1;
+    if (vol->hb_event[hb]) OT_HIP_TRY(hipEventSynchronize(vol->hb_event[hb]));
+    BatchFrame* host = vol->hbframes + hb * MAX_BATCH;
+    const IntegrateParams ip0 = make_integrate_params(vol, nullptr, nullptr, vol->mult, &in, frames[0].extrinsic);
+    for (int k = 0; k < n; ++k) {
+        const PendingFrame& f = frames[k];
+        BatchFrame& b = host[k];
+        b.depth16 = f.depth;
+        b.depthf = f.depth ? vol->bdepth + npx * k : f.depthf;
+        b.color = (vol->color_type == OT_COLOR_RGB8) ? f.color : nullptr;
+        double pose[16];
+        inverse4(f.extrinsic, pose);
+        for (int i = 0; i < 12; ++i) b.pose[i] = pose[i];
+        float E[16];
+        for (int i = 0; i < 16; ++i) E[i] = (float)f.extrinsic[i];
+        for (int i = 0; i < 12; ++i) b.E[i] = E[i];
+        b.es[0] = E[0 * 4 + 2] * ip0.vl;
+        b.es[1] = E[1 * 4 + 2] * ip0.vl;
+        b.es[2] = E[2 * 4 + 2] * ip0.vl;
+        b.scale = (float)f.depth_scale;
+        b.trunc = f.depth_trunc;
+    }
+    OT_HIP_TRY(hipMemcpyAsync(vol->bframes, host, sizeof(BatchFrame) * n, hipMemcpyHostToDevice, stream));
+    if (!vol->hb_event[hb]) OT_HIP_TRY(hipEventCreateWithFlags(&vol->hb_event[hb], hipEventDisableTiming));
+    OT_HIP_TRY(hipEventRecord(vol->hb_event[hb], stream));
+    OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, sizeof(int), stream));
+    hipLaunchKernelGGL(k_batch_depth, dim3((unsigned)((npx / 8 + 255) / 256 + 1), n), dim3(256), 0, stream,
+                       (const BatchFrame*)vol->bframes, npx);
+    BatchTouchParams tp;
+    tp.W = in.width;
+    tp.stride = vol->stride;
+    tp.ws = (in.width + vol->stride - 1) / vol->stride;
+    tp.hs = (in.height + vol->stride - 1) / vol->stride;
+    tp.fx = in.fx;
+    tp.fy = in.fy;
+    tp.cx = in.cx;
+    tp.cy = in.cy;
+    tp.trunc = vol->sdf_trunc;
+    tp.unit_len = vol->unit_length;
+    tp.slot_cap = (int)vol->hash_cap;
+    hipLaunchKernelGGL(k_batch_touch, dim3((unsigned)((tp.ws * tp.hs + 255) / 256), n), dim3(256), 0, stream,
+                       (const BatchFrame*)vol->bframes, tp, vol->dev);
+    const int grid = (int)std::min<int64_t>(vol->max_units, 2048);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (vol->profiling) {
+        OT_HIP_TRY(hipEventCreate(&e0));
+        OT_HIP_TRY(hipEventCreate(&e1));
+        OT_HIP_TRY(hipEventRecord(e0, stream));
+    }
+    hipLaunchKernelGGL(k_batch_integrate, dim3(grid), dim3(256), 0, stream, (const BatchFrame*)vol->bframes, ip0,
+                       vol->dev);
+    OT_LAUNCH_CHECK();
+    if (vol->profiling) {
+        OT_HIP_TRY(hipEventRecord(e1, stream));
+        vol->prof_events.emplace_back(e0, e1);
+    }
+    vol->frame_id += n;
+    vol->sorted_frame = -1;
+    return OT_OK;
+}
+
+static ot_status integrate_single(ot_tsdf* vol, const PendingFrame& f, hipStream_t stream) {
+    if (!f.depth) return integrate_float(vol, f.depthf, f.color, &f.intr, f.extrinsic, stream);
+    const int64_t npx = (int64_t)f.intr.width * f.intr.height;
+    if (vol->depth_f_cap < npx) {
+        if (vol->depth_f) {
+            OT_HIP_TRY(hipStreamSynchronize(stream));
+            OT_HIP_TRY(hipFree(vol->depth_f));
+        }
+        OT_HIP_TRY(hipMalloc(&vol->depth_f, sizeof(float) * npx));
+        vol->depth_f_cap = npx;
+    }
+    ot_status st = ot_depth_to_float(f.depth, vol->depth_f, npx, f.depth_scale, f.depth_trunc, stream);
+    if (st != OT_OK) return st;
+    return integrate_float(vol, vol->depth_f, f.color, &f.intr, f.extrinsic, stream);
+}
+
 ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream) {
-    if (vol->pending.empty()) return OT_OK;
+    size_t i = 0;
     std::vector<PendingFrame> frames;
     frames.swap(vol->pending);
-    for (const PendingFrame& f : frames) {
-        const int64_t npx = (int64_t)f.intr.width * f.intr.height;
-        if (vol->depth_f_cap < npx) {
-            if (vol->depth_f) {
-                OT_HIP_TRY(hipStreamSynchronize(stream));
-                OT_HIP_TRY(hipFree(vol->depth_f));
-            }
-            OT_HIP_TRY(hipMalloc(&vol->depth_f, sizeof(float) * npx));
-            vol->depth_f_cap = npx;
-        }
-        ot_status st = ot_depth_to_float(f.depth, vol->depth_f, npx, f.depth_scale, f.depth_trunc, stream);
+    while (i < frames.size()) {
+        // a batch: consecutive frames with identical intrinsics, at most batch_max (<= 64)
+        size_t n = 1;
+        const int cap = std::min(vol->batch_max, MAX_BATCH);
+        while (i + n < frames.size() && (int)n < cap &&
+               std::memcmp(&frames[i + n].intr, &frames[i].intr, sizeof(ot_intrinsics)) == 0)
+            ++n;
+        ot_status st = (n == 1) ? integrate_single(vol, frames[i], stream)
+                                : integrate_batch(vol, frames.data() + i, (int)n, stream);
         if (st != OT_OK) return st;
-        st = integrate_float(vol, vol->depth_f, f.color, &f.intr, f.extrinsic, stream);
-        if (st != OT_OK) return st;
+        i += n;
     }
     return OT_OK;
 }
@@ -465,6 +789,11 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
     if ((e = hipMalloc(&d.unit_keys, sizeof(int) * 3 * max_units)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.vox, sizeof(float) * (size_t)UNIT_FLOATS * max_units)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&v->sorted_ids, sizeof(unsigned) * max_units)) != hipSuccess) return cleanup(e);
+    if ((e = hipMalloc(&d.fmask, sizeof(unsigned long long) * cap)) != hipSuccess) return cleanup(e);
+    if ((e = hipMalloc(&d.bslots, sizeof(int) * cap)) != hipSuccess) return cleanup(e);
+    if ((e = hipMalloc(&v->bframes, sizeof(BatchFrame) * MAX_BATCH)) != hipSuccess) return cleanup(e);
+    if ((e = hipHostMalloc(&v->hbframes, sizeof(BatchFrame) * MAX_BATCH * 2, hipHostMallocDefault)) != hipSuccess)
+        return cleanup(e);
     ot_status st = ot_tsdf_reset(v);
     if (st != OT_OK) {
         ot_tsdf_destroy(v);
@@ -480,9 +809,13 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
     void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, v->mult,
-                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t};
+                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, d.fmask, d.bslots,
+                    v->bframes, v->bdepth};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (v->hbframes) (void)hipHostFree(v->hbframes);
+    for (hipEvent_t ev : v->hb_event)
+        if (ev) (void)hipEventDestroy(ev);
     delete v;
     return OT_OK;
 }
@@ -493,6 +826,7 @@ ot_status ot_tsdf_reset(ot_tsdf* v) {
     OT_HIP_TRY(hipMemset(d.hkeys, 0xFF, sizeof(unsigned long long) * v->hash_cap));
     OT_HIP_TRY(hipMemset(d.hvals, 0xFF, sizeof(int) * v->hash_cap));
     OT_HIP_TRY(hipMemset(d.stamp, 0xFF, sizeof(int) * v->hash_cap));
+    OT_HIP_TRY(hipMemset(d.fmask, 0, sizeof(unsigned long long) * v->hash_cap));
     OT_HIP_TRY(hipMemset(d.counters, 0, sizeof(int) * N_COUNTERS));
     OT_HIP_TRY(hipMemset(d.stats, 0, sizeof(unsigned long long) * 4));
     OT_HIP_TRY(hipDeviceSynchronize());
@@ -508,9 +842,17 @@ ot_status ot_tsdf_integrate(ot_tsdf* vol, const float* depth, const uint8_t* col
                             const double extrinsic[16], void* stream) {
     ot_status st = check_frame(vol, depth, color, in, extrinsic);
     if (st != OT_OK) return st;
-    st = tsdf_flush(vol, S(stream));  // keep call order across the two entry points
-    if (st != OT_OK) return st;
-    return integrate_float(vol, depth, color, in, extrinsic, S(stream));
+    PendingFrame f;
+    f.depth = nullptr;
+    f.depthf = depth;
+    f.color = color;
+    f.intr = *in;
+    std::memcpy(f.extrinsic, extrinsic, sizeof(double) * 16);
+    f.depth_scale = 1.0;
+    f.depth_trunc = 0.0;
+    vol->pending.push_back(f);
+    if ((int)vol->pending.size() >= std::min(vol->batch_max, MAX_BATCH)) return tsdf_flush(vol, S(stream));
+    return OT_OK;
 }
 
 ot_status ot_tsdf_integrate_u16(ot_tsdf* vol, const uint16_t* depth, const uint8_t* color, const ot_intrinsics* in,
@@ -519,13 +861,14 @@ ot_status ot_tsdf_integrate_u16(ot_tsdf* vol, const uint16_t* depth, const uint8
     if (st != OT_OK) return st;
     PendingFrame f;
     f.depth = depth;
+    f.depthf = nullptr;
     f.color = color;
     f.intr = *in;
     std::memcpy(f.extrinsic, extrinsic, sizeof(double) * 16);
     f.depth_scale = depth_scale;
     f.depth_trunc = depth_trunc;
     vol->pending.push_back(f);
-    if ((int)vol->pending.size() >= vol->batch_max) return tsdf_flush(vol, S(stream));
+    if ((int)vol->pending.size() >= std::min(vol->batch_max, MAX_BATCH)) return tsdf_flush(vol, S(stream));
     return OT_OK;
 }
 

@@ -25,10 +25,11 @@ class ScalableTSDFVolume:
     volume_unit_resolution=16, depth_sampling_stride=4).
 
     Extra keyword arguments (not in Open3D): `max_units` (block-pool capacity in HBM) and `batch_frames`
-    (frames queued per fused integration launch; results are identical for any value)."""
+    (frames queued per fused integration launch, default 32, max 64; 1 = integrate immediately).  Results
+    are bit-identical for any value: a batch applies its frames to each voxel in call order."""
 
     def __init__(self, voxel_length, sdf_trunc, color_type=TSDFVolumeColorType.NoColor, volume_unit_resolution=16,
-                 depth_sampling_stride=4, max_units=0, batch_frames=1):
+                 depth_sampling_stride=4, max_units=0, batch_frames=None):
         D.require_gpu()
         ct = int(color_type)
         if ct == TSDFVolumeColorType.Gray32:
@@ -43,7 +44,7 @@ class ScalableTSDFVolume:
                self.depth_sampling_stride, int(max_units), C.byref(h))
         self._h = h
         self._keep = []  # frames queued for a batched launch stay referenced until the flush
-        if batch_frames != 1:
+        if batch_frames is not None:
             self.set_batch(batch_frames)
 
     def __del__(self):
@@ -83,7 +84,9 @@ class ScalableTSDFVolume:
             L.call("ot_tsdf_integrate_u16", self._h, D.ptr(d16), D.ptr(cdev), C.byref(intr),
                    ext.ctypes.data_as(C.c_void_p), scale, trunc, D.stream_ptr())
         else:
-            L.call("ot_tsdf_integrate", self._h, D.ptr(depth.dev()), D.ptr(cdev), C.byref(intr),
+            ddev = depth.dev()
+            self._keep.append((ddev, cdev))
+            L.call("ot_tsdf_integrate", self._h, D.ptr(ddev), D.ptr(cdev), C.byref(intr),
                    ext.ctypes.data_as(C.c_void_p), D.stream_ptr())
 
     def flush(self):

@@ -77,7 +77,7 @@ def test_unproject_stride_and_empty(pkg, O, gpu, synth, seq16):
     assert len(empty.points) == 0
 
 
-def _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=1, trunc=3.0):
+def _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=None, trunc=3.0, float_path=False):
     integ = _integration(pkg)
     intr_t = ref_intr(synth)
     intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
@@ -88,6 +88,8 @@ def _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=1, trunc=3.0):
         rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
             pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=trunc,
             convert_rgb_to_intensity=False)
+        if float_path:
+            rgbd._raw_depth = None  # force the float-depth entry point (ot_tsdf_integrate)
         vol.integrate(rgbd, intr, ext[k])
         ref.integrate(O.depth_to_float(depth[k], 1000.0, trunc), color[k], intr_t, ext[k])
     return vol, ref
@@ -107,11 +109,26 @@ def _compare_volumes(vol, ref):
 
 
 @pytest.mark.parametrize("voxel", [0.01, 0.005])
-def test_tsdf_integrate_bitexact(pkg, O, gpu, synth, seq16, voxel):
+@pytest.mark.parametrize("batch", [1, 3, None])
+def test_tsdf_integrate_bitexact(pkg, O, gpu, synth, seq16, voxel, batch):
     depth, color, ext = seq16
-    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, voxel)
+    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=batch)
     n = _compare_volumes(vol, ref)
     assert n > 300
+
+
+def test_tsdf_float_path_batched(pkg, O, gpu, synth, seq16):
+    depth, color, ext = seq16
+    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, float_path=True)
+    _compare_volumes(vol, ref)
+
+
+def test_tsdf_many_batches_5mm(pkg, O, gpu, synth):
+    """70 frames of a 70-frame ring at 5 mm: two 32-frame batches, one 6-frame batch; full 360 deg coverage."""
+    depth, color, ext = synth.make_sequence(n_frames=70)
+    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005)
+    n = _compare_volumes(vol, ref)
+    assert n > 3000
 
 
 def test_tsdf_lexical_order_matters(pkg, O, gpu, synth, seq16):
