@@ -55,8 +55,10 @@ constexpr int MAX_BATCH = 64;  // frames per fused launch (one bit each in fmask
 // per-frame parameters of a batch (device resident)
 struct BatchFrame {
     const uint16_t* depth16;  // raw depth (u16 path) or nullptr
-    const float* depthf;      // float depth read by the kernels (batch slot for u16 input, else the caller's)
-    const uint8_t* color;     // RGB8 or nullptr
+    const float* depthf;      // caller's float depth (float path) or nullptr
+    const uint8_t* color;     // caller's RGB8 or nullptr
+    float2* dm;               // packed per-pixel (depth, ray multiplier) written by k_batch_prep
+    uint32_t* rgba;           // packed per-pixel colour r | g << 8 | b << 16 written by k_batch_prep
     double pose[12];          // rows 0..2 of inverse(extrinsic) (stride unprojection, float64)
     float E[12];              // rows 0..2 of (float)extrinsic
     float es[3];              // column 2 of (float)extrinsic * voxel_length
@@ -107,8 +109,9 @@ struct ot_tsdf {
     ot::BatchFrame* hbframes = nullptr;    // pinned host staging [2][MAX_BATCH]
     hipEvent_t hb_event[2] = {nullptr, nullptr};
     int hb_next = 0;
-    float* bdepth = nullptr;               // device [MAX_BATCH][h][w]
-    int64_t bdepth_cap = 0;
+    float2* bdm = nullptr;                 // device [batch][h][w] packed (depth, multiplier)
+    uint32_t* brgba = nullptr;             // device [batch][h][w] packed colour
+    int64_t bdepth_cap = 0;                // pixels (frames * h * w) the two buffers hold
     // sorted-unit cache (rank -> id), valid for `sorted_units` units
     unsigned* sorted_ids = nullptr;
     int64_t sorted_units = -1;

@@ -237,45 +237,33 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
 
 // ============================================================================ batched (temporal blocking)
 // One launch per batch of F <= 64 frames:
-//   k_batch_depth     : u16 -> float depth for every frame of the batch (grid.y = frame)
+//   k_batch_prep      : per-pixel (depth, multiplier) float2 + packed colour for every frame (grid.y = frame)
 //   k_batch_touch     : stride samples of every frame; a unit touched by frame f gets bit f in its slot's
 //                       fmask (64-bit atomicOr); the first bit set in a batch appends the slot to bslots
-//   k_batch_integrate : one workgroup per touched slot: allocates the unit if new, loads its 16^3 voxel state
-//                       into registers (80 VGPRs/lane), applies the batch's frames in call order (ascending
+//   k_batch_integrate : one 512-lane workgroup per touched slot: allocates the unit if new, loads its 16^3 voxel
+//                       state into registers (40 VGPRs/lane), applies the batch's frames in call order (ascending
 //                       bits of fmask), writes the state back once.  Per-voxel arithmetic is the per-frame
 //                       path's, so results are bit-identical to integrating frame by frame.
-__global__ __launch_bounds__(256) void k_batch_depth(const BatchFrame* __restrict__ frames, int64_t npx) {
+// Per-pixel staging of a batch: (depth, multiplier) as float2 and the colour as one u32, so the integrate
+// kernel fetches a voxel's inputs with two aligned loads it can issue ahead of use.
+// depth: u16 path converted exactly as Image::ConvertDepthToFloatImage; float path copied.
+__global__ __launch_bounds__(256) void k_batch_prep(const BatchFrame* __restrict__ frames, const float* __restrict__ mult,
+                                                    int64_t npx) {
     const BatchFrame& fr = frames[blockIdx.y];
-    if (!fr.depth16) return;
-    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
-    if (i0 >= npx) return;
-    const uint16_t* in = fr.depth16;
-    float* out = const_cast<float*>(fr.depthf);
-    const float scale = fr.scale;
-    const double trunc = fr.trunc;
-    if (i0 + 8 <= npx && ((reinterpret_cast<uintptr_t>(in + i0) & 15) == 0)) {
-        const uint4 raw = *reinterpret_cast<const uint4*>(in + i0);
-        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
-        float f[8];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            f[2 * k] = (float)(w[k] & 0xFFFFu);
-            f[2 * k + 1] = (float)(w[k] >> 16);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            f[k] = f[k] / scale;
-            if ((double)f[k] >= trunc) f[k] = 0.0f;
-        }
-        *reinterpret_cast<float4*>(out + i0) = make_float4(f[0], f[1], f[2], f[3]);
-        *reinterpret_cast<float4*>(out + i0 + 4) = make_float4(f[4], f[5], f[6], f[7]);
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= npx) return;
+    float dv;
+    if (fr.depth16) {
+        dv = (float)fr.depth16[i];
+        dv = dv / fr.scale;
+        if ((double)dv >= fr.trunc) dv = 0.0f;
     } else {
-        for (int64_t i = i0; i < npx && i < i0 + 8; ++i) {
-            float f = (float)in[i];
-            f = f / scale;
-            if ((double)f >= trunc) f = 0.0f;
-            out[i] = f;
-        }
+        dv = fr.depthf[i];
+    }
+    fr.dm[i] = make_float2(dv, mult[i]);
+    if (fr.color) {
+        const uint8_t* c = fr.color + i * 3;
+        fr.rgba[i] = (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16);
     }
 }
 
@@ -306,44 +294,117 @@ __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, i
     }
 }
 
-__global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restrict__ frames, BatchTouchParams p,
-                                                     TsdfDev d) {
-    const int f = blockIdx.y;
-    const int s = blockIdx.x * 256 + threadIdx.x;
-    if (s >= p.ws * p.hs) return;
-    const BatchFrame& fr = frames[f];
-    const int r = (s / p.ws) * p.stride, c = (s % p.ws) * p.stride;
-    const float df = fr.depthf[(int64_t)r * p.W + c];
-    if (!(df > 0.0f)) return;
-    const double z = (double)df;
-    const double x = ((double)c - p.cx) * z / p.fx;
-    const double y = ((double)r - p.cy) * z / p.fy;
-    double q[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const double a = fr.pose[k * 4 + 0] * x;
-        const double b = fr.pose[k * 4 + 1] * y;
-        const double cc = fr.pose[k * 4 + 2] * z;
-        q[k] = ((a + b) + cc) + fr.pose[k * 4 + 3];
+// Touch pass with LDS de-duplication.  A workgroup owns a 16x16 tile of stride samples and a group of TF frames;
+// each (unit key, frame) hit is first merged into an LDS table (key -> frame bitmask, 64-bit LDS atomics), then
+// every distinct unit of the tile does ONE global hash insert + ONE atomicOr of its merged mask.  A key that does
+// not fit the LDS table falls back to the direct global path.
+constexpr int TT = 16;          // tile edge in samples
+constexpr int TF = 8;           // frames per workgroup
+constexpr int LTAB = 2048;      // LDS table entries (32 KiB)
+
+__device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* masks, unsigned long long key,
+                                 unsigned long long bit) {
+    unsigned h = (unsigned)mix64(key) & (LTAB - 1);
+    for (int probe = 0; probe < 64; ++probe) {
+        unsigned long long k = keys[h];
+        if (k == KEY_EMPTY) {
+            const unsigned long long old = atomicCAS(&keys[h], KEY_EMPTY, key);
+            k = (old == KEY_EMPTY) ? key : old;
+        }
+        if (k == key) {
+            atomicOr(&masks[h], bit);
+            return true;
+        }
+        h = (h + 1) & (LTAB - 1);
     }
-    int lo[3], hi[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        lo[k] = (int)floor((q[k] - p.trunc) / p.unit_len);
-        hi[k] = (int)floor((q[k] + p.trunc) / p.unit_len);
-    }
-    for (int ux = lo[0]; ux <= hi[0]; ++ux)
-        for (int uy = lo[1]; uy <= hi[1]; ++uy)
-            for (int uz = lo[2]; uz <= hi[2]; ++uz) touch_unit_batch(d, f, p.slot_cap, ux, uy, uz);
+    return false;
 }
 
-__global__ __launch_bounds__(256) void k_batch_integrate(const BatchFrame* __restrict__ frames, IntegrateParams p,
-                                                         TsdfDev d) {
+__global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restrict__ frames, BatchTouchParams p,
+                                                     TsdfDev d, int nframes) {
+    __shared__ unsigned long long s_keys[LTAB];
+    __shared__ unsigned long long s_masks[LTAB];
+    const int tid = threadIdx.x;
+    for (int e = tid; e < LTAB; e += 256) {
+        s_keys[e] = KEY_EMPTY;
+        s_masks[e] = 0ull;
+    }
+    __syncthreads();
+    const int tiles_x = (p.ws + TT - 1) / TT;
+    const int sx = (blockIdx.x % tiles_x) * TT + (tid & (TT - 1));
+    const int sy = (blockIdx.x / tiles_x) * TT + (tid / TT);
+    const int f0 = blockIdx.y * TF;
+    if (sx < p.ws && sy < p.hs) {
+        const int r = sy * p.stride, c = sx * p.stride;
+        for (int f = f0; f < f0 + TF && f < nframes; ++f) {
+            const BatchFrame& fr = frames[f];
+            const float df = fr.dm[(int64_t)r * p.W + c].x;
+            if (!(df > 0.0f)) continue;
+            const double z = (double)df;
+            const double x = ((double)c - p.cx) * z / p.fx;
+            const double y = ((double)r - p.cy) * z / p.fy;
+            double q[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const double a = fr.pose[k * 4 + 0] * x;
+                const double b = fr.pose[k * 4 + 1] * y;
+                const double cc = fr.pose[k * 4 + 2] * z;
+                q[k] = ((a + b) + cc) + fr.pose[k * 4 + 3];
+            }
+            int lo[3], hi[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = (int)floor((q[k] - p.trunc) / p.unit_len);
+                hi[k] = (int)floor((q[k] + p.trunc) / p.unit_len);
+            }
+            const unsigned long long bit = 1ull << f;
+            for (int ux = lo[0]; ux <= hi[0]; ++ux)
+                for (int uy = lo[1]; uy <= hi[1]; ++uy)
+                    for (int uz = lo[2]; uz <= hi[2]; ++uz) {
+                        if (!key_in_range(ux, uy, uz)) {
+                            atomicOr(&d.counters[C_HASHERR], 2);
+                            continue;
+                        }
+                        if (!lds_merge(s_keys, s_masks, pack_key(ux, uy, uz), bit))
+                            touch_unit_batch(d, f, p.slot_cap, ux, uy, uz);
+                    }
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < LTAB; e += 256) {
+        const unsigned long long key = s_keys[e];
+        if (key == KEY_EMPTY) continue;
+        const int slot = hash_insert(d, key);
+        if (slot < 0) {
+            atomicOr(&d.counters[C_HASHERR], 1);
+            continue;
+        }
+        const unsigned long long m = s_masks[e];
+        if ((d.fmask[slot] & m) == m) continue;  // fast path; a stale read only costs the atomic below
+        const unsigned long long old = atomicOr(&d.fmask[slot], m);
+        if (old == 0ull) {
+            const int pos = atomicAdd(&d.counters[C_BATCH_PAIRS], 1);
+            if (pos < p.slot_cap) d.bslots[pos] = slot;
+            else atomicOr(&d.counters[C_HASHERR], 1);
+        }
+    }
+}
+
+// 512 lanes per unit: lane = (half h, column x, y); half h owns z in [8h, 8h + 8).  The camera-space voxel
+// position still advances by exactly z sequential additions of Es.col(2) from the column origin, as in
+// Open3D, so both halves reproduce the single-lane z walk bit for bit.
+constexpr int BZ = 8;
+constexpr int BLANES = UNIT_VOX / BZ;  // 512
+
+__global__ __launch_bounds__(BLANES) void k_batch_integrate(const BatchFrame* __restrict__ frames, IntegrateParams p,
+                                                            TsdfDev d) {
     __shared__ int s_id;
     __shared__ unsigned long long s_mask;
+    __shared__ unsigned long long red[BLANES / 64];
     const int n = d.counters[C_BATCH_PAIRS];
     const int tid = threadIdx.x;
-    const int x = tid >> 4, y = tid & 15;
+    const int col = tid & 255, half = tid >> 8;
+    const int x = col >> 4, y = col & 15, z0 = half * BZ;
     unsigned long long upd = 0, pairs = 0;
     for (int t = blockIdx.x; t < n; t += gridDim.x) {
         const int slot = d.bslots[t];
@@ -368,29 +429,30 @@ __global__ __launch_bounds__(256) void k_batch_integrate(const BatchFrame* __res
             }
             s_id = id;
             s_mask = mask;
+            pairs += (unsigned long long)__popcll(mask);
         }
         __syncthreads();
         const int ent = s_id;
         const unsigned long long mask = s_mask;
-        __syncthreads();  // s_id / s_mask may be rewritten by the next iteration
+        __syncthreads();  // s_id / s_mask are rewritten by the next iteration
         if (ent == -1) continue;
         const int id = ent & 0x7FFFFFFF;
         const bool fresh = ent < 0;
         int kx, ky, kz;
         unpack_key(d.hkeys[slot], kx, ky, kz);
         float* base = d.vox + (size_t)id * UNIT_FLOATS;
-        float ts[UNIT_RES], wt[UNIT_RES], cr[UNIT_RES], cg[UNIT_RES], cb[UNIT_RES];
+        float ts[BZ], wt[BZ], cr[BZ], cg[BZ], cb[BZ];
 #pragma unroll
-        for (int z = 0; z < UNIT_RES; ++z) {
-            const int vi = z * 256 + tid;
+        for (int k = 0; k < BZ; ++k) {
+            const int vi = (z0 + k) * 256 + col;
             if (fresh) {
-                ts[z] = wt[z] = cr[z] = cg[z] = cb[z] = 0.0f;
+                ts[k] = wt[k] = cr[k] = cg[k] = cb[k] = 0.0f;
             } else {
-                ts[z] = base[vi];
-                wt[z] = base[UNIT_VOX + vi];
-                cr[z] = base[2 * UNIT_VOX + vi];
-                cg[z] = base[3 * UNIT_VOX + vi];
-                cb[z] = base[4 * UNIT_VOX + vi];
+                ts[k] = base[vi];
+                wt[k] = base[UNIT_VOX + vi];
+                cr[k] = base[2 * UNIT_VOX + vi];
+                cg[k] = base[3 * UNIT_VOX + vi];
+                cb[k] = base[4 * UNIT_VOX + vi];
             }
         }
         const float ox = (float)((double)kx * p.unit_len);
@@ -402,8 +464,9 @@ __global__ __launch_bounds__(256) void k_batch_integrate(const BatchFrame* __res
         for (unsigned long long m = mask; m; m &= m - 1) {
             const int f = __ffsll((long long)m) - 1;
             const BatchFrame& fr = frames[f];
-            const float* depth = fr.depthf;
-            const uint8_t* color = fr.color;
+            const float2* dm = fr.dm;
+            const uint32_t* rgba = fr.rgba;
+            const bool use_color = fr.color != nullptr;
             float pc[3];
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
@@ -413,56 +476,76 @@ __global__ __launch_bounds__(256) void k_batch_integrate(const BatchFrame* __res
                 pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
             }
             const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
-            ++pairs;
-#pragma unroll
-            for (int z = 0; z < UNIT_RES; ++z) {
-                if (pc[2] > 0.0f) {
-                    const float u_f = ((pc[0] * p.fx) / pc[2] + p.cx) + 0.5f;
-                    const float v_f = ((pc[1] * p.fy) / pc[2] + p.cy) + 0.5f;
-                    if (u_f >= 0.0001f && u_f < p.safe_w && v_f >= 0.0001f && v_f < p.safe_h) {
-                        const int pix = (int)v_f * p.W + (int)u_f;
-                        const float dd = depth[pix];
-                        if (dd > 0.0f) {
-                            const float sdf = (dd - pc[2]) * p.mult[pix];
-                            if (sdf > -p.trunc) {
-                                const float sv = sdf * p.trunc_inv;
-                                const float tn = (sv < 1.0f) ? sv : 1.0f;
-                                const float w = wt[z];
-                                const float w1 = w + 1.0f;
-                                ts[z] = (ts[z] * w + tn) / w1;
-                                if (color) {
-                                    const uint8_t* c = color + (int64_t)pix * 3;
-                                    cr[z] = (cr[z] * w + (float)c[0]) / w1;
-                                    cg[z] = (cg[z] * w + (float)c[1]) / w1;
-                                    cb[z] = (cb[z] * w + (float)c[2]) / w1;
-                                }
-                                wt[z] = w1;
-                                ++upd;
-                            }
-                        }
-                    }
-                }
+            for (int k = 0; k < z0; ++k) {  // wave-uniform: advance to this half's first voxel
                 pc[0] += es0;
                 pc[1] += es1;
                 pc[2] += es2;
             }
+            // phase A: projections of the BZ voxels
+            int pixv[BZ];
+            float pcz[BZ];
+#pragma unroll
+            for (int k = 0; k < BZ; ++k) {
+                const float u_f = ((pc[0] * p.fx) / pc[2] + p.cx) + 0.5f;
+                const float v_f = ((pc[1] * p.fy) / pc[2] + p.cy) + 0.5f;
+                const bool ok = (pc[2] > 0.0f) && u_f >= 0.0001f && u_f < p.safe_w && v_f >= 0.0001f &&
+                                v_f < p.safe_h;
+                pixv[k] = ok ? ((int)v_f * p.W + (int)u_f) : -1;
+                pcz[k] = pc[2];
+                pc[0] += es0;
+                pc[1] += es1;
+                pc[2] += es2;
+            }
+            // phase B: all gathers issued before any use
+            float2 dmv[BZ];
+            uint32_t cv[BZ];
+#pragma unroll
+            for (int k = 0; k < BZ; ++k) {
+                const int q = pixv[k] < 0 ? 0 : pixv[k];
+                dmv[k] = dm[q];
+                cv[k] = use_color ? rgba[q] : 0u;
+            }
+            // phase C: updates
+#pragma unroll
+            for (int k = 0; k < BZ; ++k) {
+                if (pixv[k] >= 0 && dmv[k].x > 0.0f) {
+                    const float sdf = (dmv[k].x - pcz[k]) * dmv[k].y;
+                    if (sdf > -p.trunc) {
+                        const float sv = sdf * p.trunc_inv;
+                        const float tn = (sv < 1.0f) ? sv : 1.0f;
+                        const float w = wt[k];
+                        const float w1 = w + 1.0f;
+                        ts[k] = (ts[k] * w + tn) / w1;  // exact IEEE division: tsdf is bit-exact
+                        if (use_color) {
+                            // colour running mean: one hardware reciprocal (1 ulp) for the three channels —
+                            // within the 1e-4 colour contract; Open3D keeps colour in float64 anyway
+                            const float rw = __builtin_amdgcn_rcpf(w1);
+                            cr[k] = (cr[k] * w + (float)(cv[k] & 0xFFu)) * rw;
+                            cg[k] = (cg[k] * w + (float)((cv[k] >> 8) & 0xFFu)) * rw;
+                            cb[k] = (cb[k] * w + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                        }
+                        wt[k] = w1;
+                        ++upd;
+                    }
+                }
+            }
         }
 #pragma unroll
-        for (int z = 0; z < UNIT_RES; ++z) {
-            const int vi = z * 256 + tid;
-            base[vi] = ts[z];
-            base[UNIT_VOX + vi] = wt[z];
-            base[2 * UNIT_VOX + vi] = cr[z];
-            base[3 * UNIT_VOX + vi] = cg[z];
-            base[4 * UNIT_VOX + vi] = cb[z];
+        for (int k = 0; k < BZ; ++k) {
+            const int vi = (z0 + k) * 256 + col;
+            base[vi] = ts[k];
+            base[UNIT_VOX + vi] = wt[k];
+            base[2 * UNIT_VOX + vi] = cr[k];
+            base[3 * UNIT_VOX + vi] = cg[k];
+            base[4 * UNIT_VOX + vi] = cb[k];
         }
     }
     upd = wave_sum(upd);
-    __shared__ unsigned long long red[4];
     if (lane_id() == 0) red[tid >> 6] = upd;
     __syncthreads();
     if (tid == 0) {
-        const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+        unsigned long long tot = 0;
+        for (int w = 0; w < BLANES / 64; ++w) tot += red[w];
         if (tot) atomicAdd(&d.stats[S_UPDATES], tot);
         if (pairs) atomicAdd(&d.stats[S_UNIT_INTEGRATIONS], pairs);
     }
@@ -597,13 +680,16 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     if (st != OT_OK) return st;
     const int64_t npx = (int64_t)in.width * in.height;
     if (vol->bdepth_cap < npx * n) {
-        if (vol->bdepth) {
+        if (vol->bdm) {
             OT_HIP_TRY(hipStreamSynchronize(stream));
-            OT_HIP_TRY(hipFree(vol->bdepth));
-            vol->bdepth = nullptr;
+            OT_HIP_TRY(hipFree(vol->bdm));
+            OT_HIP_TRY(hipFree(vol->brgba));
+            vol->bdm = nullptr;
+            vol->brgba = nullptr;
         }
-        const int64_t cap = npx * std::max(n, vol->batch_max);
-        OT_HIP_TRY(hipMalloc(&vol->bdepth, sizeof(float) * cap));
+        const int64_t cap = npx * std::max(n, std::min(vol->batch_max, MAX_BATCH));
+        OT_HIP_TRY(hipMalloc(&vol->bdm, sizeof(float2) * cap));
+        OT_HIP_TRY(hipMalloc(&vol->brgba, sizeof(uint32_t) * cap));
         vol->bdepth_cap = cap;
     }
     // per-frame parameters: pinned host staging (double-buffered, event-guarded) -> device
@@ -616,8 +702,10 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         const PendingFrame& f = frames[k];
         BatchFrame& b = host[k];
         b.depth16 = f.depth;
-        b.depthf = f.depth ? vol->bdepth + npx * k : f.depthf;
+        b.depthf = f.depth ? nullptr : f.depthf;
         b.color = (vol->color_type == OT_COLOR_RGB8) ? f.color : nullptr;
+        b.dm = vol->bdm + npx * k;
+        b.rgba = vol->brgba + npx * k;
         double pose[16];
         inverse4(f.extrinsic, pose);
         for (int i = 0; i < 12; ++i) b.pose[i] = pose[i];
@@ -634,8 +722,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     if (!vol->hb_event[hb]) OT_HIP_TRY(hipEventCreateWithFlags(&vol->hb_event[hb], hipEventDisableTiming));
     OT_HIP_TRY(hipEventRecord(vol->hb_event[hb], stream));
     OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, sizeof(int), stream));
-    hipLaunchKernelGGL(k_batch_depth, dim3((unsigned)((npx / 8 + 255) / 256 + 1), n), dim3(256), 0, stream,
-                       (const BatchFrame*)vol->bframes, npx);
+    hipLaunchKernelGGL(k_batch_prep, dim3((unsigned)((npx + 255) / 256), n), dim3(256), 0, stream,
+                       (const BatchFrame*)vol->bframes, (const float*)vol->mult, npx);
     BatchTouchParams tp;
     tp.W = in.width;
     tp.stride = vol->stride;
@@ -648,8 +736,9 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.trunc = vol->sdf_trunc;
     tp.unit_len = vol->unit_length;
     tp.slot_cap = (int)vol->hash_cap;
-    hipLaunchKernelGGL(k_batch_touch, dim3((unsigned)((tp.ws * tp.hs + 255) / 256), n), dim3(256), 0, stream,
-                       (const BatchFrame*)vol->bframes, tp, vol->dev);
+    const unsigned tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
+    hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
+                       (const BatchFrame*)vol->bframes, tp, vol->dev, n);
     const int grid = (int)std::min<int64_t>(vol->max_units, 2048);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
@@ -657,7 +746,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         OT_HIP_TRY(hipEventCreate(&e1));
         OT_HIP_TRY(hipEventRecord(e0, stream));
     }
-    hipLaunchKernelGGL(k_batch_integrate, dim3(grid), dim3(256), 0, stream, (const BatchFrame*)vol->bframes, ip0,
+    hipLaunchKernelGGL(k_batch_integrate, dim3(grid), dim3(BLANES), 0, stream, (const BatchFrame*)vol->bframes, ip0,
                        vol->dev);
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
@@ -810,7 +899,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     ot_tsdf_set_profiling(v, 0);
     void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, v->mult,
                     v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, d.fmask, d.bslots,
-                    v->bframes, v->bdepth};
+                    v->bframes, v->bdm, v->brgba};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (v->hbframes) (void)hipHostFree(v->hbframes);
