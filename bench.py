@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
     ap.add_argument("--cpu-frames", type=int, default=64, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--calib", action="store_true", help="after timing, run export_units once (PMC calibration)")
     return ap.parse_args()
 
 
@@ -145,9 +146,15 @@ def main():
         traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_integrate", "kernel_ms_avg": round(kernel_ms_avg, 5), "launches_per_step": klaunch.value,
+                "kernel": "k_integrate" if args.batch == 1 else "k_batch_integrate", "kernel_ms_avg": round(kernel_ms_avg, 5), "launches_per_step": klaunch.value,
                 "algorithmic_bytes_per_launch": round(per_launch_bytes),
                 "voxel_updates_per_frame": round(upd.value / args.frames)}
+
+    if args.calib:  # a kernel with a known read byte count and the integrate kernel's pool access pattern
+        nu = n_units.value
+        bufs = [torch.empty((nu, 4096, k), dtype=torch.float32, device="cuda") for k in (1, 1, 3)]
+        L.call("ot_tsdf_export_units", vol, None, *[C.c_void_p(b.data_ptr()) for b in bufs], stream)
+        torch.cuda.synchronize()
 
     cpu = None
     if rank == 0 and args.cpu_frames > 0:
