@@ -390,20 +390,27 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
     }
 }
 
-// 512 lanes per unit: lane = (half h, column x, y); half h owns z in [8h, 8h + 8).  The camera-space voxel
-// position still advances by exactly z sequential additions of Es.col(2) from the column origin, as in
-// Open3D, so both halves reproduce the single-lane z walk bit for bit.
-constexpr int BZ = 8;
-constexpr int BLANES = UNIT_VOX / BZ;  // 512
+// 4096/BZ lanes per unit: lane = (z-group h, column x, y); group h owns z in [BZ*h, BZ*h + BZ).  The camera-space
+// voxel position still advances by exactly z sequential additions of Es.col(2) from the column origin, as in
+// Open3D, so every group reproduces the single-lane z walk bit for bit.
+#ifndef OT_BZ
+#define OT_BZ 4
+#endif
+constexpr int BZ = OT_BZ;              // voxels per lane along z
+constexpr int BLANES = UNIT_VOX / BZ;  // lanes per unit (1024 at BZ = 4)
+constexpr int BCOLS = 256;             // (x, y) columns per unit
 
-__global__ __launch_bounds__(BLANES) void k_batch_integrate(const BatchFrame* __restrict__ frames, IntegrateParams p,
+#ifndef OT_MINB
+#define OT_MINB 2
+#endif
+__global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integrate(const BatchFrame* __restrict__ frames, IntegrateParams p,
                                                             TsdfDev d) {
     __shared__ int s_id;
     __shared__ unsigned long long s_mask;
     __shared__ unsigned long long red[BLANES / 64];
     const int n = d.counters[C_BATCH_PAIRS];
     const int tid = threadIdx.x;
-    const int col = tid & 255, half = tid >> 8;
+    const int col = tid & (BCOLS - 1), half = tid / BCOLS;
     const int x = col >> 4, y = col & 15, z0 = half * BZ;
     unsigned long long upd = 0, pairs = 0;
     for (int t = blockIdx.x; t < n; t += gridDim.x) {
@@ -445,7 +452,11 @@ __global__ __launch_bounds__(BLANES) void k_batch_integrate(const BatchFrame* __
 #pragma unroll
         for (int k = 0; k < BZ; ++k) {
             const int vi = (z0 + k) * 256 + col;
+#ifdef OT_ABL_NOSTATE  // timing-only ablation build: no voxel-state traffic (results are wrong)
+            if (true) {
+#else
             if (fresh) {
+#endif
                 ts[k] = wt[k] = cr[k] = cg[k] = cb[k] = 0.0f;
             } else {
                 ts[k] = base[vi];
@@ -502,8 +513,13 @@ __global__ __launch_bounds__(BLANES) void k_batch_integrate(const BatchFrame* __
 #pragma unroll
             for (int k = 0; k < BZ; ++k) {
                 const int q = pixv[k] < 0 ? 0 : pixv[k];
+#ifdef OT_ABL_NOGATHER  // timing-only ablation build: no frame gathers (results are wrong)
+                dmv[k] = make_float2(pcz[k] + 0.01f * (float)(q & 7), 1.0f);
+                cv[k] = (unsigned)q;
+#else
                 dmv[k] = dm[q];
                 cv[k] = use_color ? rgba[q] : 0u;
+#endif
             }
             // phase C: updates
 #pragma unroll
@@ -515,8 +531,16 @@ __global__ __launch_bounds__(BLANES) void k_batch_integrate(const BatchFrame* __
                         const float tn = (sv < 1.0f) ? sv : 1.0f;
                         const float w = wt[k];
                         const float w1 = w + 1.0f;
+#ifdef OT_ABL_FASTDIV  // timing-only: tsdf division via reciprocal (not bit-exact)
+                        ts[k] = (ts[k] * w + tn) * __builtin_amdgcn_rcpf(w1);
+#else
                         ts[k] = (ts[k] * w + tn) / w1;  // exact IEEE division: tsdf is bit-exact
+#endif
+#ifdef OT_ABL_NOCOLOR
+                        if (false) {
+#else
                         if (use_color) {
+#endif
                             // colour running mean: one hardware reciprocal (1 ulp) for the three channels —
                             // within the 1e-4 colour contract; Open3D keeps colour in float64 anyway
                             const float rw = __builtin_amdgcn_rcpf(w1);
@@ -530,6 +554,11 @@ __global__ __launch_bounds__(BLANES) void k_batch_integrate(const BatchFrame* __
                 }
             }
         }
+#ifdef OT_ABL_NOSTATE  // keep every result live without storing it (guide §5.4 rule 17)
+#pragma unroll
+        for (int k = 0; k < BZ; ++k) asm volatile("" ::"v"(ts[k]), "v"(wt[k]), "v"(cr[k]), "v"(cg[k]), "v"(cb[k]));
+        continue;
+#endif
 #pragma unroll
         for (int k = 0; k < BZ; ++k) {
             const int vi = (z0 + k) * 256 + col;
