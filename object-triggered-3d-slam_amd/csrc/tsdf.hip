@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
 // voxel position still advances by exactly z sequential additions of Es.col(2) from the column origin, as in
 // Open3D, so every group reproduces the single-lane z walk bit for bit.
 #ifndef OT_BZ
-#define OT_BZ 4
+#define OT_BZ 8
 #endif
 constexpr int BZ = OT_BZ;              // voxels per lane along z
 constexpr int BLANES = UNIT_VOX / BZ;  // lanes per unit (1024 at BZ = 4)

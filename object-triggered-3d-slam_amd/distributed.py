@@ -1,0 +1,124 @@
+"""Multi-GPU execution: independent object scans sharded over ranks, one RCCL all-gather for the hybrid-map merge.
+
+The reference reconstructs objects one after another in a Python loop (reconstruct_rgbd_filter.py:154-155) and
+later concatenates their clouds behind the occupancy-grid cloud (hybrid_map.py:62-96, :115).  Objects share no
+state, so here each rank (one process per GPU, torch.distributed over RCCL/xGMI) takes a CONTIGUOUS chunk of
+the sorted object list; concatenating the per-rank results in rank order therefore reproduces the reference's
+sorted-file order exactly.  The only collective is the final all-gather of the filtered clouds:
+  1. all_gather of per-rank point counts (int64[world])
+  2. all_gather_into_tensor of count-padded float64 [max_n, 3] buffers (float64 keeps the merge bit-exact;
+     <= 32 objects x 100k points x 24 B ~ 77 MB over xGMI, a few ms)
+then every rank trims the padding; rank 0 prepends the map cloud and writes the PLY.
+Works unchanged on gloo (CPU tensors) for the world-size-2 CPU tests.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+
+def shard(items, rank, world):
+    """Contiguous chunk `rank` of `items` (sorted order preserved across ranks)."""
+    n = len(items)
+    lo = (n * rank) // world
+    hi = (n * (rank + 1)) // world
+    return list(items[lo:hi])
+
+
+def all_gather_rows(local, group=None):
+    """Concatenate every rank's (n_r, k) tensor in rank order on every rank.  `local` lives on the backend's
+    device (HIP tensor for nccl/RCCL, CPU for gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    k = local.shape[1]
+    counts = torch.zeros(world, dtype=torch.int64, device=local.device)
+    mine = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    dist.all_gather_into_tensor(counts, mine, group=group)
+    counts_h = counts.cpu().tolist()
+    m = max(counts_h) if counts_h else 0
+    if m == 0:
+        return local.new_zeros((0, k))
+    pad = local.new_zeros((m, k))
+    pad[: local.shape[0]] = local
+    out = local.new_empty((world * m, k))
+    dist.all_gather_into_tensor(out, pad, group=group)
+    return torch.cat([out[r * m: r * m + c] for r, c in enumerate(counts_h)], dim=0)
+
+
+def merge_object_clouds(local_clouds, group=None):
+    """Rank-ordered concatenation of this rank's object clouds with everyone else's (points only: colours are
+    repainted uniformly by the hybrid map, hybrid_map.py:88)."""
+    import torch
+
+    dev = local_clouds[0].device if local_clouds else None
+    if dev is None:
+        import torch.distributed as dist
+
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else \
+            torch.device("cpu")
+    local = torch.cat(local_clouds, 0) if local_clouds else torch.zeros((0, 3), dtype=torch.float64, device=dev)
+    return all_gather_rows(local.to(torch.float64), group)
+
+
+def reconstruct_and_merge(cfg, yaml_file=None, pgm_file=None, save_path=None, objects=None, o3d=None):
+    """configs[3]/[4] driver: every rank reconstructs its shard of the objects on its own GPU (integrate ->
+    extract -> normals -> sample 100k -> Z mask, reconstruct_rgbd_filter.py:60-141), then the filtered clouds
+    are all-gathered; rank 0 builds and writes the hybrid map (map cloud first, then objects in sorted order).
+    Returns the merged point array on rank 0 (None elsewhere)."""
+    import importlib
+
+    import torch
+    import torch.distributed as dist
+
+    pkg = __package__
+    R = importlib.import_module(pkg + ".reconstruct")
+    o3d = o3d or importlib.import_module(pkg)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    labels = R.get_unique_object_names(cfg) if objects is None else sorted(objects)
+    mine = shard(labels, rank, world)
+    clouds = []
+    for label in mine:
+        pts = _reconstruct_points(R, cfg, label, o3d)
+        if pts is not None:
+            clouds.append(pts)
+    merged = merge_object_clouds(clouds)
+    if rank != 0:
+        return None
+    objs = o3d.geometry.PointCloud()
+    objs.points = merged
+    if len(objs.points):
+        objs.paint_uniform_color([1.0, 0.0, 0.0])
+    out = objs
+    if yaml_file and pgm_file:
+        hm = importlib.import_module(pkg + ".hybrid_map")
+        map_pcd = hm.create_map_cloud(yaml_file, pgm_file, o3d)
+        if map_pcd is not None:
+            out = map_pcd + objs if len(objs.points) else map_pcd
+    if save_path:
+        os.makedirs(os.path.dirname(os.path.abspath(save_path)), exist_ok=True)
+        o3d.io.write_point_cloud(save_path, out)
+    return np.asarray(out.points)
+
+
+def _reconstruct_points(R, cfg, label, o3d):
+    """In-memory variant of reconstruct_object(output="points") returning the filtered points as a device
+    tensor (no PLY round trip: the reference's float64 PLY write/read is lossless)."""
+    colors, depths, poses = R._frame_lists(cfg, label)
+    if not colors:
+        return None
+    intrinsic = R._intrinsic(o3d, cfg)
+    volume = R._new_volume(o3d, cfg)
+    for i in range(len(colors)):
+        try:
+            R._integrate_frame(o3d, cfg, volume, intrinsic, colors, depths, poses, i)
+        except Exception:
+            pass
+    mesh = volume.extract_triangle_mesh()
+    mesh.compute_vertex_normals()
+    if len(mesh.vertices) == 0:
+        return None
+    pcd = mesh.sample_points_uniformly(number_of_points=cfg.n_samples)
+    return pcd.filter_min_z(cfg.z_filter)._xyz.dev()
