@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=64, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--calib", action="store_true", help="after timing, run export_units once (PMC calibration)")
+    ap.add_argument("--filter-frames", type=int, default=64,
+                    help="configs[2] stream length (1280x720 unproject + 5 mm voxel + SOR); 0 = skip")
     return ap.parse_args()
 
 
@@ -159,6 +161,7 @@ def main():
     cpu = None
     if rank == 0 and args.cpu_frames > 0:
         cpu = cpu_baseline(depth, color, ext, intr_t, args)
+    filt = filter_stream(args, L, lib, synth, torch, rank) if (args.filter_frames > 0 and rank == 0) else None
 
     out = {"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
@@ -168,13 +171,83 @@ def main():
                       "frames_per_step": args.frames, "width": W, "height": H, "voxel_length": args.voxel,
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
-           "roofline": roofline, "cpu_baseline": cpu}
+           "roofline": roofline, "cpu_baseline": cpu, "filtered": filt}
     if rank == 0:
         print(json.dumps(out), flush=True)
     L.call("ot_tsdf_destroy", vol)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def filter_stream(args, L, lib, synth, torch, rank):
+    """configs[2]: 1280x720 RGB-D stream, per frame unproject (depth_trunc 5 m) -> voxel_down_sample(0.005) ->
+    remove_statistical_outlier(20, 2.0) -> gather kept points, all through the C ABI on device buffers.
+    16 distinct synthetic frames are cycled to the requested stream length.  Mpoints/s counts valid input
+    points per second; the CPU oracle runs the same chain on 2 frames for the baseline."""
+    intr_t = synth.REF_INTRINSICS_1280
+    W, H = intr_t[0], intr_t[1]
+    nuniq = 16
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=rank), n_frames=nuniq, intr=intr_t)
+    d16 = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
+    col = torch.from_numpy(color).cuda().contiguous()
+    npx = W * H
+    df = torch.empty((H, W), dtype=torch.float32, device="cuda")
+    xyz = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    rgb = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    vx = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    vc = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    idx = torch.empty((npx,), dtype=torch.int64, device="cuda")
+    out = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    intr = L.ot_intrinsics(W, H, *intr_t[2:])
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    exts = np.ascontiguousarray(ext)
+    P, K, Kk = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+    ptr = lambda t: C.c_void_p(t.data_ptr())
+
+    def frame(k):
+        f = k % nuniq
+        L.call("ot_depth_to_float", C.c_void_p(d16.data_ptr() + f * npx * 2), ptr(df), npx, 1000.0, 5.0, stream)
+        L.call("ot_unproject", ptr(df), C.c_void_p(col.data_ptr() + f * npx * 3), C.byref(intr),
+               exts[f].ctypes.data_as(C.c_void_p), 1, ptr(xyz), ptr(rgb), npx, C.byref(P), stream)
+        L.call("ot_voxel_down_sample", ptr(xyz), ptr(rgb), None, P.value, 0.005, ptr(vx), ptr(vc), None, None,
+               C.byref(K), stream)
+        L.call("ot_remove_statistical_outlier", ptr(vx), K.value, 20, 2.0, ptr(idx), None, C.byref(Kk), stream)
+        L.call("ot_gather_rows3", ptr(vx), ptr(idx), Kk.value, ptr(out), stream)
+        return P.value, K.value, Kk.value
+
+    for k in range(4):
+        frame(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pts = vox = kept = 0
+    for k in range(args.filter_frames):
+        p, v, kk = frame(k)
+        pts, vox, kept = pts + p, vox + v, kept + kk
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # CPU oracle on 2 frames of the same stream
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    t1 = time.perf_counter()
+    cpu_pts = 0
+    for f in range(2):
+        dff = O.depth_to_float(depth[f], 1000.0, 5.0)
+        x, c = O.unproject(dff, color[f], intr_t, ext[f])
+        v, vcc, _, _ = O.voxel_down_sample(x, c, 0.005)
+        O.remove_statistical_outlier(v, 20, 2.0)
+        cpu_pts += x.shape[0]
+    cdt = time.perf_counter() - t1
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return {"workload": "configs[2]: 1280x720 RGB-D stream, unproject + voxel_down_sample(0.005) + "
+                        "remove_statistical_outlier(20, 2.0) per frame",
+            "frames": args.filter_frames, "mpoints_per_s": round(pts / dt / 1e6, 2),
+            "frames_per_s": round(args.filter_frames / dt, 2), "ms_per_frame": round(dt * 1e3 / args.filter_frames, 3),
+            "points_per_frame": round(pts / args.filter_frames), "voxels_per_frame": round(vox / args.filter_frames),
+            "kept_per_frame": round(kept / args.filter_frames),
+            "cpu_baseline": {"mpoints_per_s": round(cpu_pts / cdt / 1e6, 3), "cores": cores, "kind": "port",
+                             "sample": "2 frames of the same stream, CPU oracle chain"}}
 
 
 def cpu_baseline(depth, color, ext, intr_t, args):
