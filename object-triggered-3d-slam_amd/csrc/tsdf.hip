@@ -247,23 +247,58 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
 // Per-pixel staging of a batch: (depth, multiplier) as float2 and the colour as one u32, so the integrate
 // kernel fetches a voxel's inputs with two aligned loads it can issue ahead of use.
 // depth: u16 path converted exactly as Image::ConvertDepthToFloatImage; float path copied.
+__device__ inline float prep_depth(const BatchFrame& fr, uint32_t raw16) {
+    float dv = (float)raw16;
+    dv = dv / fr.scale;
+    if ((double)dv >= fr.trunc) dv = 0.0f;
+    return dv;
+}
+
+// 4 pixels per lane: 8-B depth load, 12-B colour load (3 aligned dwords), 16-B multiplier load,
+// 2 x 16-B (depth, multiplier) stores and one 16-B colour store.
 __global__ __launch_bounds__(256) void k_batch_prep(const BatchFrame* __restrict__ frames, const float* __restrict__ mult,
                                                     int64_t npx) {
     const BatchFrame& fr = frames[blockIdx.y];
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= npx) return;
-    float dv;
-    if (fr.depth16) {
-        dv = (float)fr.depth16[i];
-        dv = dv / fr.scale;
-        if ((double)dv >= fr.trunc) dv = 0.0f;
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 >= npx) return;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(fr.depth16) & 7) == 0) &&
+                         ((reinterpret_cast<uintptr_t>(fr.depthf) & 15) == 0) &&
+                         ((reinterpret_cast<uintptr_t>(fr.color) & 3) == 0);
+    if (aligned && i0 + 4 <= npx && (npx & 3) == 0) {
+        float d[4];
+        if (fr.depth16) {
+            const uint2 raw = *reinterpret_cast<const uint2*>(fr.depth16 + i0);
+            d[0] = prep_depth(fr, raw.x & 0xFFFFu);
+            d[1] = prep_depth(fr, raw.x >> 16);
+            d[2] = prep_depth(fr, raw.y & 0xFFFFu);
+            d[3] = prep_depth(fr, raw.y >> 16);
+        } else {
+            const float4 v = *reinterpret_cast<const float4*>(fr.depthf + i0);
+            d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+        }
+        const float4 m = *reinterpret_cast<const float4*>(mult + i0);
+        float4* dm = reinterpret_cast<float4*>(fr.dm + i0);
+        dm[0] = make_float4(d[0], m.x, d[1], m.y);
+        dm[1] = make_float4(d[2], m.z, d[3], m.w);
+        if (fr.color) {
+            const uint32_t* c = reinterpret_cast<const uint32_t*>(fr.color + i0 * 3);  // 12 B, 4-B aligned
+            const uint32_t w0 = c[0], w1 = c[1], w2 = c[2];
+            // bytes: r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+            const uint32_t p0 = w0 & 0xFFFFFFu;
+            const uint32_t p1 = (w0 >> 24) | ((w1 & 0xFFFFu) << 8);
+            const uint32_t p2 = (w1 >> 16) | ((w2 & 0xFFu) << 16);
+            const uint32_t p3 = w2 >> 8;
+            *reinterpret_cast<uint4*>(fr.rgba + i0) = make_uint4(p0, p1, p2, p3);
+        }
     } else {
-        dv = fr.depthf[i];
-    }
-    fr.dm[i] = make_float2(dv, mult[i]);
-    if (fr.color) {
-        const uint8_t* c = fr.color + i * 3;
-        fr.rgba[i] = (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16);
+        for (int64_t i = i0; i < npx && i < i0 + 4; ++i) {
+            const float dv = fr.depth16 ? prep_depth(fr, fr.depth16[i]) : fr.depthf[i];
+            fr.dm[i] = make_float2(dv, mult[i]);
+            if (fr.color) {
+                const uint8_t* c = fr.color + i * 3;
+                fr.rgba[i] = (uint32_t)c[0] | ((uint32_t)c[1] << 8) | ((uint32_t)c[2] << 16);
+            }
+        }
     }
 }
 
@@ -522,6 +557,32 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
 #endif
             }
             // phase C: updates
+#ifdef OT_BRANCHLESS
+            // select-based update: every lane evaluates the arithmetic, results are kept only where
+            // Open3D's conditions hold (identical values; removes exec-mask branches)
+#pragma unroll
+            for (int k = 0; k < BZ; ++k) {
+                const float sdf = (dmv[k].x - pcz[k]) * dmv[k].y;
+                const bool doit = (pixv[k] >= 0) && (dmv[k].x > 0.0f) && (sdf > -p.trunc);
+                const float sv = sdf * p.trunc_inv;
+                const float tn = (sv < 1.0f) ? sv : 1.0f;
+                const float w = wt[k];
+                const float w1 = w + 1.0f;
+                const float tsn = (ts[k] * w + tn) / w1;
+                ts[k] = doit ? tsn : ts[k];
+                if (use_color) {
+                    const float rw = __builtin_amdgcn_rcpf(w1);
+                    const float nr = (cr[k] * w + (float)(cv[k] & 0xFFu)) * rw;
+                    const float ng = (cg[k] * w + (float)((cv[k] >> 8) & 0xFFu)) * rw;
+                    const float nb = (cb[k] * w + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                    cr[k] = doit ? nr : cr[k];
+                    cg[k] = doit ? ng : cg[k];
+                    cb[k] = doit ? nb : cb[k];
+                }
+                wt[k] = doit ? w1 : w;
+                upd += doit ? 1u : 0u;
+            }
+#else
 #pragma unroll
             for (int k = 0; k < BZ; ++k) {
                 if (pixv[k] >= 0 && dmv[k].x > 0.0f) {
@@ -553,6 +614,7 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
                     }
                 }
             }
+#endif
         }
 #ifdef OT_ABL_NOSTATE  // keep every result live without storing it (guide §5.4 rule 17)
 #pragma unroll
@@ -751,7 +813,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     if (!vol->hb_event[hb]) OT_HIP_TRY(hipEventCreateWithFlags(&vol->hb_event[hb], hipEventDisableTiming));
     OT_HIP_TRY(hipEventRecord(vol->hb_event[hb], stream));
     OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, sizeof(int), stream));
-    hipLaunchKernelGGL(k_batch_prep, dim3((unsigned)((npx + 255) / 256), n), dim3(256), 0, stream,
+    hipLaunchKernelGGL(k_batch_prep, dim3((unsigned)((npx / 4 + 255) / 256 + 1), n), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, (const float*)vol->mult, npx);
     BatchTouchParams tp;
     tp.W = in.width;
