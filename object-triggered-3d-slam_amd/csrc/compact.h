@@ -7,6 +7,8 @@
 // the row-major order Open3D produces for unprojection and the order numpy boolean masks keep.
 #pragma once
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace ot {
@@ -159,8 +161,13 @@ struct Bounds {
     int err;
 };
 
+// per-axis min / max of float64 [n][3] points, exact and order independent: each workgroup reduces its slice
+// through the wave shuffles and LDS into one partial record; a one-workgroup pass folds the partials.
+// (No same-address atomics: 1024 workgroups x 6 contended u64 atomics cost ~0.3 ms on MI355X.)
+constexpr int BOUNDS_BLOCKS = 512;
 namespace {
-__global__ __launch_bounds__(256) void k_bounds(const double* __restrict__ xyz, int64_t n, Bounds* b) {
+__global__ __launch_bounds__(256) void k_bounds_partial(const double* __restrict__ xyz, int64_t n,
+                                                        unsigned long long* __restrict__ part) {
     unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0, 0, 0};
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
 #pragma unroll
@@ -170,6 +177,7 @@ __global__ __launch_bounds__(256) void k_bounds(const double* __restrict__ xyz, 
             mx[a] = o > mx[a] ? o : mx[a];
         }
     }
+    __shared__ unsigned long long s[4][6];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
 #pragma unroll
@@ -180,14 +188,46 @@ __global__ __launch_bounds__(256) void k_bounds(const double* __restrict__ xyz, 
             mx[a] = t > mx[a] ? t : mx[a];
         }
     }
-    if (lane_id() == 0) {
-#pragma unroll
+    if (lane_id() == 0)
         for (int a = 0; a < 3; ++a) {
-            atomicMin(&b->mn[a], mn[a]);
-            atomicMax(&b->mx[a], mx[a]);
+            s[threadIdx.x >> 6][a] = mn[a];
+            s[threadIdx.x >> 6][3 + a] = mx[a];
         }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int q = threadIdx.x;
+        unsigned long long v = s[0][q];
+        for (int w = 1; w < 4; ++w) v = q < 3 ? (s[w][q] < v ? s[w][q] : v) : (s[w][q] > v ? s[w][q] : v);
+        part[blockIdx.x * 6 + q] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bounds_final(const unsigned long long* __restrict__ part, int nb, Bounds* b) {
+    __shared__ unsigned long long s[256][6];
+    unsigned long long v[6] = {~0ull, ~0ull, ~0ull, 0, 0, 0};
+    for (int i = threadIdx.x; i < nb; i += 256)
+        for (int q = 0; q < 6; ++q) {
+            const unsigned long long x = part[i * 6 + q];
+            v[q] = q < 3 ? (x < v[q] ? x : v[q]) : (x > v[q] ? x : v[q]);
+        }
+    for (int q = 0; q < 6; ++q) s[threadIdx.x][q] = v[q];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int q = threadIdx.x;
+        unsigned long long r = s[0][q];
+        for (int i = 1; i < 256; ++i) r = q < 3 ? (s[i][q] < r ? s[i][q] : r) : (s[i][q] > r ? s[i][q] : r);
+        if (q < 3) b->mn[q] = r;
+        else b->mx[q - 3] = r;
+        if (q == 0) b->err = 0;
     }
 }
 }  // namespace
+
+// Launch both passes; `part` needs BOUNDS_BLOCKS * 6 u64.
+inline void launch_bounds(const double* xyz, int64_t n, Bounds* b, unsigned long long* part, hipStream_t stream) {
+    const unsigned nb = (unsigned)std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), BOUNDS_BLOCKS);
+    hipLaunchKernelGGL(k_bounds_partial, dim3(nb), dim3(256), 0, stream, xyz, n, part);
+    hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, stream, (const unsigned long long*)part, (int)nb, b);
+}
 
 }  // namespace ot

@@ -106,12 +106,15 @@ __global__ __launch_bounds__(256) void k_ror(GridDev g, int64_t n, double r2, in
 }
 
 // ------------------------------------------------------------------------------------------------ SOR
-// Bubble-insert d into the ascending register list best[0..kk) (compile-time indices only => registers).
+// Register top-k list, RIGHT-aligned: best[KMAX-kk .. KMAX-1] hold the kk smallest squared distances in
+// ascending order and best[0 .. KMAX-kk-1] = -inf (never displaced).  best[KMAX-1] is therefore always the
+// current k-th distance at a compile-time index, so a candidate that cannot enter costs one compare.
 template <int KMAX>
-__device__ inline void topk_insert(double (&best)[KMAX], int kk, double d) {
+__device__ inline void topk_insert(double (&best)[KMAX], double d) {
+    if (!(d < best[KMAX - 1])) return;
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
-        if (i < kk && d < best[i]) {
+        if (d < best[i]) {
             const double t = best[i];
             best[i] = d;
             d = t;
@@ -124,7 +127,7 @@ __device__ inline void scan_cell(const GridDev& g, const double q[3], int x, int
                                  int kk, long long& have) {
     const int2 se = grid_find(g, x, y, z);
     for (int m = se.x; m < se.y; ++m) {
-        topk_insert<KMAX>(best, kk, d2_l2(q, g.sxyz + (int64_t)m * 3));
+        topk_insert<KMAX>(best, d2_l2(q, g.sxyz + (int64_t)m * 3));
         ++have;
     }
 }
@@ -138,11 +141,11 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
     const int cx = cell_coord(q[0], g.origin[0], g.h), cy = cell_coord(q[1], g.origin[1], g.h),
               cz = cell_coord(q[2], g.origin[2], g.h);
+    const int kk = (int)((int64_t)k < n ? k : n);
     double best[KMAX];
 #pragma unroll
-    for (int i = 0; i < KMAX; ++i) best[i] = INFINITY;
+    for (int i = 0; i < KMAX; ++i) best[i] = (i < KMAX - kk) ? -INFINITY : INFINITY;
     long long have = 0;
-    const int kk = (int)((int64_t)k < n ? k : n);
     bool done = false;
     for (int r = 0; r <= SOR_RMAX && !done; ++r) {
         // cells at Chebyshev distance exactly r
@@ -157,10 +160,7 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
                 }
             }
         if (have >= kk) {
-            double kth = 0.0;
-#pragma unroll
-            for (int i = 0; i < KMAX; ++i)
-                if (i == kk - 1) kth = best[i];
+            const double kth = best[KMAX - 1];
             // every point within distance (r - margin) * h of q lies in rings 0..r
             const double guard = (r > 0 ? (double)r - 0.01 : 0.0) * g.h;
             if (kth <= guard * guard || have >= n) done = true;
@@ -168,14 +168,14 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     }
     if (!done) {  // isolated point: exact scan of the whole cloud
 #pragma unroll
-        for (int i = 0; i < KMAX; ++i) best[i] = INFINITY;
-        for (int64_t m = 0; m < n; ++m) topk_insert<KMAX>(best, kk, d2_l2(q, g.sxyz + m * 3));
+        for (int i = 0; i < KMAX; ++i) best[i] = (i < KMAX - kk) ? -INFINITY : INFINITY;
+        for (int64_t m = 0; m < n; ++m) topk_insert<KMAX>(best, d2_l2(q, g.sxyz + m * 3));
     }
     double s = 0.0;
     int cnt = 0;
 #pragma unroll
     for (int i = 0; i < KMAX; ++i)
-        if (i < kk && best[i] < INFINITY) {
+        if (i >= KMAX - kk && best[i] < INFINITY) {
             s += sqrt(best[i]);
             ++cnt;
         }
@@ -324,15 +324,9 @@ using namespace ot;
 static ot_status bounds_host(const double* xyz, int64_t n, hipStream_t stream, double mn[3], double mx[3]) {
     Bounds* b = (Bounds*)scratch(sizeof(Bounds) + 64, 11);
     if (!b) return fail(OT_ERR_HIP, "scratch allocation failed");
-    Bounds init;
-    for (int a = 0; a < 3; ++a) {
-        init.mn[a] = ~0ull;
-        init.mx[a] = 0ull;
-    }
-    init.err = 0;
-    OT_HIP_TRY(hipMemcpyAsync(b, &init, sizeof(Bounds), hipMemcpyHostToDevice, stream));
-    const unsigned gb = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
-    hipLaunchKernelGGL(k_bounds, dim3(gb), dim3(256), 0, stream, xyz, n, b);
+    unsigned long long* part = (unsigned long long*)scratch(sizeof(unsigned long long) * BOUNDS_BLOCKS * 6, 19);
+    if (!part) return fail(OT_ERR_HIP, "scratch allocation failed");
+    launch_bounds(xyz, n, b, part, stream);
     OT_LAUNCH_CHECK();
     Bounds hb;
     OT_HIP_TRY(hipMemcpyAsync(&hb, b, sizeof(Bounds), hipMemcpyDeviceToHost, stream));

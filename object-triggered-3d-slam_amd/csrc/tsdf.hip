@@ -334,7 +334,10 @@ __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, i
 // every distinct unit of the tile does ONE global hash insert + ONE atomicOr of its merged mask.  A key that does
 // not fit the LDS table falls back to the direct global path.
 constexpr int TT = 16;          // tile edge in samples
-constexpr int TF = 8;           // frames per workgroup
+#ifndef OT_TF
+#define OT_TF 4
+#endif
+constexpr int TF = OT_TF;       // frames per workgroup
 constexpr int LTAB = 2048;      // LDS table entries (32 KiB)
 
 __device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* masks, unsigned long long key,

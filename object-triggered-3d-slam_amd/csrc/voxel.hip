@@ -107,15 +107,9 @@ extern "C" ot_status ot_voxel_down_sample(const double* xyz, const double* rgb, 
     unsigned* vin = (unsigned*)(kout + n);
     unsigned* vout = vin + n;
     int* heads = (int*)(vout + n);
-    Bounds init;
-    for (int a = 0; a < 3; ++a) {
-        init.mn[a] = ~0ull;
-        init.mx[a] = 0ull;
-    }
-    init.err = 0;
-    OT_HIP_TRY(hipMemcpyAsync(b, &init, sizeof(Bounds), hipMemcpyHostToDevice, stream));
-    const unsigned gb = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
-    hipLaunchKernelGGL(k_bounds, dim3(gb), dim3(256), 0, stream, xyz, n, b);
+    unsigned long long* part = (unsigned long long*)scratch(sizeof(unsigned long long) * BOUNDS_BLOCKS * 6, 18);
+    if (!part) return fail(OT_ERR_HIP, "scratch allocation failed");
+    launch_bounds(xyz, n, b, part, stream);
     hipLaunchKernelGGL(k_voxel_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, xyz, n, voxel_size, b,
                        kin, vin);
     OT_LAUNCH_CHECK();
