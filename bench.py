@@ -150,6 +150,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "k_integrate" if args.batch == 1 else "k_batch_integrate", "kernel_ms_avg": round(kernel_ms_avg, 5), "launches_per_step": klaunch.value,
                 "algorithmic_bytes_per_launch": round(per_launch_bytes),
+                "effective": args.batch != 1,  # voxel state reused on chip across a batch
                 "voxel_updates_per_frame": round(upd.value / args.frames)}
 
     if args.calib:  # a kernel with a known read byte count and the integrate kernel's pool access pattern
