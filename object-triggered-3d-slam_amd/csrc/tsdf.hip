@@ -235,6 +235,33 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Correctly rounded f32 division without the scale/fixup steps.  hipcc expands `n / d` (IEEE mode) into
+//   d' = div_scale(d), r0 = rcp(d'), n' = div_scale(n), e = fma(-d', r0, 1), r = fma(e, r0, r0),
+//   q1 = n' r, rem1 = fma(-d', q1, n'), q2 = fma(rem1, r, q1), rem2 = fma(-d', q2, n'),
+//   q3 = div_fmas(rem2, r, q2), q = div_fixup(q3, d, n).
+// V_DIV_SCALE_F32 leaves its operand unchanged (VCC = 0) unless d is denormal or > 2^126, |n| < 2^-103,
+// exp(n) - exp(d) >= 96, or n/d is denormal; div_fmas is then a plain FMA and div_fixup only rewrites
+// special values (0, inf, NaN).  Inside the guard band below none of those triggers fire, so the sequence
+// here is instruction-for-instruction the same arithmetic and returns the same bits; r (the refined
+// reciprocal) is computed once per divisor and shared by every quotient with that divisor.
+__device__ inline float recip_refined(float d) {
+    const float r0 = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, r0, 1.0f);
+    return __builtin_fmaf(e, r0, r0);
+}
+__device__ inline float div_with_recip(float n, float d, float r) {
+    const float q1 = n * r;
+    const float rem1 = __builtin_fmaf(-d, q1, n);
+    const float q2 = __builtin_fmaf(rem1, r, q1);
+    const float rem2 = __builtin_fmaf(-d, q2, n);
+    return __builtin_fmaf(rem2, r, q2);
+}
+__device__ inline bool div_guard_ok(float n, float d) {
+    const float an = fabsf(n);
+    return d >= 0x1p-40f && d <= 0x1p40f && (an == 0.0f || (an >= 0x1p-40f && an <= 0x1p40f));
+}
+
 // ============================================================================ batched (temporal blocking)
 // One launch per batch of F <= 64 frames:
 //   k_batch_prep      : per-pixel (depth, multiplier) float2 + packed colour for every frame (grid.y = frame)
@@ -449,7 +476,8 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
     const int n = d.counters[C_BATCH_PAIRS];
     const int tid = threadIdx.x;
     const int col = tid & (BCOLS - 1), half = tid / BCOLS;
-    const int x = col >> 4, y = col & 15, z0 = half * BZ;
+    const int x = col >> 4, y = col & 15;
+    const int z0 = __builtin_amdgcn_readfirstlane(half * BZ);  // wave-uniform (a wave never spans two halves)
     unsigned long long upd = 0, pairs = 0;
     for (int t = blockIdx.x; t < n; t += gridDim.x) {
         const int slot = d.bslots[t];
@@ -477,8 +505,10 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
             pairs += (unsigned long long)__popcll(mask);
         }
         __syncthreads();
-        const int ent = s_id;
-        const unsigned long long mask = s_mask;
+        const int ent = __builtin_amdgcn_readfirstlane(s_id);
+        const unsigned long long mask_l = s_mask;
+        const unsigned long long mask = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(mask_l >> 32)) << 32) |
+                                        (unsigned)__builtin_amdgcn_readfirstlane((int)(mask_l & 0xFFFFFFFFu));
         __syncthreads();  // s_id / s_mask are rewritten by the next iteration
         if (ent == -1) continue;
         const int id = ent & 0x7FFFFFFF;
@@ -530,13 +560,23 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
                 pc[1] += es1;
                 pc[2] += es2;
             }
-            // phase A: projections of the BZ voxels
+            // phase A: projections of the BZ voxels (u and v share pc.z's refined reciprocal)
             int pixv[BZ];
             float pcz[BZ];
 #pragma unroll
             for (int k = 0; k < BZ; ++k) {
-                const float u_f = ((pc[0] * p.fx) / pc[2] + p.cx) + 0.5f;
-                const float v_f = ((pc[1] * p.fy) / pc[2] + p.cy) + 0.5f;
+                const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
+                float qu, qv;
+                if (div_guard_ok(nu, pc[2]) && div_guard_ok(nv, pc[2])) {
+                    const float r = recip_refined(pc[2]);
+                    qu = div_with_recip(nu, pc[2], r);
+                    qv = div_with_recip(nv, pc[2], r);
+                } else {
+                    qu = nu / pc[2];
+                    qv = nv / pc[2];
+                }
+                const float u_f = (qu + p.cx) + 0.5f;
+                const float v_f = (qv + p.cy) + 0.5f;
                 const bool ok = (pc[2] > 0.0f) && u_f >= 0.0001f && u_f < p.safe_w && v_f >= 0.0001f &&
                                 v_f < p.safe_h;
                 pixv[k] = ok ? ((int)v_f * p.W + (int)u_f) : -1;
@@ -571,7 +611,8 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
                 const float tn = (sv < 1.0f) ? sv : 1.0f;
                 const float w = wt[k];
                 const float w1 = w + 1.0f;
-                const float tsn = (ts[k] * w + tn) / w1;
+                const float num = ts[k] * w + tn;
+                const float tsn = div_guard_ok(num, w1) ? div_with_recip(num, w1, recip_refined(w1)) : num / w1;
                 ts[k] = doit ? tsn : ts[k];
                 if (use_color) {
                     const float rw = __builtin_amdgcn_rcpf(w1);
@@ -598,7 +639,10 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
 #ifdef OT_ABL_FASTDIV  // timing-only: tsdf division via reciprocal (not bit-exact)
                         ts[k] = (ts[k] * w + tn) * __builtin_amdgcn_rcpf(w1);
 #else
-                        ts[k] = (ts[k] * w + tn) / w1;  // exact IEEE division: tsdf is bit-exact
+                        {
+                            const float num = ts[k] * w + tn;  // exact IEEE quotient (bit-exact tsdf)
+                            ts[k] = div_guard_ok(num, w1) ? div_with_recip(num, w1, recip_refined(w1)) : num / w1;
+                        }
 #endif
 #ifdef OT_ABL_NOCOLOR
                         if (false) {
