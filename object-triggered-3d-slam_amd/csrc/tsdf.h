@@ -29,6 +29,7 @@ constexpr int C_UNITS = 1;     // units allocated
 constexpr int C_OVERFLOW = 2;  // pool exhausted (units dropped)
 constexpr int C_HASHERR = 3;   // hash full or key out of range
 constexpr int C_BATCH_PAIRS = 4;  // (frame, unit) pairs in the current batch
+constexpr int C_BATCH_NEXT = 5;   // work-queue head of k_batch_integrate
 constexpr int N_COUNTERS = 8;
 
 // stats[] slots (u64)

@@ -41,8 +41,17 @@ struct IntegrateParams {
     float E[12];
     float es0, es1, es2;
     float vl, half, trunc, trunc_inv, safe_w, safe_h;
+    float proj_eps;  // certified fast projection: |u - rint(u)| > proj_eps decides floor and bounds exactly
     double unit_len;
 };
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+// Raw buffer resource over [base, base + bytes): gfx9 dword3 (0x00020000, 32-bit raw data); loads past the end
+// return 0 instead of faulting.
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
 
 __device__ inline int hash_insert(const TsdfDev& d, unsigned long long key) {
     unsigned slot = (unsigned)mix64(key) & (unsigned)d.hash_mask;
@@ -257,6 +266,9 @@ __device__ inline float div_with_recip(float n, float d, float r) {
     const float rem2 = __builtin_fmaf(-d, q2, n);
     return __builtin_fmaf(rem2, r, q2);
 }
+#ifndef OT_DIV_MODE
+#define OT_DIV_MODE 0
+#endif
 __device__ inline bool div_guard_ok(float n, float d) {
     const float an = fabsf(n);
     return d >= 0x1p-40f && d <= 0x1p40f && (an == 0.0f || (an >= 0x1p-40f && an <= 0x1p40f));
@@ -477,11 +489,35 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
     const int tid = threadIdx.x;
     const int col = tid & (BCOLS - 1), half = tid / BCOLS;
     const int x = col >> 4, y = col & 15;
+#ifdef OT_NO_UNIFORM
+    const int z0 = half * BZ;
+#else
     const int z0 = __builtin_amdgcn_readfirstlane(half * BZ);  // wave-uniform (a wave never spans two halves)
-    unsigned long long upd = 0, pairs = 0;
+#endif
+    unsigned upd = 0;  // per lane: <= 8 voxels x 64 frames x units per lane, far below 2^32
+    unsigned long long pairs = 0;
+    const int npx = p.W * p.H;
+#ifndef OT_WORK_QUEUE
     for (int t = blockIdx.x; t < n; t += gridDim.x) {
         const int slot = d.bslots[t];
         if (tid == 0) {
+#else
+    // work queue: units carry 1..64 frames, so a static stride leaves the tail unbalanced.  Thread 0 claims the
+    // next unit one iteration ahead (the atomic's latency hides behind the current unit).
+    __shared__ int s_slot;
+    int claim = 0;
+    if (tid == 0) claim = atomicAdd(&d.counters[C_BATCH_NEXT], 1);
+    for (;;) {
+        int slot = -1;
+        if (tid == 0) {
+            const int t = claim;
+            if (t < n) claim = atomicAdd(&d.counters[C_BATCH_NEXT], 1);
+            slot = t < n ? d.bslots[t] : -1;
+            s_slot = slot;
+            if (slot < 0) s_id = -2;  // queue drained
+        }
+        if (tid == 0 && slot >= 0) {
+#endif
             const unsigned long long mask = d.fmask[slot];
             d.fmask[slot] = 0ull;  // ready for the next batch (this workgroup owns the slot)
             int id = d.hvals[slot];
@@ -505,11 +541,22 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
             pairs += (unsigned long long)__popcll(mask);
         }
         __syncthreads();
+#ifdef OT_NO_UNIFORM
+        const int ent = s_id;
+        const unsigned long long mask = s_mask;
+#else
         const int ent = __builtin_amdgcn_readfirstlane(s_id);
         const unsigned long long mask_l = s_mask;
         const unsigned long long mask = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(mask_l >> 32)) << 32) |
                                         (unsigned)__builtin_amdgcn_readfirstlane((int)(mask_l & 0xFFFFFFFFu));
-        __syncthreads();  // s_id / s_mask are rewritten by the next iteration
+#endif
+#ifdef OT_WORK_QUEUE
+        slot = __builtin_amdgcn_readfirstlane(s_slot);
+#endif
+        __syncthreads();  // s_id / s_mask / s_slot are rewritten by the next iteration
+#ifdef OT_WORK_QUEUE
+        if (ent == -2) break;  // uniform
+#endif
         if (ent == -1) continue;
         const int id = ent & 0x7FFFFFFF;
         const bool fresh = ent < 0;
@@ -540,11 +587,114 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
         const float px = (p.half + p.vl * (float)x) + ox;
         const float py = (p.half + p.vl * (float)y) + oy;
         const float pz = p.half + oz;
+#ifdef OT_PIPELINE
+        // Software-pipelined frame loop: the projections and gathers of the NEXT frame are issued before the
+        // updates of the current one, so each frame's gather latency hides behind a frame of arithmetic.
+        // The voxel state is still updated strictly in frame order.
+        unsigned ok_c = 0u, ok_n = 0u;  // bit k: voxel k projects inside the image
+        float pcz_c[BZ], pcz_n[BZ];
+        float2 dm_c[BZ], dm_n[BZ];
+        uint32_t cv_c[BZ], cv_n[BZ];
+        bool col_c = false, col_n = false;
+        unsigned long long m = mask;
+        auto stage = [&](int f, unsigned& okm, float (&pczv)[BZ], float2 (&dmv)[BZ], uint32_t (&cvv)[BZ],
+                         bool& use_color) {
+            const BatchFrame& fr = frames[f];
+            use_color = fr.color != nullptr;
+            float pc[3];
+            int pixv[BZ];
+            okm = 0u;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const float a = fr.E[r * 4 + 0] * px;
+                const float b = fr.E[r * 4 + 1] * py;
+                const float c = fr.E[r * 4 + 2] * pz;
+                pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
+            }
+            const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
+            for (int k = 0; k < z0; ++k) {
+                pc[0] += es0;
+                pc[1] += es1;
+                pc[2] += es2;
+            }
+#pragma unroll
+            for (int k = 0; k < BZ; ++k) {
+                const float u_f = ((pc[0] * p.fx) / pc[2] + p.cx) + 0.5f;
+                const float v_f = ((pc[1] * p.fy) / pc[2] + p.cy) + 0.5f;
+                const bool ok = (pc[2] > 0.0f) && u_f >= 0.0001f && u_f < p.safe_w && v_f >= 0.0001f &&
+                                v_f < p.safe_h;
+                pixv[k] = ok ? ((int)v_f * p.W + (int)u_f) : 0;
+                okm |= ok ? (1u << k) : 0u;
+                pczv[k] = pc[2];
+                pc[0] += es0;
+                pc[1] += es1;
+                pc[2] += es2;
+            }
+            const float2* dmp = fr.dm;
+            const uint32_t* rgba = fr.rgba;
+#pragma unroll
+            for (int k = 0; k < BZ; ++k) {
+                dmv[k] = dmp[pixv[k]];
+                cvv[k] = use_color ? rgba[pixv[k]] : 0u;
+            }
+        };
+        auto consume = [&](unsigned okm, const float (&pczv)[BZ], const float2 (&dmv)[BZ],
+                           const uint32_t (&cvv)[BZ], bool use_color) {
+#pragma unroll
+            for (int k = 0; k < BZ; ++k) {
+                if (((okm >> k) & 1u) && dmv[k].x > 0.0f) {
+                    const float sdf = (dmv[k].x - pczv[k]) * dmv[k].y;
+                    if (sdf > -p.trunc) {
+                        const float sv = sdf * p.trunc_inv;
+                        const float tn = (sv < 1.0f) ? sv : 1.0f;
+                        const float w = wt[k];
+                        const float w1 = w + 1.0f;
+                        ts[k] = (ts[k] * w + tn) / w1;  // exact IEEE division: tsdf is bit-exact
+                        if (use_color) {
+                            const float rw = __builtin_amdgcn_rcpf(w1);
+                            cr[k] = (cr[k] * w + (float)(cvv[k] & 0xFFu)) * rw;
+                            cg[k] = (cg[k] * w + (float)((cvv[k] >> 8) & 0xFFu)) * rw;
+                            cb[k] = (cb[k] * w + (float)((cvv[k] >> 16) & 0xFFu)) * rw;
+                        }
+                        wt[k] = w1;
+                        ++upd;
+                    }
+                }
+            }
+        };
+        if (m) {
+            stage(__ffsll((long long)m) - 1, ok_c, pcz_c, dm_c, cv_c, col_c);
+            m &= m - 1;
+        }
+        for (bool more = mask != 0; more;) {
+            const bool has_next = m != 0;
+            if (has_next) {
+                stage(__ffsll((long long)m) - 1, ok_n, pcz_n, dm_n, cv_n, col_n);
+                m &= m - 1;
+            }
+            consume(ok_c, pcz_c, dm_c, cv_c, col_c);
+            more = has_next;
+            if (has_next) {
+#pragma unroll
+                for (int k = 0; k < BZ; ++k) {
+                    pcz_c[k] = pcz_n[k];
+                    dm_c[k] = dm_n[k];
+                    cv_c[k] = cv_n[k];
+                }
+                col_c = col_n;
+                ok_c = ok_n;
+            }
+        }
+#else
         for (unsigned long long m = mask; m; m &= m - 1) {
             const int f = __ffsll((long long)m) - 1;
             const BatchFrame& fr = frames[f];
             const float2* dm = fr.dm;
             const uint32_t* rgba = fr.rgba;
+#ifndef OT_GLOBAL_GATHER
+            const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(dm, npx * 8);
+            const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(rgba, npx * 4);
+#endif
             const bool use_color = fr.color != nullptr;
             float pc[3];
 #pragma unroll
@@ -566,20 +716,53 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
 #pragma unroll
             for (int k = 0; k < BZ; ++k) {
                 const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
+#ifndef OT_EXACTPROJ
+                // Certified fast projection.  Only floor(u), floor(v) and the bound tests are used, so u = nu * rcp(z)
+                // decides them exactly unless u lies within proj_eps of an integer (the bound tests 0.0001 and
+                // W - 0.0001 sit 1e-4 from integers); those rare waves redo the IEEE quotients below.
+                const float rz = __builtin_amdgcn_rcpf(pc[2]);
+                float u_f = (nu * rz + p.cx) + 0.5f;
+                float v_f = (nv * rz + p.cy) + 0.5f;
+                const bool sure = !(pc[2] > 0.0f) ||
+                                  ((fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
+                                   (fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
+                if (!sure) {
+                    u_f = ((nu / pc[2]) + p.cx) + 0.5f;
+                    v_f = ((nv / pc[2]) + p.cy) + 0.5f;
+                }
+#else
                 float qu, qv;
-                if (div_guard_ok(nu, pc[2]) && div_guard_ok(nv, pc[2])) {
+#if OT_DIV_MODE == 0
+                qu = nu / pc[2];
+                qv = nv / pc[2];
+#elif OT_DIV_MODE == 2  // timing-only: shared reciprocal without the guard
+                {
                     const float r = recip_refined(pc[2]);
                     qu = div_with_recip(nu, pc[2], r);
                     qv = div_with_recip(nv, pc[2], r);
-                } else {
-                    qu = nu / pc[2];
-                    qv = nv / pc[2];
                 }
+#else
+                {
+                    // guard folded into a select: both quotients are always computed the fast way and the
+                    // (rare) out-of-band lanes redo them with the full IEEE expansion
+                    const float r = recip_refined(pc[2]);
+                    qu = div_with_recip(nu, pc[2], r);
+                    qv = div_with_recip(nv, pc[2], r);
+                    if (!(div_guard_ok(nu, pc[2]) && div_guard_ok(nv, pc[2]))) {
+                        qu = nu / pc[2];
+                        qv = nv / pc[2];
+                    }
+                }
+#endif
                 const float u_f = (qu + p.cx) + 0.5f;
                 const float v_f = (qv + p.cy) + 0.5f;
-                const bool ok = (pc[2] > 0.0f) && u_f >= 0.0001f && u_f < p.safe_w && v_f >= 0.0001f &&
-                                v_f < p.safe_h;
-                pixv[k] = ok ? ((int)v_f * p.W + (int)u_f) : -1;
+#endif
+                // non-short-circuit test: both quotients of all BZ voxels stay in one basic block, so the
+                // scheduler interleaves their independent division chains (a && here sinks the v division
+                // behind a per-voxel exec-mask branch)
+                const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) &
+                                (v_f < p.safe_h);
+                pixv[k] = ok ? (int)__umul24((unsigned)(int)v_f, (unsigned)p.W) + (int)u_f : -1;
                 pcz[k] = pc[2];
                 pc[0] += es0;
                 pc[1] += es1;
@@ -595,8 +778,15 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
                 dmv[k] = make_float2(pcz[k] + 0.01f * (float)(q & 7), 1.0f);
                 cv[k] = (unsigned)q;
 #else
+#ifdef OT_GLOBAL_GATHER
                 dmv[k] = dm[q];
                 cv[k] = use_color ? rgba[q] : 0u;
+#else
+                // buffer loads: wave-uniform resource + 32-bit byte offset (no per-lane 64-bit address math)
+                const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, q * 8, 0, 0);
+                dmv[k] = make_float2(__uint_as_float(raw.x), __uint_as_float(raw.y));
+                cv[k] = use_color ? __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, q * 4, 0, 0) : 0u;
+#endif
 #endif
             }
             // phase C: updates
@@ -612,7 +802,11 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
                 const float w = wt[k];
                 const float w1 = w + 1.0f;
                 const float num = ts[k] * w + tn;
+#if OT_DIV_MODE == 0
+                const float tsn = num / w1;
+#else
                 const float tsn = div_guard_ok(num, w1) ? div_with_recip(num, w1, recip_refined(w1)) : num / w1;
+#endif
                 ts[k] = doit ? tsn : ts[k];
                 if (use_color) {
                     const float rw = __builtin_amdgcn_rcpf(w1);
@@ -641,7 +835,13 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
 #else
                         {
                             const float num = ts[k] * w + tn;  // exact IEEE quotient (bit-exact tsdf)
-                            ts[k] = div_guard_ok(num, w1) ? div_with_recip(num, w1, recip_refined(w1)) : num / w1;
+#if OT_DIV_MODE == 0
+                            ts[k] = num / w1;
+#else
+                            float q = div_with_recip(num, w1, recip_refined(w1));
+                            if (!div_guard_ok(num, w1)) q = num / w1;
+                            ts[k] = q;
+#endif
                         }
 #endif
 #ifdef OT_ABL_NOCOLOR
@@ -663,6 +863,7 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
             }
 #endif
         }
+#endif
 #ifdef OT_ABL_NOSTATE  // keep every result live without storing it (guide §5.4 rule 17)
 #pragma unroll
         for (int k = 0; k < BZ; ++k) asm volatile("" ::"v"(ts[k]), "v"(wt[k]), "v"(cr[k]), "v"(cg[k]), "v"(cb[k]));
@@ -678,8 +879,8 @@ __global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integr
             base[4 * UNIT_VOX + vi] = cb[k];
         }
     }
-    upd = wave_sum(upd);
-    if (lane_id() == 0) red[tid >> 6] = upd;
+    const unsigned long long upd64 = wave_sum((unsigned long long)upd);
+    if (lane_id() == 0) red[tid >> 6] = upd64;
     __syncthreads();
     if (tid == 0) {
         unsigned long long tot = 0;
@@ -743,6 +944,9 @@ static IntegrateParams make_integrate_params(const ot_tsdf* vol, const float* de
     p.trunc_inv = 1.0f / p.trunc;
     p.safe_w = (float)in->width - 0.0001f;
     p.safe_h = (float)in->height - 0.0001f;
+    // |fast u - IEEE u| <= 2^-21 (max(W, H) + 2) on [-1, W + 1] (rcp 1 ulp, four roundings); the bound tests sit
+    // 1e-4 from integers, so any margin above both keeps every decision identical (see k_batch_integrate)
+    p.proj_eps = (float)(std::ldexp((double)std::max(in->width, in->height) + 2.0, -21) + 1.2e-4);
     p.unit_len = vol->unit_length;
     return p;
 }
@@ -812,6 +1016,26 @@ static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t
     return OT_OK;
 }
 
+#ifndef OT_GRID_MULT
+#define OT_GRID_MULT 1
+#endif
+// Persistent work-queue grid of k_batch_integrate: the workgroups that are co-resident on the device (cached per
+// device; a benign race at worst computes the same value twice).
+static int integrate_grid() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 2048;
+    if (!cache[dev]) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_batch_integrate, BLANES, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 ||
+            cus <= 0)
+            return 2048;
+        cache[dev] = per_cu * cus * OT_GRID_MULT;
+    }
+    return cache[dev];
+}
+
 static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n, hipStream_t stream) {
     const ot_intrinsics& in = frames[0].intr;
     ot_status st = ensure_mult(vol, &in, stream);
@@ -859,7 +1083,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     OT_HIP_TRY(hipMemcpyAsync(vol->bframes, host, sizeof(BatchFrame) * n, hipMemcpyHostToDevice, stream));
     if (!vol->hb_event[hb]) OT_HIP_TRY(hipEventCreateWithFlags(&vol->hb_event[hb], hipEventDisableTiming));
     OT_HIP_TRY(hipEventRecord(vol->hb_event[hb], stream));
-    OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, sizeof(int), stream));
+    static_assert(C_BATCH_NEXT == C_BATCH_PAIRS + 1, "one memset clears both");
+    OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, 2 * sizeof(int), stream));
     hipLaunchKernelGGL(k_batch_prep, dim3((unsigned)((npx / 4 + 255) / 256 + 1), n), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, (const float*)vol->mult, npx);
     BatchTouchParams tp;
@@ -877,7 +1102,11 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     const unsigned tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
     hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, tp, vol->dev, n);
+#ifndef OT_WORK_QUEUE
     const int grid = (int)std::min<int64_t>(vol->max_units, 2048);
+#else
+    const int grid = integrate_grid();
+#endif
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
         OT_HIP_TRY(hipEventCreate(&e0));
