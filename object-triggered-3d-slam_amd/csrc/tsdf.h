@@ -29,8 +29,7 @@ constexpr int C_UNITS = 1;     // units allocated
 constexpr int C_OVERFLOW = 2;  // pool exhausted (units dropped)
 constexpr int C_HASHERR = 3;   // hash full or key out of range
 constexpr int C_BATCH_PAIRS = 4;  // (frame, unit) pairs in the current batch
-constexpr int C_BATCH_NEXT = 5;   // work-queue head of k_batch_integrate
-constexpr int N_COUNTERS = 8;
+constexpr int N_COUNTERS = 16;
 
 // stats[] slots (u64)
 constexpr int S_UPDATES = 0;
@@ -47,6 +46,7 @@ struct TsdfDev {
     float* vox;
     unsigned long long* fmask;  // per hash slot: frames of the current batch that touch the unit (bit f)
     int* bslots;                // hash slots touched by the current batch (first-touch order)
+    void* work;                 // per touched slot of the batch: unit header (UnitWork, 32 B) for the integrate
     int hash_mask;
     int max_units;
 };

@@ -244,45 +244,16 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
     }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// Correctly rounded f32 division without the scale/fixup steps.  hipcc expands `n / d` (IEEE mode) into
-//   d' = div_scale(d), r0 = rcp(d'), n' = div_scale(n), e = fma(-d', r0, 1), r = fma(e, r0, r0),
-//   q1 = n' r, rem1 = fma(-d', q1, n'), q2 = fma(rem1, r, q1), rem2 = fma(-d', q2, n'),
-//   q3 = div_fmas(rem2, r, q2), q = div_fixup(q3, d, n).
-// V_DIV_SCALE_F32 leaves its operand unchanged (VCC = 0) unless d is denormal or > 2^126, |n| < 2^-103,
-// exp(n) - exp(d) >= 96, or n/d is denormal; div_fmas is then a plain FMA and div_fixup only rewrites
-// special values (0, inf, NaN).  Inside the guard band below none of those triggers fire, so the sequence
-// here is instruction-for-instruction the same arithmetic and returns the same bits; r (the refined
-// reciprocal) is computed once per divisor and shared by every quotient with that divisor.
-__device__ inline float recip_refined(float d) {
-    const float r0 = __builtin_amdgcn_rcpf(d);
-    const float e = __builtin_fmaf(-d, r0, 1.0f);
-    return __builtin_fmaf(e, r0, r0);
-}
-__device__ inline float div_with_recip(float n, float d, float r) {
-    const float q1 = n * r;
-    const float rem1 = __builtin_fmaf(-d, q1, n);
-    const float q2 = __builtin_fmaf(rem1, r, q1);
-    const float rem2 = __builtin_fmaf(-d, q2, n);
-    return __builtin_fmaf(rem2, r, q2);
-}
-#ifndef OT_DIV_MODE
-#define OT_DIV_MODE 0
-#endif
-__device__ inline bool div_guard_ok(float n, float d) {
-    const float an = fabsf(n);
-    return d >= 0x1p-40f && d <= 0x1p40f && (an == 0.0f || (an >= 0x1p-40f && an <= 0x1p40f));
-}
-
 // ============================================================================ batched (temporal blocking)
 // One launch per batch of F <= 64 frames:
 //   k_batch_prep      : per-pixel (depth, multiplier) float2 + packed colour for every frame (grid.y = frame)
 //   k_batch_touch     : stride samples of every frame; a unit touched by frame f gets bit f in its slot's
 //                       fmask (64-bit atomicOr); the first bit set in a batch appends the slot to bslots
-//   k_batch_integrate : one 512-lane workgroup per touched slot: allocates the unit if new, loads its 16^3 voxel
-//                       state into registers (40 VGPRs/lane), applies the batch's frames in call order (ascending
-//                       bits of fmask), writes the state back once.  Per-voxel arithmetic is the per-frame
-//                       path's, so results are bit-identical to integrating frame by frame.
+//   k_batch_units     : per touched slot: allocate the unit if new, move its frame mask into a 32-B header
+//   k_batch_integrate : persistent independent waves over (unit, slice) items: a slice's 64 x BZ voxels are
+//                       loaded into registers (5 x BZ VGPRs/lane), the batch's frames are applied in call order
+//                       (ascending bits of the mask) and the state is written back once.  Per-voxel arithmetic is
+//                       the per-frame path's, so results are bit-identical to integrating frame by frame.
 // Per-pixel staging of a batch: (depth, multiplier) as float2 and the colour as one u32, so the integrate
 // kernel fetches a voxel's inputs with two aligned loads it can issue ahead of use.
 // depth: u16 path converted exactly as Image::ConvertDepthToFloatImage; float path copied.
@@ -467,427 +438,252 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
     }
 }
 
-// 4096/BZ lanes per unit: lane = (z-group h, column x, y); group h owns z in [BZ*h, BZ*h + BZ).  The camera-space
-// voxel position still advances by exactly z sequential additions of Es.col(2) from the column origin, as in
-// Open3D, so every group reproduces the single-lane z walk bit for bit.
+// ------------------------------------------------------------------------------------------------ integrate
+// Work item = (unit, slice): a slice is one wave of 64 (x, y) columns times BZ consecutive z, so a unit is
+// SLICES = 4 * (16 / BZ) independent waves.  Lane (x, y) of slice (g, h) owns z in [BZ*h, BZ*h + BZ); its
+// camera-space position still advances by exactly z sequential additions of Es.col(2) from the column origin,
+// as in Open3D, so every slice reproduces the single-lane z walk bit for bit.  Waves never synchronise: the
+// unit header (id, key, frame mask) is resolved once by k_batch_units and read with scalar loads.
 #ifndef OT_BZ
 #define OT_BZ 8
 #endif
-constexpr int BZ = OT_BZ;              // voxels per lane along z
-constexpr int BLANES = UNIT_VOX / BZ;  // lanes per unit (1024 at BZ = 4)
-constexpr int BCOLS = 256;             // (x, y) columns per unit
+constexpr int BZ = OT_BZ;                     // voxels per lane along z
+constexpr int SLICES = 4 * (UNIT_RES / BZ);   // waves per unit
 
-#ifndef OT_MINB
-#define OT_MINB 2
-#endif
-__global__ __launch_bounds__(BLANES, OT_MINB * BLANES / 256) void k_batch_integrate(const BatchFrame* __restrict__ frames, IntegrateParams p,
-                                                            TsdfDev d) {
-    __shared__ int s_id;
-    __shared__ unsigned long long s_mask;
-    __shared__ unsigned long long red[BLANES / 64];
+struct UnitWork {
+    int id;                   // pool id, | 0x80000000 when fresh (state starts at zero), -1 when dropped
+    int kx, ky, kz;           // unit key
+    unsigned long long mask;  // frames of the batch that touch the unit (bit f = frame f)
+    unsigned long long pad;
+};
+
+// Unit headers of the batch: allocate new units, move and clear the frame masks (ready for the next batch).
+__global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __restrict__ work) {
+    __shared__ unsigned long long red[4];
     const int n = d.counters[C_BATCH_PAIRS];
-    const int tid = threadIdx.x;
-    const int col = tid & (BCOLS - 1), half = tid / BCOLS;
-    const int x = col >> 4, y = col & 15;
-#ifdef OT_NO_UNIFORM
-    const int z0 = half * BZ;
-#else
-    const int z0 = __builtin_amdgcn_readfirstlane(half * BZ);  // wave-uniform (a wave never spans two halves)
-#endif
-    unsigned upd = 0;  // per lane: <= 8 voxels x 64 frames x units per lane, far below 2^32
     unsigned long long pairs = 0;
-    const int npx = p.W * p.H;
-#ifndef OT_WORK_QUEUE
-    for (int t = blockIdx.x; t < n; t += gridDim.x) {
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
         const int slot = d.bslots[t];
-        if (tid == 0) {
-#else
-    // work queue: units carry 1..64 frames, so a static stride leaves the tail unbalanced.  Thread 0 claims the
-    // next unit one iteration ahead (the atomic's latency hides behind the current unit).
-    __shared__ int s_slot;
-    int claim = 0;
-    if (tid == 0) claim = atomicAdd(&d.counters[C_BATCH_NEXT], 1);
-    for (;;) {
-        int slot = -1;
-        if (tid == 0) {
-            const int t = claim;
-            if (t < n) claim = atomicAdd(&d.counters[C_BATCH_NEXT], 1);
-            slot = t < n ? d.bslots[t] : -1;
-            s_slot = slot;
-            if (slot < 0) s_id = -2;  // queue drained
-        }
-        if (tid == 0 && slot >= 0) {
-#endif
-            const unsigned long long mask = d.fmask[slot];
-            d.fmask[slot] = 0ull;  // ready for the next batch (this workgroup owns the slot)
-            int id = d.hvals[slot];
-            if (id < 0) {
-                id = atomicAdd(&d.counters[C_UNITS], 1);
-                if (id >= d.max_units) {
-                    atomicOr(&d.counters[C_OVERFLOW], 1);
-                    id = -1;
-                } else {
-                    int kx, ky, kz;
-                    unpack_key(d.hkeys[slot], kx, ky, kz);
-                    d.hvals[slot] = id;
-                    d.unit_keys[id * 3 + 0] = kx;
-                    d.unit_keys[id * 3 + 1] = ky;
-                    d.unit_keys[id * 3 + 2] = kz;
-                    id |= (int)0x80000000u;  // fresh: state starts at zero
-                }
-            }
-            s_id = id;
-            s_mask = mask;
-            pairs += (unsigned long long)__popcll(mask);
-        }
-        __syncthreads();
-#ifdef OT_NO_UNIFORM
-        const int ent = s_id;
-        const unsigned long long mask = s_mask;
-#else
-        const int ent = __builtin_amdgcn_readfirstlane(s_id);
-        const unsigned long long mask_l = s_mask;
-        const unsigned long long mask = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(mask_l >> 32)) << 32) |
-                                        (unsigned)__builtin_amdgcn_readfirstlane((int)(mask_l & 0xFFFFFFFFu));
-#endif
-#ifdef OT_WORK_QUEUE
-        slot = __builtin_amdgcn_readfirstlane(s_slot);
-#endif
-        __syncthreads();  // s_id / s_mask / s_slot are rewritten by the next iteration
-#ifdef OT_WORK_QUEUE
-        if (ent == -2) break;  // uniform
-#endif
-        if (ent == -1) continue;
-        const int id = ent & 0x7FFFFFFF;
-        const bool fresh = ent < 0;
+        const unsigned long long mask = d.fmask[slot];
+        d.fmask[slot] = 0ull;
         int kx, ky, kz;
         unpack_key(d.hkeys[slot], kx, ky, kz);
-        float* base = d.vox + (size_t)id * UNIT_FLOATS;
-        float ts[BZ], wt[BZ], cr[BZ], cg[BZ], cb[BZ];
-#pragma unroll
-        for (int k = 0; k < BZ; ++k) {
-            const int vi = (z0 + k) * 256 + col;
-#ifdef OT_ABL_NOSTATE  // timing-only ablation build: no voxel-state traffic (results are wrong)
-            if (true) {
-#else
-            if (fresh) {
-#endif
-                ts[k] = wt[k] = cr[k] = cg[k] = cb[k] = 0.0f;
+        int id = d.hvals[slot];
+        if (id < 0) {
+            id = atomicAdd(&d.counters[C_UNITS], 1);
+            if (id >= d.max_units) {
+                atomicOr(&d.counters[C_OVERFLOW], 1);
+                id = -1;
             } else {
-                ts[k] = base[vi];
-                wt[k] = base[UNIT_VOX + vi];
-                cr[k] = base[2 * UNIT_VOX + vi];
-                cg[k] = base[3 * UNIT_VOX + vi];
-                cb[k] = base[4 * UNIT_VOX + vi];
+                d.hvals[slot] = id;
+                d.unit_keys[id * 3 + 0] = kx;
+                d.unit_keys[id * 3 + 1] = ky;
+                d.unit_keys[id * 3 + 2] = kz;
+                id |= (int)0x80000000u;
             }
         }
-        const float ox = (float)((double)kx * p.unit_len);
-        const float oy = (float)((double)ky * p.unit_len);
-        const float oz = (float)((double)kz * p.unit_len);
-        const float px = (p.half + p.vl * (float)x) + ox;
-        const float py = (p.half + p.vl * (float)y) + oy;
-        const float pz = p.half + oz;
-#ifdef OT_PIPELINE
-        // Software-pipelined frame loop: the projections and gathers of the NEXT frame are issued before the
-        // updates of the current one, so each frame's gather latency hides behind a frame of arithmetic.
-        // The voxel state is still updated strictly in frame order.
-        unsigned ok_c = 0u, ok_n = 0u;  // bit k: voxel k projects inside the image
-        float pcz_c[BZ], pcz_n[BZ];
-        float2 dm_c[BZ], dm_n[BZ];
-        uint32_t cv_c[BZ], cv_n[BZ];
-        bool col_c = false, col_n = false;
-        unsigned long long m = mask;
-        auto stage = [&](int f, unsigned& okm, float (&pczv)[BZ], float2 (&dmv)[BZ], uint32_t (&cvv)[BZ],
-                         bool& use_color) {
-            const BatchFrame& fr = frames[f];
-            use_color = fr.color != nullptr;
-            float pc[3];
-            int pixv[BZ];
-            okm = 0u;
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const float a = fr.E[r * 4 + 0] * px;
-                const float b = fr.E[r * 4 + 1] * py;
-                const float c = fr.E[r * 4 + 2] * pz;
-                pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
-            }
-            const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
-            for (int k = 0; k < z0; ++k) {
-                pc[0] += es0;
-                pc[1] += es1;
-                pc[2] += es2;
-            }
-#pragma unroll
-            for (int k = 0; k < BZ; ++k) {
-                const float u_f = ((pc[0] * p.fx) / pc[2] + p.cx) + 0.5f;
-                const float v_f = ((pc[1] * p.fy) / pc[2] + p.cy) + 0.5f;
-                const bool ok = (pc[2] > 0.0f) && u_f >= 0.0001f && u_f < p.safe_w && v_f >= 0.0001f &&
-                                v_f < p.safe_h;
-                pixv[k] = ok ? ((int)v_f * p.W + (int)u_f) : 0;
-                okm |= ok ? (1u << k) : 0u;
-                pczv[k] = pc[2];
-                pc[0] += es0;
-                pc[1] += es1;
-                pc[2] += es2;
-            }
-            const float2* dmp = fr.dm;
-            const uint32_t* rgba = fr.rgba;
-#pragma unroll
-            for (int k = 0; k < BZ; ++k) {
-                dmv[k] = dmp[pixv[k]];
-                cvv[k] = use_color ? rgba[pixv[k]] : 0u;
-            }
-        };
-        auto consume = [&](unsigned okm, const float (&pczv)[BZ], const float2 (&dmv)[BZ],
-                           const uint32_t (&cvv)[BZ], bool use_color) {
-#pragma unroll
-            for (int k = 0; k < BZ; ++k) {
-                if (((okm >> k) & 1u) && dmv[k].x > 0.0f) {
-                    const float sdf = (dmv[k].x - pczv[k]) * dmv[k].y;
-                    if (sdf > -p.trunc) {
-                        const float sv = sdf * p.trunc_inv;
-                        const float tn = (sv < 1.0f) ? sv : 1.0f;
-                        const float w = wt[k];
-                        const float w1 = w + 1.0f;
-                        ts[k] = (ts[k] * w + tn) / w1;  // exact IEEE division: tsdf is bit-exact
-                        if (use_color) {
-                            const float rw = __builtin_amdgcn_rcpf(w1);
-                            cr[k] = (cr[k] * w + (float)(cvv[k] & 0xFFu)) * rw;
-                            cg[k] = (cg[k] * w + (float)((cvv[k] >> 8) & 0xFFu)) * rw;
-                            cb[k] = (cb[k] * w + (float)((cvv[k] >> 16) & 0xFFu)) * rw;
-                        }
-                        wt[k] = w1;
-                        ++upd;
-                    }
-                }
-            }
-        };
-        if (m) {
-            stage(__ffsll((long long)m) - 1, ok_c, pcz_c, dm_c, cv_c, col_c);
-            m &= m - 1;
-        }
-        for (bool more = mask != 0; more;) {
-            const bool has_next = m != 0;
-            if (has_next) {
-                stage(__ffsll((long long)m) - 1, ok_n, pcz_n, dm_n, cv_n, col_n);
-                m &= m - 1;
-            }
-            consume(ok_c, pcz_c, dm_c, cv_c, col_c);
-            more = has_next;
-            if (has_next) {
+        UnitWork w;
+        w.id = id;
+        w.kx = kx;
+        w.ky = ky;
+        w.kz = kz;
+        w.mask = mask;
+        w.pad = 0ull;
+        work[t] = w;
+        pairs += (unsigned long long)__popcll(mask);
+    }
+    pairs = wave_sum(pairs);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = pairs;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+        if (tot) atomicAdd(&d.stats[S_UNIT_INTEGRATIONS], tot);
+    }
+}
+
+#ifndef OT_WAVES_PER_EU
+#define OT_WAVES_PER_EU 4
+#endif
+// One workgroup of SLICES waves per unit, so a unit's frame footprint is gathered through one CU's L1; units are
+// assigned by a static grid stride that every wave derives on its own: no barriers, no LDS, no atomics.
+__global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrate(
+    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work) {
+    const int lane = threadIdx.x & 63;
+    const int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // slice of this wave
+    const int n = d.counters[C_BATCH_PAIRS];
+    const int npx = p.W * p.H;
+    unsigned upd = 0;  // per lane: <= BZ voxels x 64 frames x units per workgroup, far below 2^32
+    {
+        for (int u = blockIdx.x; u < n; u += gridDim.x) {
+            const UnitWork& w = work[u];
+            const int ent = w.id;
+            const unsigned long long mask = w.mask;
+            if (ent != -1) {
+                const int id = ent & 0x7FFFFFFF;
+                const bool fresh = ent < 0;
+                const int col = (s & 3) * 64 + lane;
+                const int x = col >> 4, y = col & 15;
+                const int z0 = (s >> 2) * BZ;
+                float* base = d.vox + (size_t)id * UNIT_FLOATS;
+                float ts[BZ], wt[BZ], cr[BZ], cg[BZ], cb[BZ];
 #pragma unroll
                 for (int k = 0; k < BZ; ++k) {
-                    pcz_c[k] = pcz_n[k];
-                    dm_c[k] = dm_n[k];
-                    cv_c[k] = cv_n[k];
-                }
-                col_c = col_n;
-                ok_c = ok_n;
-            }
-        }
+                    const int vi = (z0 + k) * 256 + col;
+#ifdef OT_ABL_NOSTATE  // timing-only ablation build: no voxel-state traffic (results are wrong)
+                    if (true) {
 #else
-        for (unsigned long long m = mask; m; m &= m - 1) {
-            const int f = __ffsll((long long)m) - 1;
-            const BatchFrame& fr = frames[f];
-            const float2* dm = fr.dm;
-            const uint32_t* rgba = fr.rgba;
-#ifndef OT_GLOBAL_GATHER
-            const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(dm, npx * 8);
-            const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(rgba, npx * 4);
+                    if (fresh) {
 #endif
-            const bool use_color = fr.color != nullptr;
-            float pc[3];
+                        ts[k] = wt[k] = cr[k] = cg[k] = cb[k] = 0.0f;
+                    } else {
+                        ts[k] = base[vi];
+                        wt[k] = base[UNIT_VOX + vi];
+                        cr[k] = base[2 * UNIT_VOX + vi];
+                        cg[k] = base[3 * UNIT_VOX + vi];
+                        cb[k] = base[4 * UNIT_VOX + vi];
+                    }
+                }
+                const float ox = (float)((double)w.kx * p.unit_len);
+                const float oy = (float)((double)w.ky * p.unit_len);
+                const float oz = (float)((double)w.kz * p.unit_len);
+                const float px = (p.half + p.vl * (float)x) + ox;
+                const float py = (p.half + p.vl * (float)y) + oy;
+                const float pz = p.half + oz;
+                for (unsigned long long m = mask; m; m &= m - 1) {
+                    const int f = __ffsll((long long)m) - 1;
+                    const BatchFrame& fr = frames[f];
+                    const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(fr.dm, npx * 8);
+                    const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
+                    const bool use_color = fr.color != nullptr;
+                    float pc[3];
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const float a = fr.E[r * 4 + 0] * px;
-                const float b = fr.E[r * 4 + 1] * py;
-                const float c = fr.E[r * 4 + 2] * pz;
-                pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
-            }
-            const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
-            for (int k = 0; k < z0; ++k) {  // wave-uniform: advance to this half's first voxel
-                pc[0] += es0;
-                pc[1] += es1;
-                pc[2] += es2;
-            }
-            // phase A: projections of the BZ voxels (u and v share pc.z's refined reciprocal)
-            int pixv[BZ];
-            float pcz[BZ];
+                    for (int r = 0; r < 3; ++r) {
+                        const float a = fr.E[r * 4 + 0] * px;
+                        const float b = fr.E[r * 4 + 1] * py;
+                        const float c = fr.E[r * 4 + 2] * pz;
+                        pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
+                    }
+                    const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
+                    for (int k = 0; k < z0; ++k) {  // wave-uniform: advance to this slice's first voxel
+                        pc[0] += es0;
+                        pc[1] += es1;
+                        pc[2] += es2;
+                    }
+                    // phase A: projections of the BZ voxels
+                    int pixv[BZ];
+                    float pcz[BZ];
 #pragma unroll
-            for (int k = 0; k < BZ; ++k) {
-                const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
+                    for (int k = 0; k < BZ; ++k) {
+                        const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
 #ifndef OT_EXACTPROJ
-                // Certified fast projection.  Only floor(u), floor(v) and the bound tests are used, so u = nu * rcp(z)
-                // decides them exactly unless u lies within proj_eps of an integer (the bound tests 0.0001 and
-                // W - 0.0001 sit 1e-4 from integers); those rare waves redo the IEEE quotients below.
-                const float rz = __builtin_amdgcn_rcpf(pc[2]);
-                float u_f = (nu * rz + p.cx) + 0.5f;
-                float v_f = (nv * rz + p.cy) + 0.5f;
-                const bool sure = !(pc[2] > 0.0f) ||
-                                  ((fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
-                                   (fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
-                if (!sure) {
-                    u_f = ((nu / pc[2]) + p.cx) + 0.5f;
-                    v_f = ((nv / pc[2]) + p.cy) + 0.5f;
-                }
+                        // Certified fast projection.  Only floor(u), floor(v) and the bound tests are used, so
+                        // u = nu * rcp(z) decides them exactly unless u lies within proj_eps of an integer (the
+                        // bound tests 0.0001 and W - 0.0001 sit 1e-4 from integers); those rare waves redo the
+                        // IEEE quotients.
+                        const float rz = __builtin_amdgcn_rcpf(pc[2]);
+                        float u_f = (nu * rz + p.cx) + 0.5f;
+                        float v_f = (nv * rz + p.cy) + 0.5f;
+                        const bool sure = !(pc[2] > 0.0f) ||
+                                          ((fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
+                                           (fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
+                        if (!sure) {
+                            u_f = ((nu / pc[2]) + p.cx) + 0.5f;
+                            v_f = ((nv / pc[2]) + p.cy) + 0.5f;
+                        }
 #else
-                float qu, qv;
-#if OT_DIV_MODE == 0
-                qu = nu / pc[2];
-                qv = nv / pc[2];
-#elif OT_DIV_MODE == 2  // timing-only: shared reciprocal without the guard
-                {
-                    const float r = recip_refined(pc[2]);
-                    qu = div_with_recip(nu, pc[2], r);
-                    qv = div_with_recip(nv, pc[2], r);
-                }
-#else
-                {
-                    // guard folded into a select: both quotients are always computed the fast way and the
-                    // (rare) out-of-band lanes redo them with the full IEEE expansion
-                    const float r = recip_refined(pc[2]);
-                    qu = div_with_recip(nu, pc[2], r);
-                    qv = div_with_recip(nv, pc[2], r);
-                    if (!(div_guard_ok(nu, pc[2]) && div_guard_ok(nv, pc[2]))) {
-                        qu = nu / pc[2];
-                        qv = nv / pc[2];
+                        const float u_f = ((nu / pc[2]) + p.cx) + 0.5f;
+                        const float v_f = ((nv / pc[2]) + p.cy) + 0.5f;
+#endif
+                        // non-short-circuit test keeps all BZ projections in one basic block
+                        const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) &
+                                        (v_f < p.safe_h);
+                        pixv[k] = ok ? (int)__umul24((unsigned)(int)v_f, (unsigned)p.W) + (int)u_f : -1;
+                        pcz[k] = pc[2];
+                        pc[0] += es0;
+                        pc[1] += es1;
+                        pc[2] += es2;
                     }
-                }
-#endif
-                const float u_f = (qu + p.cx) + 0.5f;
-                const float v_f = (qv + p.cy) + 0.5f;
-#endif
-                // non-short-circuit test: both quotients of all BZ voxels stay in one basic block, so the
-                // scheduler interleaves their independent division chains (a && here sinks the v division
-                // behind a per-voxel exec-mask branch)
-                const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) &
-                                (v_f < p.safe_h);
-                pixv[k] = ok ? (int)__umul24((unsigned)(int)v_f, (unsigned)p.W) + (int)u_f : -1;
-                pcz[k] = pc[2];
-                pc[0] += es0;
-                pc[1] += es1;
-                pc[2] += es2;
-            }
-            // phase B: all gathers issued before any use
-            float2 dmv[BZ];
-            uint32_t cv[BZ];
+                    // phase B: all gathers issued before any use (buffer loads: wave-uniform resource + 32-bit
+                    // byte offset, no per-lane 64-bit address math)
+                    float2 dmv[BZ];
+                    uint32_t cv[BZ];
 #pragma unroll
-            for (int k = 0; k < BZ; ++k) {
-                const int q = pixv[k] < 0 ? 0 : pixv[k];
+                    for (int k = 0; k < BZ; ++k) {
+                        const int qx = pixv[k] < 0 ? 0 : pixv[k];
 #ifdef OT_ABL_NOGATHER  // timing-only ablation build: no frame gathers (results are wrong)
-                dmv[k] = make_float2(pcz[k] + 0.01f * (float)(q & 7), 1.0f);
-                cv[k] = (unsigned)q;
+                        dmv[k] = make_float2(pcz[k] + 0.01f * (float)(qx & 7), 1.0f);
+                        cv[k] = (unsigned)qx;
 #else
-#ifdef OT_GLOBAL_GATHER
-                dmv[k] = dm[q];
-                cv[k] = use_color ? rgba[q] : 0u;
-#else
-                // buffer loads: wave-uniform resource + 32-bit byte offset (no per-lane 64-bit address math)
-                const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, q * 8, 0, 0);
-                dmv[k] = make_float2(__uint_as_float(raw.x), __uint_as_float(raw.y));
-                cv[k] = use_color ? __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, q * 4, 0, 0) : 0u;
+                        const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, qx * 8, 0, 0);
+                        dmv[k] = make_float2(__uint_as_float(raw.x), __uint_as_float(raw.y));
+                        cv[k] = use_color ? __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, qx * 4, 0, 0) : 0u;
 #endif
-#endif
-            }
-            // phase C: updates
-#ifdef OT_BRANCHLESS
-            // select-based update: every lane evaluates the arithmetic, results are kept only where
-            // Open3D's conditions hold (identical values; removes exec-mask branches)
+                    }
+                    // phase C: updates in frame order
 #pragma unroll
-            for (int k = 0; k < BZ; ++k) {
-                const float sdf = (dmv[k].x - pcz[k]) * dmv[k].y;
-                const bool doit = (pixv[k] >= 0) && (dmv[k].x > 0.0f) && (sdf > -p.trunc);
-                const float sv = sdf * p.trunc_inv;
-                const float tn = (sv < 1.0f) ? sv : 1.0f;
-                const float w = wt[k];
-                const float w1 = w + 1.0f;
-                const float num = ts[k] * w + tn;
-#if OT_DIV_MODE == 0
-                const float tsn = num / w1;
-#else
-                const float tsn = div_guard_ok(num, w1) ? div_with_recip(num, w1, recip_refined(w1)) : num / w1;
-#endif
-                ts[k] = doit ? tsn : ts[k];
-                if (use_color) {
-                    const float rw = __builtin_amdgcn_rcpf(w1);
-                    const float nr = (cr[k] * w + (float)(cv[k] & 0xFFu)) * rw;
-                    const float ng = (cg[k] * w + (float)((cv[k] >> 8) & 0xFFu)) * rw;
-                    const float nb = (cb[k] * w + (float)((cv[k] >> 16) & 0xFFu)) * rw;
-                    cr[k] = doit ? nr : cr[k];
-                    cg[k] = doit ? ng : cg[k];
-                    cb[k] = doit ? nb : cb[k];
-                }
-                wt[k] = doit ? w1 : w;
-                upd += doit ? 1u : 0u;
-            }
-#else
-#pragma unroll
-            for (int k = 0; k < BZ; ++k) {
-                if (pixv[k] >= 0 && dmv[k].x > 0.0f) {
-                    const float sdf = (dmv[k].x - pcz[k]) * dmv[k].y;
-                    if (sdf > -p.trunc) {
-                        const float sv = sdf * p.trunc_inv;
-                        const float tn = (sv < 1.0f) ? sv : 1.0f;
-                        const float w = wt[k];
-                        const float w1 = w + 1.0f;
-#ifdef OT_ABL_FASTDIV  // timing-only: tsdf division via reciprocal (not bit-exact)
-                        ts[k] = (ts[k] * w + tn) * __builtin_amdgcn_rcpf(w1);
-#else
+                    for (int k = 0; k < BZ; ++k) {
+#ifndef OT_BRANCHY  // select form (default): identical values, no exec-mask branches
+                        const float sdf = (dmv[k].x - pcz[k]) * dmv[k].y;
+                        const bool doit = (pixv[k] >= 0) & (dmv[k].x > 0.0f) & (sdf > -p.trunc);
                         {
-                            const float num = ts[k] * w + tn;  // exact IEEE quotient (bit-exact tsdf)
-#if OT_DIV_MODE == 0
-                            ts[k] = num / w1;
 #else
-                            float q = div_with_recip(num, w1, recip_refined(w1));
-                            if (!div_guard_ok(num, w1)) q = num / w1;
-                            ts[k] = q;
+                        if (pixv[k] >= 0 && dmv[k].x > 0.0f) {
+                            const float sdf = (dmv[k].x - pcz[k]) * dmv[k].y;
+                            const bool doit = sdf > -p.trunc;
+                            if (doit) {
 #endif
-                        }
+                                const float sv = sdf * p.trunc_inv;
+                                const float tn = (sv < 1.0f) ? sv : 1.0f;
+                                const float wv = wt[k];
+                                const float w1 = wv + 1.0f;
+#ifdef OT_ABL_FASTDIV  // timing-only: tsdf division via reciprocal (not bit-exact)
+                                const float tsn = (ts[k] * wv + tn) * __builtin_amdgcn_rcpf(w1);
+#else
+                                const float tsn = (ts[k] * wv + tn) / w1;  // exact IEEE quotient: tsdf bit-exact
 #endif
+                                ts[k] = doit ? tsn : ts[k];
 #ifdef OT_ABL_NOCOLOR
-                        if (false) {
+                                if (false) {
 #else
-                        if (use_color) {
+                                if (use_color) {
 #endif
-                            // colour running mean: one hardware reciprocal (1 ulp) for the three channels —
-                            // within the 1e-4 colour contract; Open3D keeps colour in float64 anyway
-                            const float rw = __builtin_amdgcn_rcpf(w1);
-                            cr[k] = (cr[k] * w + (float)(cv[k] & 0xFFu)) * rw;
-                            cg[k] = (cg[k] * w + (float)((cv[k] >> 8) & 0xFFu)) * rw;
-                            cb[k] = (cb[k] * w + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                                    // colour running mean: one hardware reciprocal (1 ulp) for the three
+                                    // channels — within the 1e-4 colour contract (Open3D keeps colour in f64)
+                                    const float rw = __builtin_amdgcn_rcpf(w1);
+                                    const float nr = (cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
+                                    const float ng = (cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
+                                    const float nb = (cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                                    cr[k] = doit ? nr : cr[k];
+                                    cg[k] = doit ? ng : cg[k];
+                                    cb[k] = doit ? nb : cb[k];
+                                }
+                                wt[k] = doit ? w1 : wv;
+                                upd += doit ? 1u : 0u;
+#ifdef OT_BRANCHY
+                            }
+#endif
                         }
-                        wt[k] = w1;
-                        ++upd;
                     }
                 }
+#ifdef OT_ABL_NOSTATE  // keep every result live without storing it
+#pragma unroll
+                for (int k = 0; k < BZ; ++k) asm volatile("" ::"v"(ts[k]), "v"(wt[k]), "v"(cr[k]), "v"(cg[k]), "v"(cb[k]));
+#else
+#pragma unroll
+                for (int k = 0; k < BZ; ++k) {
+                    const int vi = (z0 + k) * 256 + col;
+                    base[vi] = ts[k];
+                    base[UNIT_VOX + vi] = wt[k];
+                    base[2 * UNIT_VOX + vi] = cr[k];
+                    base[3 * UNIT_VOX + vi] = cg[k];
+                    base[4 * UNIT_VOX + vi] = cb[k];
+                }
+#endif
             }
-#endif
-        }
-#endif
-#ifdef OT_ABL_NOSTATE  // keep every result live without storing it (guide §5.4 rule 17)
-#pragma unroll
-        for (int k = 0; k < BZ; ++k) asm volatile("" ::"v"(ts[k]), "v"(wt[k]), "v"(cr[k]), "v"(cg[k]), "v"(cb[k]));
-        continue;
-#endif
-#pragma unroll
-        for (int k = 0; k < BZ; ++k) {
-            const int vi = (z0 + k) * 256 + col;
-            base[vi] = ts[k];
-            base[UNIT_VOX + vi] = wt[k];
-            base[2 * UNIT_VOX + vi] = cr[k];
-            base[3 * UNIT_VOX + vi] = cg[k];
-            base[4 * UNIT_VOX + vi] = cb[k];
         }
     }
-    const unsigned long long upd64 = wave_sum((unsigned long long)upd);
-    if (lane_id() == 0) red[tid >> 6] = upd64;
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long tot = 0;
-        for (int w = 0; w < BLANES / 64; ++w) tot += red[w];
-        if (tot) atomicAdd(&d.stats[S_UPDATES], tot);
-        if (pairs) atomicAdd(&d.stats[S_UNIT_INTEGRATIONS], pairs);
-    }
+    const unsigned long long tot = wave_sum((unsigned long long)upd);
+    if (lane == 0 && tot) atomicAdd(&d.stats[S_UPDATES], tot);
 }
 
 // export: units in sorted order, voxels transposed to Open3D IndexOf order (x*256 + y*16 + z)
@@ -1017,20 +813,20 @@ static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t
 }
 
 #ifndef OT_GRID_MULT
-#define OT_GRID_MULT 1
+#define OT_GRID_MULT 4
 #endif
-// Persistent work-queue grid of k_batch_integrate: the workgroups that are co-resident on the device (cached per
-// device; a benign race at worst computes the same value twice).
+// Grid of k_batch_integrate: OT_GRID_MULT x the co-resident workgroups (cached per device; a benign race at worst
+// computes the same value twice).
 static int integrate_grid() {
     static int cache[64] = {0};
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 2048;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 4096;
     if (!cache[dev]) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_batch_integrate, BLANES, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_batch_integrate, 64 * SLICES, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 ||
             cus <= 0)
-            return 2048;
+            return 4096;
         cache[dev] = per_cu * cus * OT_GRID_MULT;
     }
     return cache[dev];
@@ -1083,8 +879,9 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     OT_HIP_TRY(hipMemcpyAsync(vol->bframes, host, sizeof(BatchFrame) * n, hipMemcpyHostToDevice, stream));
     if (!vol->hb_event[hb]) OT_HIP_TRY(hipEventCreateWithFlags(&vol->hb_event[hb], hipEventDisableTiming));
     OT_HIP_TRY(hipEventRecord(vol->hb_event[hb], stream));
-    static_assert(C_BATCH_NEXT == C_BATCH_PAIRS + 1, "one memset clears both");
-    OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, 2 * sizeof(int), stream));
+    // batch pair count and the integrate's queue heads
+    OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, sizeof(int) * (N_COUNTERS - C_BATCH_PAIRS),
+                              stream));
     hipLaunchKernelGGL(k_batch_prep, dim3((unsigned)((npx / 4 + 255) / 256 + 1), n), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, (const float*)vol->mult, npx);
     BatchTouchParams tp;
@@ -1102,19 +899,16 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     const unsigned tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
     hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, tp, vol->dev, n);
-#ifndef OT_WORK_QUEUE
-    const int grid = (int)std::min<int64_t>(vol->max_units, 2048);
-#else
+    hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work);
     const int grid = integrate_grid();
-#endif
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
         OT_HIP_TRY(hipEventCreate(&e0));
         OT_HIP_TRY(hipEventCreate(&e1));
         OT_HIP_TRY(hipEventRecord(e0, stream));
     }
-    hipLaunchKernelGGL(k_batch_integrate, dim3(grid), dim3(BLANES), 0, stream, (const BatchFrame*)vol->bframes, ip0,
-                       vol->dev);
+    hipLaunchKernelGGL(k_batch_integrate, dim3(grid), dim3(64 * SLICES), 0, stream, (const BatchFrame*)vol->bframes, ip0,
+                       vol->dev, (const UnitWork*)vol->dev.work);
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
         OT_HIP_TRY(hipEventRecord(e1, stream));
@@ -1247,6 +1041,7 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
     if ((e = hipMalloc(&v->sorted_ids, sizeof(unsigned) * max_units)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.fmask, sizeof(unsigned long long) * cap)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.bslots, sizeof(int) * cap)) != hipSuccess) return cleanup(e);
+    if ((e = hipMalloc(&d.work, sizeof(UnitWork) * cap)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&v->bframes, sizeof(BatchFrame) * MAX_BATCH)) != hipSuccess) return cleanup(e);
     if ((e = hipHostMalloc(&v->hbframes, sizeof(BatchFrame) * MAX_BATCH * 2, hipHostMallocDefault)) != hipSuccess)
         return cleanup(e);
@@ -1265,7 +1060,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
     void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, v->mult,
-                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, d.fmask, d.bslots,
+                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, d.fmask, d.bslots, d.work,
                     v->bframes, v->bdm, v->brgba};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
