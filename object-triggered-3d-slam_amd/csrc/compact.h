@@ -144,6 +144,33 @@ ot_status compact(int64_t n, Pred pred, Emit emit, hipStream_t stream, int64_t* 
     return OT_OK;
 }
 
+// Segment heads of a sorted key array AND the segment index of every item, in one stable compaction:
+// heads[s] = first position of segment s, seg[i] = segment of item i (= number of heads <= i, minus one).
+namespace {
+__global__ __launch_bounds__(CMP_THREADS) void k_segments_emit(int64_t n, const unsigned long long* __restrict__ keys,
+                                                               const int* __restrict__ block_offsets,
+                                                               int* __restrict__ heads, int* __restrict__ seg) {
+    const int64_t base = (int64_t)blockIdx.x * CMP_TILE + (int64_t)threadIdx.x * CMP_ITEMS;
+    bool head[CMP_ITEMS];
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < CMP_ITEMS; ++k) {
+        const int64_t i = base + k;
+        head[k] = (i < n) && (i == 0 || keys[i] != keys[i - 1]);
+        c += head[k] ? 1 : 0;
+    }
+    int total;
+    int pos = block_excl_scan_256(c, total) + block_offsets[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < CMP_ITEMS; ++k) {
+        const int64_t i = base + k;
+        if (i >= n) break;
+        if (head[k]) heads[pos++] = (int)i;
+        seg[i] = pos - 1;
+    }
+}
+}  // namespace
+
 // segment heads of a sorted key array (i == 0 or key changes) -> their positions
 struct SegHeadPred {
     const unsigned long long* keys;
@@ -153,6 +180,29 @@ struct SegHeadEmit {
     int* heads;
     __device__ void operator()(int64_t i, int64_t pos) const { heads[pos] = (int)i; }
 };
+
+// Host driver of k_segments_emit (count with SegHeadPred, scan, emit); returns the segment count (synchronises).
+inline ot_status compact_segments(int64_t n, const unsigned long long* keys, int* heads, int* seg, hipStream_t stream,
+                                  int64_t* n_seg_host, int scratch_slot) {
+    const int64_t nblocks = (n + CMP_TILE - 1) / CMP_TILE;
+    *n_seg_host = 0;
+    if (n <= 0) return OT_OK;
+    char* ws = (char*)scratch(sizeof(int) * (size_t)nblocks + 64, scratch_slot);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    int64_t* d_total = (int64_t*)ws;
+    int* d_counts = (int*)(ws + 64);
+    hipLaunchKernelGGL((k_compact_count<SegHeadPred>), dim3((unsigned)nblocks), dim3(CMP_THREADS), 0, stream, n,
+                       SegHeadPred{keys}, d_counts);
+    hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(1024), 0, stream, d_counts, (int)nblocks, d_total);
+    hipLaunchKernelGGL(k_segments_emit, dim3((unsigned)nblocks), dim3(CMP_THREADS), 0, stream, n, keys,
+                       (const int*)d_counts, heads, seg);
+    OT_LAUNCH_CHECK();
+    int64_t tot = 0;
+    OT_HIP_TRY(hipMemcpyAsync(&tot, d_total, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    *n_seg_host = tot;
+    return OT_OK;
+}
 
 // per-axis min / max of float64 [n][3] points via order-preserving u64 atomics (exact)
 struct Bounds {

@@ -12,7 +12,9 @@
 //                sqrt'ed and summed in ascending order, divided by the count (std::accumulate in Open3D).
 //                Cloud mean / std use a fixed-order two-level reduction in float64.
 // Queries run in sorted (cell) order, so a wave's neighbourhoods overlap and stay in L2.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "compact.h"
 #include "sort.h"
@@ -20,21 +22,36 @@
 namespace ot {
 
 struct GridDev {
-    const double* sxyz;           // points in sorted order [n][3]
+    const double* sxyz;           // points in sorted (cell) order [n][3]
     const unsigned* sidx;         // sorted position -> original index
-    unsigned long long* hkeys;    // cell hash keys
-    int2* hval;                   // cell hash values: [start, end)
+    const int* pcell;             // sorted position -> cell index (position in the sorted cell list)
+    const int2* nbr3;             // per cell: 9 merged z-column ranges covering its 3x3x3 cell block
+    const int2* nbr5;             // per cell: 25 merged z-column ranges covering its 5x5x5 block (SOR only)
+    unsigned long long* hkeys;    // cell hash keys (compact keys, KEY_EMPTY = free)
+    int2* hval;                   // cell hash values: [start, end) in the sorted order
     int hash_mask;
+    int dim[3];                   // cells per axis (cell coordinates are >= 0: origin = the cloud's minimum)
+    int sy, sx;                   // key = x << sx | y << sy | z  (z in the low bits)
     double origin[3];
-    double h, inv_h;
+    double h;
 };
+
+// A block of cells around a cell as z-columns: cells (x', y', z-R .. z+R) have consecutive keys, so their points
+// are ONE contiguous range of the sorted order whichever of those cells are occupied.  The 3x3x3 block is 9
+// ranges, the 5x5x5 block 25; a 5-column minus its 3-column is the two ranges on either side.
+constexpr int NBR3 = 9;
+constexpr int NBR5 = 25;
 
 __device__ inline int cell_coord(double v, double origin, double h) { return (int)floor((v - origin) / h); }
 
-__device__ inline int2 grid_find(const GridDev& g, int x, int y, int z) {
-    if (!key_in_range(x, y, z)) return make_int2(0, 0);
-    const unsigned long long key = pack_key(x, y, z);
-    unsigned slot = (unsigned)mix64(key) & (unsigned)g.hash_mask;
+__device__ inline bool cell_valid(const GridDev& g, int x, int y, int z) {
+    return x >= 0 && x < g.dim[0] && y >= 0 && y < g.dim[1] && z >= 0 && z < g.dim[2];
+}
+__device__ inline unsigned long long cell_key(const GridDev& g, int x, int y, int z) {
+    return ((unsigned long long)x << g.sx) | ((unsigned long long)y << g.sy) | (unsigned long long)z;
+}
+
+__device__ inline int2 grid_probe(const GridDev& g, unsigned long long key, unsigned slot) {
     for (int probe = 0; probe <= g.hash_mask; ++probe) {
         const unsigned long long k = g.hkeys[slot];
         if (k == key) return g.hval[slot];
@@ -44,6 +61,12 @@ __device__ inline int2 grid_find(const GridDev& g, int x, int y, int z) {
     return make_int2(0, 0);
 }
 
+__device__ inline int2 grid_find(const GridDev& g, int x, int y, int z) {
+    if (!cell_valid(g, x, y, z)) return make_int2(0, 0);
+    const unsigned long long key = cell_key(g, x, y, z);
+    return grid_probe(g, key, (unsigned)mix64(key) & (unsigned)g.hash_mask);
+}
+
 __global__ __launch_bounds__(256) void k_cell_keys(const double* __restrict__ xyz, int64_t n, GridDev g,
                                                    unsigned long long* keys, unsigned* idx, int* err) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -51,11 +74,12 @@ __global__ __launch_bounds__(256) void k_cell_keys(const double* __restrict__ xy
     const int x = cell_coord(xyz[i * 3 + 0], g.origin[0], g.h);
     const int y = cell_coord(xyz[i * 3 + 1], g.origin[1], g.h);
     const int z = cell_coord(xyz[i * 3 + 2], g.origin[2], g.h);
-    if (!key_in_range(x, y, z)) *err = 1;
-    keys[i] = pack_key(x, y, z);
+    if (!cell_valid(g, x, y, z)) *err = 1;
+    keys[i] = cell_valid(g, x, y, z) ? cell_key(g, x, y, z) : 0ull;
     idx[i] = (unsigned)i;
 }
 
+// per occupied cell: hash insert of [start, end)
 __global__ __launch_bounds__(256) void k_grid_insert(const unsigned long long* __restrict__ skeys,
                                                      const int* __restrict__ heads, int64_t ncells, int64_t n,
                                                      GridDev g) {
@@ -75,6 +99,58 @@ __global__ __launch_bounds__(256) void k_grid_insert(const unsigned long long* _
     }
 }
 
+// One lane per (cell, z-column of its (2R+1)^2 neighbourhood): 2R+1 hash lookups whose first probes are issued
+// together, merged into the column's range over z-R..z+R (and, R = 2, over z-1..z+1 for the inner 3x3 columns).
+template <int R>
+__global__ __launch_bounds__(256) void k_cell_nbr(const unsigned long long* __restrict__ skeys,
+                                                  const int* __restrict__ heads, int64_t ncells, GridDev g,
+                                                  int2* __restrict__ nbr3, int2* __restrict__ nbr5) {
+    constexpr int W = 2 * R + 1, COLS = W * W;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= ncells * COLS) return;
+    const int64_t c = gid / COLS;
+    const int t = (int)(gid - c * COLS);
+    const int dx = t / W - R, dy = t % W - R;
+    const unsigned long long key = skeys[heads[c]];
+    const int z = (int)(key & ((1ull << g.sy) - 1));
+    const int y = (int)((key >> g.sy) & ((1ull << (g.sx - g.sy)) - 1)) + dy;
+    const int x = (int)(key >> g.sx) + dx;
+    unsigned long long kq[W];
+    unsigned slot[W];
+    unsigned long long k0[W];
+    bool valid[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        valid[i] = cell_valid(g, x, y, z + i - R);
+        kq[i] = valid[i] ? cell_key(g, x, y, z + i - R) : 0ull;
+        slot[i] = (unsigned)mix64(kq[i]) & (unsigned)g.hash_mask;
+    }
+#pragma unroll
+    for (int i = 0; i < W; ++i) k0[i] = valid[i] ? g.hkeys[slot[i]] : KEY_EMPTY;
+    int2 se[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        se[i] = make_int2(0, 0);
+        if (valid[i] && k0[i] != KEY_EMPTY)
+            se[i] = (k0[i] == kq[i]) ? g.hval[slot[i]] : grid_probe(g, kq[i], (slot[i] + 1) & (unsigned)g.hash_mask);
+    }
+    int b5 = 0x7FFFFFFF, e5 = 0, b3 = 0x7FFFFFFF, e3 = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i)
+        if (se[i].y > se[i].x) {
+            b5 = min(b5, se[i].x);
+            e5 = max(e5, se[i].y);
+            if (i >= R - 1 && i <= R + 1) {
+                b3 = min(b3, se[i].x);
+                e3 = max(e3, se[i].y);
+            }
+        }
+    const int2 r5 = e5 > 0 ? make_int2(b5, e5) : make_int2(0, 0);
+    const int2 r3 = e3 > 0 ? make_int2(b3, e3) : make_int2(0, 0);
+    if (R == 2) nbr5[c * NBR5 + t] = r5;
+    if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1) nbr3[c * NBR3 + (dx + 1) * 3 + (dy + 1)] = r3;
+}
+
 __global__ __launch_bounds__(256) void k_gather_sorted(const double* __restrict__ xyz, const unsigned* __restrict__ sidx,
                                                        int64_t n, double* __restrict__ sxyz) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -89,87 +165,135 @@ __device__ inline double d2_l2(const double* q, const double* p) {
 }
 
 // ------------------------------------------------------------------------------------------------ ROR
+// cell = radius: every neighbour within the radius lies in the 3x3x3 block, i.e. in the 9 merged ranges.
 __global__ __launch_bounds__(256) void k_ror(GridDev g, int64_t n, double r2, int nb, unsigned char* keep) {
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
     const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
-    const int cx = cell_coord(q[0], g.origin[0], g.h), cy = cell_coord(q[1], g.origin[1], g.h),
-              cz = cell_coord(q[2], g.origin[2], g.h);
+    const int2* rg = g.nbr3 + (int64_t)g.pcell[j] * NBR3;
     long long cnt = 0;
-    for (int dx = -1; dx <= 1; ++dx)
-        for (int dy = -1; dy <= 1; ++dy)
-            for (int dz = -1; dz <= 1; ++dz) {
-                const int2 se = grid_find(g, cx + dx, cy + dy, cz + dz);
-                for (int k = se.x; k < se.y; ++k) cnt += d2_l2(q, g.sxyz + (int64_t)k * 3) < r2 ? 1 : 0;
-            }
+    for (int t = 0; t < NBR3; ++t) {
+        const int2 se = rg[t];
+        for (int k = se.x; k < se.y; ++k) cnt += d2_l2(q, g.sxyz + (int64_t)k * 3) < r2 ? 1 : 0;
+    }
     keep[g.sidx[j]] = cnt > nb ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------------------------ SOR
-// Register top-k list, RIGHT-aligned: best[KMAX-kk .. KMAX-1] hold the kk smallest squared distances in
-// ascending order and best[0 .. KMAX-kk-1] = -inf (never displaced).  best[KMAX-1] is therefore always the
-// current k-th distance at a compile-time index, so a candidate that cannot enter costs one compare.
+// Register top-k list, RIGHT-aligned ascending: best[KMAX-kk .. KMAX-1] hold the kk smallest squared distances
+// and best[0 .. KMAX-kk-1] = -inf.  Insertion is a branch-free min/max exchange chain, skipped for a whole wave
+// when no lane's candidate beats its current k-th distance best[KMAX-1]; lanes whose candidate does not enter
+// leave the list unchanged (their d is >= every entry).  NaN never enters (d < kth is false).
 template <int KMAX>
 __device__ inline void topk_insert(double (&best)[KMAX], double d) {
-    if (!(d < best[KMAX - 1])) return;
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
-        if (d < best[i]) {
-            const double t = best[i];
-            best[i] = d;
-            d = t;
-        }
+        const double lo = fmin(best[i], d);
+        d = fmax(best[i], d);
+        best[i] = lo;
     }
 }
 
 template <int KMAX>
-__device__ inline void scan_cell(const GridDev& g, const double q[3], int x, int y, int z, double (&best)[KMAX],
-                                 int kk, long long& have) {
-    const int2 se = grid_find(g, x, y, z);
-    for (int m = se.x; m < se.y; ++m) {
-        topk_insert<KMAX>(best, d2_l2(q, g.sxyz + (int64_t)m * 3));
-        ++have;
+__device__ inline void scan_range(const GridDev& g, const double q[3], int beg, int end, double (&best)[KMAX]) {
+    for (int m = beg; m < end; ++m) {
+        const double d = d2_l2(q, g.sxyz + (int64_t)m * 3);
+        if (d < best[KMAX - 1]) topk_insert<KMAX>(best, d);
     }
 }
 
-constexpr int SOR_RMAX = 6;  // beyond this ring a query falls back to an exact scan of every point
-
 template <int KMAX>
-__global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, double* avg) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j >= n) return;
-    const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
-    const int cx = cell_coord(q[0], g.origin[0], g.h), cy = cell_coord(q[1], g.origin[1], g.h),
-              cz = cell_coord(q[2], g.origin[2], g.h);
-    const int kk = (int)((int64_t)k < n ? k : n);
-    double best[KMAX];
+__device__ inline void topk_reset(double (&best)[KMAX], int kk) {
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) best[i] = (i < KMAX - kk) ? -INFINITY : INFINITY;
+}
+
+constexpr int SOR_RMAX = 8;  // beyond this ring a query falls back to an exact scan of every point
+
+// Exact kNN for a query the 5x5x5 block does not settle (isolated points): Chebyshev shell expansion through the
+// hash until the k-th distance lies inside the scanned cube, else a scan of the whole cloud.
+template <int KMAX>
+__device__ inline void sor_fallback(const GridDev& g, const double q[3], int64_t n, int kk,
+                                                       double (&best)[KMAX]) {
+    const int cx = cell_coord(q[0], g.origin[0], g.h), cy = cell_coord(q[1], g.origin[1], g.h),
+              cz = cell_coord(q[2], g.origin[2], g.h);
+    topk_reset<KMAX>(best, kk);
     long long have = 0;
-    bool done = false;
-    for (int r = 0; r <= SOR_RMAX && !done; ++r) {
-        // cells at Chebyshev distance exactly r
+    for (int r = 0; r <= SOR_RMAX; ++r) {
         for (int dx = -r; dx <= r; ++dx)
             for (int dy = -r; dy <= r; ++dy) {
                 const bool face = (dx == -r || dx == r || dy == -r || dy == r);
-                if (face) {
-                    for (int dz = -r; dz <= r; ++dz) scan_cell<KMAX>(g, q, cx + dx, cy + dy, cz + dz, best, kk, have);
-                } else {
-                    scan_cell<KMAX>(g, q, cx + dx, cy + dy, cz - r, best, kk, have);
-                    if (r > 0) scan_cell<KMAX>(g, q, cx + dx, cy + dy, cz + r, best, kk, have);
+                for (int dz = -r; dz <= r; dz += (face || r == 0) ? 1 : 2 * r) {
+                    const int2 se = grid_find(g, cx + dx, cy + dy, cz + dz);
+                    scan_range<KMAX>(g, q, se.x, se.y, best);
+                    have += se.y - se.x;
                 }
             }
         if (have >= kk) {
             const double kth = best[KMAX - 1];
             // every point within distance (r - margin) * h of q lies in rings 0..r
             const double guard = (r > 0 ? (double)r - 0.01 : 0.0) * g.h;
-            if (kth <= guard * guard || have >= n) done = true;
+            if (kth <= guard * guard || have >= n) return;
         }
     }
-    if (!done) {  // isolated point: exact scan of the whole cloud
+    topk_reset<KMAX>(best, kk);
+    scan_range<KMAX>(g, q, 0, (int)n, best);
+}
+
+// distance from q to the faces of its (2R+1)^3 cell block, minus a rounding margin
+__device__ inline double block_guard(const GridDev& g, const double q[3], double R) {
+    double guard = (R + 1.0) * g.h;
 #pragma unroll
-        for (int i = 0; i < KMAX; ++i) best[i] = (i < KMAX - kk) ? -INFINITY : INFINITY;
-        for (int64_t m = 0; m < n; ++m) topk_insert<KMAX>(best, d2_l2(q, g.sxyz + m * 3));
+    for (int a = 0; a < 3; ++a) {
+        const double u = (q[a] - g.origin[a]) / g.h;
+        const double f = u - floor(u);
+        guard = fmin(guard, fmin(R + f, R + 1.0 - f) * g.h);
+    }
+    return guard - 1e-6 * g.h;
+}
+
+// One lane per query (sorted order: a wave's queries share cells and candidate ranges).  Stage 1 scans the 9
+// ranges of the query's 3x3x3 block; the k-th distance is final when it does not exceed the distance from q to
+// the block's faces (>= h).  Stage 2 adds the rest of the 5x5x5 block (guard >= 2h).  Isolated points fall back.
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, double* avg) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
+    const int kk = (int)((int64_t)k < n ? k : n);
+    double best[KMAX];
+    topk_reset<KMAX>(best, kk);
+    const int c = g.pcell[j];
+    const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
+    long long have = 0;
+    for (int u = 0; u < NBR3; ++u) {
+        const int t = (u + 4) % NBR3;  // the query's own column first: the k-th distance drops early
+        const int2 se = r3[t];
+        scan_range<KMAX>(g, q, se.x, se.y, best);
+        have += se.y - se.x;
+    }
+    double guard = block_guard(g, q, 1.0);
+    bool settled = have >= n || (have >= kk && best[KMAX - 1] <= guard * guard);
+    if (!settled) {
+        const int2* r5 = g.nbr5 + (int64_t)c * NBR5;
+        for (int t = 0; t < NBR5; ++t) {
+            const int dx = t / 5 - 2, dy = t % 5 - 2;
+            const int2 o = r5[t];
+            if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1) {
+                const int2 i3 = r3[(dx + 1) * 3 + (dy + 1)];
+                if (i3.y > i3.x) {  // the column's cells at z-2 and z+2 only
+                    scan_range<KMAX>(g, q, o.x, i3.x, best);
+                    scan_range<KMAX>(g, q, i3.y, o.y, best);
+                    have += (o.y - o.x) - (i3.y - i3.x);
+                    continue;
+                }
+            }
+            scan_range<KMAX>(g, q, o.x, o.y, best);
+            have += o.y - o.x;
+        }
+        guard = block_guard(g, q, 2.0);
+        settled = have >= n || (have >= kk && best[KMAX - 1] <= guard * guard);
+        if (!settled) sor_fallback<KMAX>(g, q, n, kk, best);
     }
     double s = 0.0;
     int cnt = 0;
@@ -273,9 +397,31 @@ struct GridBuild {
     int64_t ncells = 0;
 };
 
-static ot_status build_grid(const double* xyz, int64_t n, double h, const double origin[3], hipStream_t stream,
-                            GridBuild& out) {
-    char* ws = (char*)scratch(256 + (size_t)n * (8 + 8 + 4 + 4 + 4 + 24), 8);
+static int bits_for_host(int64_t v) {  // bits to represent 0..v
+    int b = 1;
+    while (b < 62 && (v >> b) != 0) ++b;
+    return b;
+}
+
+// Cell grid of size h anchored at the cloud's minimum corner (mn, mx: exact bounds on the host).  Keys are
+// compact (only the bits the extent needs), so the stable radix sort runs ceil(bits / 8) passes.  with5: also
+// build the 5x5x5 ranges (SOR).
+static ot_status build_grid(const double* xyz, int64_t n, double h, const double mn[3], const double mx[3], bool with5,
+                            hipStream_t stream, GridBuild& out) {
+    GridDev& g = out.g;
+    g.h = h;
+    int bits[3];
+    for (int a = 0; a < 3; ++a) {
+        g.origin[a] = mn[a];
+        const double span = std::floor((mx[a] - mn[a]) / h);
+        if (!(span < 1.0e6)) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (radius too small for the extent)");
+        g.dim[a] = (int)span + 1;
+        bits[a] = bits_for_host(g.dim[a] - 1);
+    }
+    g.sy = bits[2];
+    g.sx = bits[1] + bits[2];
+    const int end_bit = bits[0] + bits[1] + bits[2];
+    char* ws = (char*)scratch(256 + (size_t)n * (8 + 8 + 4 + 4 + 4 + 4 + 24), 8);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
     int* err = (int*)ws;
     unsigned long long* kin = (unsigned long long*)(ws + 256);
@@ -283,36 +429,44 @@ static ot_status build_grid(const double* xyz, int64_t n, double h, const double
     unsigned* vin = (unsigned*)(kout + n);
     unsigned* vout = vin + n;
     int* heads = (int*)(vout + n);
-    double* sxyz = (double*)(((uintptr_t)(heads + n) + 15) & ~(uintptr_t)15);
-    GridDev& g = out.g;
-    g.h = h;
-    g.inv_h = 1.0 / h;
-    for (int a = 0; a < 3; ++a) g.origin[a] = origin[a];
+    int* pcell = heads + n;
+    double* sxyz = (double*)(((uintptr_t)(pcell + n) + 15) & ~(uintptr_t)15);
     OT_HIP_TRY(hipMemsetAsync(err, 0, sizeof(int), stream));
     hipLaunchKernelGGL(k_cell_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, xyz, n, g, kin, vin, err);
     OT_LAUNCH_CHECK();
-    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, 63, stream, 3);
+    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, end_bit, stream, 3);
     if (st != OT_OK) return st;
     int64_t ncells = 0;
-    st = compact(n, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &ncells, 9);
+    st = compact_segments(n, kout, heads, pcell, stream, &ncells, 9);  // synchronises
     if (st != OT_OK) return st;
     int e = 0;
     OT_HIP_TRY(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (radius too small for the extent)");
+    if (e) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (non-finite point coordinates)");
     int64_t cap = 1;
     while (cap < 2 * ncells + 2) cap <<= 1;
-    char* hs = (char*)scratch((size_t)cap * (8 + 8) + 64, 10);
+    char* hs = (char*)scratch((size_t)cap * (8 + 8) + (size_t)ncells * (NBR3 + (with5 ? NBR5 : 0)) * 8 + 64, 10);
     if (!hs) return fail(OT_ERR_HIP, "scratch allocation failed");
     g.hkeys = (unsigned long long*)hs;
     g.hval = (int2*)(g.hkeys + cap);
+    int2* nbr3 = g.hval + cap;
+    int2* nbr5 = with5 ? nbr3 + ncells * NBR3 : nullptr;
     g.hash_mask = (int)(cap - 1);
     OT_HIP_TRY(hipMemsetAsync(g.hkeys, 0xFF, sizeof(unsigned long long) * cap, stream));
-    hipLaunchKernelGGL(k_grid_insert, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, stream, kout, heads, ncells,
-                       n, g);
+    hipLaunchKernelGGL(k_grid_insert, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, stream, kout, heads,
+                       ncells, n, g);
+    if (with5)
+        hipLaunchKernelGGL(k_cell_nbr<2>, dim3((unsigned)((ncells * NBR5 + 255) / 256)), dim3(256), 0, stream, kout,
+                           heads, ncells, g, nbr3, nbr5);
+    else
+        hipLaunchKernelGGL(k_cell_nbr<1>, dim3((unsigned)((ncells * NBR3 + 255) / 256)), dim3(256), 0, stream, kout,
+                           heads, ncells, g, nbr3, nbr5);
     hipLaunchKernelGGL(k_gather_sorted, dim3((unsigned)((n * 3 + 255) / 256)), dim3(256), 0, stream, xyz, vout, n, sxyz);
     OT_LAUNCH_CHECK();
     g.sxyz = sxyz;
     g.sidx = vout;
+    g.pcell = pcell;
+    g.nbr3 = nbr3;
+    g.nbr5 = nbr5;
     out.ncells = ncells;
     return OT_OK;
 }
@@ -354,7 +508,7 @@ ot_status ot_remove_radius_outlier(const double* xyz, int64_t n, int32_t nb_poin
     ot_status st = bounds_host(xyz, n, stream, mn, mx);
     if (st != OT_OK) return st;
     GridBuild gb;
-    st = build_grid(xyz, n, radius, mn, stream, gb);
+    st = build_grid(xyz, n, radius, mn, mx, false, stream, gb);
     if (st != OT_OK) return st;
     unsigned char* keep = (unsigned char*)scratch((size_t)n + 64, 12);
     if (!keep) return fail(OT_ERR_HIP, "scratch allocation failed");
@@ -381,25 +535,28 @@ ot_status ot_remove_statistical_outlier(const double* xyz, int64_t n, int32_t nb
     double mn[3], mx[3];
     ot_status st = bounds_host(xyz, n, stream, mn, mx);
     if (st != OT_OK) return st;
-    // cell size: volumetric first guess, then one refinement assuming surface-like (2-D) occupancy so that
-    // an occupied cell holds ~k/3 points (the grid only changes speed, never the result)
+    // Cell size: the grid only changes speed, never the result.  Aim for ~occ_target points per occupied cell
+    // of a surface-like cloud (0.7 k: the k-th neighbour then lies ~0.7 h away, inside the 3x3x3 block that settles
+    // most queries).  First guess: the points cover half of the bounding box's largest face; refined once from the
+    // measured occupancy (2-D scaling) when it is off by more than 2.5x.
     const double k = (double)nb_neighbors;
-    double ext[3], vol = 1.0;
-    for (int a = 0; a < 3; ++a) {
-        ext[a] = std::max(mx[a] - mn[a], 1e-9);
-        vol *= ext[a];
-    }
-    double h = std::cbrt(vol * k / (double)n);
-    const double hmin = std::max(std::max(ext[0], ext[1]), ext[2]) / 1.0e6;
-    h = std::max(h, hmin);
+    static const double occ_env = [] {
+        const char* e = std::getenv("OT_SOR_OCC");
+        return e ? std::atof(e) : 0.0;
+    }();
+    const double target = occ_env > 0.0 ? occ_env : std::max(0.7 * k, 2.0);
+    double ext[3];
+    for (int a = 0; a < 3; ++a) ext[a] = std::max(mx[a] - mn[a], 1e-9);
+    std::sort(ext, ext + 3);
+    const double hmin = ext[2] / 5.0e5;
+    double h = std::max(std::sqrt(0.5 * ext[2] * ext[1] * target / (double)n), hmin);
     GridBuild gb;
-    st = build_grid(xyz, n, h, mn, stream, gb);
+    st = build_grid(xyz, n, h, mn, mx, true, stream, gb);
     if (st != OT_OK) return st;
     const double occ = (double)n / (double)std::max<int64_t>(gb.ncells, 1);
-    const double target = std::max(k / 3.0, 2.0);
-    if (occ > 2.0 * target || occ < 0.5 * target) {
+    if (occ > 2.5 * target || occ < 0.4 * target) {
         h = std::max(h * std::sqrt(target / occ), hmin);
-        st = build_grid(xyz, n, h, mn, stream, gb);
+        st = build_grid(xyz, n, h, mn, mx, true, stream, gb);
         if (st != OT_OK) return st;
     }
     char* ws = (char*)scratch((size_t)n * 8 + 1024 * 16 + 256, 12);
@@ -409,10 +566,19 @@ ot_status ot_remove_statistical_outlier(const double* xyz, int64_t n, int32_t nb
     long long* pcount = (long long*)(ws + 64 + 1024 * 8);
     double* avg = out_avg_dist ? out_avg_dist : (double*)(ws + 256 + 1024 * 16);
     const unsigned grid = (unsigned)((n + 255) / 256);
-    if (nb_neighbors <= 32)
-        hipLaunchKernelGGL(k_sor_knn<32>, dim3(grid), dim3(256), 0, stream, gb.g, n, (int)nb_neighbors, avg);
-    else
-        hipLaunchKernelGGL(k_sor_knn<64>, dim3(grid), dim3(256), 0, stream, gb.g, n, (int)nb_neighbors, avg);
+    const int kk = (int)std::min<int64_t>(nb_neighbors, n);  // list length actually needed
+#define OT_SOR_LAUNCH(KM) \
+    hipLaunchKernelGGL(k_sor_knn<KM>, dim3(grid), dim3(256), 0, stream, gb.g, n, (int)nb_neighbors, avg)
+    if (kk <= 4) OT_SOR_LAUNCH(4);
+    else if (kk <= 8) OT_SOR_LAUNCH(8);
+    else if (kk <= 12) OT_SOR_LAUNCH(12);
+    else if (kk <= 16) OT_SOR_LAUNCH(16);
+    else if (kk <= 20) OT_SOR_LAUNCH(20);
+    else if (kk <= 24) OT_SOR_LAUNCH(24);
+    else if (kk <= 32) OT_SOR_LAUNCH(32);
+    else if (kk <= 48) OT_SOR_LAUNCH(48);
+    else OT_SOR_LAUNCH(64);
+#undef OT_SOR_LAUNCH
     const int nb = (int)std::min<int64_t>(1024, (n + 255) / 256);
     hipLaunchKernelGGL(k_sor_partial, dim3(nb), dim3(256), 0, stream, avg, n, 0, stats, partial, pcount);
     hipLaunchKernelGGL(k_sor_final, dim3(1), dim3(256), 0, stream, partial, pcount, nb, 0, std_ratio, stats);

@@ -584,8 +584,8 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
                         float u_f = (nu * rz + p.cx) + 0.5f;
                         float v_f = (nv * rz + p.cy) + 0.5f;
                         const bool sure = !(pc[2] > 0.0f) ||
-                                          ((fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
-                                           (fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
+                                          ((int)(fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
+                                           (int)(fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
                         if (!sure) {
                             u_f = ((nu / pc[2]) + p.cx) + 0.5f;
                             v_f = ((nv / pc[2]) + p.cy) + 0.5f;

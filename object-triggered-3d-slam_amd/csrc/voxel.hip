@@ -8,6 +8,8 @@
 //   5. reduce      : one lane per voxel sums its points in index order and divides by the count — the same
 //                    float64 operation sequence as Open3D's AccumulatedPoint, so averages are bit-exact.
 // Output voxels are in key order (Open3D: unordered_map order; parity compares sorted sets).
+#include <cmath>
+
 #include "compact.h"
 #include "sort.h"
 
@@ -110,10 +112,25 @@ extern "C" ot_status ot_voxel_down_sample(const double* xyz, const double* rgb, 
     unsigned long long* part = (unsigned long long*)scratch(sizeof(unsigned long long) * BOUNDS_BLOCKS * 6, 18);
     if (!part) return fail(OT_ERR_HIP, "scratch allocation failed");
     launch_bounds(xyz, n, b, part, stream);
+    // key width on the host (same float64 formula as k_voxel_keys) so the radix sort runs only the passes the
+    // packed key needs
+    Bounds hb;
+    OT_HIP_TRY(hipMemcpyAsync(&hb, b, sizeof(Bounds), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    int end_bit = 0;
+    for (int a = 0; a < 3; ++a) {
+        const double vmin = ordered_to_dbl(hb.mn[a]) - voxel_size * 0.5;
+        const double vmax = ordered_to_dbl(hb.mx[a]) + voxel_size * 0.5;
+        const double span = std::floor((vmax - vmin) / voxel_size);
+        int bits = 1;
+        while (bits < 62 && span >= std::ldexp(1.0, bits)) ++bits;
+        end_bit += bits;
+    }
+    end_bit = std::min(end_bit, 64);
     hipLaunchKernelGGL(k_voxel_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, xyz, n, voxel_size, b,
                        kin, vin);
     OT_LAUNCH_CHECK();
-    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, 64, stream, 3);
+    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, end_bit, stream, 3);
     if (st != OT_OK) return st;
     int64_t K = 0;
     st = compact(n, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises

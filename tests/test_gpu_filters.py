@@ -133,3 +133,34 @@ def test_occupancy_points_bitexact(pkg, O, gpu):
            C.c_void_p(out.data_ptr()), C.byref(n), None)
     ref = O.occupancy_to_points(img, 100, 0.05, -12.5, -7.25)
     assert_bitwise(out[:n.value].cpu().numpy(), ref, "occupancy points")
+
+
+@pytest.fixture(scope="module")
+def hd_voxels(O, synth, gpu):
+    """configs[2] shape: one 1280x720 frame, unprojected (depth_trunc 5 m) and 5 mm voxel-downsampled."""
+    depth, color, ext = synth.make_sequence(n_frames=16, intr=synth.REF_INTRINSICS_1280, frames=[5])
+    df = O.depth_to_float(depth[0], 1000.0, 5.0)
+    xyz, rgb = O.unproject(df, color[0], synth.REF_INTRINSICS_1280, ext[0])
+    return O.voxel_down_sample(xyz, rgb, 0.005)[0]
+
+
+def test_sor_bench_scale_bitexact(pkg, O, hd_voxels):
+    """The bench's SOR(20, 2.0) on ~270k voxels: mean kNN distances and kept indices bit-exact."""
+    ds = hd_voxels
+    L = pkg._lib
+    d = torch.from_numpy(ds).cuda()
+    idx = torch.empty(ds.shape[0], dtype=torch.int64, device="cuda")
+    avg = torch.empty(ds.shape[0], dtype=torch.float64, device="cuda")
+    n = C.c_int64(0)
+    L.call("ot_remove_statistical_outlier", C.c_void_p(d.data_ptr()), ds.shape[0], 20, 2.0,
+           C.c_void_p(idx.data_ptr()), C.c_void_p(avg.data_ptr()), C.byref(n), None)
+    ridx, ravg = O.remove_statistical_outlier(ds, 20, 2.0)
+    assert_bitwise(avg.cpu().numpy(), ravg, "SOR mean kNN distance (bench scale)")
+    assert_bitwise(idx[:n.value].cpu().numpy(), ridx, "SOR kept indices (bench scale)")
+
+
+def test_ror_bench_scale_bitexact(pkg, O, hd_voxels):
+    ds = hd_voxels
+    out, idx = _pcd(pkg, ds).remove_radius_outlier(16, 0.02)
+    ridx = O.remove_radius_outlier(ds, 16, 0.02)
+    assert_bitwise(np.asarray(idx, np.int64), ridx, "ROR kept (bench scale)")
