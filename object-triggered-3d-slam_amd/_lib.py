@@ -10,7 +10,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libotslam_hip.so")
+# OTSLAM_LIB selects an alternative in-tree build (kernel variants for A/B timing); default: the product library
+LIB_PATH = os.environ.get("OTSLAM_LIB") or os.path.join(_HERE, "libotslam_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "otslam.h")
 
 OT_OK = 0

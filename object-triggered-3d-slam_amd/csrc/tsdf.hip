@@ -41,6 +41,7 @@ struct IntegrateParams {
     float E[12];
     float es0, es1, es2;
     float vl, half, trunc, trunc_inv, safe_w, safe_h;
+    float inv_fx, inv_fy;  // (float)(1 / (float)fx) as CreateDepthToCameraDistanceMultiplierFloatImage
     float proj_eps;  // certified fast projection: |u - rint(u)| > proj_eps decides floor and bounds exactly
     double unit_len;
 };
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
 // as in Open3D, so every slice reproduces the single-lane z walk bit for bit.  Waves never synchronise: the
 // unit header (id, key, frame mask) is resolved once by k_batch_units and read with scalar loads.
 #ifndef OT_BZ
-#define OT_BZ 8
+#define OT_BZ 4
 #endif
 constexpr int BZ = OT_BZ;                     // voxels per lane along z
 constexpr int SLICES = 4 * (UNIT_RES / BZ);   // waves per unit
@@ -521,8 +522,13 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
             if (ent != -1) {
                 const int id = ent & 0x7FFFFFFF;
                 const bool fresh = ent < 0;
+#ifndef OT_MAP416  // wave = 8 x 8 columns: a square patch of the unit's xy plane projects to fewer pixel rows
+                const int x = (s & 2) * 4 + (lane >> 3), y = (s & 1) * 8 + (lane & 7);
+                const int col = x * 16 + y;
+#else  // wave = 4 x 16 columns (4 whole x rows: 1-KiB coalesced state rows)
                 const int col = (s & 3) * 64 + lane;
                 const int x = col >> 4, y = col & 15;
+#endif
                 const int z0 = (s >> 2) * BZ;
                 float* base = d.vox + (size_t)id * UNIT_FLOATS;
                 float ts[BZ], wt[BZ], cr[BZ], cg[BZ], cb[BZ];
@@ -603,66 +609,50 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
                         pc[1] += es1;
                         pc[2] += es2;
                     }
-                    // phase B: all gathers issued before any use (buffer loads: wave-uniform resource + 32-bit
-                    // byte offset, no per-lane 64-bit address math)
-                    float2 dmv[BZ];
-                    uint32_t cv[BZ];
+                    // phase B: every depth gather issued before any use (buffer loads: wave-uniform resource +
+                    // 32-bit byte offset, no per-lane 64-bit address math)
+                    float dv[BZ], mv[BZ];
 #pragma unroll
                     for (int k = 0; k < BZ; ++k) {
                         const int qx = pixv[k] < 0 ? 0 : pixv[k];
-#ifdef OT_ABL_NOGATHER  // timing-only ablation build: no frame gathers (results are wrong)
-                        dmv[k] = make_float2(pcz[k] + 0.01f * (float)(qx & 7), 1.0f);
-                        cv[k] = (unsigned)qx;
-#else
                         const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, qx * 8, 0, 0);
-                        dmv[k] = make_float2(__uint_as_float(raw.x), __uint_as_float(raw.y));
-                        cv[k] = use_color ? __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, qx * 4, 0, 0) : 0u;
-#endif
+                        dv[k] = __uint_as_float(raw.x);
+                        mv[k] = __uint_as_float(raw.y);
                     }
-                    // phase C: updates in frame order
+                    // phase C: the depth test; colour gathered only by the lanes whose voxel updates
+                    bool doitv[BZ];
+                    float sdfv[BZ];
+                    uint32_t cv[BZ];
 #pragma unroll
                     for (int k = 0; k < BZ; ++k) {
-#ifndef OT_BRANCHY  // select form (default): identical values, no exec-mask branches
-                        const float sdf = (dmv[k].x - pcz[k]) * dmv[k].y;
-                        const bool doit = (pixv[k] >= 0) & (dmv[k].x > 0.0f) & (sdf > -p.trunc);
-                        {
-#else
-                        if (pixv[k] >= 0 && dmv[k].x > 0.0f) {
-                            const float sdf = (dmv[k].x - pcz[k]) * dmv[k].y;
-                            const bool doit = sdf > -p.trunc;
-                            if (doit) {
-#endif
-                                const float sv = sdf * p.trunc_inv;
-                                const float tn = (sv < 1.0f) ? sv : 1.0f;
-                                const float wv = wt[k];
-                                const float w1 = wv + 1.0f;
-#ifdef OT_ABL_FASTDIV  // timing-only: tsdf division via reciprocal (not bit-exact)
-                                const float tsn = (ts[k] * wv + tn) * __builtin_amdgcn_rcpf(w1);
-#else
-                                const float tsn = (ts[k] * wv + tn) / w1;  // exact IEEE quotient: tsdf bit-exact
-#endif
-                                ts[k] = doit ? tsn : ts[k];
-#ifdef OT_ABL_NOCOLOR
-                                if (false) {
-#else
-                                if (use_color) {
-#endif
-                                    // colour running mean: one hardware reciprocal (1 ulp) for the three
-                                    // channels — within the 1e-4 colour contract (Open3D keeps colour in f64)
-                                    const float rw = __builtin_amdgcn_rcpf(w1);
-                                    const float nr = (cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
-                                    const float ng = (cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
-                                    const float nb = (cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
-                                    cr[k] = doit ? nr : cr[k];
-                                    cg[k] = doit ? ng : cg[k];
-                                    cb[k] = doit ? nb : cb[k];
-                                }
-                                wt[k] = doit ? w1 : wv;
-                                upd += doit ? 1u : 0u;
-#ifdef OT_BRANCHY
-                            }
-#endif
+                        sdfv[k] = (dv[k] - pcz[k]) * mv[k];
+                        doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
+                        cv[k] = 0u;
+                        if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
+                    }
+                    // phase D: updates in frame order (select form: identical values, no exec-mask branches)
+#pragma unroll
+                    for (int k = 0; k < BZ; ++k) {
+                        const bool doit = doitv[k];
+                        const float sv = sdfv[k] * p.trunc_inv;
+                        const float tn = (sv < 1.0f) ? sv : 1.0f;
+                        const float wv = wt[k];
+                        const float w1 = wv + 1.0f;
+                        const float tsn = (ts[k] * wv + tn) / w1;  // exact IEEE quotient: tsdf bit-exact
+                        ts[k] = doit ? tsn : ts[k];
+                        if (use_color) {
+                            // colour running mean: one reciprocal for the three channels — within the 1e-4 colour
+                            // contract (Open3D keeps colour in f64)
+                            const float rw = __builtin_amdgcn_rcpf(w1);
+                            const float nr = (cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
+                            const float ng = (cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
+                            const float nb = (cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                            cr[k] = doit ? nr : cr[k];
+                            cg[k] = doit ? ng : cg[k];
+                            cb[k] = doit ? nb : cb[k];
                         }
+                        wt[k] = doit ? w1 : wv;
+                        upd += doit ? 1u : 0u;
                     }
                 }
 #ifdef OT_ABL_NOSTATE  // keep every result live without storing it
@@ -727,6 +717,8 @@ static IntegrateParams make_integrate_params(const ot_tsdf* vol, const float* de
     p.fy = (float)in->fy;
     p.cx = (float)in->cx;
     p.cy = (float)in->cy;
+    p.inv_fx = 1.0f / (float)in->fx;
+    p.inv_fy = 1.0f / (float)in->fy;
     float E[16];
     for (int k = 0; k < 16; ++k) E[k] = (float)ext[k];
     for (int k = 0; k < 12; ++k) p.E[k] = E[k];

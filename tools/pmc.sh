@@ -3,7 +3,7 @@
 # FETCH_SIZE and WRITE_SIZE cannot share a pass; no --sys-trace with --pmc).  Output: gpurun_out/pmc_<i>/.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
-ARGS=${BENCH_ARGS:-"--steps 1 --warmup 0 --cpu-frames 0 --calib"}
+ARGS=${BENCH_ARGS:-"--steps 1 --warmup 0 --cpu-frames 0 --filter-frames 0 --calib"}
 i=0
 for pass in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES" \
             "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do

@@ -1,9 +1,21 @@
 #!/bin/bash
-# Build-and-bench kernel variants on the GPU box: each entry is "<name>|<extra hipcc flags>".
+# Build kernel variants HERE (CPU container):  tools/variants.sh build "<name>|<extra hipcc flags>" ...
+#   -> object-triggered-3d-slam_amd/variants/libotslam_<name>.so
+# Time them on the GPU box:                    tools/variants.sh bench <name> ...
+#   (each: the TSDF parity tests against that library, then the bench line; OTSLAM_LIB selects the library)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-for v in "$@"; do
-  name=${v%%|*}; flags=${v#*|}
-  make -C object-triggered-3d-slam_amd/csrc clean > /dev/null && make -j16 -C object-triggered-3d-slam_amd/csrc EXTRA="$flags" > gpurun_out/build_$name.log 2>&1 || { echo "$name build failed"; continue; }
-  timeout -k 10 200 python3 bench.py --steps 3 --warmup 1 --cpu-frames 0 > gpurun_out/bench_$name.log 2>&1 || { echo "$name bench failed"; tail -3 gpurun_out/bench_$name.log; break; }
-  python3 -c "import json,sys;d=json.loads(open('gpurun_out/bench_$name.log').read().strip().splitlines()[-1]);r=d['roofline'];print('$name', d['value'], d['ms_per_step'], r['kernel_ms_avg'], r['launches_per_step'])"
+mode=$1; shift
+if [ "$mode" = build ]; then
+  for v in "$@"; do
+    name=${v%%|*}; flags=${v#*|}
+    make -j8 -C object-triggered-3d-slam_amd/csrc OUT=../variants/libotslam_$name.so BUILD=build_$name EXTRA="$flags" > /tmp/build_$name.log 2>&1 || { echo "$name build failed"; tail /tmp/build_$name.log; }
+  done
+  exit 0
+fi
+for name in "$@"; do
+  lib=$PWD/object-triggered-3d-slam_amd/variants/libotslam_$name.so
+  [ "$name" = base ] && lib=$PWD/object-triggered-3d-slam_amd/libotslam_hip.so
+  OTSLAM_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_tsdf.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/vtest_$name.log 2>&1 || { echo "$name TESTS FAILED"; tail -20 gpurun_out/vtest_$name.log; exit 1; }
+  OTSLAM_LIB=$lib timeout -k 10 200 python3 bench.py --steps 5 --warmup 1 --cpu-frames 0 --filter-frames 0 > gpurun_out/vbench_$name.log 2>&1 || { echo "$name bench failed"; tail -3 gpurun_out/vbench_$name.log; exit 1; }
+  python3 -c "import json;d=json.loads(open('gpurun_out/vbench_$name.log').read().strip().splitlines()[-1]);r=d['roofline'];print('$name', d['value'], d['ms_per_step'], r['kernel_ms_avg'], r['launches_per_step'])"
 done
