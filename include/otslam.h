@@ -105,6 +105,12 @@ ot_status ot_filter_min_z(const double* xyz, const double* rgb, int64_t n, doubl
 /* Gather rows: out[k] = in[idx[k]] for k < m (PointCloud.select_by_index / SelectByIndex). */
 ot_status ot_gather_rows3(const double* in, const int64_t* idx, int64_t m, double* out, void* stream);
 
+/* geometry.PointCloud.compute_point_cloud_distance(target) — eval_cone.py:99,103 (accuracy / completeness).
+ * out[i] = sqrt(min_j |src_i - tgt_j|^2) in float64 (exact minimum, nanoflann L2 accumulation order);
+ * 0.0 for every point when the target is empty (Open3D: no neighbour found). */
+ot_status ot_compute_point_cloud_distance(const double* src, int64_t n, const double* tgt, int64_t m,
+                                          double* out, void* stream);
+
 /* ---------------------------------------------------------------------------------------------------
  * Scalable TSDF volume — pipelines.integration.ScalableTSDFVolume (reconstruct_rgbd_filter.py:81-85)
  * ------------------------------------------------------------------------------------------------- */
@@ -188,6 +194,50 @@ ot_status ot_mesh_sample_points_uniformly(const double* vertices, const double* 
 ot_status ot_occupancy_to_points(const uint8_t* img, int32_t height, int32_t width, int32_t threshold,
                                  double resolution, double origin_x, double origin_y, double* out_xyz,
                                  int64_t* n_out_host, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------
+ * Change detection against a saved map (BASELINE configs[4])
+ * ------------------------------------------------------------------------------------------------- */
+
+/* 2d_selective_merge.py:58-69 smart_paste(base_img, overlay_img, x, y, w, h), in place on device uint8
+ * [height][width] grids: inside the rectangle, cells of `overlay` outside [unknown - threshold,
+ * unknown + threshold] (205 ± 5 in the reference) overwrite `base`.  A rectangle reaching outside the image
+ * leaves `base` unchanged (:59-60).  n_changed_host (optional) = cells whose value changed. */
+ot_status ot_grid_smart_paste(uint8_t* base, const uint8_t* overlay, int32_t height, int32_t width, int32_t x,
+                              int32_t y, int32_t w, int32_t h, int32_t unknown, int32_t threshold,
+                              int64_t* n_changed_host, void* stream);
+
+/* Voxel-key set difference of a new cloud against a saved cloud on the lattice floor((p - origin) / voxel_size)
+ * (origin: host double[3]).  out_added = keys of `new` absent from `old`, out_removed = keys of `old` absent
+ * from `new`, each int32 [k][3] sorted lexicographically (capacity: the cloud's point count). */
+ot_status ot_voxel_key_diff(const double* new_xyz, int64_t n, const double* old_xyz, int64_t m, double voxel_size,
+                            const double origin[3], int32_t* out_added, int64_t* n_added_host,
+                            int32_t* out_removed, int64_t* n_removed_host, void* stream);
+
+/* diff_node.cpp:103-160 ChangeDetectorNode::scanCallback, batched: n_scans pairs of float ranges
+ * [n_scans][n_beams] (real scan, virtual scan of the saved map).  Per beam: new_flags = a real return with no
+ * virtual return within +-search_window beams closer than distance_threshold; gone_flags = the converse.
+ * Flagged beams are moved to the map frame with poses_host[n_scans][7] = (tx, ty, tz, qx, qy, qz, qw) and
+ * binned to (int)(p / grid_resolution) cells (int32 [n_scans][n_beams][2]; 0 where not flagged). */
+ot_status ot_scan_diff(const float* real_ranges, const float* virtual_ranges, int32_t n_scans, int32_t n_beams,
+                       float real_angle_min, float real_angle_increment, float real_range_max,
+                       float virtual_angle_min, float virtual_angle_increment, double distance_threshold,
+                       int32_t search_window, const double* poses_host, double grid_resolution, uint8_t* new_flags,
+                       uint8_t* gone_flags, int32_t* new_keys, int32_t* gone_keys, void* stream);
+
+/* diff_node.cpp:163-185 updateGrid / :188-222 publishCloud: time-decayed evidence grid (host state). */
+typedef struct ot_change_grid ot_change_grid;
+ot_status ot_change_grid_create(double time_threshold, double decay_rate, double grid_resolution,
+                                ot_change_grid** out);
+ot_status ot_change_grid_destroy(ot_change_grid* grid);
+/* one scan: cells of the flagged beams (host keys [n][2], flags [n]) += dt (capped at 1.5 time_threshold);
+ * all other cells -= decay_rate * dt; cells at <= 0 are erased. */
+ot_status ot_change_grid_update(ot_change_grid* grid, const int32_t* keys_host, const uint8_t* flags_host,
+                                int64_t n, double dt);
+/* cells above time_threshold as float32 (x*res + res/2, y*res + res/2, 0), sorted by (x, y); out may be NULL
+ * to query the count. */
+ot_status ot_change_grid_publish(const ot_change_grid* grid, float* out_xyz_host, int64_t capacity,
+                                 int64_t* n_host);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,7 @@ switches with one line:
 
 Every compute call goes through the C ABI in include/otslam.h (libotslam_hip.so, HIP kernels for gfx950).
 """
-from . import camera, geometry, io, pipelines, utility  # noqa: F401
+from . import camera, change_detection, geometry, io, pipelines, utility  # noqa: F401
 from ._lib import LIB_PATH, OTError  # noqa: F401
 
 __version__ = "0.1.0"

@@ -47,6 +47,7 @@ SIGNATURES = {
     "ot_voxel_down_sample": [_p, _p, _p, _i64, _d, _p, _p, _p, _p, _pi64, _p],
     "ot_remove_statistical_outlier": [_p, _i64, _i32, _d, _p, _p, _pi64, _p],
     "ot_remove_radius_outlier": [_p, _i64, _i32, _d, _p, _pi64, _p],
+    "ot_compute_point_cloud_distance": [_p, _i64, _p, _i64, _p, _p],
     "ot_filter_min_z": [_p, _p, _i64, _d, _p, _p, _pi64, _p],
     "ot_gather_rows3": [_p, _p, _i64, _p, _p],
     "ot_tsdf_create": [_d, _d, _i32, _i32, _i32, _i64, C.POINTER(_p)],
@@ -66,6 +67,14 @@ SIGNATURES = {
     "ot_mesh_compute_vertex_normals": [_p, _i64, _p, _i64, _p, _p],
     "ot_mesh_sample_points_uniformly": [_p, _p, _p, _i64, _p, _i64, _i64, C.c_uint64, _p, _p, _p, _p],
     "ot_occupancy_to_points": [_p, _i32, _i32, _i32, _d, _d, _d, _p, _pi64, _p],
+    "ot_grid_smart_paste": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _pi64, _p],
+    "ot_voxel_key_diff": [_p, _i64, _p, _i64, _d, _p, _p, _pi64, _p, _pi64, _p],
+    "ot_scan_diff": [_p, _p, _i32, _i32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, _d, _i32, _p, _d,
+                     _p, _p, _p, _p, _p],
+    "ot_change_grid_create": [_d, _d, _d, C.POINTER(_p)],
+    "ot_change_grid_destroy": [_p],
+    "ot_change_grid_update": [_p, _p, _p, _i64, _d],
+    "ot_change_grid_publish": [_p, _p, _i64, _pi64],
 }
 _RESTYPES = {"ot_last_error": C.c_char_p, "ot_version": C.c_char_p, "ot_abi_version": C.c_int32}
 

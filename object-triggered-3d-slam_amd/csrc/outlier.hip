@@ -306,6 +306,99 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     avg[g.sidx[j]] = cnt > 0 ? s / (double)cnt : -1.0;
 }
 
+// ------------------------------------------------------------------------------------ cross-cloud 1-NN distance
+// PointCloud::ComputePointCloudDistance (eval_cone.py:99,103): per source point the distance to its nearest target
+// point, sqrt of the exact float64 squared distance.  The grid is built over the target.  A query inside the
+// target's bounding box whose cell is occupied runs the SOR stages (3x3x3 then 5x5x5 block of its cell); any other
+// query expands Chebyshev rings around the cell of q' = clamp(q, box).  For every target point p (inside the box)
+// |q - p|^2 >= |q - q'|^2 + |q' - p|^2, so the ring guard of q' plus |q - q'|^2 bounds every unscanned point.
+constexpr int NN_RMAX = 6;
+
+__device__ inline int2 grid_cell_range(const GridDev& g, int x, int y, int z, int& cell) {
+    const int2 se = grid_find(g, x, y, z);
+    cell = se.y > se.x ? g.pcell[se.x] : -1;
+    return se;
+}
+
+__device__ inline void nn_range(const GridDev& g, const double q[3], int beg, int end, double& best) {
+    for (int m = beg; m < end; ++m) best = fmin(best, d2_l2(q, g.sxyz + (int64_t)m * 3));
+}
+
+__global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __restrict__ src, int64_t n, int64_t m,
+                                                 double mnx, double mny, double mnz, double mxx, double mxy,
+                                                 double mxz, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double q[3] = {src[i * 3], src[i * 3 + 1], src[i * 3 + 2]};
+    const double lo[3] = {mnx, mny, mnz}, hi[3] = {mxx, mxy, mxz};
+    double qc[3], off2 = 0.0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        qc[a] = fmin(fmax(q[a], lo[a]), hi[a]);
+        const double dd = q[a] - qc[a];
+        off2 += dd * dd;
+    }
+    // lower bound used only for the stopping test: shave a relative margin off the exact-arithmetic bound
+    off2 *= (1.0 - 1e-9);
+    double best = INFINITY;
+    bool settled = false;
+    const int cx = cell_coord(qc[0], g.origin[0], g.h), cy = cell_coord(qc[1], g.origin[1], g.h),
+              cz = cell_coord(qc[2], g.origin[2], g.h);
+    if (off2 == 0.0) {
+        int c;
+        grid_cell_range(g, cx, cy, cz, c);
+        if (c >= 0) {
+            const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
+            for (int u = 0; u < NBR3; ++u) {
+                const int2 se = r3[(u + 4) % NBR3];
+                nn_range(g, q, se.x, se.y, best);
+            }
+            double guard = block_guard(g, q, 1.0);
+            settled = best <= guard * guard;
+            if (!settled) {
+                const int2* r5 = g.nbr5 + (int64_t)c * NBR5;
+                for (int t = 0; t < NBR5; ++t) {
+                    const int dx = t / 5 - 2, dy = t % 5 - 2;
+                    const int2 o = r5[t];
+                    if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1) {
+                        const int2 i3 = r3[(dx + 1) * 3 + (dy + 1)];
+                        if (i3.y > i3.x) {
+                            nn_range(g, q, o.x, i3.x, best);
+                            nn_range(g, q, i3.y, o.y, best);
+                            continue;
+                        }
+                    }
+                    nn_range(g, q, o.x, o.y, best);
+                }
+                guard = block_guard(g, q, 2.0);
+                settled = best <= guard * guard;
+            }
+        }
+    }
+    if (!settled) {
+        best = INFINITY;
+        long long have = 0;
+        for (int r = 0; r <= NN_RMAX && !settled; ++r) {
+            for (int dx = -r; dx <= r; ++dx)
+                for (int dy = -r; dy <= r; ++dy) {
+                    const bool face = (dx == -r || dx == r || dy == -r || dy == r);
+                    for (int dz = -r; dz <= r; dz += (face || r == 0) ? 1 : 2 * r) {
+                        const int2 se = grid_find(g, cx + dx, cy + dy, cz + dz);
+                        nn_range(g, q, se.x, se.y, best);
+                        have += se.y - se.x;
+                    }
+                }
+            const double guard = (r > 0 ? (double)r - 0.01 : 0.0) * g.h;
+            if (have >= m || (have > 0 && best <= off2 + guard * guard)) settled = true;
+        }
+        if (!settled) {
+            best = INFINITY;
+            nn_range(g, q, 0, (int)m, best);
+        }
+    }
+    out[i] = sqrt(best);
+}
+
 // fixed-order two-level reduction: blocks reduce contiguous chunks in a fixed tree, then one block reduces
 // the block partials in the same fixed order.  mode 0: sum of avg > 0 and count; mode 1: sum of (avg-mean)^2
 __global__ __launch_bounds__(256) void k_sor_partial(const double* __restrict__ avg, int64_t n, int mode,
@@ -586,6 +679,45 @@ ot_status ot_remove_statistical_outlier(const double* xyz, int64_t n, int32_t nb
     hipLaunchKernelGGL(k_sor_final, dim3(1), dim3(256), 0, stream, partial, pcount, nb, 1, std_ratio, stats);
     OT_LAUNCH_CHECK();
     return compact(n, SorPred{avg, stats}, IndexEmit{out_indices}, stream, n_kept_host, 13);
+}
+
+
+ot_status ot_compute_point_cloud_distance(const double* src, int64_t n, const double* tgt, int64_t m, double* out,
+                                          void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (n < 0 || m < 0) return fail(OT_ERR_INVALID_ARGUMENT, "[ComputePointCloudDistance] negative size");
+    if (n == 0) return OT_OK;
+    if (!src || !out || (m > 0 && !tgt) || n > 0x7FFFFFFF || m > 0x7FFFFFFF)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ComputePointCloudDistance] invalid buffers");
+    if (m == 0) {  // Open3D: no neighbour found -> 0.0
+        OT_HIP_TRY(hipMemsetAsync(out, 0, sizeof(double) * (size_t)n, stream));
+        OT_HIP_TRY(hipStreamSynchronize(stream));
+        return OT_OK;
+    }
+    double mn[3], mx[3];
+    ot_status st = bounds_host(tgt, m, stream, mn, mx);
+    if (st != OT_OK) return st;
+    // ~4 target points per occupied cell of a surface-like cloud (the grid only changes speed)
+    double ext[3];
+    for (int a = 0; a < 3; ++a) ext[a] = std::max(mx[a] - mn[a], 1e-9);
+    std::sort(ext, ext + 3);
+    const double target = 4.0;
+    const double hmin = ext[2] / 5.0e5;
+    double h = std::max(std::sqrt(0.5 * ext[2] * ext[1] * target / (double)m), hmin);
+    GridBuild gb;
+    st = build_grid(tgt, m, h, mn, mx, true, stream, gb);
+    if (st != OT_OK) return st;
+    const double occ = (double)m / (double)std::max<int64_t>(gb.ncells, 1);
+    if (occ > 2.5 * target || occ < 0.4 * target) {
+        h = std::max(h * std::sqrt(target / occ), hmin);
+        st = build_grid(tgt, m, h, mn, mx, true, stream, gb);
+        if (st != OT_OK) return st;
+    }
+    hipLaunchKernelGGL(k_nn_dist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, gb.g, src, n, m, mn[0],
+                       mn[1], mn[2], mx[0], mx[1], mx[2], out);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
 }
 
 }  // extern "C"

@@ -13,7 +13,7 @@ import numpy as np
 
 from . import _device as D
 from . import _lib as L
-from .utility import Vector3dVector, Vector3iVector
+from .utility import DoubleVector, Vector3dVector, Vector3iVector
 
 
 class _Arr:
@@ -329,6 +329,17 @@ class PointCloud:
                C.byref(k), D.stream_ptr())
         idx = idx[:k.value]
         return self._select_dev(idx), D.to_host(idx).tolist()
+
+    def compute_point_cloud_distance(self, target):
+        """PointCloud::ComputePointCloudDistance (eval_cone.py:99,103) — ot_compute_point_cloud_distance.
+        Per point of self: distance to the nearest point of `target` (float64); 0.0 when target is empty."""
+        n, m = len(self._xyz), len(target._xyz)
+        if n == 0:
+            return DoubleVector()
+        out = D.empty((n,), "float64")
+        L.call("ot_compute_point_cloud_distance", D.ptr(self._xyz.dev()), n,
+               D.ptr(target._xyz.dev()) if m else None, m, D.ptr(out), D.stream_ptr())
+        return DoubleVector(D.to_host(out))
 
     def _select_dev(self, idx):
         out = PointCloud()

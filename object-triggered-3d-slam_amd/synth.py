@@ -174,3 +174,74 @@ def write_dataset(base_dir: str, label: str, depth, color, poses_ros, start_inde
 
 def ros_poses(scene: Scene, n_frames: int) -> np.ndarray:
     return np.stack([camera_pose(scene, k, n_frames) @ np.linalg.inv(T_FIX) for k in range(n_frames)])
+
+
+# ------------------------------------------------------------------------------------ 2-D laser scans (diff_node)
+def _segments_of_boxes(boxes):
+    segs = []
+    for (x0, y0, x1, y1) in boxes:
+        segs += [(x0, y0, x1, y0), (x1, y0, x1, y1), (x1, y1, x0, y1), (x0, y1, x0, y0)]
+    return np.array(segs, np.float64).reshape(-1, 4)
+
+
+def _raycast(px, py, angles, segs, range_max):
+    """Nearest hit distance of rays from (px, py) at map angles against segments; inf when none <= range_max."""
+    dx, dy = np.cos(angles)[:, None], np.sin(angles)[:, None]
+    x0, y0, x1, y1 = (segs[:, k][None, :] for k in range(4))
+    ex, ey = x1 - x0, y1 - y0
+    den = dx * ey - dy * ex
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = ((x0 - px) * ey - (y0 - py) * ex) / den
+        u = ((x0 - px) * dy - (y0 - py) * dx) / den
+    ok = (np.abs(den) > 1e-12) & (t > 0) & (u >= 0) & (u <= 1)
+    t = np.where(ok, t, np.inf).min(axis=1)
+    return np.where(t <= range_max, t, np.inf)
+
+
+def laser_scan_batch(n_scans=32, n_beams=720, seed=0, range_max=12.0):
+    """Scan pairs for the change detector: the saved map (a 10 m x 8 m room with pillars) rendered as the virtual
+    scan, and the current world (one pillar removed, two boxes added, 1 cm range noise, a few NaN returns) as the
+    real scan, from a robot driving a loop.  Returns (real [B][N] f32, virtual [B][N] f32, poses [B][7] (tx ty tz
+    qx qy qz qw), dts [B], angle_min, angle_increment, range_max)."""
+    rng = np.random.default_rng(seed)
+    room = [(-5.0, -4.0, 5.0, 4.0)]
+    pillars = [(-2.2, -1.2, -1.8, -0.8), (1.8, 0.8, 2.2, 1.2), (-0.3, 2.0, 0.3, 2.6)]
+    added = [(0.5, -2.5, 1.3, -1.9), (-3.5, 1.0, -2.9, 1.8)]
+    saved = _segments_of_boxes(room + pillars)
+    world = _segments_of_boxes(room + pillars[1:] + added)
+    amin, ainc = -np.pi, 2 * np.pi / n_beams
+    beam = (np.float32(amin) + np.arange(n_beams, dtype=np.float32) * np.float32(ainc)).astype(np.float64)
+    real = np.empty((n_scans, n_beams), np.float32)
+    virt = np.empty((n_scans, n_beams), np.float32)
+    poses = np.zeros((n_scans, 7), np.float64)
+    for b in range(n_scans):
+        th = 2 * np.pi * b / n_scans
+        px, py, yaw = 3.0 * np.cos(th), 2.2 * np.sin(th), th + np.pi / 2
+        virt[b] = _raycast(px, py, beam + yaw, saved, range_max)
+        r = _raycast(px, py, beam + yaw, world, range_max)
+        r = r + np.where(np.isfinite(r), rng.normal(0, 0.01, n_beams), 0.0)
+        r[rng.random(n_beams) < 0.003] = np.nan
+        real[b] = r
+        poses[b] = (px, py, 0.0, 0.0, 0.0, np.sin(yaw / 2), np.cos(yaw / 2))
+    dts = np.full(n_scans, 0.1) + rng.uniform(0, 0.02, n_scans)
+    return real, virt, poses, dts, float(np.float32(amin)), float(np.float32(ainc)), float(range_max)
+
+
+def occupancy_pair(h=1024, w=1024, seed=0):
+    """A saved occupancy grid (PGM convention: 0 occupied, 254 free, 205 unknown) and a newer grid of the same area
+    with moved obstacles, newly explored free space and unknown cells — the two maps of 2d_selective_merge.py."""
+    rng = np.random.default_rng(seed)
+    old = np.full((h, w), 205, np.uint8)
+    old[h // 8: 7 * h // 8, w // 8: 7 * w // 8] = 254
+    for _ in range(40):
+        r, c = rng.integers(h // 8, 7 * h // 8 - 20, 2)
+        old[r:r + rng.integers(4, 20), c:c + rng.integers(4, 20)] = 0
+    new = old.copy()
+    new[: h // 4, :] = 205                                   # not re-observed
+    new[7 * h // 8:, w // 4: 3 * w // 4] = 254               # newly explored
+    for _ in range(25):
+        r, c = rng.integers(h // 4, 7 * h // 8 - 20, 2)
+        new[r:r + rng.integers(4, 20), c:c + rng.integers(4, 20)] = rng.choice([0, 254])
+    noise = rng.random((h, w)) < 0.01
+    new[noise] = rng.integers(195, 216, int(noise.sum()))   # values around the unknown band edges
+    return old, new

@@ -61,6 +61,13 @@ class IntVector(list):
     pass
 
 
+class DoubleVector(np.ndarray):
+    """open3d.utility.DoubleVector: a float64 vector (numpy view; np.mean / np.asarray work unchanged)."""
+
+    def __new__(cls, data=()):
+        return np.ascontiguousarray(np.asarray(data, dtype=np.float64).reshape(-1)).view(cls)
+
+
 class VerbosityLevel:
     Error = 0
     Warning = 1

@@ -57,6 +57,10 @@ def lib():
             "oro_remove_statistical_outlier": (_i64, [_p, _i64, _i32, _d, _p, _p]),
             "oro_remove_radius_outlier": (_i64, [_p, _i64, _i32, _d, _p]),
             "oro_occupancy_to_points": (_i64, [_p, _i32, _i32, _i32, _d, _d, _d, _p]),
+            "oro_point_cloud_distance": (None, [_p, _i64, _p, _i64, _p]),
+            "oro_scan_diff": (None, [_p, _p, _i32, _i32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, _d,
+                                     _i32, _p, _d, _p, _p, _p, _p]),
+            "oro_change_grid_run": (_i64, [_p, _p, _i32, _i32, _p, _d, _d, _d, _p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -227,3 +231,65 @@ def occupancy_to_points(img, threshold, res, ox, oy):
     out = np.empty((h * w, 3), np.float64)
     k = lib().oro_occupancy_to_points(_ptr(im), h, w, threshold, res, ox, oy, _ptr(out))
     return out[:k].copy()
+
+
+def point_cloud_distance(src, tgt):
+    """PointCloud.compute_point_cloud_distance (eval_cone.py:99,103): exhaustive float64 1-NN distances."""
+    a = _c(src, np.float64).reshape(-1, 3)
+    b = _c(tgt, np.float64).reshape(-1, 3)
+    out = np.empty(max(a.shape[0], 1), np.float64)
+    lib().oro_point_cloud_distance(_ptr(a), a.shape[0], _ptr(b), b.shape[0], _ptr(out))
+    return out[:a.shape[0]].copy()
+
+
+def smart_paste(base_img, overlay_img, x, y, w, h, unknown=205, threshold=5):
+    """2d_selective_merge.py:58-69 restated with numpy (returns a new array; out-of-image rectangle: unchanged)."""
+    out = np.array(base_img, dtype=np.uint8, copy=True)
+    hi_, wi_ = out.shape
+    if x < 0 or y < 0 or x + w > wi_ or y + h > hi_:
+        return out
+    new = np.asarray(overlay_img, dtype=np.uint8)[y:y + h, x:x + w].astype(np.int64)
+    known = (new < unknown - threshold) | (new > unknown + threshold)
+    roi = out[y:y + h, x:x + w]
+    roi[known] = new[known].astype(np.uint8)
+    return out
+
+
+def voxel_key_diff(new_xyz, old_xyz, voxel_size, origin):
+    """Lattice-key set difference: (keys of new absent from old, keys of old absent from new), each sorted."""
+    def keys(p):
+        p = np.asarray(p, np.float64).reshape(-1, 3)
+        k = np.floor((p - np.asarray(origin, np.float64)) / voxel_size).astype(np.int64)
+        return np.unique(k, axis=0) if len(k) else np.zeros((0, 3), np.int64)
+
+    a, b = keys(new_xyz), keys(old_xyz)
+    sa = {tuple(r) for r in a.tolist()}
+    sb = {tuple(r) for r in b.tolist()}
+    added = np.array(sorted(sa - sb), np.int64).reshape(-1, 3)
+    removed = np.array(sorted(sb - sa), np.int64).reshape(-1, 3)
+    return added.astype(np.int32), removed.astype(np.int32)
+
+
+def scan_diff(real, virt, r_amin, r_inc, r_max, v_amin, v_inc, thresh, window, poses, grid_res):
+    """diff_node.cpp:103-160 per beam of a batch of scans (see otslam_oracle.cpp)."""
+    R = _c(real, np.float32)
+    V = _c(virt, np.float32)
+    B, N = R.shape
+    P = _c(poses, np.float64).reshape(B, 7)
+    nf, gf = np.zeros((B, N), np.uint8), np.zeros((B, N), np.uint8)
+    nk, gk = np.zeros((B, N, 2), np.int32), np.zeros((B, N, 2), np.int32)
+    lib().oro_scan_diff(_ptr(R), _ptr(V), B, N, r_amin, r_inc, r_max, v_amin, v_inc, thresh, window, _ptr(P),
+                        grid_res, _ptr(nf), _ptr(gf), _ptr(nk), _ptr(gk))
+    return nf, gf, nk, gk
+
+
+def change_grid_run(keys, flags, dts, time_thresh, decay_rate, grid_res):
+    """updateGrid over the scans in order, then publishCloud's cells (float32 [k][3], sorted by (x, y))."""
+    K = _c(keys, np.int32)
+    F = _c(flags, np.uint8)
+    B, N = F.shape
+    D = _c(dts, np.float64)
+    n = lib().oro_change_grid_run(_ptr(K), _ptr(F), B, N, _ptr(D), time_thresh, decay_rate, grid_res, None)
+    out = np.zeros((max(n, 1), 3), np.float32)
+    lib().oro_change_grid_run(_ptr(K), _ptr(F), B, N, _ptr(D), time_thresh, decay_rate, grid_res, _ptr(out))
+    return out[:n].copy()

@@ -737,6 +737,130 @@ int64_t oro_remove_radius_outlier(const double* xyz, int64_t n, int nb_points, d
     return kept;
 }
 
+/* PointCloud::ComputePointCloudDistance (eval_cone.py:99,103): per source point sqrt of the minimum squared
+ * distance to the target (KDTreeFlann SearchKNN(1); nanoflann L2 order), 0.0 when the target is empty.
+ * Exhaustive minimum (the search structure does not change the minimum); OpenMP over points as Open3D. */
+void oro_point_cloud_distance(const double* src, int64_t n, const double* tgt, int64_t m, double* out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        if (m == 0) {
+            out[i] = 0.0;
+            continue;
+        }
+        double best = INFINITY;
+        for (int64_t j = 0; j < m; ++j) best = std::min(best, dist2(src + i * 3, tgt + j * 3));
+        out[i] = std::sqrt(best);
+    }
+}
+
+/* ChangeDetectorNode::scanCallback (diff_node.cpp:103-160) for a batch of scan pairs, written as the node does it
+ * (float beam geometry with std::cos / std::sin / std::hypot on floats, double map transform from the
+ * quaternion, C++ truncation to grid cells).  poses [n_scans][7] = tx ty tz qx qy qz qw. */
+void oro_scan_diff(const float* real, const float* virt, int n_scans, int n_beams, float r_amin, float r_inc,
+                   float r_max, float v_amin, float v_inc, double thresh, int window, const double* poses,
+                   double grid_res, uint8_t* new_flag, uint8_t* gone_flag, int32_t* new_key, int32_t* gone_key) {
+    for (int b = 0; b < n_scans; ++b) {
+        const float* R = real + (int64_t)b * n_beams;
+        const float* V = virt + (int64_t)b * n_beams;
+        const double* P = poses + (int64_t)b * 7;
+        const double qx = P[3], qy = P[4], qz = P[5], qw = P[6];
+        const double yaw = std::atan2(2.0 * (qw * qz + qx * qy), 1.0 - 2.0 * (qy * qy + qz * qz));
+        auto to_key = [&](float r, float angle, int32_t* k) {
+            const float lx = r * std::cos(angle);
+            const float ly = r * std::sin(angle);
+            const double px = P[0] + (lx * std::cos(yaw) - ly * std::sin(yaw));
+            const double py = P[1] + (lx * std::sin(yaw) + ly * std::cos(yaw));
+            k[0] = (int)(px / grid_res);
+            k[1] = (int)(py / grid_res);
+        };
+        for (int i = 0; i < n_beams; ++i) {
+            const int64_t t = (int64_t)b * n_beams + i;
+            new_flag[t] = gone_flag[t] = 0;
+            new_key[t * 2] = new_key[t * 2 + 1] = gone_key[t * 2] = gone_key[t * 2 + 1] = 0;
+        }
+        for (int i = 0; i < n_beams; ++i) {  // 1. new
+            const float r_real = R[i];
+            if (std::isnan(r_real) || std::isinf(r_real) || r_real > r_max) continue;
+            const float angle = r_amin + i * r_inc;
+            const float rx = r_real * std::cos(angle), ry = r_real * std::sin(angle);
+            bool near_wall = false;
+            for (int j = std::max(0, i - window); j < std::min(n_beams, i + window); ++j) {
+                const float r_virt = V[j];
+                if (std::isinf(r_virt)) continue;
+                const float v_angle = v_amin + j * v_inc;
+                const float vx = r_virt * std::cos(v_angle), vy = r_virt * std::sin(v_angle);
+                if (std::hypot(rx - vx, ry - vy) < thresh) {
+                    near_wall = true;
+                    break;
+                }
+            }
+            if (!near_wall) {
+                const int64_t t = (int64_t)b * n_beams + i;
+                new_flag[t] = 1;
+                to_key(r_real, angle, new_key + t * 2);
+            }
+        }
+        for (int i = 0; i < n_beams; ++i) {  // 2. removed
+            const float r_virt = V[i];
+            if (std::isinf(r_virt) || std::isnan(r_virt)) continue;
+            const float angle = v_amin + i * v_inc;
+            const float vx = r_virt * std::cos(angle), vy = r_virt * std::sin(angle);
+            bool still = false;
+            for (int j = std::max(0, i - window); j < std::min(n_beams, i + window); ++j) {
+                const float r_real = R[j];
+                if (std::isinf(r_real) || r_real > r_max) continue;
+                const float r_angle = r_amin + j * r_inc;
+                const float rx = r_real * std::cos(r_angle), ry = r_real * std::sin(r_angle);
+                if (std::hypot(vx - rx, vy - ry) < thresh) {
+                    still = true;
+                    break;
+                }
+            }
+            if (!still) {
+                const int64_t t = (int64_t)b * n_beams + i;
+                gone_flag[t] = 1;
+                to_key(r_virt, angle, gone_key + t * 2);
+            }
+        }
+    }
+}
+
+/* updateGrid + publishCloud (diff_node.cpp:163-222) over a sequence of scans: float cell values, per scan
+ * hit cells += dt (cap 1.5 time_thresh), others -= decay * dt, erase at <= 0.  Returns the published cell count;
+ * out_xyz (float32 [k][3]) sorted by (x, y). */
+int64_t oro_change_grid_run(const int32_t* keys, const uint8_t* flags, int n_scans, int n_beams, const double* dts,
+                            double time_thresh, double decay_rate, double grid_res, float* out_xyz) {
+    std::map<std::pair<int, int>, float> grid;
+    for (int b = 0; b < n_scans; ++b) {
+        std::map<std::pair<int, int>, bool> hits;
+        for (int i = 0; i < n_beams; ++i) {
+            const int64_t t = (int64_t)b * n_beams + i;
+            if (flags[t]) hits[{keys[t * 2], keys[t * 2 + 1]}] = true;
+        }
+        const double dt = dts[b];
+        for (const auto& h : hits) {
+            grid[h.first] += dt;
+            if (grid[h.first] > (time_thresh * 1.5)) grid[h.first] = time_thresh * 1.5;
+        }
+        for (auto it = grid.begin(); it != grid.end();) {
+            if (hits.find(it->first) == hits.end()) it->second -= (decay_rate * dt);
+            if (it->second <= 0.0) it = grid.erase(it);
+            else ++it;
+        }
+    }
+    int64_t k = 0;
+    for (const auto& c : grid)
+        if (c.second > time_thresh) {
+            if (out_xyz) {
+                out_xyz[k * 3 + 0] = (float)((c.first.first * grid_res) + (grid_res / 2.0));
+                out_xyz[k * 3 + 1] = (float)((c.first.second * grid_res) + (grid_res / 2.0));
+                out_xyz[k * 3 + 2] = 0.0f;
+            }
+            ++k;
+        }
+    return k;
+}
+
 /* hybrid_map.create_map_cloud (hybrid_map.py:25-60). */
 int64_t oro_occupancy_to_points(const uint8_t* img, int h, int w, int threshold, double res, double ox, double oy,
                                 double* out) {

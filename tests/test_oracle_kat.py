@@ -187,3 +187,46 @@ def test_occupancy_kat(O):
     pts = O.occupancy_to_points(img, 100, 0.05, -1.0, -2.0)
     exp = np.array([[-1.0 + 1 * 0.05, -2.0 + 3 * 0.05, 0.0], [-1.0 + 4 * 0.05, -2.0 + 0 * 0.05, 0.0]])
     assert_bitwise(pts, exp, "occupancy points")
+
+
+def test_point_cloud_distance_kat(O):
+    """Oracle 1-NN distance == numpy brute force; empty target -> zeros (Open3D: no neighbour found)."""
+    rng = np.random.default_rng(5)
+    a, b = rng.normal(size=(300, 3)), rng.normal(size=(200, 3))
+    d = O.point_cloud_distance(a, b)
+    diff = a[:, None, :] - b[None, :, :]
+    ref = np.sqrt(((diff[..., 0] * diff[..., 0] + diff[..., 1] * diff[..., 1]) + diff[..., 2] * diff[..., 2]).min(1))
+    assert np.array_equal(d, ref)
+    assert not np.any(O.point_cloud_distance(a, np.zeros((0, 3))))
+
+
+def test_smart_paste_kat(O):
+    """2d_selective_merge.py:58-69 on a hand-checked grid: only values outside [200, 210] are pasted."""
+    base = np.full((3, 4), 7, np.uint8)
+    over = np.array([[0, 200, 205, 210], [211, 254, 199, 100], [1, 2, 3, 4]], np.uint8)
+    out = O.smart_paste(base, over, 0, 0, 4, 2)
+    assert out.tolist() == [[0, 7, 7, 7], [211, 254, 199, 100], [7, 7, 7, 7]]
+    assert np.array_equal(O.smart_paste(base, over, 2, 0, 3, 1), base)  # rectangle leaves the image
+
+
+def test_scan_diff_and_grid_kat(O):
+    """Identical scans flag nothing; a return 1 m beyond the wall is 'new' and its wall beam 'gone'; the grid
+    publishes a cell only after its evidence exceeds time_threshold."""
+    n = 90
+    amin, ainc = np.float32(-np.pi / 4), np.float32(np.pi / 2 / 90)
+    virt = np.full((1, n), 3.0, np.float32)
+    pose = np.array([[0, 0, 0, 0, 0, 0, 1.0]])
+    nf, gf, _, _ = O.scan_diff(virt, virt, float(amin), float(ainc), 10.0, float(amin), float(ainc), 0.5, 20, pose, 0.1)
+    assert nf.sum() == 0 and gf.sum() == 0
+    real = virt.copy()
+    real[0, 45] = 4.0
+    nf, gf, nk, gk = O.scan_diff(real, virt, float(amin), float(ainc), 10.0, float(amin), float(ainc), 0.5, 20, pose,
+                                 0.1)
+    assert nf[0].nonzero()[0].tolist() == [45] and gf.sum() == 0
+    a = amin + np.float32(45) * ainc
+    assert nk[0, 45].tolist() == [int(np.float64(np.float32(4.0) * np.float32(np.cos(a))) / 0.1),
+                                  int(np.float64(np.float32(4.0) * np.float32(np.sin(a))) / 0.1)]
+    keys = np.repeat(nk, 3, axis=0)
+    flags = np.repeat(nf, 3, axis=0)
+    assert len(O.change_grid_run(keys[:1], flags[:1], [1.0], 2.0, 0.5, 0.1)) == 0   # 1.0 <= 2.0
+    assert len(O.change_grid_run(keys, flags, [1.0, 1.0, 1.0], 2.0, 0.5, 0.1)) == 1  # capped 3.0 > 2.0
