@@ -47,6 +47,11 @@ def parse():
     ap.add_argument("--calib", action="store_true", help="after timing, run export_units once (PMC calibration)")
     ap.add_argument("--filter-frames", type=int, default=64,
                     help="configs[2] stream length (1280x720 unproject + 5 mm voxel + SOR); 0 = skip")
+    ap.add_argument("--objects", type=int, default=8,
+                    help="configs[3]: object scans shared by all ranks (full per-object pipeline + RCCL merge); 0 = skip")
+    ap.add_argument("--object-frames", type=int, default=64, help="configs[3]: frames per object scan")
+    ap.add_argument("--hybrid-objects", type=int, default=32,
+                    help="configs[4]: object clouds in the hybrid-map fusion + change detection; 0 = skip")
     return ap.parse_args()
 
 
@@ -58,6 +63,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # configs[3] scans are rendered before this process touches the GPU (the render pool forks workers)
+    synth0 = importlib.import_module(PKG + ".synth")
+    obj_ids = list(range(args.objects))[(args.objects * rank) // world:(args.objects * (rank + 1)) // world]
+    obj_scans = _render_objects(synth0, obj_ids, args.object_frames) if args.objects > 0 else None
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -159,6 +168,10 @@ def main():
         L.call("ot_tsdf_export_units", vol, None, *[C.c_void_p(b.data_ptr()) for b in bufs], stream)
         torch.cuda.synchronize()
 
+    objects = objects_pipeline(args, L, lib, synth, torch, dist, rank, world, obj_ids, obj_scans) \
+        if args.objects > 0 else None
+    hybrid = hybrid_fusion(args, L, synth, torch, dist, rank, world) if args.hybrid_objects > 0 else None
+
     cpu = None
     if rank == 0 and args.cpu_frames > 0:
         cpu = cpu_baseline(depth, color, ext, intr_t, args)
@@ -172,13 +185,156 @@ def main():
                       "frames_per_step": args.frames, "width": W, "height": H, "voxel_length": args.voxel,
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
-           "roofline": roofline, "cpu_baseline": cpu, "filtered": filt}
+           "roofline": roofline, "cpu_baseline": cpu, "filtered": filt, "objects": objects, "hybrid_map": hybrid}
     if rank == 0:
         print(json.dumps(out), flush=True)
     L.call("ot_tsdf_destroy", vol)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _timed(torch, dist, world, fn, steps):
+    """max-over-ranks seconds per call of fn() (barrier + synchronize on both sides of the timed calls)."""
+    fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = (time.perf_counter() - t0) / steps
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, out
+
+
+def _render_objects(synth, ids, n_frames):
+    """Synthetic ring scans of object_scene(i) for the given ids (process pool when a rank renders several)."""
+    if len(ids) <= 1:
+        return [synth.make_sequence(synth.object_scene(i), n_frames=n_frames) for i in ids]
+    from concurrent.futures import ProcessPoolExecutor
+
+    import multiprocessing as mp
+
+    with ProcessPoolExecutor(max_workers=min(len(ids), 8), mp_context=mp.get_context("fork")) as ex:
+        futs = [ex.submit(synth.make_sequence, synth.object_scene(i), n_frames) for i in ids]
+        return [f.result() for f in futs]
+
+
+def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
+    """configs[3]: --objects independent object scans x --object-frames 640x480 frames, contiguous shards per rank
+    (reconstruct_rgbd_filter.py:154-155).  Per object, on device: integrate every frame (5 mm, sdf_trunc 0.04) ->
+    extract_triangle_mesh -> compute_vertex_normals -> sample_points_uniformly(100000) -> z >= 0.03 mask
+    (reconstruct_rgbd_filter.py:81-132); then the RCCL all-gather merge of the filtered clouds in sorted order
+    (distributed.merge_object_clouds).  frames/s = all frames of all objects / max-over-ranks wall time."""
+    pkg = importlib.import_module(PKG)
+    D = importlib.import_module(PKG + ".distributed")
+    intr_t = synth.REF_INTRINSICS_640
+    W, H = intr_t[0], intr_t[1]
+    intr = L.ot_intrinsics(W, H, *intr_t[2:])
+    dev = []
+    for depth, color, ext in scans:
+        dev.append((torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous(),
+                    torch.from_numpy(color).cuda().contiguous(), np.ascontiguousarray(ext, dtype=np.float64)))
+    vols = [pkg.pipelines.integration.ScalableTSDFVolume(
+        voxel_length=args.voxel, sdf_trunc=args.sdf_trunc,
+        color_type=pkg.pipelines.integration.TSDFVolumeColorType.RGB8) for _ in dev]
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    npx = W * H
+    sizes = {}
+
+    def run():
+        clouds = []
+        for vol, (d16, col, ext) in zip(vols, dev):
+            vol.reset()
+            for k in range(ext.shape[0]):
+                st = lib.ot_tsdf_integrate_u16(vol._h, C.c_void_p(d16.data_ptr() + k * npx * 2),
+                                               C.c_void_p(col.data_ptr() + k * npx * 3), C.byref(intr),
+                                               ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
+                if st:
+                    raise RuntimeError(lib.ot_last_error().decode())
+            mesh = vol.extract_triangle_mesh()
+            mesh.compute_vertex_normals()
+            pcd = mesh.sample_points_uniformly(number_of_points=100000)
+            clouds.append(pcd.filter_min_z(0.03)._xyz.dev())
+        merged = D.merge_object_clouds(clouds)
+        sizes["local"] = sum(int(c.shape[0]) for c in clouds)
+        return merged
+
+    dt, merged = _timed(torch, dist, world, run, 3)
+    return {"workload": f"configs[3]: {args.objects} object scans x {args.object_frames} 640x480 frames, "
+                        f"{args.voxel * 1000:g} mm TSDF -> mesh -> normals -> 100k samples -> z mask per object, "
+                        f"contiguous object shards over {world} GPU(s), RCCL all-gather merge",
+            "frames_per_s": round(args.objects * args.object_frames / dt, 1), "ms": round(dt * 1e3, 3),
+            "objects_per_rank": len(ids), "merged_points": int(merged.shape[0])}
+
+
+def hybrid_fusion(args, L, synth, torch, dist, rank, world):
+    """configs[4]: hybrid-map fusion with change detection against a saved map.  Inputs resident in HBM: a
+    1024x1024 occupancy grid @ 5 cm (saved + new) and --hybrid-objects object clouds (~100k points, sharded over
+    ranks) with their saved-map versions.  Timed per fusion: per rank, voxel-key diff (2 cm lattice) of each of
+    its objects vs the saved version; rank 0, smart_paste merge of the new grid onto the saved one
+    (2d_selective_merge.py) and the occupied-cell cloud (hybrid_map.py:25-60); then the RCCL all-gather of the
+    object clouds (hybrid_map.py:62-96, map cloud first)."""
+    import ctypes as Cc
+
+    Dm = importlib.import_module(PKG + ".distributed")
+    CD = importlib.import_module(PKG + ".change_detection")
+    ids = Dm.shard(list(range(args.hybrid_objects)), rank, world)
+    objs = [torch.from_numpy(synth.object_cloud(i)).cuda() for i in ids]
+    saved = [torch.from_numpy(synth.object_cloud(i, moved=True)).cuda() for i in ids]
+    old_map, new_map = synth.occupancy_pair(1024, 1024, seed=0)
+    d_old = torch.from_numpy(old_map).cuda()
+    d_new = torch.from_numpy(new_map).cuda()
+    d_base = torch.empty_like(d_old)
+    occ = torch.empty((1024 * 1024, 3), dtype=torch.float64, device="cuda")
+    keys_a = torch.empty((120000, 3), dtype=torch.int32, device="cuda")
+    keys_r = torch.empty((120000, 3), dtype=torch.int32, device="cuda")
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    origin = (Cc.c_double * 3)(-1.0, -1.0, -1.0)
+    stats = {}
+
+    def run():
+        added = removed = 0
+        for a, b in zip(objs, saved):
+            na, nr = C.c_int64(0), C.c_int64(0)
+            L.call("ot_voxel_key_diff", C.c_void_p(a.data_ptr()), a.shape[0], C.c_void_p(b.data_ptr()), b.shape[0],
+                   0.02, origin, C.c_void_p(keys_a.data_ptr()), C.byref(na), C.c_void_p(keys_r.data_ptr()),
+                   C.byref(nr), stream)
+            added, removed = added + na.value, removed + nr.value
+        nq = C.c_int64(0)
+        if rank == 0:
+            d_base.copy_(d_old)
+            ch = C.c_int64(0)
+            L.call("ot_grid_smart_paste", C.c_void_p(d_base.data_ptr()), C.c_void_p(d_new.data_ptr()), 1024, 1024,
+                   0, 0, 1024, 1024, CD.UNKNOWN_PIXEL, CD.PASTE_THRESHOLD, C.byref(ch), stream)
+            L.call("ot_occupancy_to_points", C.c_void_p(d_base.data_ptr()), 1024, 1024, 100, 0.05, -25.6, -25.6,
+                   C.c_void_p(occ.data_ptr()), C.byref(nq), stream)
+            stats["changed_cells"] = ch.value
+        merged = Dm.merge_object_clouds(objs)
+        if rank == 0:
+            merged = torch.cat([occ[:nq.value], merged], 0)
+        stats.update(added=added, removed=removed)
+        return merged
+
+    dt, merged = _timed(torch, dist, world, run, 5)
+    npts = sum(int(o.shape[0]) for o in objs)
+    t = torch.tensor([npts], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t)
+    return {"workload": f"configs[4]: 1024x1024 occupancy grid @ 5 cm + {args.hybrid_objects} object clouds, "
+                        "change detection vs the saved map (smart_paste grid merge + 2 cm voxel-key diff per object), "
+                        f"hybrid cloud assembled by RCCL all-gather over {world} GPU(s)",
+            "ms": round(dt * 1e3, 3), "mpoints_per_s": round(int(t.item()) / dt / 1e6, 2),
+            "merged_points": int(merged.shape[0]) if rank == 0 else None,
+            "changed_grid_cells": stats.get("changed_cells"), "added_keys_rank0": stats.get("added"),
+            "removed_keys_rank0": stats.get("removed")}
 
 
 def filter_stream(args, L, lib, synth, torch, rank):

@@ -99,13 +99,76 @@ __global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V,
     area[t] = 0.5 * sqrt((c0 * c0 + c1 * c1) + c2 * c2);
 }
 
-// Open3D's sequential recurrences (GetSurfaceArea + the CDF loop), one lane; then n_t = round(cdf_t * N)
-__global__ void k_area_cdf(double* area, int64_t nt) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double s = 0.0;
-    for (int64_t t = 0; t < nt; ++t) s += area[t];
-    area[0] /= s;
-    for (int64_t t = 1; t < nt; ++t) area[t] = area[t] / s + area[t - 1];
+// Open3D's sequential recurrences (GetSurfaceArea: s = (((a0 + a1) + a2) + ...), then the CDF loop
+// cdf_t = a_t / s + cdf_{t-1}) are serial float64 chains, kept in their exact order by ONE wave: the wave streams
+// the input with coalesced 16-B-per-lane loads kept CDF_DEPTH chunks ahead, parks each 128-value chunk in LDS,
+// and lane 0 runs the dependent v_add_f64 chain over it (ds_read_b128 operands).  The divisions a_t / s are a
+// separate lane-parallel pass; the CDF chunk goes back through LDS to one coalesced store.  Padding adds +0.0,
+// an exact no-op for these non-negative sums.
+constexpr int CDF_CHUNK = 128;  // values per chunk (2 per lane)
+constexpr int CDF_DEPTH = 8;    // chunks in flight
+
+__device__ inline double2 cdf_load(const double* __restrict__ x, int64_t nt, int64_t base, int lane) {
+    const int64_t i = base + 2 * lane;
+    if (i + 1 < nt) return *reinterpret_cast<const double2*>(x + i);  // x is 16-B aligned, base even
+    return make_double2(i < nt ? x[i] : 0.0, 0.0);
+}
+
+template <bool CDF>
+__device__ inline void cdf_chunk(double2 v, double* lds, double& acc, int lane, int64_t base, int64_t nt,
+                                 double* __restrict__ out) {
+    reinterpret_cast<double2*>(lds)[lane] = v;
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll 8
+        for (int k = 0; k < CDF_CHUNK; k += 2) {
+            const double2 p = reinterpret_cast<const double2*>(lds)[k >> 1];
+            if (CDF) {
+                double2 r;
+                acc = p.x + acc;
+                r.x = acc;
+                acc = p.y + acc;
+                r.y = acc;
+                reinterpret_cast<double2*>(lds)[k >> 1] = r;
+            } else {
+                acc = acc + p.x;
+                acc = acc + p.y;
+            }
+        }
+    }
+    __syncthreads();
+    if (CDF) {
+        const double2 r = reinterpret_cast<const double2*>(lds)[lane];
+        const int64_t i = base + 2 * lane;
+        if (i + 1 < nt) *reinterpret_cast<double2*>(out + i) = r;
+        else if (i < nt) out[i] = r.x;
+        __syncthreads();
+    }
+}
+
+template <bool CDF>
+__global__ __launch_bounds__(64) void k_serial_chain(const double* __restrict__ x, int64_t nt, double* __restrict__ out) {
+    __shared__ double lds[CDF_CHUNK];
+    const int lane = threadIdx.x;
+    double acc = 0.0;  // sum: s = 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0 exactly
+    double2 r[CDF_DEPTH];
+#pragma unroll
+    for (int d = 0; d < CDF_DEPTH; ++d) r[d] = cdf_load(x, nt, (int64_t)d * CDF_CHUNK, lane);
+    for (int64_t base = 0; base < nt; base += (int64_t)CDF_CHUNK * CDF_DEPTH) {
+#pragma unroll
+        for (int d = 0; d < CDF_DEPTH; ++d) {
+            const int64_t b = base + (int64_t)d * CDF_CHUNK;
+            if (b < nt) cdf_chunk<CDF>(r[d], lds, acc, lane, b, nt, out);
+            r[d] = cdf_load(x, nt, b + (int64_t)CDF_CHUNK * CDF_DEPTH, lane);
+        }
+    }
+    if (!CDF && lane == 0) out[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_area_div(const double* __restrict__ area, int64_t nt,
+                                                  const double* __restrict__ sum, double* __restrict__ q) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < nt) q[t] = area[t] / sum[0];
 }
 
 __global__ __launch_bounds__(256) void k_round_counts(const double* __restrict__ cdf, int64_t nt, int64_t N,
@@ -207,12 +270,17 @@ ot_status ot_mesh_sample_points_uniformly(const double* V, const double* VN, con
     if (nt <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] Input mesh has no triangles.");
     if (!V || !T || !P || (PN && !VN) || (PC && !VC) || nv <= 0)
         return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid arguments");
-    char* ws = (char*)scratch((size_t)nt * 16 + 256, 17);
+    char* ws = (char*)scratch((size_t)nt * 32 + 256, 17);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-    double* area = (double*)ws;
-    long long* ncum = (long long*)(area + nt);
+    double* sum = (double*)ws;
+    double* area = sum + 8;  // 64-B offset: 16-B aligned rows for the chain's double2 loads
+    double* q = area + ((nt + 1) & ~(int64_t)1);  // 16-B aligned for the chain's double2 loads
+    long long* ncum = (long long*)(q + ((nt + 1) & ~(int64_t)1));
     hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, V, T, nt, area);
-    hipLaunchKernelGGL(k_area_cdf, dim3(1), dim3(64), 0, stream, area, nt);
+    hipLaunchKernelGGL(k_serial_chain<false>, dim3(1), dim3(64), 0, stream, (const double*)area, nt, sum);
+    hipLaunchKernelGGL(k_area_div, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, (const double*)area, nt,
+                       (const double*)sum, q);
+    hipLaunchKernelGGL(k_serial_chain<true>, dim3(1), dim3(64), 0, stream, (const double*)q, nt, area);
     hipLaunchKernelGGL(k_round_counts, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, area, nt, n_points,
                        ncum);
     hipLaunchKernelGGL(k_sample, dim3((unsigned)((n_points + 255) / 256)), dim3(256), 0, stream, V, PN ? VN : nullptr,

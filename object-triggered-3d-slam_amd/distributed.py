@@ -32,6 +32,8 @@ def all_gather_rows(local, group=None):
     import torch
     import torch.distributed as dist
 
+    if not dist.is_initialized():  # single process: nothing to exchange
+        return local
     world = dist.get_world_size(group)
     k = local.shape[1]
     counts = torch.zeros(world, dtype=torch.int64, device=local.device)
@@ -57,7 +59,8 @@ def merge_object_clouds(local_clouds, group=None):
     if dev is None:
         import torch.distributed as dist
 
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else \
+        dev = torch.device("cuda", torch.cuda.current_device()) if (not dist.is_initialized() or
+                                                                   dist.get_backend(group) == "nccl") else \
             torch.device("cpu")
     local = torch.cat(local_clouds, 0) if local_clouds else torch.zeros((0, 3), dtype=torch.float64, device=dev)
     return all_gather_rows(local.to(torch.float64), group)

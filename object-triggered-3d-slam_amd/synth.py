@@ -245,3 +245,25 @@ def occupancy_pair(h=1024, w=1024, seed=0):
     noise = rng.random((h, w)) < 0.01
     new[noise] = rng.integers(195, 216, int(noise.sum()))   # values around the unknown band edges
     return old, new
+
+
+def object_cloud(object_id: int, n_points: int = 100000, moved: bool = False):
+    """A filtered object cloud as the reconstruction writes it (points on the visible box faces of
+    object_scene(object_id), z >= 0.03), for the hybrid-map fusion configs.  `moved` = the object as the
+    saved map last saw it for every third object (shifted 6 cm, 10 % fewer samples) — the change to detect."""
+    sc = object_scene(object_id)
+    b = sc.boxes[0]
+    lo, hi = np.array(b.lo, np.float64), np.array(b.hi, np.float64)
+    if moved and object_id % 3 == 0:
+        lo, hi = lo + [0.06, 0.0, 0.0], hi + [0.06, 0.0, 0.0]
+        n_points = int(n_points * 0.9)
+    rng = np.random.default_rng(1000 + object_id + (7919 if moved else 0))
+    u = rng.random((n_points, 3))
+    face = rng.integers(0, 5, n_points)  # 4 sides + top
+    p = lo + u * (hi - lo)
+    ax = np.where(face < 2, 0, np.where(face < 4, 1, 2))
+    side = np.where(face % 2 == 0, lo[ax], hi[ax])
+    side = np.where(face == 4, hi[2], side)
+    p[np.arange(n_points), ax] = side
+    p += rng.normal(0, 0.002, p.shape)
+    return p[p[:, 2] >= 0.03]
