@@ -49,11 +49,11 @@ __device__ inline int block_excl_scan_256(int v, int& total) {
 
 template <class Pred>
 __global__ __launch_bounds__(CMP_THREADS) void k_compact_count(int64_t n, Pred pred, int* block_counts) {
-    const int64_t base = (int64_t)blockIdx.x * CMP_TILE + (int64_t)threadIdx.x * CMP_ITEMS;
+    const int64_t tile = (int64_t)blockIdx.x * CMP_TILE;
     int c = 0;
 #pragma unroll
     for (int k = 0; k < CMP_ITEMS; ++k) {
-        int64_t i = base + k;
+        const int64_t i = tile + (int64_t)k * CMP_THREADS + threadIdx.x;  // lane-strided, as the emit pass
         if (i < n && pred(i)) ++c;
     }
     c = wave_sum(c);
@@ -99,23 +99,39 @@ __global__ __launch_bounds__(1024) void k_scan_inplace(int* v, int n, int64_t* t
 }  // namespace
 
 
+// Emit: a workgroup's tile of CMP_TILE items is walked in CMP_ITEMS lane-strided slices (item = tile + k*256 +
+// lane), so consecutive lanes emit consecutive output positions and the emit functor's stores coalesce; slice k's
+// kept items precede slice k+1's, which keeps the global input order.
 template <class Pred, class Emit>
 __global__ __launch_bounds__(CMP_THREADS) void k_compact_emit(int64_t n, Pred pred, Emit emit,
                                                               const int* block_offsets) {
-    const int64_t base = (int64_t)blockIdx.x * CMP_TILE + (int64_t)threadIdx.x * CMP_ITEMS;
+    __shared__ int wsum[CMP_ITEMS][CMP_THREADS / 64];
+    const int64_t tile = (int64_t)blockIdx.x * CMP_TILE;
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
     bool keep[CMP_ITEMS];
-    int c = 0;
+    int pre[CMP_ITEMS];
 #pragma unroll
     for (int k = 0; k < CMP_ITEMS; ++k) {
-        int64_t i = base + k;
+        const int64_t i = tile + (int64_t)k * CMP_THREADS + threadIdx.x;
         keep[k] = (i < n) && pred(i);
-        c += keep[k] ? 1 : 0;
+        int tot;
+        pre[k] = wave_excl_count(keep[k], tot);
+        if (lane == 0) wsum[k][wid] = tot;
     }
-    int total;
-    int pos = block_excl_scan_256(c, total) + block_offsets[blockIdx.x];
+    __syncthreads();
+    int pos = block_offsets[blockIdx.x];
 #pragma unroll
-    for (int k = 0; k < CMP_ITEMS; ++k)
-        if (keep[k]) emit(base + k, (int64_t)pos++);
+    for (int k = 0; k < CMP_ITEMS; ++k) {
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < CMP_THREADS / 64; ++w) {
+            const int c = wsum[k][w];
+            off += (w < wid) ? c : 0;
+            tot += c;
+        }
+        if (keep[k]) emit(tile + (int64_t)k * CMP_THREADS + threadIdx.x, (int64_t)(pos + off + pre[k]));
+        pos += tot;
+    }
 }
 
 // Host driver: runs the three launches on `stream` and returns the kept count on the host (synchronises).
@@ -150,23 +166,37 @@ namespace {
 __global__ __launch_bounds__(CMP_THREADS) void k_segments_emit(int64_t n, const unsigned long long* __restrict__ keys,
                                                                const int* __restrict__ block_offsets,
                                                                int* __restrict__ heads, int* __restrict__ seg) {
-    const int64_t base = (int64_t)blockIdx.x * CMP_TILE + (int64_t)threadIdx.x * CMP_ITEMS;
+    __shared__ int wsum[CMP_ITEMS][CMP_THREADS / 64];
+    const int64_t tile = (int64_t)blockIdx.x * CMP_TILE;
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
     bool head[CMP_ITEMS];
-    int c = 0;
+    int pre[CMP_ITEMS];
 #pragma unroll
     for (int k = 0; k < CMP_ITEMS; ++k) {
-        const int64_t i = base + k;
+        const int64_t i = tile + (int64_t)k * CMP_THREADS + threadIdx.x;
         head[k] = (i < n) && (i == 0 || keys[i] != keys[i - 1]);
-        c += head[k] ? 1 : 0;
+        int tot;
+        pre[k] = wave_excl_count(head[k], tot);
+        if (lane == 0) wsum[k][wid] = tot;
     }
-    int total;
-    int pos = block_excl_scan_256(c, total) + block_offsets[blockIdx.x];
+    __syncthreads();
+    int pos = block_offsets[blockIdx.x];
 #pragma unroll
     for (int k = 0; k < CMP_ITEMS; ++k) {
-        const int64_t i = base + k;
-        if (i >= n) break;
-        if (head[k]) heads[pos++] = (int)i;
-        seg[i] = pos - 1;
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < CMP_THREADS / 64; ++w) {
+            const int c = wsum[k][w];
+            off += (w < wid) ? c : 0;
+            tot += c;
+        }
+        const int64_t i = tile + (int64_t)k * CMP_THREADS + threadIdx.x;
+        const int my = pos + off + pre[k];  // segments starting before item i (exclusive)
+        if (i < n) {
+            if (head[k]) heads[my] = (int)i;
+            seg[i] = my + (head[k] ? 1 : 0) - 1;
+        }
+        pos += tot;
     }
 }
 }  // namespace

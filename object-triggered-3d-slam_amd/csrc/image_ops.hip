@@ -58,7 +58,8 @@ struct UnprojPred {
     const float* depth;
     int w, ws, stride;
     __device__ bool operator()(int64_t s) const {
-        const int r = (int)(s / ws) * stride, c = (int)(s % ws) * stride;
+        const unsigned su = (unsigned)s, q = su / (unsigned)ws;  // sample index < 2^31
+        const int r = (int)q * stride, c = (int)(su - q * (unsigned)ws) * stride;
         return depth[(int64_t)r * w + c] > 0.0f;
     }
 };
@@ -71,7 +72,8 @@ struct UnprojEmit {
     double* xyz;
     double* rgb;
     __device__ void operator()(int64_t s, int64_t pos) const {
-        const int r = (int)(s / ws) * stride, c = (int)(s % ws) * stride;
+        const unsigned su = (unsigned)s, q = su / (unsigned)ws;
+        const int r = (int)q * stride, c = (int)(su - q * (unsigned)ws) * stride;
         const int64_t pix = (int64_t)r * w + c;
         const double z = (double)depth[pix];
         const double x = ((double)c - cx) * z / fx;
@@ -123,7 +125,8 @@ struct OccEmit {
     double res, ox, oy;
     double* out;
     __device__ void operator()(int64_t i, int64_t pos) const {
-        const int r = (int)(i / w), c = (int)(i % w);
+        const unsigned iu = (unsigned)i, q = iu / (unsigned)w;  // h * w < 2^31 (checked on the host)
+        const int r = (int)q, c = (int)(iu - q * (unsigned)w);
         out[pos * 3 + 0] = ox + ((double)c * res);
         out[pos * 3 + 1] = oy + ((double)(h - 1 - r) * res);
         out[pos * 3 + 2] = 0.0;
@@ -176,6 +179,7 @@ ot_status ot_unproject(const float* depth, const uint8_t* color, const ot_intrin
     const int ws = (in->width + stride - 1) / stride, hs = (in->height + stride - 1) / stride;
     const int64_t n = (int64_t)ws * hs;
     if (capacity < n) return fail(OT_ERR_CAPACITY, "[CreatePointCloudFromRGBDImage] output capacity too small");
+    if (n > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[CreatePointCloudFromRGBDImage] image too large");
     UnprojPred pred{depth, in->width, ws, stride};
     UnprojEmit emit;
     emit.depth = depth;
@@ -213,7 +217,7 @@ ot_status ot_gather_rows3(const double* in, const int64_t* idx, int64_t m, doubl
 ot_status ot_occupancy_to_points(const uint8_t* img, int32_t height, int32_t width, int32_t threshold,
                                  double resolution, double origin_x, double origin_y, double* out_xyz,
                                  int64_t* n_out_host, void* stream) {
-    if (!img || !out_xyz || !n_out_host || height <= 0 || width <= 0)
+    if (!img || !out_xyz || !n_out_host || height <= 0 || width <= 0 || (int64_t)height * width > 0x7FFFFFFF)
         return fail(OT_ERR_INVALID_ARGUMENT, "[create_map_cloud] invalid arguments");
     OccPred pred{img, threshold};
     OccEmit emit{width, height, resolution, origin_x, origin_y, out_xyz};

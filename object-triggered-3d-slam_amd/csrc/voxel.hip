@@ -59,13 +59,30 @@ __global__ __launch_bounds__(256) void k_voxel_reduce(const double* __restrict__
     const int64_t beg = heads[s];
     const int64_t end = (s + 1 < K) ? heads[s + 1] : n;
     double p[3] = {0, 0, 0}, c[3] = {0, 0, 0}, q[3] = {0, 0, 0};
-    for (int64_t j = beg; j < end; ++j) {
-        const int64_t i = sidx[j];
+    // points in batches of 4: the batch's index and row loads are all issued before its (in-order) sums
+    constexpr int VB = 4;
+    for (int64_t j0 = beg; j0 < end; j0 += VB) {
+        int64_t ii[VB];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            p[a] += xyz[i * 3 + a];
-            if (rgb) c[a] += rgb[i * 3 + a];
-            if (nrm) q[a] += nrm[i * 3 + a];
+        for (int k = 0; k < VB; ++k) ii[k] = sidx[j0 + k < end ? j0 + k : j0];
+        double xp[VB][3], xc[VB][3], xq[VB][3];
+#pragma unroll
+        for (int k = 0; k < VB; ++k)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                xp[k][a] = xyz[ii[k] * 3 + a];
+                xc[k][a] = rgb ? rgb[ii[k] * 3 + a] : 0.0;
+                xq[k][a] = nrm ? nrm[ii[k] * 3 + a] : 0.0;
+            }
+#pragma unroll
+        for (int k = 0; k < VB; ++k) {
+            if (j0 + k >= end) break;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                p[a] += xp[k][a];
+                if (rgb) c[a] += xc[k][a];
+                if (nrm) q[a] += xq[k][a];
+            }
         }
     }
     const double cnt = (double)(end - beg);
