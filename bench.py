@@ -31,6 +31,7 @@ PKG = "object-triggered-3d-slam_amd"
 
 METRIC = "RGB-D frames/sec (640×480, 5mm voxel TSDF) at 1/2/4/8 GPU; Mpoints/s filtered"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+COLL_DEV = "cuda"
 
 
 def parse():
@@ -67,11 +68,20 @@ def main():
     synth0 = importlib.import_module(PKG + ".synth")
     obj_ids = list(range(args.objects))[(args.objects * rank) // world:(args.objects * (rank + 1)) // world]
     obj_scans = _render_objects(synth0, obj_ids, args.object_frames) if args.objects > 0 else None
+    # OT_BENCH_BACKEND=gloo + OT_BENCH_SHARE_GPU=1 rehearse the N-rank path on a one-GPU box (every rank on
+    # device 0, collectives through host memory); the driver's runs use RCCL ("nccl"), one GPU per rank.
+    backend = os.environ.get("OT_BENCH_BACKEND", "nccl")
+    dev_index = 0 if os.environ.get("OT_BENCH_SHARE_GPU") == "1" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
+    global COLL_DEV
+    COLL_DEV = "cuda" if backend == "nccl" else "cpu"  # device of the small timing / count tensors
 
     pkg = importlib.import_module(PKG)
     synth = importlib.import_module(PKG + ".synth")
@@ -123,7 +133,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -208,7 +218,7 @@ def _timed(torch, dist, world, fn, steps):
         dist.barrier()
     dt = (time.perf_counter() - t0) / steps
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt, out
@@ -325,7 +335,7 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
 
     dt, merged = _timed(torch, dist, world, run, 5)
     npts = sum(int(o.shape[0]) for o in objs)
-    t = torch.tensor([npts], dtype=torch.int64, device="cuda")
+    t = torch.tensor([npts], dtype=torch.int64, device=COLL_DEV)
     if world > 1:
         dist.all_reduce(t)
     return {"workload": f"configs[4]: 1024x1024 occupancy grid @ 5 cm + {args.hybrid_objects} object clouds, "

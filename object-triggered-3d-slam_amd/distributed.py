@@ -34,6 +34,8 @@ def all_gather_rows(local, group=None):
 
     if not dist.is_initialized():  # single process: nothing to exchange
         return local
+    if dist.get_backend(group) == "gloo" and local.is_cuda:  # gloo collectives run through host memory
+        return all_gather_rows(local.cpu(), group).to(local.device)
     world = dist.get_world_size(group)
     k = local.shape[1]
     counts = torch.zeros(world, dtype=torch.int64, device=local.device)
