@@ -225,6 +225,14 @@ ot_status ot_scan_diff(const float* real_ranges, const float* virtual_ranges, in
                        int32_t search_window, const double* poses_host, double grid_resolution, uint8_t* new_flags,
                        uint8_t* gone_flags, int32_t* new_keys, int32_t* gone_keys, void* stream);
 
+/* virtual_scan_node.cpp:245-292 publish_virtual_scan, batched: the saved map (OccupancyGrid int8 [height][width],
+ * 100 = occupied; resolution / origin as the message's float fields) ray-marched per beam in steps of one
+ * resolution from each robot pose (poses_host [n_scans][3] = x, y, yaw — yaw as tf2::getYaw); out_ranges float32
+ * [n_scans][n_beams], +inf where no occupied cell is met before range_max or the map edge. */
+ot_status ot_virtual_scan(const int8_t* grid, int32_t height, int32_t width, float resolution, float origin_x,
+                          float origin_y, int32_t n_scans, int32_t n_beams, float angle_min, float angle_increment,
+                          float range_max, const double* poses_host, float* out_ranges, void* stream);
+
 /* diff_node.cpp:163-185 updateGrid / :188-222 publishCloud: time-decayed evidence grid (host state). */
 typedef struct ot_change_grid ot_change_grid;
 ot_status ot_change_grid_create(double time_threshold, double decay_rate, double grid_resolution,

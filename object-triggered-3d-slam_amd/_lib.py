@@ -71,6 +71,8 @@ SIGNATURES = {
     "ot_voxel_key_diff": [_p, _i64, _p, _i64, _d, _p, _p, _pi64, _p, _pi64, _p],
     "ot_scan_diff": [_p, _p, _i32, _i32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, _d, _i32, _p, _d,
                      _p, _p, _p, _p, _p],
+    "ot_virtual_scan": [_p, _i32, _i32, C.c_float, C.c_float, C.c_float, _i32, _i32, C.c_float, C.c_float,
+                        C.c_float, _p, _p, _p],
     "ot_change_grid_create": [_d, _d, _d, C.POINTER(_p)],
     "ot_change_grid_destroy": [_p],
     "ot_change_grid_update": [_p, _p, _p, _i64, _d],

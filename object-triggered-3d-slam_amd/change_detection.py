@@ -9,6 +9,9 @@ Host-side mirrors of the reference's change-detection code, backed by the HIP ke
   comparison batched over many scans on the GPU and the time-decayed evidence grid kept in native host code.
 * ``voxel_key_diff(new, old, voxel_size, origin)`` — added / removed lattice cells of an object cloud versus the
   saved map's cloud (the 3-D half of configs[4]'s diff).
+* ``virtual_scan(grid, resolution, origin, template, poses)`` — ros2_ws/src/lidar_detection/src/virtual_scan_node.cpp
+  (VirtualScanNode): the scan the saved map would return at each robot pose (the diff node's /virtual_scan input),
+  ray-marched per beam on the GPU; ``occupancy_from_pgm`` / ``tf2_get_yaw`` prepare its inputs.
 
 Every compute call goes through the C ABI; there is no CPU implementation in this module.
 """
@@ -166,6 +169,46 @@ class ChangeDetector:
                 L.call("ot_change_grid_publish", g, xyz.ctypes.data_as(C.c_void_p), n.value, C.byref(n))
             out.append(xyz)
         return out[0], out[1]
+
+
+def tf2_get_yaw(qx, qy, qz, qw):
+    """tf2::getYaw(quaternion) (tf2/utils.h: Matrix3x3(q).getEulerYPR): yaw of the rotation matrix of q."""
+    d = qx * qx + qy * qy + qz * qz + qw * qw
+    s = 2.0 / d
+    xs, ys, zs = qx * s, qy * s, qz * s
+    wz, xx, xy = qw * zs, qx * xs, qx * ys
+    yy, zz = qy * ys, qz * zs
+    m00, m10, m20 = 1.0 - (yy + zz), xy + wz, qx * zs - qw * ys
+    if abs(m20) >= 1:  # gimbal lock: tf2 returns yaw 0
+        return 0.0
+    cp = np.cos(-np.arcsin(m20))
+    return float(np.arctan2(m10 / cp, m00 / cp))
+
+
+def occupancy_from_pgm(img, negate=0, occupied_thresh=0.65, free_thresh=0.196):
+    """map_server's trinary PGM -> OccupancyGrid data (int8: 100 occupied, 0 free, -1 unknown)."""
+    v = np.asarray(img, dtype=np.float64)
+    p = v / 255.0 if negate else (255.0 - v) / 255.0
+    out = np.full(v.shape, -1, np.int8)
+    out[p > occupied_thresh] = 100
+    out[p < free_thresh] = 0
+    return out[::-1].copy()  # PGM row 0 is the top of the map; OccupancyGrid row 0 is the bottom (origin)
+
+
+def virtual_scan(grid, resolution, origin, template: LaserScan, poses, n_beams=None):
+    """virtual_scan_node.cpp:245-292 (VirtualScanNode, "copycat" mode): the LaserScan the saved map would produce
+    at each robot pose, with the template scan's angles and range_max.  grid: OccupancyGrid int8 [h][w]
+    (row 0 at origin); poses [B][3] = (x, y, yaw).  Returns float32 ranges [B][n_beams] (+inf = no hit)."""
+    g = _as_dev(grid, np.int8)
+    if g.dim() != 2:
+        raise RuntimeError("[VirtualScan] grid must be [height][width]")
+    P = np.ascontiguousarray(np.asarray(poses, np.float64).reshape(-1, 3))
+    n = int(n_beams if n_beams is not None else len(template.ranges))
+    out = D.empty((P.shape[0], n), "float32")
+    L.call("ot_virtual_scan", D.ptr(g), int(g.shape[0]), int(g.shape[1]), float(resolution), float(origin[0]),
+           float(origin[1]), P.shape[0], n, float(template.angle_min), float(template.angle_increment),
+           float(template.range_max), P.ctypes.data_as(C.c_void_p), D.ptr(out), D.stream_ptr())
+    return D.to_host(out)
 
 
 def _as_dev(a, dtype):

@@ -206,6 +206,37 @@ __global__ __launch_bounds__(256) void k_scan_diff(const float* __restrict__ rea
     gone_key[t * 2 + 1] = ky;
 }
 
+// ------------------------------------------------------------------------------------------- virtual scan
+// virtual_scan_node.cpp:258-290: per beam, march the ray from the robot in steps of one map resolution:
+// dist += res; p = robot + dist * (cos, sin)(global angle); cell = (int)((p - origin) / res); stop off-map; a cell
+// equal to 100 (occupied) returns dist as the range.  All double, as the node; cos / sin of the global angle come
+// from a host table (libm double cos / sin, as the node links).
+__global__ __launch_bounds__(256) void k_virtual_scan(const int8_t* __restrict__ grid, int height, int width,
+                                                      double res, double ox, double oy, int n_scans, int n_beams,
+                                                      double range_max, const double* __restrict__ robot,
+                                                      const double2* __restrict__ cs, float* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)n_scans * n_beams) return;
+    const int b = (int)(t / n_beams);
+    const double rx = robot[b * 2 + 0], ry = robot[b * 2 + 1];
+    const double2 c = cs[t];
+    float r = INFINITY;
+    double dist = 0.0;
+    while (dist < range_max) {
+        dist += res;
+        const double px = rx + dist * c.x;
+        const double py = ry + dist * c.y;
+        const int gx = (int)((px - ox) / res);
+        const int gy = (int)((py - oy) / res);
+        if (gx < 0 || gx >= width || gy < 0 || gy >= height) break;
+        if (grid[(int64_t)gy * width + gx] == 100) {
+            r = (float)dist;
+            break;
+        }
+    }
+    out[t] = r;
+}
+
 }  // namespace ot
 
 // time-decayed evidence grid of diff_node.cpp (host state; the per-scan update is O(cells))
@@ -317,6 +348,42 @@ ot_status ot_scan_diff(const float* real_ranges, const float* virtual_ranges, in
                        grid_resolution, new_flags, gone_flags, new_keys, gone_keys);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(stream));  // hp / cs are released on return
+    return OT_OK;
+}
+
+ot_status ot_virtual_scan(const int8_t* grid, int32_t height, int32_t width, float resolution, float origin_x,
+                          float origin_y, int32_t n_scans, int32_t n_beams, float angle_min, float angle_increment,
+                          float range_max, const double* poses_host, float* out_ranges, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!grid || !poses_host || !out_ranges || height <= 0 || width <= 0 || n_scans < 0 || n_beams < 0 ||
+        !(resolution > 0.0f) || (int64_t)height * width > 0x7FFFFFFF)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[VirtualScan] invalid arguments");
+    const int64_t nt = (int64_t)n_scans * n_beams;
+    if (nt == 0) return OT_OK;
+    // global beam angles as the node forms them: angle = angle_min + i * angle_increment (float), promoted to
+    // double and added to the robot yaw; their cos / sin from the host libm
+    std::vector<double2> cs((size_t)nt);
+    std::vector<double> robot((size_t)n_scans * 2);
+    for (int b = 0; b < n_scans; ++b) {
+        const double x = poses_host[b * 3 + 0], y = poses_host[b * 3 + 1], yaw = poses_host[b * 3 + 2];
+        robot[(size_t)b * 2] = x;
+        robot[(size_t)b * 2 + 1] = y;
+        for (int i = 0; i < n_beams; ++i) {
+            const double angle = angle_min + i * angle_increment;
+            const double g = yaw + angle;
+            cs[(size_t)b * n_beams + i] = make_double2(std::cos(g), std::sin(g));
+        }
+    }
+    double2* dcs = (double2*)scratch(sizeof(double2) * (size_t)nt + 64, 39);
+    double* drob = (double*)scratch(sizeof(double) * robot.size() + 64, 40);
+    if (!dcs || !drob) return fail(OT_ERR_HIP, "scratch allocation failed");
+    OT_HIP_TRY(hipMemcpyAsync(dcs, cs.data(), sizeof(double2) * cs.size(), hipMemcpyHostToDevice, stream));
+    OT_HIP_TRY(hipMemcpyAsync(drob, robot.data(), sizeof(double) * robot.size(), hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(k_virtual_scan, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, grid, height, width,
+                       (double)resolution, (double)origin_x, (double)origin_y, n_scans, n_beams, (double)range_max,
+                       (const double*)drob, (const double2*)dcs, out_ranges);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(stream));  // host tables are released on return
     return OT_OK;
 }
 

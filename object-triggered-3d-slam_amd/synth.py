@@ -267,3 +267,22 @@ def object_cloud(object_id: int, n_points: int = 100000, moved: bool = False):
     p[np.arange(n_points), ax] = side
     p += rng.normal(0, 0.002, p.shape)
     return p[p[:, 2] >= 0.03]
+
+
+def room_occupancy(resolution=0.05, margin=1.0):
+    """The saved map of laser_scan_batch's room as an OccupancyGrid (int8: 100 walls/pillars, 0 free, -1 outside),
+    origin at (-5 - margin, -4 - margin).  Returns (grid [h][w] int8, resolution, (origin_x, origin_y))."""
+    ox, oy = -5.0 - margin, -4.0 - margin
+    w = int(round((10.0 + 2 * margin) / resolution))
+    h = int(round((8.0 + 2 * margin) / resolution))
+    xs = ox + (np.arange(w) + 0.5) * resolution
+    ys = oy + (np.arange(h) + 0.5) * resolution
+    X, Y = np.meshgrid(xs, ys)
+    g = np.full((h, w), -1, np.int8)
+    inside = (X > -5.0) & (X < 5.0) & (Y > -4.0) & (Y < 4.0)
+    g[inside] = 0
+    wall = inside & ((X < -5.0 + resolution) | (X > 5.0 - resolution) | (Y < -4.0 + resolution) | (Y > 4.0 - resolution))
+    g[wall] = 100
+    for (x0, y0, x1, y1) in [(-2.2, -1.2, -1.8, -0.8), (1.8, 0.8, 2.2, 1.2), (-0.3, 2.0, 0.3, 2.6)]:
+        g[(X >= x0) & (X <= x1) & (Y >= y0) & (Y <= y1)] = 100
+    return g, resolution, (ox, oy)

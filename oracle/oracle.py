@@ -61,6 +61,8 @@ def lib():
             "oro_scan_diff": (None, [_p, _p, _i32, _i32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, _d,
                                      _i32, _p, _d, _p, _p, _p, _p]),
             "oro_change_grid_run": (_i64, [_p, _p, _i32, _i32, _p, _d, _d, _d, _p]),
+            "oro_virtual_scan": (None, [_p, _i32, _i32, C.c_float, C.c_float, C.c_float, _i32, _i32, C.c_float,
+                                        C.c_float, C.c_float, _p, _p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -293,3 +295,14 @@ def change_grid_run(keys, flags, dts, time_thresh, decay_rate, grid_res):
     out = np.zeros((max(n, 1), 3), np.float32)
     lib().oro_change_grid_run(_ptr(K), _ptr(F), B, N, _ptr(D), time_thresh, decay_rate, grid_res, _ptr(out))
     return out[:n].copy()
+
+
+def virtual_scan(grid, resolution, origin_x, origin_y, n_beams, angle_min, angle_increment, range_max, poses):
+    """virtual_scan_node.cpp:245-292 for poses [B][3] (x, y, yaw): float32 ranges [B][n_beams]."""
+    g = _c(grid, np.int8)
+    h, w = g.shape
+    P = _c(poses, np.float64).reshape(-1, 3)
+    out = np.empty((P.shape[0], n_beams), np.float32)
+    lib().oro_virtual_scan(_ptr(g), h, w, resolution, origin_x, origin_y, P.shape[0], n_beams, angle_min,
+                           angle_increment, range_max, _ptr(P), _ptr(out))
+    return out

@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <numeric>
 #include <unordered_map>
@@ -859,6 +860,36 @@ int64_t oro_change_grid_run(const int32_t* keys, const uint8_t* flags, int n_sca
             ++k;
         }
     return k;
+}
+
+/* VirtualScanNode::publish_virtual_scan (virtual_scan_node.cpp:245-292) for a batch of robot poses
+ * (poses [n][3] = x, y, yaw), written as the node does it. */
+void oro_virtual_scan(const int8_t* data, int height, int width, float resolution, float origin_x, float origin_y,
+                      int n_scans, int n_beams, float angle_min, float angle_increment, float range_max,
+                      const double* poses, float* out) {
+    for (int b = 0; b < n_scans; ++b) {
+        const double robot_x = poses[b * 3], robot_y = poses[b * 3 + 1], robot_yaw = poses[b * 3 + 2];
+        for (int i = 0; i < n_beams; ++i) {
+            float r = std::numeric_limits<float>::infinity();
+            const double angle = angle_min + i * angle_increment;
+            const double global_angle = robot_yaw + angle;
+            double dist = 0.0;
+            const double step = resolution;
+            while (dist < range_max) {
+                dist += step;
+                const double ray_x = robot_x + dist * cos(global_angle);
+                const double ray_y = robot_y + dist * sin(global_angle);
+                const int grid_x = (int)((ray_x - origin_x) / resolution);
+                const int grid_y = (int)((ray_y - origin_y) / resolution);
+                if (grid_x < 0 || grid_x >= width || grid_y < 0 || grid_y >= height) break;
+                if (data[grid_y * width + grid_x] == 100) {
+                    r = dist;
+                    break;
+                }
+            }
+            out[(int64_t)b * n_beams + i] = r;
+        }
+    }
 }
 
 /* hybrid_map.create_map_cloud (hybrid_map.py:25-60). */

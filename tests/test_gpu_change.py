@@ -85,3 +85,20 @@ def test_voxel_key_diff_bitexact(pkg, O, seq16, synth, gpu):
 
 def rr_all(O, b, origin):
     return O.voxel_key_diff(np.zeros((0, 3)), b, 0.05, origin)[1]
+
+
+def test_virtual_scan_bitexact(pkg, synth, O, gpu):
+    """virtual_scan_node.cpp:245-292: ray-marched ranges from the saved occupancy grid, bit-exact vs the oracle's
+    literal restatement, for a batch of robot poses (1440 beams, 10 m range as the node's LiDAR)."""
+    cd = pkg.change_detection
+    grid, res, origin = synth.room_occupancy(0.05)
+    rng = np.random.default_rng(8)
+    poses = np.stack([rng.uniform(-4, 4, 24), rng.uniform(-3, 3, 24), rng.uniform(-np.pi, np.pi, 24)], 1)
+    tmpl = cd.LaserScan(np.zeros(1440, np.float32), 0.0, float(np.float32(6.28 / 1440)), 10.0)
+    got = cd.virtual_scan(grid, res, origin, tmpl, poses)
+    ref = O.virtual_scan(grid, res, origin[0], origin[1], 1440, 0.0, float(np.float32(6.28 / 1440)), 10.0, poses)
+    assert np.isfinite(ref).mean() > 0.9
+    assert_bitwise(got, ref, "virtual scan ranges")
+    # robot outside the map: every ray leaves the grid at once
+    off = cd.virtual_scan(grid, res, origin, tmpl, [[50.0, 50.0, 0.0]])
+    assert np.isinf(off).all()

@@ -230,3 +230,17 @@ def test_scan_diff_and_grid_kat(O):
     flags = np.repeat(nf, 3, axis=0)
     assert len(O.change_grid_run(keys[:1], flags[:1], [1.0], 2.0, 0.5, 0.1)) == 0   # 1.0 <= 2.0
     assert len(O.change_grid_run(keys, flags, [1.0, 1.0, 1.0], 2.0, 0.5, 0.1)) == 1  # capped 3.0 > 2.0
+
+
+def test_virtual_scan_kat(O):
+    """A wall 1 m east of the robot on a 0.1 m grid: the eastward beam stops at the first step whose cell is the wall."""
+    g = np.zeros((20, 20), np.int8)
+    g[:, 15] = 100  # cells x in [1.5, 1.6) with origin 0
+    r = O.virtual_scan(g, 0.1, 0.0, 0.0, 4, 0.0, float(np.float32(np.pi / 2)), 10.0, np.array([[0.55, 1.05, 0.0]]))
+    d = 0.0
+    while True:
+        d += np.float64(np.float32(0.1))
+        if int((0.55 + d - 0.0) / np.float64(np.float32(0.1))) >= 15:
+            break
+    assert r[0, 0] == np.float32(d)
+    assert np.isinf(r[0, 2])  # westward beam leaves the map
