@@ -186,6 +186,8 @@ def main():
     if rank == 0 and args.cpu_frames > 0:
         cpu = cpu_baseline(depth, color, ext, intr_t, args)
     filt = filter_stream(args, L, lib, synth, torch, rank) if (args.filter_frames > 0 and rank == 0) else None
+    single = single_frame(L, synth, torch, depth, color, ext, intr_t) if (rank == 0 and args.cpu_frames > 0) \
+        else None
 
     out = {"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
@@ -195,13 +197,61 @@ def main():
                       "frames_per_step": args.frames, "width": W, "height": H, "voxel_length": args.voxel,
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
-           "roofline": roofline, "cpu_baseline": cpu, "filtered": filt, "objects": objects, "hybrid_map": hybrid}
+           "roofline": roofline, "cpu_baseline": cpu, "filtered": filt, "objects": objects, "hybrid_map": hybrid,
+           "single_frame": single}
     if rank == 0:
         print(json.dumps(out), flush=True)
     L.call("ot_tsdf_destroy", vol)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def single_frame(L, synth, torch, depth, color, ext, intr_t, reps=50):
+    """configs[0]: one 640x480 RGB-D frame -> create_from_color_and_depth (depth_trunc 5 m) ->
+    create_from_rgbd_image -> voxel_down_sample(0.005) (check_one_frame.py:22-28), the reference's own CPU case.
+    Reported beside the CPU restatement of the same calls on the same frame (the GPU slice is the parity case)."""
+    W, H = intr_t[0], intr_t[1]
+    npx = W * H
+    d16 = torch.from_numpy(depth[0].view(np.int16)).cuda().view(torch.uint16).contiguous()
+    col = torch.from_numpy(color[0]).cuda().contiguous()
+    df = torch.empty((H, W), dtype=torch.float32, device="cuda")
+    xyz = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    rgb = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    vx = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    vc = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+    intr = L.ot_intrinsics(W, H, *intr_t[2:])
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ident = np.eye(4)
+    P, K = C.c_int64(0), C.c_int64(0)
+    ptr = lambda t: C.c_void_p(t.data_ptr())
+
+    def run():
+        L.call("ot_depth_to_float", ptr(d16), ptr(df), npx, 1000.0, 5.0, stream)
+        L.call("ot_unproject", ptr(df), ptr(col), C.byref(intr), ident.ctypes.data_as(C.c_void_p), 1, ptr(xyz),
+               ptr(rgb), npx, C.byref(P), stream)
+        L.call("ot_voxel_down_sample", ptr(xyz), ptr(rgb), None, P.value, 0.005, ptr(vx), ptr(vc), None, None,
+               C.byref(K), stream)
+
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    gdt = (time.perf_counter() - t0) / reps
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    t1 = time.perf_counter()
+    for _ in range(3):
+        x, c = O.unproject(O.depth_to_float(depth[0], 1000.0, 5.0), color[0], intr_t, ident)
+        v = O.voxel_down_sample(x, c, 0.005)[0]
+    cdt = (time.perf_counter() - t1) / 3
+    return {"workload": "configs[0]: one 640x480 RGB-D frame, create_from_rgbd_image + voxel_down_sample(0.005) "
+                        "(check_one_frame.py:22-28)", "points": P.value, "voxels": K.value,
+            "gpu_ms": round(gdt * 1e3, 3), "cpu_ms": round(cdt * 1e3, 3), "cpu_voxels": int(v.shape[0]),
+            "cpu_kind": "port (serial, as Open3D's unprojection and voxel downsample)"}
 
 
 def _timed(torch, dist, world, fn, steps):

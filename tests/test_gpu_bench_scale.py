@@ -1,0 +1,59 @@
+"""GPU parity at the benchmark's full size (BASELINE.json configs[1]): the 256-frame 640x480 synthetic scan bench.py
+times, integrated at 5 mm through the same C-ABI entry point (ot_tsdf_integrate_u16, 32-frame fused batches), is
+bit-exact against the CPU oracle on every unit key, voxel weight and tsdf value; colours within 1e-4; and the
+exact voxel-update / unit-integration counters agree (they are the `roofline` accounting's inputs).
+The oracle takes ~5-10 s with OpenMP here."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_workload_bitexact(pkg, O, synth, gpu):
+    L = pkg._lib
+    lib = L.load()
+    intr_t = synth.REF_INTRINSICS_640
+    W, H = intr_t[0], intr_t[1]
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=0), n_frames=256, intr=intr_t)
+    d16 = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
+    col = torch.from_numpy(color).cuda().contiguous()
+    ext = np.ascontiguousarray(ext, dtype=np.float64)
+    intr = L.ot_intrinsics(W, H, *intr_t[2:])
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    vol = C.c_void_p()
+    L.call("ot_tsdf_create", 0.005, 0.04, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
+    try:
+        npx = W * H
+        for k in range(256):
+            st = lib.ot_tsdf_integrate_u16(vol, C.c_void_p(d16.data_ptr() + k * npx * 2),
+                                           C.c_void_p(col.data_ptr() + k * npx * 3), C.byref(intr),
+                                           ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
+            assert st == 0, lib.ot_last_error()
+        nu = C.c_int64(0)
+        L.call("ot_tsdf_num_units", vol, C.byref(nu))
+        keys = torch.empty((nu.value, 3), dtype=torch.int32, device="cuda")
+        tsdf = torch.empty((nu.value, 4096), dtype=torch.float32, device="cuda")
+        weight = torch.empty((nu.value, 4096), dtype=torch.float32, device="cuda")
+        colr = torch.empty((nu.value, 4096, 3), dtype=torch.float32, device="cuda")
+        L.call("ot_tsdf_export_units", vol, C.c_void_p(keys.data_ptr()), C.c_void_p(tsdf.data_ptr()),
+               C.c_void_p(weight.data_ptr()), C.c_void_p(colr.data_ptr()), stream)
+        upd, units = C.c_int64(0), C.c_int64(0)
+        L.call("ot_tsdf_counters", vol, C.byref(upd), C.byref(units))
+    finally:
+        L.call("ot_tsdf_destroy", vol)
+    ref = O.TSDF(0.005, 0.04, 1, 4)
+    for k in range(256):
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
+    rk, rt, rw, rc = ref.export()
+    assert nu.value == rk.shape[0] > 5000
+    assert_bitwise(keys.cpu().numpy(), rk, "unit keys (bench workload)")
+    assert_bitwise(weight.cpu().numpy(), rw, "voxel weights (bench workload)")
+    assert_bitwise(tsdf.cpu().numpy(), rt, "voxel tsdf (bench workload)")
+    np.testing.assert_allclose(colr.cpu().numpy(), rc, rtol=1e-4, atol=1e-4 * 255)
+    assert upd.value == ref.total_updates()
+    assert units.value == ref.unit_integrations()
