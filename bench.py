@@ -310,7 +310,7 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
     sizes = {}
 
     def run():
-        clouds = []
+        meshes = []
         for vol, (d16, col, ext) in zip(vols, dev):
             vol.reset()
             for k in range(ext.shape[0]):
@@ -321,8 +321,10 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
                     raise RuntimeError(lib.ot_last_error().decode())
             mesh = vol.extract_triangle_mesh()
             mesh.compute_vertex_normals()
-            pcd = mesh.sample_points_uniformly(number_of_points=100000)
-            clouds.append(pcd.filter_min_z(0.03)._xyz.dev())
+            meshes.append(mesh)
+        # the objects' 100k-point samplings in one call: their serial area-CDF chains run side by side
+        pcds = pkg.geometry.TriangleMesh.sample_points_uniformly_batch(meshes, number_of_points=100000)
+        clouds = [p.filter_min_z(0.03)._xyz.dev() for p in pcds]
         merged = D.merge_object_clouds(clouds)
         sizes["local"] = sum(int(c.shape[0]) for c in clouds)
         return merged

@@ -185,6 +185,23 @@ ot_status ot_mesh_sample_points_uniformly(const double* vertices, const double* 
                                           uint64_t seed, double* out_xyz, double* out_normals,
                                           double* out_colors, void* stream);
 
+/* The same sampling for several meshes in one call (e.g. the objects of a multi-object run on one GPU): results
+ * are identical to one ot_mesh_sample_points_uniformly call per mesh; the meshes' serial area-CDF chains run side
+ * by side instead of one after another.  jobs_host: host array; every pointer inside is a device pointer. */
+typedef struct ot_mesh_sample_job {
+    const double* vertices;
+    const double* vertex_normals;  /* may be NULL */
+    const double* vertex_colors;   /* may be NULL */
+    int64_t n_vertices;
+    const int32_t* triangles;
+    int64_t n_triangles;
+    double* out_xyz;               /* [n_points][3] */
+    double* out_normals;           /* may be NULL */
+    double* out_colors;            /* may be NULL */
+} ot_mesh_sample_job;
+ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs_host, int32_t n_jobs,
+                                                int64_t n_points, uint64_t seed, void* stream);
+
 /* ---------------------------------------------------------------------------------------------------
  * Hybrid map — fusion/hybrid_map.py
  * ------------------------------------------------------------------------------------------------- */

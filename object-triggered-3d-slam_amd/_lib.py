@@ -29,6 +29,12 @@ class ot_intrinsics(C.Structure):
                 ("cx", C.c_double), ("cy", C.c_double)]
 
 
+class ot_mesh_sample_job(C.Structure):
+    _fields_ = [("vertices", C.c_void_p), ("vertex_normals", C.c_void_p), ("vertex_colors", C.c_void_p),
+                ("n_vertices", C.c_int64), ("triangles", C.c_void_p), ("n_triangles", C.c_int64),
+                ("out_xyz", C.c_void_p), ("out_normals", C.c_void_p), ("out_colors", C.c_void_p)]
+
+
 _p = C.c_void_p
 _d = C.c_double
 _i32 = C.c_int32
@@ -66,6 +72,7 @@ SIGNATURES = {
     "ot_tsdf_fetch_triangle_mesh": [_p, _p, _p, _p, _p],
     "ot_mesh_compute_vertex_normals": [_p, _i64, _p, _i64, _p, _p],
     "ot_mesh_sample_points_uniformly": [_p, _p, _p, _i64, _p, _i64, _i64, C.c_uint64, _p, _p, _p, _p],
+    "ot_mesh_sample_points_uniformly_batch": [_p, _i32, _i64, C.c_uint64, _p],
     "ot_occupancy_to_points": [_p, _i32, _i32, _i32, _d, _d, _d, _p, _pi64, _p],
     "ot_grid_smart_paste": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _pi64, _p],
     "ot_voxel_key_diff": [_p, _i64, _p, _i64, _d, _p, _p, _pi64, _p, _pi64, _p],

@@ -10,6 +10,8 @@
 // then generated in parallel, one lane per output point: binary search of its triangle in the n_t array,
 // r1/r2 from a counter-based RNG (splitmix64 of seed + counter; Open3D's mt19937 is unseeded), barycentric
 // a = 1 - sqrt(r1), b = sqrt(r1)(1 - r2), c = sqrt(r1) r2.
+#include <vector>
+
 #include "compact.h"
 #include "sort.h"
 
@@ -146,9 +148,16 @@ __device__ inline void cdf_chunk(double2 v, double* lds, double& acc, int lane, 
     }
 }
 
+// one serial chain per workgroup (one wave): a single mesh, or one mesh of a batch (independent chains of
+// several meshes run side by side on different CUs)
+struct ChainJob {
+    const double* x;
+    int64_t n;
+    double* out;
+};
+
 template <bool CDF>
-__global__ __launch_bounds__(64) void k_serial_chain(const double* __restrict__ x, int64_t nt, double* __restrict__ out) {
-    __shared__ double lds[CDF_CHUNK];
+__device__ inline void serial_chain(const double* __restrict__ x, int64_t nt, double* __restrict__ out, double* lds) {
     const int lane = threadIdx.x;
     double acc = 0.0;  // sum: s = 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0 exactly
     double2 r[CDF_DEPTH];
@@ -163,6 +172,19 @@ __global__ __launch_bounds__(64) void k_serial_chain(const double* __restrict__ 
         }
     }
     if (!CDF && lane == 0) out[0] = acc;
+}
+
+template <bool CDF>
+__global__ __launch_bounds__(64) void k_serial_chain(const double* __restrict__ x, int64_t nt, double* __restrict__ out) {
+    __shared__ double lds[CDF_CHUNK];
+    serial_chain<CDF>(x, nt, out, lds);
+}
+
+template <bool CDF>
+__global__ __launch_bounds__(64) void k_serial_chain_batch(const ChainJob* __restrict__ jobs) {
+    __shared__ double lds[CDF_CHUNK];
+    const ChainJob j = jobs[blockIdx.x];
+    serial_chain<CDF>(j.x, j.n, j.out, lds);
 }
 
 __global__ __launch_bounds__(256) void k_area_div(const double* __restrict__ area, int64_t nt,
@@ -287,6 +309,65 @@ ot_status ot_mesh_sample_points_uniformly(const double* V, const double* VN, con
                        PC ? VC : nullptr, T, ncum, nt, n_points, (unsigned long long)seed, P, PN, PC);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
+}
+
+ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points,
+                                                uint64_t seed, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
+    if (n_jobs < 0 || (n_jobs > 0 && !jobs)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
+    if (n_jobs == 0) return OT_OK;
+    size_t bytes = 256;
+    for (int j = 0; j < n_jobs; ++j) {
+        const ot_mesh_sample_job& m = jobs[j];
+        if (m.n_triangles <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] Input mesh has no triangles.");
+        if (!m.vertices || !m.triangles || !m.out_xyz || (m.out_normals && !m.vertex_normals) ||
+            (m.out_colors && !m.vertex_colors) || m.n_vertices <= 0)
+            return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid arguments");
+        bytes += (size_t)m.n_triangles * 32 + 256;
+    }
+    char* ws = (char*)scratch(bytes + sizeof(ChainJob) * 2 * (size_t)n_jobs + 256, 17);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    std::vector<ChainJob> sum_jobs(n_jobs), cdf_jobs(n_jobs);
+    std::vector<double*> areas(n_jobs), qs(n_jobs), sums(n_jobs);
+    std::vector<long long*> ncums(n_jobs);
+    char* cur = ws;
+    for (int j = 0; j < n_jobs; ++j) {
+        const int64_t nt = jobs[j].n_triangles, nt2 = (nt + 1) & ~(int64_t)1;
+        sums[j] = (double*)cur;
+        areas[j] = sums[j] + 8;
+        qs[j] = areas[j] + nt2;
+        ncums[j] = (long long*)(qs[j] + nt2);
+        cur = (char*)(ncums[j] + nt2) + 64;
+        cur = (char*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
+        sum_jobs[j] = ChainJob{areas[j], nt, sums[j]};
+        cdf_jobs[j] = ChainJob{qs[j], nt, areas[j]};
+        hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, jobs[j].vertices,
+                           jobs[j].triangles, nt, areas[j]);
+    }
+    ChainJob* djobs = (ChainJob*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
+    OT_HIP_TRY(hipMemcpyAsync(djobs, sum_jobs.data(), sizeof(ChainJob) * n_jobs, hipMemcpyHostToDevice, stream));
+    OT_HIP_TRY(hipMemcpyAsync(djobs + n_jobs, cdf_jobs.data(), sizeof(ChainJob) * n_jobs, hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(k_serial_chain_batch<false>, dim3(n_jobs), dim3(64), 0, stream, (const ChainJob*)djobs);
+    for (int j = 0; j < n_jobs; ++j) {
+        const int64_t nt = jobs[j].n_triangles;
+        hipLaunchKernelGGL(k_area_div, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, (const double*)areas[j],
+                           nt, (const double*)sums[j], qs[j]);
+    }
+    hipLaunchKernelGGL(k_serial_chain_batch<true>, dim3(n_jobs), dim3(64), 0, stream, (const ChainJob*)(djobs + n_jobs));
+    for (int j = 0; j < n_jobs; ++j) {
+        const ot_mesh_sample_job& m = jobs[j];
+        const int64_t nt = m.n_triangles;
+        hipLaunchKernelGGL(k_round_counts, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, areas[j], nt,
+                           n_points, ncums[j]);
+        hipLaunchKernelGGL(k_sample, dim3((unsigned)((n_points + 255) / 256)), dim3(256), 0, stream, m.vertices,
+                           m.out_normals ? m.vertex_normals : nullptr, m.out_colors ? m.vertex_colors : nullptr,
+                           m.triangles, ncums[j], nt, n_points, (unsigned long long)seed, m.out_xyz, m.out_normals,
+                           m.out_colors);
+    }
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(stream));  // the host job tables are released on return
     return OT_OK;
 }
 

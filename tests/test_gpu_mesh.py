@@ -88,3 +88,22 @@ def test_z_filter_tail(O, meshes):
     assert_bitwise(np.asarray(out.points), rx, "filtered points")
     assert 0 < len(out.points) < 100000
     assert not out.has_normals()
+
+
+def test_sampling_batch_matches_single(pkg, O, synth, seq16, meshes):
+    """TriangleMesh.sample_points_uniformly_batch: the per-mesh clouds equal the single-mesh calls (and the oracle)
+    for meshes of different sizes sampled together."""
+    mesh, (V, VC, T) = meshes
+    mesh.compute_vertex_normals()
+    depth, color, ext = seq16
+    vol2, _ = _volumes(pkg, O, synth, depth[:1], color[:1], ext[:1], 0.02)
+    mesh2 = vol2.extract_triangle_mesh()
+    clouds = pkg.geometry.TriangleMesh.sample_points_uniformly_batch([mesh, mesh2, mesh], number_of_points=20000,
+                                                                     seed=5)
+    for m, c in zip([mesh, mesh2, mesh], clouds):
+        one = m.sample_points_uniformly(number_of_points=20000, seed=5)
+        assert_bitwise(np.asarray(c.points), np.asarray(one.points), "batched vs single sampling")
+        if m.has_vertex_normals():
+            assert_bitwise(np.asarray(c.normals), np.asarray(one.normals), "batched normals")
+    P, _, _ = O.sample_points_uniformly(V, T, 20000, 5, VN=O.vertex_normals(V, T), VC=VC)
+    assert_bitwise(np.asarray(clouds[0].points), P, "batched vs oracle")
