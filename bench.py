@@ -8,7 +8,7 @@ reconstruct_rgbd_filter.py:154-155) => weak scaling, no data-path collective; ba
 timing.  Prints ONE JSON line on rank 0.
 
 Also reported:
-  roofline     — dominant kernel (k_integrate): algorithmic bytes per launch (5*W*H + 40*U_f)
+  roofline     — dominant kernel (k_batch_integrate): algorithmic bytes per launch (5*W*H + 40*U_f)
                  over its mean device time measured with HIP events on the launch stream;
   cpu_baseline — the CPU oracle (strict-IEEE restatement of Open3D's ScalableTSDFVolume, OpenMP where Open3D
                  places it) on a bounded sample of the same frames, rank 0 only.
@@ -356,20 +356,27 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
     d_new = torch.from_numpy(new_map).cuda()
     d_base = torch.empty_like(d_old)
     occ = torch.empty((1024 * 1024, 3), dtype=torch.float64, device="cuda")
-    keys_a = torch.empty((120000, 3), dtype=torch.int32, device="cuda")
-    keys_r = torch.empty((120000, 3), dtype=torch.int32, device="cuda")
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     origin = (Cc.c_double * 3)(-1.0, -1.0, -1.0)
     stats = {}
 
+    # this rank's object clouds concatenated once (resident input), with host row offsets per object
+    empty = torch.zeros((0, 3), dtype=torch.float64, device="cuda")
+    cat_new = torch.cat(objs, 0).contiguous() if objs else empty
+    cat_old = torch.cat(saved, 0).contiguous() if saved else empty
+    off_new = np.concatenate([[0], np.cumsum([int(o.shape[0]) for o in objs])]).astype(np.int64)
+    off_old = np.concatenate([[0], np.cumsum([int(o.shape[0]) for o in saved])]).astype(np.int64)
+    keys_a = torch.empty((int(off_new[-1]) + 1, 4), dtype=torch.int32, device="cuda")
+    keys_r = torch.empty((int(off_old[-1]) + 1, 4), dtype=torch.int32, device="cuda")
+
     def run():
-        added = removed = 0
-        for a, b in zip(objs, saved):
-            na, nr = C.c_int64(0), C.c_int64(0)
-            L.call("ot_voxel_key_diff", C.c_void_p(a.data_ptr()), a.shape[0], C.c_void_p(b.data_ptr()), b.shape[0],
-                   0.02, origin, C.c_void_p(keys_a.data_ptr()), C.byref(na), C.c_void_p(keys_r.data_ptr()),
-                   C.byref(nr), stream)
-            added, removed = added + na.value, removed + nr.value
+        # change detection of every object vs its saved version: one multi-object voxel-key diff
+        na, nr = C.c_int64(0), C.c_int64(0)
+        if objs:
+                L.call("ot_voxel_key_diff_multi", C.c_void_p(cat_new.data_ptr()), off_new.ctypes.data_as(C.c_void_p),
+                   C.c_void_p(cat_old.data_ptr()), off_old.ctypes.data_as(C.c_void_p), len(objs), 0.02, origin,
+                   C.c_void_p(keys_a.data_ptr()), C.byref(na), C.c_void_p(keys_r.data_ptr()), C.byref(nr), stream)
+        added, removed = na.value, nr.value
         nq = C.c_int64(0)
         if rank == 0:
             d_base.copy_(d_old)

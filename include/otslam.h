@@ -231,6 +231,15 @@ ot_status ot_voxel_key_diff(const double* new_xyz, int64_t n, const double* old_
                             const double origin[3], int32_t* out_added, int64_t* n_added_host,
                             int32_t* out_removed, int64_t* n_removed_host, void* stream);
 
+/* The same for n_objects objects at once (a hybrid map's object clouds vs their saved versions): clouds are
+ * concatenated, object j = rows [offsets[j], offsets[j+1]) (host offsets, n_objects + 1 each); outputs are
+ * int32 [k][4] = (object, x, y, z), sorted by object then key.  Lattice coordinates must lie in (-2^16, 2^16);
+ * at most 2048 objects.  Equals n_objects calls of ot_voxel_key_diff. */
+ot_status ot_voxel_key_diff_multi(const double* new_xyz, const int64_t* new_offsets, const double* old_xyz,
+                                  const int64_t* old_offsets, int32_t n_objects, double voxel_size,
+                                  const double origin[3], int32_t* out_added, int64_t* n_added_host,
+                                  int32_t* out_removed, int64_t* n_removed_host, void* stream);
+
 /* diff_node.cpp:103-160 ChangeDetectorNode::scanCallback, batched: n_scans pairs of float ranges
  * [n_scans][n_beams] (real scan, virtual scan of the saved map).  Per beam: new_flags = a real return with no
  * virtual return within +-search_window beams closer than distance_threshold; gone_flags = the converse.

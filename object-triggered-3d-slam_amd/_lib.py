@@ -76,6 +76,7 @@ SIGNATURES = {
     "ot_occupancy_to_points": [_p, _i32, _i32, _i32, _d, _d, _d, _p, _pi64, _p],
     "ot_grid_smart_paste": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _pi64, _p],
     "ot_voxel_key_diff": [_p, _i64, _p, _i64, _d, _p, _p, _pi64, _p, _pi64, _p],
+    "ot_voxel_key_diff_multi": [_p, _p, _p, _p, _i32, _d, _p, _p, _pi64, _p, _pi64, _p],
     "ot_scan_diff": [_p, _p, _i32, _i32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, _d, _i32, _p, _d,
                      _p, _p, _p, _p, _p],
     "ot_virtual_scan": [_p, _i32, _i32, C.c_float, C.c_float, C.c_float, _i32, _i32, C.c_float, C.c_float,

@@ -80,6 +80,32 @@ def voxel_key_diff(new_cloud, old_cloud, voxel_size, origin):
     return D.to_host(added[:na.value]), D.to_host(removed[:nr.value])
 
 
+def voxel_key_diff_multi(new_clouds, old_clouds, voxel_size, origin):
+    """voxel_key_diff for many objects in one pass (object j of new_clouds vs object j of old_clouds).  Returns
+    (added, removed) as int32 [k][4] = (object, x, y, z), sorted by object then cell."""
+    if len(new_clouds) != len(old_clouds):
+        raise RuntimeError("[voxel_key_diff] new and old object lists differ in length")
+    import torch
+
+    def cat(clouds):
+        parts = [_xyz_dev(c) for c in clouds]
+        off = np.zeros(len(parts) + 1, np.int64)
+        off[1:] = np.cumsum([int(p.shape[0]) for p in parts])
+        xyz = torch.cat(parts, 0).contiguous() if parts else D.empty((0, 3), "float64")
+        return xyz, off
+
+    a, oa = cat(new_clouds)
+    b, ob = cat(old_clouds)
+    added = D.empty((max(int(oa[-1]), 1), 4), "int32")
+    removed = D.empty((max(int(ob[-1]), 1), 4), "int32")
+    na, nr = C.c_int64(0), C.c_int64(0)
+    o = (C.c_double * 3)(*[float(v) for v in origin])
+    L.call("ot_voxel_key_diff_multi", D.ptr(a) if oa[-1] else None, oa.ctypes.data_as(C.c_void_p),
+           D.ptr(b) if ob[-1] else None, ob.ctypes.data_as(C.c_void_p), len(new_clouds), float(voxel_size), o,
+           D.ptr(added), C.byref(na), D.ptr(removed), C.byref(nr), D.stream_ptr())
+    return D.to_host(added[:na.value]), D.to_host(removed[:nr.value])
+
+
 def _xyz_dev(c):
     if hasattr(c, "_xyz"):
         return c._xyz.dev()

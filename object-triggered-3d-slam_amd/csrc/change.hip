@@ -119,6 +119,75 @@ static ot_status unique_keys(const double* xyz, int64_t n, double vs, const doub
     return OT_OK;
 }
 
+// Multi-object form: key = object id (11 bits) | x, y, z (17 bits each, biased by 2^16), so ONE sort / unique /
+// set difference serves every object of a hybrid map; equal keys imply the same object.
+constexpr int MK_BITS = 17;
+constexpr int MK_BIAS = 1 << 16;
+
+__global__ __launch_bounds__(256) void k_lattice_keys_obj(const double* __restrict__ xyz, int64_t n, int obj,
+                                                          double vs, double ox, double oy, double oz,
+                                                          unsigned long long* keys, int* err) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double f[3] = {floor((xyz[i * 3 + 0] - ox) / vs), floor((xyz[i * 3 + 1] - oy) / vs),
+                         floor((xyz[i * 3 + 2] - oz) / vs)};
+    unsigned long long k = (unsigned long long)obj;
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        ok = ok && fabs(f[a]) < (double)MK_BIAS;
+        k = (k << MK_BITS) | (unsigned long long)(ok ? (int)f[a] + MK_BIAS : 0);
+    }
+    if (!ok) *err = 1;
+    keys[i] = k;
+}
+
+struct ObjKeyEmit {
+    const unsigned long long* a;
+    int32_t* out;  // [k][4]: object, x, y, z
+    __device__ void operator()(int64_t i, int64_t pos) const {
+        const unsigned long long k = a[i];
+        const unsigned m = (1u << MK_BITS) - 1u;
+        out[pos * 4 + 0] = (int)(k >> (3 * MK_BITS));
+        out[pos * 4 + 1] = (int)((k >> (2 * MK_BITS)) & m) - MK_BIAS;
+        out[pos * 4 + 2] = (int)((k >> MK_BITS) & m) - MK_BIAS;
+        out[pos * 4 + 3] = (int)(k & m) - MK_BIAS;
+    }
+};
+
+// sorted unique object-lattice keys of the concatenated clouds of n_obj objects (offsets: host, n_obj + 1)
+static ot_status unique_obj_keys(const double* xyz, const int64_t* off, int n_obj, double vs, const double o[3],
+                                 unsigned long long* uniq, int64_t* nu, int slot, hipStream_t stream) {
+    *nu = 0;
+    const int64_t n = off[n_obj];
+    if (n == 0) return OT_OK;
+    char* ws = (char*)scratch(256 + (size_t)n * (8 + 8 + 4 + 4), slot);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    int* err = (int*)ws;
+    unsigned long long* kin = (unsigned long long*)(ws + 256);
+    unsigned long long* kout = kin + n;
+    unsigned* vin = (unsigned*)(kout + n);
+    unsigned* vout = vin + n;
+    OT_HIP_TRY(hipMemsetAsync(err, 0, sizeof(int), stream));
+    for (int j = 0; j < n_obj; ++j) {
+        const int64_t m = off[j + 1] - off[j];
+        if (m > 0)
+            hipLaunchKernelGGL(k_lattice_keys_obj, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
+                               xyz + off[j] * 3, m, j, vs, o[0], o[1], o[2], kin + off[j], err);
+    }
+    OT_LAUNCH_CHECK();
+    int bits = 3 * MK_BITS;
+    while (bits < 64 && ((unsigned long long)(n_obj - 1) >> (bits - 3 * MK_BITS)) != 0) ++bits;
+    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, bits, stream, 3);  // values unused
+    if (st != OT_OK) return st;
+    st = compact(n, UniqPred{kout}, UniqEmit{kout, uniq}, stream, nu, slot + 1);  // synchronises
+    if (st != OT_OK) return st;
+    int e = 0;
+    OT_HIP_TRY(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
+    if (e) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] lattice key out of range (voxel_size too small)");
+    return OT_OK;
+}
+
 // ------------------------------------------------------------------------------------------- scan diff
 struct ScanPose {
     double tx, ty, cyaw, syaw;  // translation and cos / sin of the map-frame yaw (host-computed)
@@ -304,6 +373,41 @@ ot_status ot_voxel_key_diff(const double* new_xyz, int64_t n, const double* old_
     if (nb > 0) {
         if (!out_removed) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] out_removed is NULL");
         st = compact(nb, AbsentPred{ub, ua, na}, KeyEmit{ub, out_removed}, stream, n_removed_host, 36);
+        if (st != OT_OK) return st;
+    }
+    return OT_OK;
+}
+
+ot_status ot_voxel_key_diff_multi(const double* new_xyz, const int64_t* new_offsets, const double* old_xyz,
+                                  const int64_t* old_offsets, int32_t n_objects, double voxel_size,
+                                  const double origin[3], int32_t* out_added, int64_t* n_added_host,
+                                  int32_t* out_removed, int64_t* n_removed_host, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!n_added_host || !n_removed_host || !origin || !new_offsets || !old_offsets || n_objects < 0 ||
+        n_objects > (1 << 11))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] invalid arguments");
+    *n_added_host = *n_removed_host = 0;
+    if (!(voxel_size > 0.0)) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] voxel_size <= 0.");
+    if (n_objects == 0) return OT_OK;
+    const int64_t n = new_offsets[n_objects], m = old_offsets[n_objects];
+    if (n < 0 || m < 0 || (n > 0 && !new_xyz) || (m > 0 && !old_xyz) || n > 0x7FFFFFFF || m > 0x7FFFFFFF)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] invalid buffers");
+    unsigned long long* ua = (unsigned long long*)scratch((size_t)std::max<int64_t>(n, 1) * 8 + 64, 31);
+    unsigned long long* ub = (unsigned long long*)scratch((size_t)std::max<int64_t>(m, 1) * 8 + 64, 32);
+    if (!ua || !ub) return fail(OT_ERR_HIP, "scratch allocation failed");
+    int64_t na = 0, nb = 0;
+    ot_status st = unique_obj_keys(new_xyz, new_offsets, n_objects, voxel_size, origin, ua, &na, 33, stream);
+    if (st != OT_OK) return st;
+    st = unique_obj_keys(old_xyz, old_offsets, n_objects, voxel_size, origin, ub, &nb, 33, stream);
+    if (st != OT_OK) return st;
+    if (na > 0) {
+        if (!out_added) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] out_added is NULL");
+        st = compact(na, AbsentPred{ua, ub, nb}, ObjKeyEmit{ua, out_added}, stream, n_added_host, 35);
+        if (st != OT_OK) return st;
+    }
+    if (nb > 0) {
+        if (!out_removed) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] out_removed is NULL");
+        st = compact(nb, AbsentPred{ub, ua, na}, ObjKeyEmit{ub, out_removed}, stream, n_removed_host, 36);
         if (st != OT_OK) return st;
     }
     return OT_OK;

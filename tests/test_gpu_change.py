@@ -102,3 +102,21 @@ def test_virtual_scan_bitexact(pkg, synth, O, gpu):
     # robot outside the map: every ray leaves the grid at once
     off = cd.virtual_scan(grid, res, origin, tmpl, [[50.0, 50.0, 0.0]])
     assert np.isinf(off).all()
+
+
+def test_voxel_key_diff_multi_matches_single(pkg, synth, gpu):
+    """voxel_key_diff_multi over several objects == one voxel_key_diff per object (object column + cells)."""
+    cd = pkg.change_detection
+    new = [synth.object_cloud(i, n_points=20000) for i in range(6)]
+    old = [synth.object_cloud(i, n_points=20000, moved=True) for i in range(6)]
+    new[4] = np.zeros((0, 3))  # an object missing from the new scan: everything removed
+    origin = (-1.0, -1.0, -1.0)
+    added, removed = cd.voxel_key_diff_multi(new, old, 0.02, origin)
+    ra, rr = [], []
+    for j in range(6):
+        a, r = cd.voxel_key_diff(new[j], old[j], 0.02, origin)
+        ra.append(np.concatenate([np.full((len(a), 1), j, np.int32), a], 1))
+        rr.append(np.concatenate([np.full((len(r), 1), j, np.int32), r], 1))
+    assert_bitwise(added, np.concatenate(ra), "multi added")
+    assert_bitwise(removed, np.concatenate(rr), "multi removed")
+    assert (removed[:, 0] == 4).sum() > 0 and (added[:, 0] == 4).sum() == 0
