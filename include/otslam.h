@@ -185,9 +185,15 @@ ot_status ot_mesh_sample_points_uniformly(const double* vertices, const double* 
                                           uint64_t seed, double* out_xyz, double* out_normals,
                                           double* out_colors, void* stream);
 
+/* mesh.get_surface_area() — Open3D TriangleMesh::GetSurfaceArea, the first of SamplePointsUniformly's two serial
+ * float64 chains (reconstruct_rgbd_filter.py:123): ((0 + a_0) + a_1) + ... over the triangle areas in index order,
+ * bit-exact.  area_host: host double. */
+ot_status ot_mesh_get_surface_area(const double* vertices, int64_t n_vertices, const int32_t* triangles,
+                                   int64_t n_triangles, double* area_host, void* stream);
+
 /* The same sampling for several meshes in one call (e.g. the objects of a multi-object run on one GPU): results
- * are identical to one ot_mesh_sample_points_uniformly call per mesh; the meshes' serial area-CDF chains run side
- * by side instead of one after another.  jobs_host: host array; every pointer inside is a device pointer. */
+ * are identical to one ot_mesh_sample_points_uniformly call per mesh; the meshes' area sums and CDFs are computed
+ * side by side.  jobs_host: host array; every pointer inside is a device pointer. */
 typedef struct ot_mesh_sample_job {
     const double* vertices;
     const double* vertex_normals;  /* may be NULL */

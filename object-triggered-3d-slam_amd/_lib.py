@@ -73,6 +73,7 @@ SIGNATURES = {
     "ot_mesh_compute_vertex_normals": [_p, _i64, _p, _i64, _p, _p],
     "ot_mesh_sample_points_uniformly": [_p, _p, _p, _i64, _p, _i64, _i64, C.c_uint64, _p, _p, _p, _p],
     "ot_mesh_sample_points_uniformly_batch": [_p, _i32, _i64, C.c_uint64, _p],
+    "ot_mesh_get_surface_area": [_p, _i64, _p, _i64, C.POINTER(C.c_double), _p],
     "ot_occupancy_to_points": [_p, _i32, _i32, _i32, _d, _d, _d, _p, _pi64, _p],
     "ot_grid_smart_paste": [_p, _p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _pi64, _p],
     "ot_voxel_key_diff": [_p, _i64, _p, _i64, _d, _p, _p, _pi64, _p, _pi64, _p],
@@ -96,6 +97,12 @@ class OTError(RuntimeError):
     """Raised for any non-OK status; message mirrors Open3D's utility::LogError text."""
 
 
+# test hooks exported by the library but outside the drop-in boundary (not declared in include/otslam.h)
+TEST_SIGNATURES = {
+    "otx_serial_chain_f64": [_p, _i64, _i32, _p, _p],
+}
+
+
 def load():
     """Load libotslam_hip.so (raises RuntimeError, never falls back)."""
     global _lib
@@ -108,7 +115,7 @@ def load():
             raise RuntimeError(f"HIP extension missing: {LIB_PATH} (run __graft_entry__.build())")
         lib = C.CDLL(LIB_PATH)
         missing = []
-        for name, argtypes in SIGNATURES.items():
+        for name, argtypes in {**SIGNATURES, **TEST_SIGNATURES}.items():
             try:
                 f = getattr(lib, name)
             except AttributeError:

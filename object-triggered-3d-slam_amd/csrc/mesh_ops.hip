@@ -102,89 +102,265 @@ __global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V,
 }
 
 // Open3D's sequential recurrences (GetSurfaceArea: s = (((a0 + a1) + a2) + ...), then the CDF loop
-// cdf_t = a_t / s + cdf_{t-1}) are serial float64 chains, kept in their exact order by ONE wave: the wave streams
-// the input with coalesced 16-B-per-lane loads kept CDF_DEPTH chunks ahead, parks each 128-value chunk in LDS,
-// and lane 0 runs the dependent v_add_f64 chain over it (ds_read_b128 operands).  The divisions a_t / s are a
-// separate lane-parallel pass; the CDF chunk goes back through LDS to one coalesced store.  Padding adds +0.0,
-// an exact no-op for these non-negative sums.
-constexpr int CDF_CHUNK = 128;  // values per chunk (2 per lane)
-constexpr int CDF_DEPTH = 8;    // chunks in flight
+// cdf_t = a_t / s + cdf_{t-1}) are serial float64 chains whose every rounding must be reproduced.  They are
+// computed exactly in parallel from one identity: while the running value s stays inside one binade
+// [2^e, 2^(e+1)) (grid spacing u = 2^(e-52)), fl(s + a) = s + u * rint(a / u) for any a >= 0 that is not a tie
+// (a / u exactly k + 1/2).  So inside a binade the chain is an INTEGER prefix sum of r_t = rint(a_t / u),
+// independent of s.  The input is cut into 256-value chunks:
+//   k_chain_bsum   approximate chunk sums (any order)            -> bsum
+//   k_chain_guess  approximate exclusive prefix -> guessed binade e_b of s at each chunk start
+//   k_chain_chunk  M_b = sum r_t at u_b = 2^(e_b-52), flag ties / negative / non-finite / r >= 2^53
+//   k_chain_walk   one wave per chain: from the exact s at a chunk start it accepts a run of chunks at once
+//                  (wave prefix of M_b) while e(s) == e_b, no flag and N + prefix <= 2^53 - 1 (N = s / u, so
+//                  every intermediate sum stays inside the binade); any other chunk (s == 0 at the start,
+//                  binade crossing, tie, wrong guess) is walked serially in Open3D's order by one lane
+//   k_chain_emit   (CDF) every accepted chunk's values (N_b + prefix_t) * u_b, exact integers times 2^k
+// The guesses only decide which chunks take the fast path; every accepted value is proven exact by the walk's
+// check, so any input (zeros, ties, NaN, huge ranges) gives the serial chain's bits.
+constexpr int CH = 256;                // values per chunk: 64 lanes x 4
+constexpr int EX_NONE = -100000;       // no usable binade guess
+constexpr long long R_MAX = 1ll << 53;
 
-__device__ inline double2 cdf_load(const double* __restrict__ x, int64_t nt, int64_t base, int lane) {
-    const int64_t i = base + 2 * lane;
-    if (i + 1 < nt) return *reinterpret_cast<const double2*>(x + i);  // x is 16-B aligned, base even
-    return make_double2(i < nt ? x[i] : 0.0, 0.0);
+struct ChainJob {
+    const double* x;  // 16-B aligned input
+    int64_t n;
+    double* out;  // CDF values (n), or the sum (out[0])
+    double* bsum;
+    int32_t* ex;
+    long long* msum;
+    int32_t* kind;  // 0 fast, 1 flagged by k_chain_chunk, 2 walked serially
+    double* start;  // exact s entering each fast chunk
+};
+
+__device__ inline double pow2(int k) { return __longlong_as_double((long long)(k + 1023) << 52); }
+
+// binade exponent of a positive finite s inside the range pow2() covers for both u and 1/u, else EX_NONE
+__device__ inline int binade(double s) {
+    if (!(s > 0.0) || !(s < 1e300)) return EX_NONE;
+    const int e = (int)((__double_as_longlong(s) >> 52) & 0x7FF) - 1023;
+    return e >= -960 ? e : EX_NONE;
+}
+
+__device__ inline void chunk_load4(const double* __restrict__ x, int64_t n, int64_t base, int lane, double v[4]) {
+    const int64_t i = base + 4 * lane;
+    if (i + 3 < n) {
+        const double2 p = *reinterpret_cast<const double2*>(x + i);
+        const double2 q = *reinterpret_cast<const double2*>(x + i + 2);
+        v[0] = p.x, v[1] = p.y, v[2] = q.x, v[3] = q.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = i + k < n ? x[i + k] : 0.0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_chain_bsum(const ChainJob* __restrict__ jobs) {
+    const ChainJob j = jobs[blockIdx.y];
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nb = (j.n + CH - 1) / CH;
+    if (b >= nb) return;
+    const int lane = threadIdx.x & 63;
+    double v[4];
+    chunk_load4(j.x, j.n, b * CH, lane, v);
+    double s = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) j.bsum[b] = s;
+}
+
+__global__ __launch_bounds__(256) void k_chain_guess(const ChainJob* __restrict__ jobs) {
+    __shared__ double sh[256];
+    const ChainJob j = jobs[blockIdx.x];
+    const int t = threadIdx.x;
+    const int64_t nb = (j.n + CH - 1) / CH, per = (nb + 255) / 256;
+    const int64_t lo = t * per, hi = lo + per < nb ? lo + per : nb;
+    double loc = 0.0;
+    for (int64_t i = lo; i < hi; ++i) loc += j.bsum[i];
+    sh[t] = loc;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {  // Hillis-Steele inclusive scan
+        const double o = t >= d ? sh[t - d] : 0.0;
+        __syncthreads();
+        sh[t] += o;
+        __syncthreads();
+    }
+    double p = sh[t] - loc;  // approximate exclusive prefix (only a guess)
+    for (int64_t i = lo; i < hi; ++i) {
+        j.ex[i] = binade(p);
+        p += j.bsum[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_chain_chunk(const ChainJob* __restrict__ jobs) {
+    const ChainJob j = jobs[blockIdx.y];
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nb = (j.n + CH - 1) / CH;
+    if (b >= nb) return;
+    const int lane = threadIdx.x & 63;
+    const int e = j.ex[b];
+    bool bad = e == EX_NONE;
+    long long r = 0;
+    if (!bad) {
+        double v[4];
+        chunk_load4(j.x, j.n, b * CH, lane, v);
+        const double scale = pow2(52 - e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double m = v[k] * scale;  // exact: power-of-two scaling
+            const bool ok = m >= 0.0 && m < (double)R_MAX && m - floor(m) != 0.5;
+            bad |= !ok;
+            r += ok ? (long long)rint(m) : 0;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    const bool any_bad = __ballot(bad) != 0;
+    if (lane == 0) {
+        j.msum[b] = r < R_MAX ? r : R_MAX;  // saturated: such a chunk fails the walk's range check anyway
+        j.kind[b] = any_bad ? 1 : 0;
+    }
+}
+
+// one chunk in Open3D's order from s (lane 0, operands staged in LDS); CDF values stored coalesced
+template <bool CDF>
+__device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, double* lds, int lane) {
+    double v[4];
+    chunk_load4(j.x, j.n, b * CH, lane, v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lds[4 * lane + k] = v[k];
+    __syncthreads();
+    const int64_t base = b * CH;
+    const int cnt = j.n - base < CH ? (int)(j.n - base) : CH;
+    if (lane == 0) {
+        double acc = s;
+        for (int k = 0; k < cnt; ++k) {
+            acc = lds[k] + acc;
+            if (CDF) lds[k] = acc;
+        }
+        lds[CH] = acc;
+    }
+    __syncthreads();
+    const double out = lds[CH];
+    if (CDF) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = base + 4 * lane + k;
+            if (i < j.n) j.out[i] = lds[4 * lane + k];
+        }
+    }
+    __syncthreads();
+    return out;
 }
 
 template <bool CDF>
-__device__ inline void cdf_chunk(double2 v, double* lds, double& acc, int lane, int64_t base, int64_t nt,
-                                 double* __restrict__ out) {
-    reinterpret_cast<double2*>(lds)[lane] = v;
-    __syncthreads();
-    if (lane == 0) {
-#pragma unroll 8
-        for (int k = 0; k < CDF_CHUNK; k += 2) {
-            const double2 p = reinterpret_cast<const double2*>(lds)[k >> 1];
-            if (CDF) {
-                double2 r;
-                acc = p.x + acc;
-                r.x = acc;
-                acc = p.y + acc;
-                r.y = acc;
-                reinterpret_cast<double2*>(lds)[k >> 1] = r;
-            } else {
-                acc = acc + p.x;
-                acc = acc + p.y;
+__global__ __launch_bounds__(64) void k_chain_walk(const ChainJob* __restrict__ jobs) {
+    __shared__ double lds[CH + 2];
+    const ChainJob j = jobs[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int64_t nb = (j.n + CH - 1) / CH;
+    double s = 0.0;  // sum: 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0
+    int e_n = EX_NONE, k_n = 1;
+    long long m_n = 0;
+    if (lane < nb) e_n = j.ex[lane], m_n = j.msum[lane], k_n = j.kind[lane];
+    for (int64_t g = 0; g < nb; g += 64) {
+        const int64_t b = g + lane;
+        const int e_b = e_n, k_b = k_n;
+        const long long m_b = m_n;
+        if (b + 64 < nb) e_n = j.ex[b + 64], m_n = j.msum[b + 64], k_n = j.kind[b + 64];  // next group in flight
+        const int lim = nb - g < 64 ? (int)(nb - g) : 64;
+        int local = 0;
+        while (local < lim) {
+            const int e = binade(s);
+            if (e != EX_NONE) {
+                const double u = pow2(e - 52);
+                const long long N = (long long)(s * pow2(52 - e));  // exact integer in [2^52, 2^53)
+                const bool act = lane >= local;
+                const long long v = act ? m_b : 0;
+                long long incl = v;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const long long t = __shfl_up(incl, d);
+                    if (lane >= d) incl += t;
+                }
+                const bool ok = lane < lim && e_b == e && k_b == 0 && N + incl <= R_MAX - 1;
+                const unsigned long long badm = __ballot(act && !ok);
+                int fb = badm ? __ffsll((long long)badm) - 1 : 64;
+                fb = fb < lim ? fb : lim;
+                if (fb > local) {
+                    if (act && lane < fb) j.start[b] = (double)(N + incl - v) * u;
+                    const long long tot = __shfl(incl, fb - 1);
+                    s = (double)(N + tot) * u;
+                    local = fb;
+                }
+            }
+            if (local < lim) {  // not provable from s: walk this chunk serially
+                s = chain_serial_chunk<CDF>(j, g + local, s, lds, lane);
+                if (lane == 0) j.kind[g + local] = 2;
+                ++local;
             }
         }
     }
-    __syncthreads();
-    if (CDF) {
-        const double2 r = reinterpret_cast<const double2*>(lds)[lane];
-        const int64_t i = base + 2 * lane;
-        if (i + 1 < nt) *reinterpret_cast<double2*>(out + i) = r;
-        else if (i < nt) out[i] = r.x;
-        __syncthreads();
+    if (!CDF && lane == 0) j.out[0] = s;
+}
+
+__global__ __launch_bounds__(256) void k_chain_emit(const ChainJob* __restrict__ jobs) {
+    const ChainJob j = jobs[blockIdx.y];
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nb = (j.n + CH - 1) / CH;
+    if (b >= nb || j.kind[b] != 0) return;
+    const int lane = threadIdx.x & 63;
+    const int e = j.ex[b];
+    const double u = pow2(e - 52), scale = pow2(52 - e);
+    const long long N = (long long)(j.start[b] * scale);
+    double v[4];
+    chunk_load4(j.x, j.n, b * CH, lane, v);
+    long long r[4], loc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        loc += (long long)rint(v[k] * scale);
+        r[k] = loc;
+    }
+    long long incl = loc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const long long t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    const long long base = N + incl - loc;
+    double o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (double)(base + r[k]) * u;
+    const int64_t i = b * CH + 4 * lane;
+    if (i + 3 < j.n) {
+        *reinterpret_cast<double2*>(j.out + i) = make_double2(o[0], o[1]);
+        *reinterpret_cast<double2*>(j.out + i + 2) = make_double2(o[2], o[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i + k < j.n) j.out[i + k] = o[k];
     }
 }
 
-// one serial chain per workgroup (one wave): a single mesh, or one mesh of a batch (independent chains of
-// several meshes run side by side on different CUs)
-struct ChainJob {
-    const double* x;
-    int64_t n;
-    double* out;
-};
-
+// the chains of n_jobs independent inputs (device job table), side by side
 template <bool CDF>
-__device__ inline void serial_chain(const double* __restrict__ x, int64_t nt, double* __restrict__ out, double* lds) {
-    const int lane = threadIdx.x;
-    double acc = 0.0;  // sum: s = 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0 exactly
-    double2 r[CDF_DEPTH];
-#pragma unroll
-    for (int d = 0; d < CDF_DEPTH; ++d) r[d] = cdf_load(x, nt, (int64_t)d * CDF_CHUNK, lane);
-    for (int64_t base = 0; base < nt; base += (int64_t)CDF_CHUNK * CDF_DEPTH) {
-#pragma unroll
-        for (int d = 0; d < CDF_DEPTH; ++d) {
-            const int64_t b = base + (int64_t)d * CDF_CHUNK;
-            if (b < nt) cdf_chunk<CDF>(r[d], lds, acc, lane, b, nt, out);
-            r[d] = cdf_load(x, nt, b + (int64_t)CDF_CHUNK * CDF_DEPTH, lane);
-        }
-    }
-    if (!CDF && lane == 0) out[0] = acc;
+void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream) {
+    const int64_t nb = (max_n + CH - 1) / CH;
+    const dim3 grid((unsigned)((nb + 3) / 4), (unsigned)n_jobs);
+    hipLaunchKernelGGL(k_chain_bsum, grid, dim3(256), 0, stream, djobs);
+    hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(256), 0, stream, djobs);
+    hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
+    hipLaunchKernelGGL(k_chain_walk<CDF>, dim3(n_jobs), dim3(64), 0, stream, djobs);
+    if (CDF) hipLaunchKernelGGL(k_chain_emit, grid, dim3(256), 0, stream, djobs);
 }
 
-template <bool CDF>
-__global__ __launch_bounds__(64) void k_serial_chain(const double* __restrict__ x, int64_t nt, double* __restrict__ out) {
-    __shared__ double lds[CDF_CHUNK];
-    serial_chain<CDF>(x, nt, out, lds);
-}
+// per-chain auxiliary arrays (reused by the sum and the CDF chains, which run one after the other)
+inline size_t chain_aux_bytes(int64_t n) { return (size_t)((n + CH - 1) / CH + 1) * 40 + 256; }
 
-template <bool CDF>
-__global__ __launch_bounds__(64) void k_serial_chain_batch(const ChainJob* __restrict__ jobs) {
-    __shared__ double lds[CDF_CHUNK];
-    const ChainJob j = jobs[blockIdx.x];
-    serial_chain<CDF>(j.x, j.n, j.out, lds);
+inline char* chain_aux(char* cur, int64_t n, ChainJob& jb) {
+    const int64_t nb = (n + CH - 1) / CH + 1;
+    jb.bsum = (double*)cur;
+    jb.start = jb.bsum + nb;
+    jb.msum = (long long*)(jb.start + nb);
+    jb.ex = (int32_t*)(jb.msum + nb);
+    jb.kind = jb.ex + nb;
+    cur = (char*)(jb.kind + nb);
+    return (char*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
 }
 
 __global__ __launch_bounds__(256) void k_area_div(const double* __restrict__ area, int64_t nt,
@@ -286,30 +462,9 @@ ot_status ot_mesh_compute_vertex_normals(const double* V, int64_t nv, const int3
 
 ot_status ot_mesh_sample_points_uniformly(const double* V, const double* VN, const double* VC, int64_t nv,
                                           const int32_t* T, int64_t nt, int64_t n_points, uint64_t seed, double* P,
-                                          double* PN, double* PC, void* stream_) {
-    hipStream_t stream = S(stream_);
-    if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
-    if (nt <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] Input mesh has no triangles.");
-    if (!V || !T || !P || (PN && !VN) || (PC && !VC) || nv <= 0)
-        return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid arguments");
-    char* ws = (char*)scratch((size_t)nt * 32 + 256, 17);
-    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-    double* sum = (double*)ws;
-    double* area = sum + 8;  // 64-B offset: 16-B aligned rows for the chain's double2 loads
-    double* q = area + ((nt + 1) & ~(int64_t)1);  // 16-B aligned for the chain's double2 loads
-    long long* ncum = (long long*)(q + ((nt + 1) & ~(int64_t)1));
-    hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, V, T, nt, area);
-    hipLaunchKernelGGL(k_serial_chain<false>, dim3(1), dim3(64), 0, stream, (const double*)area, nt, sum);
-    hipLaunchKernelGGL(k_area_div, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, (const double*)area, nt,
-                       (const double*)sum, q);
-    hipLaunchKernelGGL(k_serial_chain<true>, dim3(1), dim3(64), 0, stream, (const double*)q, nt, area);
-    hipLaunchKernelGGL(k_round_counts, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, area, nt, n_points,
-                       ncum);
-    hipLaunchKernelGGL(k_sample, dim3((unsigned)((n_points + 255) / 256)), dim3(256), 0, stream, V, PN ? VN : nullptr,
-                       PC ? VC : nullptr, T, ncum, nt, n_points, (unsigned long long)seed, P, PN, PC);
-    OT_LAUNCH_CHECK();
-    OT_HIP_TRY(hipStreamSynchronize(stream));
-    return OT_OK;
+                                          double* PN, double* PC, void* stream) {
+    const ot_mesh_sample_job job{V, VN, VC, nv, T, nt, P, PN, PC};
+    return ot_mesh_sample_points_uniformly_batch(&job, 1, n_points, seed, stream);
 }
 
 ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points,
@@ -319,43 +474,48 @@ ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, 
     if (n_jobs < 0 || (n_jobs > 0 && !jobs)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
     if (n_jobs == 0) return OT_OK;
     size_t bytes = 256;
+    int64_t max_nt = 0;
     for (int j = 0; j < n_jobs; ++j) {
         const ot_mesh_sample_job& m = jobs[j];
         if (m.n_triangles <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] Input mesh has no triangles.");
         if (!m.vertices || !m.triangles || !m.out_xyz || (m.out_normals && !m.vertex_normals) ||
             (m.out_colors && !m.vertex_colors) || m.n_vertices <= 0)
             return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid arguments");
-        bytes += (size_t)m.n_triangles * 32 + 256;
+        bytes += (size_t)m.n_triangles * 32 + 256 + chain_aux_bytes(m.n_triangles);
+        max_nt = m.n_triangles > max_nt ? m.n_triangles : max_nt;
     }
     char* ws = (char*)scratch(bytes + sizeof(ChainJob) * 2 * (size_t)n_jobs + 256, 17);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-    std::vector<ChainJob> sum_jobs(n_jobs), cdf_jobs(n_jobs);
+    std::vector<ChainJob> chain(2 * (size_t)n_jobs);  // [sum chains | CDF chains]
     std::vector<double*> areas(n_jobs), qs(n_jobs), sums(n_jobs);
     std::vector<long long*> ncums(n_jobs);
     char* cur = ws;
     for (int j = 0; j < n_jobs; ++j) {
         const int64_t nt = jobs[j].n_triangles, nt2 = (nt + 1) & ~(int64_t)1;
         sums[j] = (double*)cur;
-        areas[j] = sums[j] + 8;
+        areas[j] = sums[j] + 8;  // 64-B offset: 16-B aligned rows for the chains' double2 loads
         qs[j] = areas[j] + nt2;
         ncums[j] = (long long*)(qs[j] + nt2);
         cur = (char*)(ncums[j] + nt2) + 64;
         cur = (char*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
-        sum_jobs[j] = ChainJob{areas[j], nt, sums[j]};
-        cdf_jobs[j] = ChainJob{qs[j], nt, areas[j]};
+        ChainJob& cs = chain[j];
+        cs.x = areas[j], cs.n = nt, cs.out = sums[j];
+        cur = chain_aux(cur, nt, cs);
+        ChainJob& cc = chain[n_jobs + j];
+        cc = cs;
+        cc.x = qs[j], cc.out = areas[j];  // the CDF overwrites the areas once q = a / s is formed
         hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, jobs[j].vertices,
                            jobs[j].triangles, nt, areas[j]);
     }
     ChainJob* djobs = (ChainJob*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
-    OT_HIP_TRY(hipMemcpyAsync(djobs, sum_jobs.data(), sizeof(ChainJob) * n_jobs, hipMemcpyHostToDevice, stream));
-    OT_HIP_TRY(hipMemcpyAsync(djobs + n_jobs, cdf_jobs.data(), sizeof(ChainJob) * n_jobs, hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(k_serial_chain_batch<false>, dim3(n_jobs), dim3(64), 0, stream, (const ChainJob*)djobs);
+    OT_HIP_TRY(hipMemcpyAsync(djobs, chain.data(), sizeof(ChainJob) * 2 * n_jobs, hipMemcpyHostToDevice, stream));
+    launch_chains<false>(djobs, n_jobs, max_nt, stream);
     for (int j = 0; j < n_jobs; ++j) {
         const int64_t nt = jobs[j].n_triangles;
         hipLaunchKernelGGL(k_area_div, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, (const double*)areas[j],
                            nt, (const double*)sums[j], qs[j]);
     }
-    hipLaunchKernelGGL(k_serial_chain_batch<true>, dim3(n_jobs), dim3(64), 0, stream, (const ChainJob*)(djobs + n_jobs));
+    launch_chains<true>(djobs + n_jobs, n_jobs, max_nt, stream);
     for (int j = 0; j < n_jobs; ++j) {
         const ot_mesh_sample_job& m = jobs[j];
         const int64_t nt = m.n_triangles;
@@ -367,7 +527,52 @@ ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, 
                            m.out_colors);
     }
     OT_LAUNCH_CHECK();
-    OT_HIP_TRY(hipStreamSynchronize(stream));  // the host job tables are released on return
+    OT_HIP_TRY(hipStreamSynchronize(stream));  // the host job table is released on return
+    return OT_OK;
+}
+
+ot_status ot_mesh_get_surface_area(const double* V, int64_t nv, const int32_t* T, int64_t nt, double* area_host,
+                                   void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (nv < 0 || nt < 0 || !area_host || (nt > 0 && (!V || !T || nv == 0)))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[GetSurfaceArea] invalid arguments");
+    if (nt == 0) {
+        *area_host = 0.0;
+        return OT_OK;
+    }
+    const int64_t nt2 = (nt + 1) & ~(int64_t)1;
+    char* ws = (char*)scratch((size_t)nt2 * 8 + chain_aux_bytes(nt) + sizeof(ChainJob) + 512, 17);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    ChainJob jb{};
+    double* sum = (double*)ws;
+    double* area = sum + 8;
+    jb.x = area, jb.n = nt, jb.out = sum;
+    char* cur = chain_aux((char*)(area + nt2), nt, jb);
+    ChainJob* djob = (ChainJob*)cur;
+    hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, V, T, nt, area);
+    OT_HIP_TRY(hipMemcpyAsync(djob, &jb, sizeof(ChainJob), hipMemcpyHostToDevice, stream));
+    launch_chains<false>(djob, 1, nt, stream);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipMemcpyAsync(area_host, sum, sizeof(double), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
+}
+
+// test hook (not part of the drop-in boundary): the bare chains on a device array x (16-B aligned) -- cdf != 0:
+// out[t] = x_t + out[t-1] for all t (numpy.cumsum's order); cdf == 0: out[0] = ((0 + x_0) + x_1) + ...
+ot_status otx_serial_chain_f64(const double* x, int64_t n, int32_t cdf, double* out, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (n <= 0 || !x || !out || ((uintptr_t)x & 15)) return fail(OT_ERR_INVALID_ARGUMENT, "[chain] invalid arguments");
+    char* ws = (char*)scratch(chain_aux_bytes(n) + sizeof(ChainJob) + 256, 17);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    ChainJob jb{};
+    jb.x = x, jb.n = n, jb.out = out;
+    ChainJob* djob = (ChainJob*)chain_aux(ws, n, jb);
+    OT_HIP_TRY(hipMemcpyAsync(djob, &jb, sizeof(ChainJob), hipMemcpyHostToDevice, stream));
+    if (cdf) launch_chains<true>(djob, 1, n, stream);
+    else launch_chains<false>(djob, 1, n, stream);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
 }
 

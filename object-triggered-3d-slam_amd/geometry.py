@@ -499,6 +499,15 @@ class TriangleMesh:
         self._vn = _Arr(dev=out)
         return self
 
+    def get_surface_area(self):
+        """TriangleMesh::GetSurfaceArea: the float64 sum of the triangle areas in index order (the first serial
+        chain of SamplePointsUniformly, reconstruct_rgbd_filter.py:123) — ot_mesh_get_surface_area."""
+        out = C.c_double(0.0)
+        nt = len(self._t)
+        L.call("ot_mesh_get_surface_area", D.ptr(self._v.dev()) if nt else None, len(self._v),
+               D.ptr(self._t.dev()) if nt else None, nt, C.byref(out), D.stream_ptr())
+        return out.value
+
     def sample_points_uniformly(self, number_of_points=100, use_triangle_normal=False, seed=0):
         """TriangleMesh::SamplePointsUniformly (reconstruct_rgbd_filter.py:123) with a seeded counter RNG."""
         if number_of_points <= 0:

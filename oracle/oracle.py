@@ -53,6 +53,7 @@ def lib():
             "oro_tsdf_fetch_mesh": (None, [_p, _p, _p, _p]),
             "oro_mesh_vertex_normals": (None, [_p, _i64, _p, _i64, _p]),
             "oro_mesh_sample_uniform": (_i32, [_p, _p, _p, _i64, _p, _i64, _i64, C.c_uint64, _p, _p, _p]),
+            "oro_mesh_surface_area": (C.c_double, [_p, _p, _i64]),
             "oro_filter_min_z": (_i64, [_p, _p, _i64, _d, _p, _p]),
             "oro_remove_statistical_outlier": (_i64, [_p, _i64, _i32, _d, _p, _p]),
             "oro_remove_radius_outlier": (_i64, [_p, _i64, _i32, _d, _p]),
@@ -180,6 +181,12 @@ def vertex_normals(V, T):
     N = np.empty_like(V)
     lib().oro_mesh_vertex_normals(_ptr(V), V.shape[0], _ptr(T), T.shape[0], _ptr(N))
     return N
+
+
+def surface_area(V, T):
+    V = _c(V, np.float64)
+    T = _c(T, np.int32)
+    return float(lib().oro_mesh_surface_area(_ptr(V), _ptr(T), T.shape[0]))
 
 
 def sample_points_uniformly(V, T, n_points, seed, VN=None, VC=None):

@@ -550,6 +550,25 @@ static inline double u01(uint64_t seed, uint64_t ctr) {
     return (double)(z >> 11) * (1.0 / 9007199254740992.0);
 }
 
+/* TriangleMesh::GetSurfaceArea (Open3D TriangleMesh.cpp; called by SamplePointsUniformly, Appendix A.8): the
+ * triangle areas 0.5 |(p0 - p1) x (p0 - p2)| summed in index order. */
+double oro_mesh_surface_area(const double* V, const int32_t* T, int64_t nt) {
+    double surface = 0.0;
+    for (int64_t t = 0; t < nt; ++t) {
+        const double *p0 = V + T[t * 3] * 3, *p1 = V + T[t * 3 + 1] * 3, *p2 = V + T[t * 3 + 2] * 3;
+        double x[3], y[3], c[3];
+        for (int d = 0; d < 3; ++d) {
+            x[d] = p0[d] - p1[d];
+            y[d] = p0[d] - p2[d];
+        }
+        c[0] = x[1] * y[2] - x[2] * y[1];
+        c[1] = x[2] * y[0] - x[0] * y[2];
+        c[2] = x[0] * y[1] - x[1] * y[0];
+        surface += 0.5 * std::sqrt((c[0] * c[0] + c[1] * c[1]) + c[2] * c[2]);
+    }
+    return surface;
+}
+
 /* TriangleMesh::SamplePointsUniformly (Appendix A.8) with the seeded RNG. */
 int oro_mesh_sample_uniform(const double* V, const double* VN, const double* VC, int64_t nv, const int32_t* T,
                             int64_t nt, int64_t n_points, uint64_t seed, double* P, double* PN, double* PC) {

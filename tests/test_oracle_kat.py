@@ -244,3 +244,16 @@ def test_virtual_scan_kat(O):
             break
     assert r[0, 0] == np.float32(d)
     assert np.isinf(r[0, 2])  # westward beam leaves the map
+
+
+def test_oracle_surface_area_is_index_order_sum(O):
+    """oro_mesh_surface_area (Open3D GetSurfaceArea) == numpy areas summed strictly left to right."""
+    rng = np.random.default_rng(11)
+    V = rng.random((400, 3))
+    T = rng.integers(0, 400, (5000, 3)).astype(np.int32)
+    x = V[T[:, 0]] - V[T[:, 1]]
+    y = V[T[:, 0]] - V[T[:, 2]]
+    c = np.stack([x[:, 1] * y[:, 2] - x[:, 2] * y[:, 1], x[:, 2] * y[:, 0] - x[:, 0] * y[:, 2],
+                  x[:, 0] * y[:, 1] - x[:, 1] * y[:, 0]], 1)
+    a = 0.5 * np.sqrt((c[:, 0] * c[:, 0] + c[:, 1] * c[:, 1]) + c[:, 2] * c[:, 2])
+    assert O.surface_area(V, T) == np.cumsum(a)[-1]
