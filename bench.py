@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--objects", type=int, default=8,
                     help="configs[3]: object scans shared by all ranks (full per-object pipeline + RCCL merge); 0 = skip")
     ap.add_argument("--object-frames", type=int, default=64, help="configs[3]: frames per object scan")
+    ap.add_argument("--spatial", type=int, default=1,
+                    help="N > 1: also time one object spatially sharded over the N GPUs (SURVEY 8(e))")
     ap.add_argument("--hybrid-objects", type=int, default=32,
                     help="configs[4]: object clouds in the hybrid-map fusion + change detection; 0 = skip")
     return ap.parse_args()
@@ -182,6 +184,9 @@ def main():
         if args.objects > 0 else None
     hybrid = hybrid_fusion(args, L, synth, torch, dist, rank, world) if args.hybrid_objects > 0 else None
 
+    spatial = spatial_shard(args, L, lib, synth, torch, dist, rank, world, n_units.value) \
+        if (world > 1 and args.spatial) else None
+
     cpu = None
     if rank == 0 and args.cpu_frames > 0:
         cpu = cpu_baseline(depth, color, ext, intr_t, args)
@@ -198,13 +203,84 @@ def main():
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
            "roofline": roofline, "cpu_baseline": cpu, "filtered": filt, "objects": objects, "hybrid_map": hybrid,
-           "single_frame": single}
+           "single_frame": single, "spatial": spatial}
     if rank == 0:
         print(json.dumps(out), flush=True)
     L.call("ot_tsdf_destroy", vol)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
+    """ONE object's scan (seed 0) on every rank, its volume spatially sharded (ot_tsdf_set_shard:
+    rank r keeps the units with owner(key) == r), so N GPUs integrate one object together (strong scaling; at
+    N = 1 this is the headline itself).  Timed like the headline (reset + all frames + flush, max over ranks).
+    Then the shards are assembled into one volume (all-gather of packed unit rows + import) -- timed apart as
+    the per-object cost before marching cubes; its unit count must equal the unsharded volume's (rank 0's
+    headline volume is the same seed-0 scan)."""
+    import importlib
+
+    Dm = importlib.import_module(PKG + ".distributed")
+    intr_t = synth.REF_INTRINSICS_640
+    W, H = intr_t[0], intr_t[1]
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=0), n_frames=args.frames, intr=intr_t)
+    d_depth = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
+    d_color = torch.from_numpy(color).cuda().contiguous()
+    ext = np.ascontiguousarray(ext, dtype=np.float64)
+    intr = L.ot_intrinsics(W, H, *intr_t[2:])
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    vol = C.c_void_p()
+    L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
+    L.call("ot_tsdf_set_shard", vol, rank, world)
+    if args.batch > 0:
+        L.call("ot_tsdf_set_batch", vol, args.batch)
+    npx = W * H
+    dptrs = [C.c_void_p(d_depth.data_ptr() + k * npx * 2) for k in range(args.frames)]
+    cptrs = [C.c_void_p(d_color.data_ptr() + k * npx * 3) for k in range(args.frames)]
+    eptrs = [ext[k].ctypes.data_as(C.c_void_p) for k in range(args.frames)]
+    integrate, pintr = lib.ot_tsdf_integrate_u16, C.byref(intr)
+
+    def step():
+        L.call("ot_tsdf_reset", vol)
+        for k in range(args.frames):
+            if integrate(vol, dptrs[k], cptrs[k], pintr, eptrs[k], 1000.0, 3.0, stream):
+                raise RuntimeError(lib.ot_last_error().decode())
+        L.call("ot_tsdf_flush", vol, stream)
+
+    dt, _ = _timed(torch, dist, world, step, args.steps)
+    nu = C.c_int64(0)
+    L.call("ot_tsdf_num_units", vol, C.byref(nu))
+    cnt = Dm.all_gather_rows(torch.tensor([[nu.value]], dtype=torch.int64, device=COLL_DEV)).flatten().tolist()
+
+    def assemble():
+        n = nu.value
+        keys = torch.empty((n, 3), dtype=torch.int32, device="cuda")
+        f = [torch.empty((n, 4096, k), dtype=torch.float32, device="cuda") for k in (1, 1, 3)]
+        L.call("ot_tsdf_export_units", vol, C.c_void_p(keys.data_ptr()), *[C.c_void_p(t.data_ptr()) for t in f],
+               stream)
+        rows = Dm.pack_units(keys, *f)
+        rows = Dm.all_gather_rows(rows if COLL_DEV == "cuda" else rows.cpu())
+        rows = rows.cuda()
+        merged = C.c_void_p()
+        L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, max(32768, rows.shape[0]),
+               C.byref(merged))
+        k2, t2, w2, c2 = Dm.unpack_units(rows)
+        L.call("ot_tsdf_import_units", merged, rows.shape[0], C.c_void_p(k2.data_ptr()), C.c_void_p(t2.data_ptr()),
+               C.c_void_p(w2.data_ptr()), C.c_void_p(c2.data_ptr()), stream)
+        total = C.c_int64(0)
+        L.call("ot_tsdf_num_units", merged, C.byref(total))
+        L.call("ot_tsdf_destroy", merged)
+        return total.value
+
+    t_asm, merged_units = _timed(torch, dist, world, assemble, 1)
+    L.call("ot_tsdf_destroy", vol)
+    return {"workload": f"configs[1] scan (seed 0) as ONE object spatially sharded over {world} GPU(s): unit owner = "
+                        f"hash(key) mod {world}, every rank integrates every frame into its own units",
+            "scaling": "strong", "frames_per_s": round(args.frames * 1.0 / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+            "units_per_rank_min": min(cnt), "units_per_rank_max": max(cnt), "assemble_ms": round(t_asm * 1e3, 2),
+            "assembled_units": merged_units, "units_match_unsharded": merged_units == units_rank0 if rank == 0
+            else None}
 
 
 def single_frame(L, synth, torch, depth, color, ext, intr_t, reps=50):

@@ -158,6 +158,18 @@ ot_status ot_tsdf_kernel_time(ot_tsdf* vol, double* total_ms_host, int64_t* laun
 ot_status ot_tsdf_export_units(ot_tsdf* vol, int32_t* keys, float* tsdf, float* weight, float* color,
                                void* stream);
 
+/* The inverse of ot_tsdf_export_units (same layouts): insert n units, overwriting any unit with the same key;
+ * keys must be unique within one call.  color may be NULL (zeros).  Used to assemble a spatially sharded volume
+ * on one GPU before extract_triangle_mesh.  Device pointers. */
+ot_status ot_tsdf_import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf, const float* weight,
+                               const float* color, void* stream);
+
+/* Spatial sharding of ONE object's volume over `world` GPUs (not an Open3D API): this volume
+ * allocates and integrates only the units whose owner hash(key) mod world == rank.  Every rank integrates every
+ * frame; each voxel still sees the frames in call order, so the union of the ranks' exported units is bit-identical
+ * to one unsharded volume.  Call before the first integrate. */
+ot_status ot_tsdf_set_shard(ot_tsdf* vol, int32_t rank, int32_t world);
+
 /* volume.extract_triangle_mesh() — reconstruct_rgbd_filter.py:112 (marching cubes, Appendix A.4).
  * Runs the extraction and stores the mesh inside the handle; returns its sizes.  Vertices are ordered by
  * (unit key, local voxel, edge) — a canonical order; Open3D's is hash order. */

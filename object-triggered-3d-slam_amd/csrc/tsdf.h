@@ -49,7 +49,16 @@ struct TsdfDev {
     void* work;                 // per touched slot of the batch: unit header (UnitWork, 32 B) for the integrate
     int hash_mask;
     int max_units;
+    int shard_rank;   // spatial sharding of one volume over `shard_world` GPUs: this volume keeps only the units
+    int shard_world;  // with owner(key) == shard_rank (<= 1: no sharding)
 };
+
+// owner rank of a unit: a hash independent of the table's slot hash mix64(key), so a shard's keys
+// still spread over all slots
+__host__ __device__ inline bool unit_owned(const TsdfDev& d, unsigned long long key) {
+    if (d.shard_world <= 1) return true;
+    return (int)((unsigned)(mix64(key + 0x9E3779B97F4A7C15ull) >> 32) % (unsigned)d.shard_world) == d.shard_rank;
+}
 
 constexpr int MAX_BATCH = 64;  // frames per fused launch (one bit each in fmask)
 

@@ -86,6 +86,7 @@ __device__ inline void touch_unit(const TsdfDev& d, int frame, int x, int y, int
         return;
     }
     const unsigned long long key = pack_key(x, y, z);
+    if (!unit_owned(d, key)) return;
     const int slot = hash_insert(d, key);
     if (slot < 0) {
         atomicOr(&d.counters[C_HASHERR], 1);
@@ -325,7 +326,9 @@ __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, i
         atomicOr(&d.counters[C_HASHERR], 2);
         return;
     }
-    const int slot = hash_insert(d, pack_key(x, y, z));
+    const unsigned long long key = pack_key(x, y, z);
+    if (!unit_owned(d, key)) return;
+    const int slot = hash_insert(d, key);
     if (slot < 0) {
         atomicOr(&d.counters[C_HASHERR], 1);
         return;
@@ -414,8 +417,9 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
                             atomicOr(&d.counters[C_HASHERR], 2);
                             continue;
                         }
-                        if (!lds_merge(s_keys, s_masks, pack_key(ux, uy, uz), bit))
-                            touch_unit_batch(d, f, p.slot_cap, ux, uy, uz);
+                        const unsigned long long key = pack_key(ux, uy, uz);
+                        if (!unit_owned(d, key)) continue;
+                        if (!lds_merge(s_keys, s_masks, key, bit)) touch_unit_batch(d, f, p.slot_cap, ux, uy, uz);
                     }
         }
     }
@@ -694,6 +698,55 @@ __global__ __launch_bounds__(256) void k_export(TsdfDev d, const unsigned* sorte
             color[o * 3 + 1] = base[3 * UNIT_VOX + vi];
             color[o * 3 + 2] = base[4 * UNIT_VOX + vi];
         }
+    }
+}
+
+// import: the inverse of k_export (keys unique within one call; an existing unit is overwritten)
+__global__ __launch_bounds__(256) void k_import(TsdfDev d, const int32_t* __restrict__ keys,
+                                                const float* __restrict__ tsdf, const float* __restrict__ weight,
+                                                const float* __restrict__ color) {
+    __shared__ int s_id;
+    const int r = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        const int x = keys[(int64_t)r * 3], y = keys[(int64_t)r * 3 + 1], z = keys[(int64_t)r * 3 + 2];
+        int id = -1;
+        if (!key_in_range(x, y, z)) {
+            atomicOr(&d.counters[C_HASHERR], 2);
+        } else {
+            const int slot = hash_insert(d, pack_key(x, y, z));
+            if (slot < 0) {
+                atomicOr(&d.counters[C_HASHERR], 1);
+            } else {
+                id = d.hvals[slot];
+                if (id < 0) {
+                    id = atomicAdd(&d.counters[C_UNITS], 1);
+                    if (id >= d.max_units) {
+                        atomicOr(&d.counters[C_OVERFLOW], 1);
+                        id = -1;
+                    } else {
+                        d.hvals[slot] = id;
+                        d.unit_keys[id * 3 + 0] = x;
+                        d.unit_keys[id * 3 + 1] = y;
+                        d.unit_keys[id * 3 + 2] = z;
+                    }
+                }
+            }
+        }
+        s_id = id;
+    }
+    __syncthreads();
+    const int id = s_id;
+    if (id < 0) return;
+    float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    for (int z = 0; z < UNIT_RES; ++z) {
+        const int vi = z * 256 + tid;
+        const int64_t o = (int64_t)r * UNIT_VOX + tid * 16 + z;
+        base[vi] = tsdf[o];
+        base[UNIT_VOX + vi] = weight[o];
+        base[2 * UNIT_VOX + vi] = color ? color[o * 3 + 0] : 0.0f;
+        base[3 * UNIT_VOX + vi] = color ? color[o * 3 + 1] : 0.0f;
+        base[4 * UNIT_VOX + vi] = color ? color[o * 3 + 2] : 0.0f;
     }
 }
 
@@ -1188,6 +1241,36 @@ ot_status ot_tsdf_export_units(ot_tsdf* vol, int32_t* keys, float* tsdf, float* 
     hipLaunchKernelGGL(k_export, dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev, vol->sorted_ids, keys, tsdf,
                        weight, color);
     OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(S(stream)));
+    return OT_OK;
+}
+
+ot_status ot_tsdf_set_shard(ot_tsdf* vol, int32_t rank, int32_t world) {
+    if (!vol || world < 1 || rank < 0 || rank >= world)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] shard needs 0 <= rank < world");
+    int nu = 0;
+    OT_HIP_TRY(hipMemcpy(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost));
+    if (nu != 0 || !vol->pending.empty())
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] set the shard before the first integrate");
+    vol->dev.shard_rank = rank;
+    vol->dev.shard_world = world;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf, const float* weight,
+                               const float* color, void* stream) {
+    if (!vol || n < 0 || (n > 0 && (!keys || !tsdf || !weight)))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: invalid arguments");
+    if (n > vol->max_units) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: more units than max_units");
+    ot_status st = tsdf_flush(vol, S(stream));
+    if (st != OT_OK) return st;
+    if (n == 0) return OT_OK;
+    hipLaunchKernelGGL(k_import, dim3((unsigned)n), dim3(256), 0, S(stream), vol->dev, keys, tsdf, weight,
+                       vol->color_type == OT_COLOR_RGB8 ? color : nullptr);
+    OT_LAUNCH_CHECK();
+    vol->sorted_units = -1;  // the sorted-unit cache no longer matches
+    st = check_errors(vol, S(stream));
+    if (st != OT_OK) return st;
     OT_HIP_TRY(hipStreamSynchronize(S(stream)));
     return OT_OK;
 }

@@ -52,6 +52,44 @@ def all_gather_rows(local, group=None):
     return torch.cat([out[r * m: r * m + c] for r, c in enumerate(counts_h)], dim=0)
 
 
+UNIT_WORDS = 3 + 4096 * 5  # packed unit row: key int3 | tsdf f32 | weight f32 | colour f32 x3 (bit patterns)
+
+
+def pack_units(keys, tsdf, weight, color):
+    """export_units' arrays -> one int32 row per unit (float fields carried as raw bits, so the exchange is exact)."""
+    import torch
+
+    n = keys.shape[0]
+    parts = [keys.reshape(n, 3).to(torch.int32), tsdf.reshape(n, 4096).view(torch.int32),
+             weight.reshape(n, 4096).view(torch.int32), color.reshape(n, 4096 * 3).view(torch.int32)]
+    return torch.cat(parts, 1)
+
+
+def unpack_units(rows):
+    import torch
+
+    n = rows.shape[0]
+    f = rows[:, 3:].contiguous().view(torch.float32)
+    return (rows[:, :3].contiguous(), f[:, :4096].contiguous(), f[:, 4096:8192].contiguous(),
+            f[:, 8192:].contiguous().view(n, 4096, 3))
+
+
+def assemble_sharded_volume(volume, group=None):
+    """Spatial sharding of one object: every rank integrated the same frames into a volume created
+    with set_shard(rank, world); this all-gathers the ranks' units (one RCCL all-gather of packed unit rows) and
+    imports them into one fresh volume on every rank, bit-identical to an unsharded volume -- the input of
+    extract_triangle_mesh, which needs neighbouring units across shard borders."""
+    from .pipelines.integration import ScalableTSDFVolume
+
+    rows = all_gather_rows(pack_units(*volume.export_units()), group)
+    merged = ScalableTSDFVolume(volume.voxel_length, volume.sdf_trunc, color_type=volume.color_type,
+                                volume_unit_resolution=volume.volume_unit_resolution,
+                                depth_sampling_stride=volume.depth_sampling_stride,
+                                max_units=max(32768, int(rows.shape[0])))
+    merged.import_units(*unpack_units(rows))
+    return merged
+
+
 def merge_object_clouds(local_clouds, group=None):
     """Rank-ordered concatenation of this rank's object clouds with everyone else's (points only: colours are
     repainted uniformly by the hybrid map, hybrid_map.py:88)."""

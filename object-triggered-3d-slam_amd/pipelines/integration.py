@@ -119,6 +119,23 @@ class ScalableTSDFVolume:
                D.stream_ptr())
         return keys, tsdf, weight, color
 
+    def import_units(self, keys, tsdf, weight, color=None):
+        """Insert units in export_units' layout (device tensors or arrays); the inverse of export_units."""
+        keys = D.to_device(keys, "int32")
+        n = int(keys.shape[0])
+        tsdf = D.to_device(tsdf, "float32")
+        weight = D.to_device(weight, "float32")
+        color = D.to_device(color, "float32") if color is not None else None
+        if tuple(tsdf.shape[-1:]) != (4096,) or tsdf.shape[0] != n or weight.shape[0] != n or (
+                color is not None and color.shape[0] != n):
+            raise RuntimeError("[ScalableTSDFVolume] import_units: shapes do not match export_units")
+        L.call("ot_tsdf_import_units", self._h, n, D.ptr(keys), D.ptr(tsdf), D.ptr(weight), D.ptr(color),
+               D.stream_ptr())
+
+    def set_shard(self, rank, world):
+        """Keep only the units owned by `rank` of `world` (spatial sharding of one object)."""
+        L.call("ot_tsdf_set_shard", self._h, int(rank), int(world))
+
     def extract_triangle_mesh(self):
         """ScalableTSDFVolume::ExtractTriangleMesh — GPU marching cubes (mc.hip)."""
         nv, nt = C.c_int64(0), C.c_int64(0)

@@ -68,3 +68,46 @@ def test_shard_contiguous_sorted():
         parts = [D.shard(labels, r, world) for r in range(world)]
         assert sum(parts, []) == labels
         assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+def _unit_worker(rank, world, port, sizes, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D = importlib.import_module(PKG + ".distributed")
+    k, t, w, c = _fake_units(rank, sizes[rank])
+    rows = D.all_gather_rows(D.pack_units(k, t, w, c))
+    q.put((rank, [a.numpy() for a in D.unpack_units(rows)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _fake_units(seed, n):
+    rng = np.random.default_rng(seed + 100)
+    keys = torch.from_numpy(rng.integers(-500, 500, (n, 3)).astype(np.int32))
+    bits = rng.integers(0, 2 ** 32, (n, 4096 * 5), dtype=np.uint64).astype(np.uint32).view(np.float32)
+    f = torch.from_numpy(bits.copy())  # arbitrary bit patterns (NaN payloads, -0, denormals) must survive
+    return keys, f[:, :4096].contiguous(), f[:, 4096:8192].contiguous(), f[:, 8192:].contiguous().view(n, 4096, 3)
+
+
+@pytest.mark.parametrize("sizes", [[3, 5], [0, 2]])
+def test_sharded_unit_exchange_gloo(sizes):
+    """assemble_sharded_volume's exchange: packed unit rows all-gathered over 2 ranks unpack to the rank-ordered
+    concatenation of every field, bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_unit_worker, args=(r, 2, port, sizes, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = [np.concatenate([_fake_units(r, sizes[r])[i].numpy() for r in range(2)]) for i in range(4)]
+    for r in range(2):
+        for got, e in zip(out[r], exp):
+            assert got.shape == e.shape and np.array_equal(got.view(np.uint32) if got.dtype == np.float32 else got,
+                                                           e.view(np.uint32) if e.dtype == np.float32 else e)

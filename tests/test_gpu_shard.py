@@ -1,0 +1,76 @@
+"""Spatial sharding of one object's volume: `world` volumes, each keeping only the units with
+owner(key) == rank, integrate the same frames.  The union of their exported units equals one unsharded volume bit
+for bit (keys, tsdf, weight and colour: every voxel sees the same frames in the same order), the update counters
+add up, and importing all shards into one volume gives the unsharded volume's marching-cubes mesh exactly."""
+import importlib
+
+import numpy as np
+import pytest
+
+from conftest import assert_bitwise, ref_intr
+
+pytestmark = pytest.mark.gpu
+
+
+def _integrate(pkg, seq, voxel, shard=None):
+    depth, color, ext = seq
+    integ = pkg.pipelines.integration
+    intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(importlib.import_module(pkg.__name__ + ".synth")))
+    vol = integ.ScalableTSDFVolume(voxel_length=voxel, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
+    if shard is not None:
+        vol.set_shard(*shard)
+    for k in range(depth.shape[0]):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+            convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+    return vol
+
+
+def _host(t):
+    return t.cpu().numpy()
+
+
+@pytest.mark.parametrize("voxel,world", [(0.01, 3), (0.005, 8)])
+def test_shard_union_bitexact(pkg, seq16, gpu, voxel, world):
+    full = _integrate(pkg, seq16, voxel)
+    fk, ft, fw, fc = (_host(a) for a in full.export_units())
+    parts = [_integrate(pkg, seq16, voxel, (r, world)) for r in range(world)]
+    exports = [[_host(a) for a in v.export_units()] for v in parts]
+    counts = [e[0].shape[0] for e in exports]
+    assert sum(counts) == fk.shape[0] and min(counts) > 0.5 * fk.shape[0] / world
+    keys = np.concatenate([e[0] for e in exports])
+    order = np.lexsort((keys[:, 2], keys[:, 1], keys[:, 0]))
+    assert_bitwise(keys[order], fk, "shard union keys")
+    assert_bitwise(np.concatenate([e[1] for e in exports])[order], ft, "shard union tsdf")
+    assert_bitwise(np.concatenate([e[2] for e in exports])[order], fw, "shard union weight")
+    assert_bitwise(np.concatenate([e[3] for e in exports])[order], fc, "shard union colour")
+    upd = [v.counters() for v in parts]
+    assert sum(u for u, _ in upd) == full.counters()[0]
+    assert sum(k for _, k in upd) == full.counters()[1]
+
+
+def test_shard_import_mesh_bitexact(pkg, seq16, gpu):
+    integ = pkg.pipelines.integration
+    full = _integrate(pkg, seq16, 0.01)
+    m0 = full.extract_triangle_mesh()
+    merged = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
+    for r in range(4):
+        merged.import_units(*_integrate(pkg, seq16, 0.01, (r, 4)).export_units())
+    assert merged.num_units() == full.num_units()
+    m1 = merged.extract_triangle_mesh()
+    assert_bitwise(np.asarray(m1.vertices), np.asarray(m0.vertices), "merged-shard mesh vertices")
+    assert_bitwise(np.asarray(m1.triangles), np.asarray(m0.triangles), "merged-shard mesh triangles")
+    assert_bitwise(np.asarray(m1.vertex_colors), np.asarray(m0.vertex_colors), "merged-shard mesh colours")
+
+
+def test_shard_argument_errors(pkg, seq16, gpu):
+    integ = pkg.pipelines.integration
+    vol = _integrate(pkg, (seq16[0][:2], seq16[1][:2], seq16[2][:2]), 0.01)
+    vol.num_units()
+    with pytest.raises(RuntimeError, match="before the first integrate"):
+        vol.set_shard(0, 2)
+    fresh = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04)
+    with pytest.raises(RuntimeError, match="rank < world"):
+        fresh.set_shard(2, 2)
+    fresh.set_shard(0, 1)  # world 1: no sharding
