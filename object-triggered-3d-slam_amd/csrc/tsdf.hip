@@ -634,6 +634,15 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
                         cv[k] = 0u;
                         if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
                     }
+#ifdef OT_COUNT_IDLE  // diagnostic build: wave-frames with no updating lane (stats[2]) of all wave-frames (stats[3])
+                    if (lane == 0) atomicAdd(&d.stats[3], 1ull);
+                    {
+                        bool any = false;
+#pragma unroll
+                        for (int k = 0; k < BZ; ++k) any |= doitv[k];
+                        if (__ballot(any) == 0ull && lane == 0) atomicAdd(&d.stats[2], 1ull);
+                    }
+#endif
                     // phase D: updates in frame order (select form: identical values, no exec-mask branches)
 #pragma unroll
                     for (int k = 0; k < BZ; ++k) {
@@ -1242,6 +1251,16 @@ ot_status ot_tsdf_export_units(ot_tsdf* vol, int32_t* keys, float* tsdf, float* 
                        weight, color);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(S(stream)));
+    return OT_OK;
+}
+
+// test / diagnostic hook (not part of the drop-in boundary): the volume's raw u64 stats[4] (0 voxel updates,
+// 1 unit integrations; 2, 3 filled by -DOT_COUNT_IDLE builds)
+ot_status otx_tsdf_stats(ot_tsdf* vol, uint64_t* out4) {
+    if (!vol || !out4) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    ot_status st = tsdf_flush(vol, nullptr);
+    if (st != OT_OK) return st;
+    OT_HIP_TRY(hipMemcpy(out4, vol->dev.stats, sizeof(uint64_t) * 4, hipMemcpyDeviceToHost));
     return OT_OK;
 }
 
