@@ -12,4 +12,9 @@ tail -1 gpurun_out/bench.log
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py $BENCH_ARGS > gpurun_out/bench_prof.log 2>&1 || { echo PROF_FAILED; tail -30 gpurun_out/bench_prof.log; exit 1; }
 python3 tools/prof_summary.py gpurun_out/prof gpurun_out/prof/kernel_stats.csv
+# headline leg alone: its k_batch_integrate average is the one bench.py's roofline reports (HIP events)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_h -o bench -- python3 bench.py \
+    --objects 0 --hybrid-objects 0 --filter-frames 0 --cpu-frames 0 > gpurun_out/bench_prof_h.log 2>&1 || { echo PROF_H_FAILED; tail -30 gpurun_out/bench_prof_h.log; exit 1; }
+python3 tools/prof_summary.py gpurun_out/prof_h gpurun_out/prof_h/kernel_stats.csv
+tail -1 gpurun_out/bench_prof_h.log
 echo DONE
