@@ -267,14 +267,18 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
     long long have = 0;
     for (int u = 0; u < NBR3; ++u) {
-        const int t = (u + 4) % NBR3;  // the query's own column first: the k-th distance drops early
+        // own column, then the 4 face-adjacent columns, then the 4 diagonal ones: the k-th distance tightens
+        // before the farthest candidates, so fewer of them pass the early-reject test into the insertion chain
+        const int t = (int)((0x862075314ull >> (4 * u)) & 0xF);
         const int2 se = r3[t];
         scan_range<KMAX>(g, q, se.x, se.y, best);
         have += se.y - se.x;
     }
     double guard = block_guard(g, q, 1.0);
     bool settled = have >= n || (have >= kk && best[KMAX - 1] <= guard * guard);
+    int stage = 1;
     if (!settled) {
+        stage = 2;
         const int2* r5 = g.nbr5 + (int64_t)c * NBR5;
         for (int t = 0; t < NBR5; ++t) {
             const int dx = t / 5 - 2, dy = t % 5 - 2;
@@ -293,7 +297,12 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
         }
         guard = block_guard(g, q, 2.0);
         settled = have >= n || (have >= kk && best[KMAX - 1] <= guard * guard);
-        if (!settled) sor_fallback<KMAX>(g, q, n, kk, best);
+        if (!settled) {
+            stage = 3;
+#ifndef OT_SOR_NOFB  // timing-only ablation build: isolated queries skip the exact fallback (results wrong)
+            sor_fallback<KMAX>(g, q, n, kk, best);
+#endif
+        }
     }
     double s = 0.0;
     int cnt = 0;
@@ -303,7 +312,12 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
             s += sqrt(best[i]);
             ++cnt;
         }
+#ifdef OT_SOR_DIAG  // diagnostic build (tools/sor_work.py): (sorted position, stage, candidates scanned)
+    avg[g.sidx[j]] = (double)((j << 26) | ((long long)stage << 24) | (have < (1 << 24) ? have : (1 << 24) - 1));
+#else
+    (void)stage;
     avg[g.sidx[j]] = cnt > 0 ? s / (double)cnt : -1.0;
+#endif
 }
 
 // ------------------------------------------------------------------------------------ cross-cloud 1-NN distance

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Diagnostic PMC passes for k_batch_integrate (one rocprofv3 run per pass; --pmc never combined with tracing
+# Diagnostic PMC passes for k_batch_integrate (KPREFIX selects other kernels; OTSLAM_LIB a variant library) (one rocprofv3 run per pass; --pmc never combined with tracing
 # domains other than --kernel-trace).  Output: gpurun_out/diag_<i>/ and a per-kernel summary on stdout.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -25,6 +25,7 @@ for d in sys.argv[1:]:
         for row in csv.DictReader(open(f)):
             k = row.get("Kernel_Name", "").split("(")[0].split("::")[-1]
             per[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
-out = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items() if k.startswith("k_batch")}
+pref = os.environ.get("KPREFIX", "k_batch")
+out = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items() if k.startswith(pref)}
 print(json.dumps(out, indent=1))
 PY
