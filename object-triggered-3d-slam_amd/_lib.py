@@ -103,6 +103,7 @@ class OTError(RuntimeError):
 TEST_SIGNATURES = {
     "otx_serial_chain_f64": [_p, _i64, _i32, _p, _p],
     "otx_tsdf_stats": [_p, _p],
+    "otx_sort_pairs_u64_u32": [_p, _p, _p, _p, _i64, _i32, _p],
 }
 
 

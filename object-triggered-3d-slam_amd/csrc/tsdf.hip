@@ -759,10 +759,44 @@ __global__ __launch_bounds__(256) void k_import(TsdfDev d, const int32_t* __rest
     }
 }
 
-__global__ void k_pack_unit_keys(TsdfDev d, int n, unsigned long long* keys, unsigned* ids) {
+// per-axis min / max of the unit keys (one workgroup; a few thousand units)
+__global__ __launch_bounds__(256) void k_unit_bounds(TsdfDev d, int n, int* out6) {
+    __shared__ int mn[3], mx[3];
+    if (threadIdx.x < 3) {
+        mn[threadIdx.x] = 0x7FFFFFFF;
+        mx[threadIdx.x] = -0x7FFFFFFF;
+    }
+    __syncthreads();
+    int lo[3] = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF}, hi[3] = {-0x7FFFFFFF, -0x7FFFFFFF, -0x7FFFFFFF};
+    for (int i = threadIdx.x; i < n; i += 256)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = min(lo[a], d.unit_keys[i * 3 + a]);
+            hi[a] = max(hi[a], d.unit_keys[i * 3 + a]);
+        }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        atomicMin(&mn[a], lo[a]);
+        atomicMax(&mx[a], hi[a]);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        out6[threadIdx.x] = mn[threadIdx.x];
+        out6[3 + threadIdx.x] = mx[threadIdx.x];
+    }
+}
+
+// order-preserving compact keys: (x - x0) << (by + bz) | (y - y0) << bz | (z - z0), only the bits the ranges need
+struct UnitKeyPack {
+    int x0, y0, z0, sy, sx;
+};
+
+__global__ void k_pack_unit_keys(TsdfDev d, int n, UnitKeyPack pk, unsigned long long* keys, unsigned* ids) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    keys[i] = pack_key(d.unit_keys[i * 3 + 0], d.unit_keys[i * 3 + 1], d.unit_keys[i * 3 + 2]);
+    keys[i] = ((unsigned long long)(d.unit_keys[i * 3 + 0] - pk.x0) << pk.sx) |
+              ((unsigned long long)(d.unit_keys[i * 3 + 1] - pk.y0) << pk.sy) |
+              (unsigned long long)(d.unit_keys[i * 3 + 2] - pk.z0);
     ids[i] = (unsigned)i;
 }
 
@@ -1032,12 +1066,25 @@ ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) 
     if (nu > 0) {
         char* ws = (char*)scratch((size_t)nu * 24 + 256, 5);
         if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-        unsigned long long* kin = (unsigned long long*)ws;
+        int* b6 = (int*)ws;
+        unsigned long long* kin = (unsigned long long*)(ws + 256);
         unsigned long long* kout = kin + nu;
         unsigned* vin = (unsigned*)(kout + nu);
-        hipLaunchKernelGGL(k_pack_unit_keys, dim3((nu + 255) / 256), dim3(256), 0, stream, vol->dev, nu, kin, vin);
+        hipLaunchKernelGGL(k_unit_bounds, dim3(1), dim3(256), 0, stream, vol->dev, nu, b6);
+        int hb[6];
+        OT_HIP_TRY(hipMemcpyAsync(hb, b6, sizeof(hb), hipMemcpyDeviceToHost, stream));
+        OT_HIP_TRY(hipStreamSynchronize(stream));
+        int bits[3];
+        for (int a = 0; a < 3; ++a) {
+            const long long span = (long long)hb[3 + a] - hb[a];
+            bits[a] = 1;
+            while (bits[a] < 31 && (span >> bits[a]) != 0) ++bits[a];
+        }
+        const UnitKeyPack pk{hb[0], hb[1], hb[2], bits[2], bits[1] + bits[2]};
+        hipLaunchKernelGGL(k_pack_unit_keys, dim3((nu + 255) / 256), dim3(256), 0, stream, vol->dev, nu, pk, kin, vin);
         OT_LAUNCH_CHECK();
-        st = sort_pairs_u64_u32(kin, kout, vin, vol->sorted_ids, (size_t)nu, 63, stream, 3);
+        st = sort_pairs_u64_u32(kin, kout, vin, vol->sorted_ids, (size_t)nu, std::min(63, bits[0] + bits[1] + bits[2]),
+                                stream, 3);
         if (st != OT_OK) return st;
     }
     vol->sorted_units = nu;
