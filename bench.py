@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--objects", type=int, default=8,
                     help="configs[3]: object scans shared by all ranks (full per-object pipeline + RCCL merge); 0 = skip")
     ap.add_argument("--object-frames", type=int, default=64, help="configs[3]: frames per object scan")
+    ap.add_argument("--object-streams", type=int, default=2,
+                    help="configs[3]: objects reconstructed concurrently per GPU (host threads x HIP streams)")
     ap.add_argument("--spatial", type=int, default=1,
                     help="N > 1: also time one object spatially sharded over the N GPUs (SURVEY 8(e))")
     ap.add_argument("--hybrid-objects", type=int, default=32,
@@ -381,23 +383,40 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
     vols = [pkg.pipelines.integration.ScalableTSDFVolume(
         voxel_length=args.voxel, sdf_trunc=args.sdf_trunc,
         color_type=pkg.pipelines.integration.TSDFVolumeColorType.RGB8) for _ in dev]
-    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     npx = W * H
     sizes = {}
+    # objects are independent: T host threads, each driving its own HIP stream (the library's scratch buffers
+    # are per thread), reconstruct them concurrently so one object's mesh kernels overlap another's integration
+    from concurrent.futures import ThreadPoolExecutor
+
+    T = max(1, min(args.object_streams, len(dev)))
+    streams = [torch.cuda.Stream() for _ in range(T)]
+    pool = ThreadPoolExecutor(max_workers=T)
+
+    def reconstruct(t):
+        out = {}
+        with torch.cuda.stream(streams[t]):
+            stream = C.c_void_p(streams[t].cuda_stream)
+            for j in range(t, len(dev), T):
+                vol, (d16, col, ext) = vols[j], dev[j]
+                vol.reset()
+                for k in range(ext.shape[0]):
+                    st = lib.ot_tsdf_integrate_u16(vol._h, C.c_void_p(d16.data_ptr() + k * npx * 2),
+                                                   C.c_void_p(col.data_ptr() + k * npx * 3), C.byref(intr),
+                                                   ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
+                    if st:
+                        raise RuntimeError(lib.ot_last_error().decode())
+                mesh = vol.extract_triangle_mesh()
+                mesh.compute_vertex_normals()
+                out[j] = mesh
+            streams[t].synchronize()
+        return out
 
     def run():
-        meshes = []
-        for vol, (d16, col, ext) in zip(vols, dev):
-            vol.reset()
-            for k in range(ext.shape[0]):
-                st = lib.ot_tsdf_integrate_u16(vol._h, C.c_void_p(d16.data_ptr() + k * npx * 2),
-                                               C.c_void_p(col.data_ptr() + k * npx * 3), C.byref(intr),
-                                               ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
-                if st:
-                    raise RuntimeError(lib.ot_last_error().decode())
-            mesh = vol.extract_triangle_mesh()
-            mesh.compute_vertex_normals()
-            meshes.append(mesh)
+        parts = {}
+        for r in pool.map(reconstruct, range(T)):
+            parts.update(r)
+        meshes = [parts[j] for j in range(len(dev))]
         # the objects' 100k-point samplings in one call: their serial area-CDF chains run side by side
         pcds = pkg.geometry.TriangleMesh.sample_points_uniformly_batch(meshes, number_of_points=100000)
         clouds = [p.filter_min_z(0.03)._xyz.dev() for p in pcds]
@@ -406,9 +425,11 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
         return merged
 
     dt, merged = _timed(torch, dist, world, run, 3)
+    pool.shutdown()
     return {"workload": f"configs[3]: {args.objects} object scans x {args.object_frames} 640x480 frames, "
                         f"{args.voxel * 1000:g} mm TSDF -> mesh -> normals -> 100k samples -> z mask per object, "
-                        f"contiguous object shards over {world} GPU(s), RCCL all-gather merge",
+                        f"contiguous object shards over {world} GPU(s) ({T} concurrent streams per GPU), "
+                        f"RCCL all-gather merge",
             "frames_per_s": round(args.objects * args.object_frames / dt, 1), "ms": round(dt * 1e3, 3),
             "objects_per_rank": len(ids), "merged_points": int(merged.shape[0])}
 

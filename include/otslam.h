@@ -117,12 +117,15 @@ ot_status ot_compute_point_cloud_distance(const double* src, int64_t n, const do
 typedef struct ot_tsdf ot_tsdf;
 
 /* ScalableTSDFVolume(voxel_length, sdf_trunc, color_type, volume_unit_resolution=16,
- * depth_sampling_stride=4).  max_units bounds the block pool in HBM (0 = default 65536 units). */
+ * depth_sampling_stride=4).  max_units bounds the block pool in HBM (0 = default 32768 units). */
 ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_type,
                          int32_t volume_unit_resolution, int32_t depth_sampling_stride, int64_t max_units,
                          ot_tsdf** out);
 ot_status ot_tsdf_destroy(ot_tsdf* vol);
 ot_status ot_tsdf_reset(ot_tsdf* vol);  /* ScalableTSDFVolume.reset() */
+/* The same reset ordered on `stream` (no device-wide synchronisation): several volumes driven from several
+ * host threads / streams do not stall each other.  Frames still queued for a batch are integrated first. */
+ot_status ot_tsdf_reset_async(ot_tsdf* vol, void* stream);
 
 /* volume.integrate(rgbd, intrinsic, extrinsic) — reconstruct_rgbd_filter.py:105.
  * depth: float32 [h][w] (already scaled/truncated); color: uint8 [h][w][3] (RGB8) or NULL (NoColor). */

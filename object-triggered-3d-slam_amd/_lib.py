@@ -59,6 +59,7 @@ SIGNATURES = {
     "ot_tsdf_create": [_d, _d, _i32, _i32, _i32, _i64, C.POINTER(_p)],
     "ot_tsdf_destroy": [_p],
     "ot_tsdf_reset": [_p],
+    "ot_tsdf_reset_async": [_p, _p],
     "ot_tsdf_integrate": [_p, _p, _p, _pint, _p, _p],
     "ot_tsdf_integrate_u16": [_p, _p, _p, _pint, _p, _d, _d, _p],
     "ot_tsdf_flush": [_p, _p],

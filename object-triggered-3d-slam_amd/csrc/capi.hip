@@ -17,11 +17,13 @@ ot_status fail(ot_status code, const std::string& msg) {
 
 // Grow-only per-device scratch buffers, indexed by slot (a caller-chosen small integer).  Growth happens
 // with hipMalloc (synchronising) only when a larger request arrives; steady-state calls reuse the buffers.
+// Per host thread: threads driving their own streams (e.g. several objects reconstructed concurrently) never
+// share a buffer.  A thread's buffers live until the process ends (worker pools are long-lived).
 struct Arena {
     std::vector<void*> ptr;
     std::vector<size_t> size;
 };
-static std::vector<Arena> g_arena;
+static thread_local std::vector<Arena> g_arena;
 
 void* scratch(size_t bytes, int slot) {
     int dev = 0;

@@ -13,6 +13,8 @@
 //   k_mc_vertices  : one lane per bitmask word, vertex = half + vl*key, += f0*vl/(f0+f1) on the edge axis,
 //                    colour (f1*c0 + f0*c1)/(f0+f1) with c = colour/255 — Open3D's float64 expressions
 //   k_mc_triangles : per-lane triangle offsets by block scan; vertex ids by popcount lookups
+#include <atomic>
+#include <mutex>
 #include "../../include/otslam_mc_tables.h"
 #include "compact.h"
 #include "sort.h"
@@ -246,15 +248,18 @@ __global__ __launch_bounds__(256) void k_mc_triangles(McDev m, int32_t* T) {
     }
 }
 
-static bool g_tables_uploaded = false;
+static std::atomic<bool> g_tables_uploaded{false};
+static std::mutex g_tables_mutex;
 
-static ot_status upload_tables() {
-    if (g_tables_uploaded) return OT_OK;
+static ot_status upload_tables() {  // once per process (one process per GPU), safe from concurrent host threads
+    if (g_tables_uploaded.load(std::memory_order_acquire)) return OT_OK;
+    std::lock_guard<std::mutex> lock(g_tables_mutex);
+    if (g_tables_uploaded.load(std::memory_order_relaxed)) return OT_OK;
     OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_tri), OT_MC_TRI_TABLE, sizeof(OT_MC_TRI_TABLE)));
     OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_eshift), OT_MC_EDGE_SHIFT, sizeof(OT_MC_EDGE_SHIFT)));
     OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_e2v), OT_MC_EDGE_TO_VERT, sizeof(OT_MC_EDGE_TO_VERT)));
     OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_shift), OT_MC_SHIFT, sizeof(OT_MC_SHIFT)));
-    g_tables_uploaded = true;
+    g_tables_uploaded.store(true, std::memory_order_release);
     return OT_OK;
 }
 

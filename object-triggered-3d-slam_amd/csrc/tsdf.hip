@@ -1190,6 +1190,25 @@ ot_status ot_tsdf_reset(ot_tsdf* v) {
     return OT_OK;
 }
 
+ot_status ot_tsdf_reset_async(ot_tsdf* v, void* stream_) {
+    if (!v) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume::Reset] volume is NULL");
+    hipStream_t stream = S(stream_);
+    ot_status st = tsdf_flush(v, stream);  // queued frames belong to the old contents: apply, then clear
+    if (st != OT_OK) return st;
+    TsdfDev& d = v->dev;
+    OT_HIP_TRY(hipMemsetAsync(d.hkeys, 0xFF, sizeof(unsigned long long) * v->hash_cap, stream));
+    OT_HIP_TRY(hipMemsetAsync(d.hvals, 0xFF, sizeof(int) * v->hash_cap, stream));
+    OT_HIP_TRY(hipMemsetAsync(d.stamp, 0xFF, sizeof(int) * v->hash_cap, stream));
+    OT_HIP_TRY(hipMemsetAsync(d.fmask, 0, sizeof(unsigned long long) * v->hash_cap, stream));
+    OT_HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * N_COUNTERS, stream));
+    OT_HIP_TRY(hipMemsetAsync(d.stats, 0, sizeof(unsigned long long) * 4, stream));
+    v->frame_id = 0;
+    v->sorted_frame = -1;
+    v->sorted_units = -1;
+    v->mesh.nv = v->mesh.nt = 0;
+    return OT_OK;
+}
+
 ot_status ot_tsdf_integrate(ot_tsdf* vol, const float* depth, const uint8_t* color, const ot_intrinsics* in,
                             const double extrinsic[16], void* stream) {
     ot_status st = check_frame(vol, depth, color, in, extrinsic);

@@ -60,7 +60,8 @@ class ScalableTSDFVolume:
         L.call("ot_tsdf_set_batch", self._h, int(frames))
 
     def reset(self):
-        L.call("ot_tsdf_reset", self._h)
+        """ScalableTSDFVolume::Reset, ordered on the current stream (no device-wide synchronisation)."""
+        L.call("ot_tsdf_reset_async", self._h, D.stream_ptr())
         self._keep.clear()
 
     def integrate(self, image: RGBDImage, intrinsic, extrinsic):
