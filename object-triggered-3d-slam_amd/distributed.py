@@ -106,10 +106,12 @@ def merge_object_clouds(local_clouds, group=None):
     return all_gather_rows(local.to(torch.float64), group)
 
 
-def reconstruct_and_merge(cfg, yaml_file=None, pgm_file=None, save_path=None, objects=None, o3d=None):
+def reconstruct_and_merge(cfg, yaml_file=None, pgm_file=None, save_path=None, objects=None, o3d=None, streams=2):
     """configs[3]/[4] driver: every rank reconstructs its shard of the objects on its own GPU (integrate ->
     extract -> normals -> sample 100k -> Z mask, reconstruct_rgbd_filter.py:60-141), then the filtered clouds
     are all-gathered; rank 0 builds and writes the hybrid map (map cloud first, then objects in sorted order).
+    `streams` objects of a rank are reconstructed concurrently (host threads, each with its own HIP stream:
+    one object's file decoding and mesh kernels overlap another's integration); the clouds keep sorted order.
     Returns the merged point array on rank 0 (None elsewhere)."""
     import importlib
 
@@ -122,11 +124,27 @@ def reconstruct_and_merge(cfg, yaml_file=None, pgm_file=None, save_path=None, ob
     rank, world = dist.get_rank(), dist.get_world_size()
     labels = R.get_unique_object_names(cfg) if objects is None else sorted(objects)
     mine = shard(labels, rank, world)
-    clouds = []
-    for label in mine:
-        pts = _reconstruct_points(R, cfg, label, o3d)
-        if pts is not None:
-            clouds.append(pts)
+    T = max(1, min(int(streams), len(mine)))
+    if T == 1:
+        results = [_reconstruct_points(R, cfg, label, o3d) for label in mine]
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+
+        def work(t):
+            s = torch.cuda.Stream()
+            out = {}
+            with torch.cuda.stream(s):
+                for j in range(t, len(mine), T):
+                    out[j] = _reconstruct_points(R, cfg, mine[j], o3d)
+                s.synchronize()
+            return out
+
+        done = {}
+        with ThreadPoolExecutor(max_workers=T) as ex:
+            for part in ex.map(work, range(T)):
+                done.update(part)
+        results = [done[j] for j in range(len(mine))]
+    clouds = [pts for pts in results if pts is not None]
     merged = merge_object_clouds(clouds)
     if rank != 0:
         return None

@@ -71,8 +71,10 @@ def test_merge_driver_single_rank(pkg, O, synth, gpu, scan_dir, tmp_path):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
         cfg = R.ScanConfig(base_dir=scan_dir)
-        pts = D.reconstruct_and_merge(cfg, save_path=str(tmp_path / "merged.ply"))
+        pts = D.reconstruct_and_merge(cfg, save_path=str(tmp_path / "merged.ply"), streams=1)
+        pts2 = D.reconstruct_and_merge(cfg, streams=2)  # objects on two concurrent host threads / streams
     finally:
         dist.destroy_process_group()
     parts = [_oracle_object(O, synth, scan_dir, lab, cfg)[0] for lab in ("Object_0", "Object_1")]
     assert_bitwise(pts, np.concatenate(parts), "merged object clouds (sorted object order)")
+    assert_bitwise(pts2, pts, "merged object clouds, 2 concurrent streams")
