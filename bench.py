@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--objects", type=int, default=8,
                     help="configs[3]: object scans shared by all ranks (full per-object pipeline + RCCL merge); 0 = skip")
     ap.add_argument("--object-frames", type=int, default=64, help="configs[3]: frames per object scan")
+    ap.add_argument("--filter-streams", type=int, default=6,
+                    help="configs[2]: frames filtered concurrently (host threads x HIP streams)")
     ap.add_argument("--object-streams", type=int, default=2,
                     help="configs[3]: objects reconstructed concurrently per GPU (host threads x HIP streams)")
     ap.add_argument("--spatial", type=int, default=1,
@@ -515,40 +517,60 @@ def filter_stream(args, L, lib, synth, torch, rank):
     d16 = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
     col = torch.from_numpy(color).cuda().contiguous()
     npx = W * H
-    df = torch.empty((H, W), dtype=torch.float32, device="cuda")
-    xyz = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
-    rgb = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
-    vx = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
-    vc = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
-    idx = torch.empty((npx,), dtype=torch.int64, device="cuda")
-    out = torch.empty((npx, 3), dtype=torch.float64, device="cuda")
     intr = L.ot_intrinsics(W, H, *intr_t[2:])
-    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     exts = np.ascontiguousarray(ext)
-    P, K, Kk = C.c_int64(0), C.c_int64(0), C.c_int64(0)
     ptr = lambda t: C.c_void_p(t.data_ptr())
+    # frames are independent: T host threads, each with its own HIP stream and buffers, take frames round-robin,
+    # so one frame's host round trips (each Open3D-shaped call returns its size) overlap another's kernels
+    from concurrent.futures import ThreadPoolExecutor
 
-    def frame(k):
+    T = max(1, args.filter_streams)
+    streams = [torch.cuda.Stream() for _ in range(T)]
+
+    def buffers():
+        f64 = lambda: torch.empty((npx, 3), dtype=torch.float64, device="cuda")
+        return {"df": torch.empty((H, W), dtype=torch.float32, device="cuda"), "xyz": f64(), "rgb": f64(),
+                "vx": f64(), "vc": f64(), "out": f64(), "idx": torch.empty((npx,), dtype=torch.int64, device="cuda")}
+
+    bufs = []
+    for t in range(T):
+        with torch.cuda.stream(streams[t]):
+            bufs.append(buffers())
+
+    def frame(k, t):
         f = k % nuniq
-        L.call("ot_depth_to_float", C.c_void_p(d16.data_ptr() + f * npx * 2), ptr(df), npx, 1000.0, 5.0, stream)
-        L.call("ot_unproject", ptr(df), C.c_void_p(col.data_ptr() + f * npx * 3), C.byref(intr),
-               exts[f].ctypes.data_as(C.c_void_p), 1, ptr(xyz), ptr(rgb), npx, C.byref(P), stream)
-        L.call("ot_voxel_down_sample", ptr(xyz), ptr(rgb), None, P.value, 0.005, ptr(vx), ptr(vc), None, None,
-               C.byref(K), stream)
-        L.call("ot_remove_statistical_outlier", ptr(vx), K.value, 20, 2.0, ptr(idx), None, C.byref(Kk), stream)
-        L.call("ot_gather_rows3", ptr(vx), ptr(idx), Kk.value, ptr(out), stream)
+        b, stream = bufs[t], C.c_void_p(streams[t].cuda_stream)
+        P, K, Kk = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+        L.call("ot_depth_to_float", C.c_void_p(d16.data_ptr() + f * npx * 2), ptr(b["df"]), npx, 1000.0, 5.0, stream)
+        L.call("ot_unproject", ptr(b["df"]), C.c_void_p(col.data_ptr() + f * npx * 3), C.byref(intr),
+               exts[f].ctypes.data_as(C.c_void_p), 1, ptr(b["xyz"]), ptr(b["rgb"]), npx, C.byref(P), stream)
+        L.call("ot_voxel_down_sample", ptr(b["xyz"]), ptr(b["rgb"]), None, P.value, 0.005, ptr(b["vx"]), ptr(b["vc"]),
+               None, None, C.byref(K), stream)
+        L.call("ot_remove_statistical_outlier", ptr(b["vx"]), K.value, 20, 2.0, ptr(b["idx"]), None, C.byref(Kk),
+               stream)
+        L.call("ot_gather_rows3", ptr(b["vx"]), ptr(b["idx"]), Kk.value, ptr(b["out"]), stream)
         return P.value, K.value, Kk.value
 
-    for k in range(4):
-        frame(k)
+    def worker(t, frames):
+        tot = [0, 0, 0]
+        with torch.cuda.stream(streams[t]):
+            for k in range(t, frames, T):
+                r = frame(k, t)
+                tot = [a + b for a, b in zip(tot, r)]
+            streams[t].synchronize()
+        return tot
+
+    pool = ThreadPoolExecutor(max_workers=T)
+    for _ in pool.map(lambda t: worker(t, 4 * T), range(T)):
+        pass
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     pts = vox = kept = 0
-    for k in range(args.filter_frames):
-        p, v, kk = frame(k)
-        pts, vox, kept = pts + p, vox + v, kept + kk
+    for p_, v_, k_ in pool.map(lambda t: worker(t, args.filter_frames), range(T)):
+        pts, vox, kept = pts + p_, vox + v_, kept + k_
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    pool.shutdown()
     # CPU oracle on 2 frames of the same stream
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -563,7 +585,7 @@ def filter_stream(args, L, lib, synth, torch, rank):
         cpu_pts += x.shape[0]
     cdt = time.perf_counter() - t1
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    return {"workload": "configs[2]: 1280x720 RGB-D stream, unproject + voxel_down_sample(0.005) + "
+    return {"workload": f"configs[2]: 1280x720 RGB-D stream ({T} concurrent streams), unproject + voxel_down_sample(0.005) + "
                         "remove_statistical_outlier(20, 2.0) per frame",
             "frames": args.filter_frames, "mpoints_per_s": round(pts / dt / 1e6, 2),
             "frames_per_s": round(args.filter_frames / dt, 2), "ms_per_frame": round(dt * 1e3 / args.filter_frames, 3),

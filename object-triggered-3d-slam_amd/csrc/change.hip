@@ -114,7 +114,8 @@ static ot_status unique_keys(const double* xyz, int64_t n, double vs, const doub
     st = compact(n, UniqPred{kout}, UniqEmit{kout, uniq}, stream, nu, slot + 1);  // synchronises
     if (st != OT_OK) return st;
     int e = 0;
-    OT_HIP_TRY(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
+    OT_HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
     if (e) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] lattice key out of range (voxel_size too small)");
     return OT_OK;
 }
@@ -183,7 +184,8 @@ static ot_status unique_obj_keys(const double* xyz, const int64_t* off, int n_ob
     st = compact(n, UniqPred{kout}, UniqEmit{kout, uniq}, stream, nu, slot + 1);  // synchronises
     if (st != OT_OK) return st;
     int e = 0;
-    OT_HIP_TRY(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
+    OT_HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
     if (e) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] lattice key out of range (voxel_size too small)");
     return OT_OK;
 }

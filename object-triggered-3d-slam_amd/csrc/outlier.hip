@@ -547,7 +547,8 @@ static ot_status build_grid(const double* xyz, int64_t n, double h, const double
     st = compact_segments(n, kout, heads, pcell, stream, &ncells, 9);  // synchronises
     if (st != OT_OK) return st;
     int e = 0;
-    OT_HIP_TRY(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
+    OT_HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
     if (e) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (non-finite point coordinates)");
     int64_t cap = 1;
     while (cap < 2 * ncells + 2) cap <<= 1;

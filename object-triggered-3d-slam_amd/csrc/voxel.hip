@@ -153,7 +153,8 @@ extern "C" ot_status ot_voxel_down_sample(const double* xyz, const double* rgb, 
     st = compact(n, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises
     if (st != OT_OK) return st;
     int err = 0;
-    OT_HIP_TRY(hipMemcpy(&err, &b->err, sizeof(int), hipMemcpyDeviceToHost));
+    OT_HIP_TRY(hipMemcpyAsync(&err, &b->err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
     if (err == 1) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel_size is too small.");
     if (err == 2) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel grid exceeds 64-bit key packing");
     hipLaunchKernelGGL(k_voxel_reduce, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, xyz, rgb, normals,
