@@ -164,3 +164,35 @@ def test_ror_bench_scale_bitexact(pkg, O, hd_voxels):
     out, idx = _pcd(pkg, ds).remove_radius_outlier(16, 0.02)
     ridx = O.remove_radius_outlier(ds, 16, 0.02)
     assert_bitwise(np.asarray(idx, np.int64), ridx, "ROR kept (bench scale)")
+
+
+def test_concurrent_streams_match_serial(pkg, O, synth, seq16, gpu):
+    """Different host threads on their own HIP streams (per-thread scratch) give the serial results bit for bit:
+    voxel_down_sample -> remove_statistical_outlier -> remove_radius_outlier on 4 clouds, 4 threads at once."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    depth, color, ext = seq16
+    intr_t = ref_intr(synth)
+    clouds = [O.unproject(O.depth_to_float(depth[f], 1000.0, 5.0), color[f], intr_t, ext[f]) for f in range(4)]
+
+    def chain(xyz, rgb):
+        ds = _pcd(pkg, xyz, rgb).voxel_down_sample(0.005)
+        _, sor = ds.remove_statistical_outlier(20, 2.0)
+        _, ror = ds.remove_radius_outlier(16, 0.02)
+        return np.asarray(ds.points), np.asarray(sor), np.asarray(ror)
+
+    serial = [chain(*c) for c in clouds]
+
+    def threaded(i):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            out = [chain(*clouds[i]) for _ in range(3)]
+            s.synchronize()
+        return out
+
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        results = list(ex.map(threaded, range(4)))
+    for i in range(4):
+        for rep in results[i]:
+            for got, exp, what in zip(rep, serial[i], ("voxels", "SOR kept", "ROR kept")):
+                assert_bitwise(got, exp, f"concurrent {what} (cloud {i})")
