@@ -228,11 +228,18 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
     __syncthreads();
     const int64_t base = b * CH;
     const int cnt = j.n - base < CH ? (int)(j.n - base) : CH;
-    if (lane == 0) {
+    if (lane == 0) {  // 8 staged operands read ahead of their dependent adds (one LDS round trip per 8)
         double acc = s;
-        for (int k = 0; k < cnt; ++k) {
-            acc = lds[k] + acc;
-            if (CDF) lds[k] = acc;
+        for (int k0 = 0; k0 < cnt; k0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = lds[k0 + i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (k0 + i < cnt) {
+                    acc = v[i] + acc;
+                    if (CDF) lds[k0 + i] = acc;
+                }
         }
         lds[CH] = acc;
     }
@@ -249,6 +256,8 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
     return out;
 }
 
+constexpr int WALK_DEPTH = 4;  // groups of 64 chunk summaries the walk keeps in flight
+
 template <bool CDF>
 __global__ __launch_bounds__(64) void k_chain_walk(const ChainJob* __restrict__ jobs) {
     __shared__ double lds[CH + 2];
@@ -256,14 +265,32 @@ __global__ __launch_bounds__(64) void k_chain_walk(const ChainJob* __restrict__ 
     const int lane = threadIdx.x;
     const int64_t nb = (j.n + CH - 1) / CH;
     double s = 0.0;  // sum: 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0
-    int e_n = EX_NONE, k_n = 1;
-    long long m_n = 0;
-    if (lane < nb) e_n = j.ex[lane], m_n = j.msum[lane], k_n = j.kind[lane];
-    for (int64_t g = 0; g < nb; g += 64) {
+    // chunk summaries of the next WALK_DEPTH groups stay in flight (a register ring; static indices only)
+    int e_r[WALK_DEPTH], k_r[WALK_DEPTH];
+    long long m_r[WALK_DEPTH];
+#pragma unroll
+    for (int q = 0; q < WALK_DEPTH; ++q) {
+        const int64_t b = (int64_t)q * 64 + lane;
+        const bool in = b < nb;
+        e_r[q] = in ? j.ex[b] : EX_NONE;
+        m_r[q] = in ? j.msum[b] : 0;
+        k_r[q] = in ? j.kind[b] : 1;
+    }
+    for (int64_t g0 = 0; g0 < nb; g0 += 64 * WALK_DEPTH)
+#pragma unroll
+    for (int q = 0; q < WALK_DEPTH; ++q) {
+        const int64_t g = g0 + (int64_t)q * 64;
+        if (g >= nb) break;
         const int64_t b = g + lane;
-        const int e_b = e_n, k_b = k_n;
-        const long long m_b = m_n;
-        if (b + 64 < nb) e_n = j.ex[b + 64], m_n = j.msum[b + 64], k_n = j.kind[b + 64];  // next group in flight
+        const int e_b = e_r[q], k_b = k_r[q];
+        const long long m_b = m_r[q];
+        {  // refill this ring slot with the group WALK_DEPTH ahead
+            const int64_t bn = b + 64 * WALK_DEPTH;
+            const bool in = bn < nb;
+            e_r[q] = in ? j.ex[bn] : EX_NONE;
+            m_r[q] = in ? j.msum[bn] : 0;
+            k_r[q] = in ? j.kind[bn] : 1;
+        }
         const int lim = nb - g < 64 ? (int)(nb - g) : 64;
         int local = 0;
         while (local < lim) {
@@ -559,8 +586,10 @@ ot_status ot_mesh_get_surface_area(const double* V, int64_t nv, const int32_t* T
 }
 
 // test hook (not part of the drop-in boundary): the bare chains on a device array x (16-B aligned) -- cdf != 0:
-// out[t] = x_t + out[t-1] for all t (numpy.cumsum's order); cdf == 0: out[0] = ((0 + x_0) + x_1) + ...
-ot_status otx_serial_chain_f64(const double* x, int64_t n, int32_t cdf, double* out, void* stream_) {
+// out[t] = x_t + out[t-1] for all t (numpy.cumsum's order); cdf == 0: out[0] = ((0 + x_0) + x_1) + ...;
+// serial_chunks_host (nullable): how many 256-value chunks the walk could not prove and ran serially
+ot_status otx_serial_chain_f64(const double* x, int64_t n, int32_t cdf, double* out, int64_t* serial_chunks_host,
+                               void* stream_) {
     hipStream_t stream = S(stream_);
     if (n <= 0 || !x || !out || ((uintptr_t)x & 15)) return fail(OT_ERR_INVALID_ARGUMENT, "[chain] invalid arguments");
     char* ws = (char*)scratch(chain_aux_bytes(n) + sizeof(ChainJob) + 256, 17);
@@ -572,6 +601,15 @@ ot_status otx_serial_chain_f64(const double* x, int64_t n, int32_t cdf, double* 
     if (cdf) launch_chains<true>(djob, 1, n, stream);
     else launch_chains<false>(djob, 1, n, stream);
     OT_LAUNCH_CHECK();
+    if (serial_chunks_host) {  // diagnostic: chunks the walk had to run serially (kind == 2)
+        const int64_t nb = (n + CH - 1) / CH;
+        std::vector<int32_t> kind((size_t)nb);
+        OT_HIP_TRY(hipMemcpyAsync(kind.data(), jb.kind, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, stream));
+        OT_HIP_TRY(hipStreamSynchronize(stream));
+        int64_t c = 0;
+        for (int32_t k : kind) c += k == 2;
+        *serial_chunks_host = c;
+    }
     OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
 }

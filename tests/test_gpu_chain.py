@@ -19,7 +19,7 @@ def _chain(pkg, x, cdf):
     L = pkg._lib
     d = torch.from_numpy(np.ascontiguousarray(x, np.float64)).cuda()
     out = torch.empty(d.shape[0] if cdf else 1, dtype=torch.float64, device="cuda")
-    L.call("otx_serial_chain_f64", C.c_void_p(d.data_ptr()), d.shape[0], int(cdf), C.c_void_p(out.data_ptr()),
+    L.call("otx_serial_chain_f64", C.c_void_p(d.data_ptr()), d.shape[0], int(cdf), C.c_void_p(out.data_ptr()), None,
            C.c_void_p(torch.cuda.current_stream().cuda_stream))
     return out.cpu().numpy()
 
