@@ -254,8 +254,9 @@ ot_status ot_voxel_key_diff(const double* new_xyz, int64_t n, const double* old_
 
 /* The same for n_objects objects at once (a hybrid map's object clouds vs their saved versions): clouds are
  * concatenated, object j = rows [offsets[j], offsets[j+1]) (host offsets, n_objects + 1 each); outputs are
- * int32 [k][4] = (object, x, y, z), sorted by object then key.  Lattice coordinates must lie in (-2^16, 2^16);
- * at most 2048 objects.  Equals n_objects calls of ot_voxel_key_diff. */
+ * int32 [k][4] = (object, x, y, z), sorted by object then key.  Lattice coordinates must lie in (-2^30, 2^30)
+ * and the joint extent plus the object id must pack into 64 bits; at most 2048 objects.  Equals n_objects calls
+ * of ot_voxel_key_diff. */
 ot_status ot_voxel_key_diff_multi(const double* new_xyz, const int64_t* new_offsets, const double* old_xyz,
                                   const int64_t* old_offsets, int32_t n_objects, double voxel_size,
                                   const double origin[3], int32_t* out_added, int64_t* n_added_host,

@@ -120,74 +120,104 @@ static ot_status unique_keys(const double* xyz, int64_t n, double vs, const doub
     return OT_OK;
 }
 
-// Multi-object form: key = object id (11 bits) | x, y, z (17 bits each, biased by 2^16), so ONE sort / unique /
-// set difference serves every object of a hybrid map; equal keys imply the same object.
-constexpr int MK_BITS = 17;
-constexpr int MK_BIAS = 1 << 16;
+// Multi-object form: key = object id | x | y | z lattice offsets, each field with only the bits its range
+// needs (one layout for the new and the old clouds, from their joint bounds), so ONE sort / unique / set
+// difference serves every object of a hybrid map in as few radix passes as the data allows; equal keys imply
+// the same object.
+struct ObjLayout {
+    int mn[3];       // lattice minimum per axis
+    int sx, sy, so;  // key = obj << so | (x - mn0) << sx | (y - mn1) << sy | (z - mn2)
+};
+
+constexpr double LATTICE_MAX = 1073741824.0;  // |lattice coordinate| < 2^30
+
+// grid-stride over the points (a fixed grid of at most LB_BLOCKS blocks): per-thread bounds, wave reductions, a
+// block reduction in LDS, then one atomic per block and field (a few thousand atomics on 6 words, not one per wave)
+constexpr int LB_BLOCKS = 512;
+__global__ __launch_bounds__(256) void k_lattice_bounds(const double* __restrict__ xyz, int64_t n, double vs,
+                                                        double ox, double oy, double oz, int* b6, int* err) {
+    __shared__ int red[6][4];
+    const double o[3] = {ox, oy, oz};
+    int lo[3] = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF}, hi[3] = {-0x7FFFFFFF, -0x7FFFFFFF, -0x7FFFFFFF};
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const double f = floor((xyz[i * 3 + a] - o[a]) / vs);
+            if (fabs(f) < LATTICE_MAX) {
+                lo[a] = min(lo[a], (int)f);
+                hi[a] = max(hi[a], (int)f);
+            } else {
+                bad = true;
+            }
+        }
+    }
+    if (bad) *err = 1;
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {  // every lane reaches the whole-wave reductions
+        const int l = __ockl_wfred_min_i32(lo[a]), h = __ockl_wfred_max_i32(hi[a]);
+        if ((threadIdx.x & 63) == 0) {
+            red[a][w] = l;
+            red[3 + a][w] = h;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int a = threadIdx.x;
+        atomicMin(&b6[a], min(min(red[a][0], red[a][1]), min(red[a][2], red[a][3])));
+        atomicMax(&b6[3 + a], max(max(red[3 + a][0], red[3 + a][1]), max(red[3 + a][2], red[3 + a][3])));
+    }
+}
 
 __global__ __launch_bounds__(256) void k_lattice_keys_obj(const double* __restrict__ xyz, int64_t n, int obj,
-                                                          double vs, double ox, double oy, double oz,
-                                                          unsigned long long* keys, int* err) {
+                                                          double vs, double ox, double oy, double oz, ObjLayout lay,
+                                                          unsigned long long* keys) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const double f[3] = {floor((xyz[i * 3 + 0] - ox) / vs), floor((xyz[i * 3 + 1] - oy) / vs),
-                         floor((xyz[i * 3 + 2] - oz) / vs)};
-    unsigned long long k = (unsigned long long)obj;
-    bool ok = true;
+    const double o[3] = {ox, oy, oz};
+    unsigned long long f[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        ok = ok && fabs(f[a]) < (double)MK_BIAS;
-        k = (k << MK_BITS) | (unsigned long long)(ok ? (int)f[a] + MK_BIAS : 0);
-    }
-    if (!ok) *err = 1;
-    keys[i] = k;
+    for (int a = 0; a < 3; ++a) f[a] = (unsigned long long)((int)floor((xyz[i * 3 + a] - o[a]) / vs) - lay.mn[a]);
+    keys[i] = ((unsigned long long)obj << lay.so) | (f[0] << lay.sx) | (f[1] << lay.sy) | f[2];
 }
 
 struct ObjKeyEmit {
     const unsigned long long* a;
     int32_t* out;  // [k][4]: object, x, y, z
+    ObjLayout lay;
     __device__ void operator()(int64_t i, int64_t pos) const {
         const unsigned long long k = a[i];
-        const unsigned m = (1u << MK_BITS) - 1u;
-        out[pos * 4 + 0] = (int)(k >> (3 * MK_BITS));
-        out[pos * 4 + 1] = (int)((k >> (2 * MK_BITS)) & m) - MK_BIAS;
-        out[pos * 4 + 2] = (int)((k >> MK_BITS) & m) - MK_BIAS;
-        out[pos * 4 + 3] = (int)(k & m) - MK_BIAS;
+        out[pos * 4 + 0] = (int)(k >> lay.so);
+        out[pos * 4 + 1] = (int)((k >> lay.sx) & ((1ull << (lay.so - lay.sx)) - 1ull)) + lay.mn[0];
+        out[pos * 4 + 2] = (int)((k >> lay.sy) & ((1ull << (lay.sx - lay.sy)) - 1ull)) + lay.mn[1];
+        out[pos * 4 + 3] = (int)(k & ((1ull << lay.sy) - 1ull)) + lay.mn[2];
     }
 };
 
 // sorted unique object-lattice keys of the concatenated clouds of n_obj objects (offsets: host, n_obj + 1)
 static ot_status unique_obj_keys(const double* xyz, const int64_t* off, int n_obj, double vs, const double o[3],
-                                 unsigned long long* uniq, int64_t* nu, int slot, hipStream_t stream) {
+                                 const ObjLayout& lay, int end_bit, unsigned long long* uniq, int64_t* nu, int slot,
+                                 hipStream_t stream) {
     *nu = 0;
     const int64_t n = off[n_obj];
     if (n == 0) return OT_OK;
     char* ws = (char*)scratch(256 + (size_t)n * (8 + 8 + 4 + 4), slot);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-    int* err = (int*)ws;
     unsigned long long* kin = (unsigned long long*)(ws + 256);
     unsigned long long* kout = kin + n;
     unsigned* vin = (unsigned*)(kout + n);
     unsigned* vout = vin + n;
-    OT_HIP_TRY(hipMemsetAsync(err, 0, sizeof(int), stream));
     for (int j = 0; j < n_obj; ++j) {
         const int64_t m = off[j + 1] - off[j];
         if (m > 0)
             hipLaunchKernelGGL(k_lattice_keys_obj, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
-                               xyz + off[j] * 3, m, j, vs, o[0], o[1], o[2], kin + off[j], err);
+                               xyz + off[j] * 3, m, j, vs, o[0], o[1], o[2], lay, kin + off[j]);
     }
     OT_LAUNCH_CHECK();
-    int bits = 3 * MK_BITS;
-    while (bits < 64 && ((unsigned long long)(n_obj - 1) >> (bits - 3 * MK_BITS)) != 0) ++bits;
-    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, bits, stream, 3);  // values unused
+    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, end_bit, stream, 3);  // values unused
     if (st != OT_OK) return st;
-    st = compact(n, UniqPred{kout}, UniqEmit{kout, uniq}, stream, nu, slot + 1);  // synchronises
-    if (st != OT_OK) return st;
-    int e = 0;
-    OT_HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, stream));
-    OT_HIP_TRY(hipStreamSynchronize(stream));
-    if (e) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] lattice key out of range (voxel_size too small)");
-    return OT_OK;
+    return compact(n, UniqPred{kout}, UniqEmit{kout, uniq}, stream, nu, slot + 1);  // synchronises
 }
 
 // ------------------------------------------------------------------------------------------- scan diff
@@ -397,19 +427,54 @@ ot_status ot_voxel_key_diff_multi(const double* new_xyz, const int64_t* new_offs
     unsigned long long* ua = (unsigned long long*)scratch((size_t)std::max<int64_t>(n, 1) * 8 + 64, 31);
     unsigned long long* ub = (unsigned long long*)scratch((size_t)std::max<int64_t>(m, 1) * 8 + 64, 32);
     if (!ua || !ub) return fail(OT_ERR_HIP, "scratch allocation failed");
+    if (n + m == 0) return OT_OK;
+    // joint lattice bounds of both cloud sets -> the key layout
+    int* b6 = (int*)scratch(64, 37);
+    if (!b6) return fail(OT_ERR_HIP, "scratch allocation failed");
+    OT_HIP_TRY(hipMemsetAsync(b6, 0x7F, sizeof(int) * 3, stream));      // +large: minima
+    OT_HIP_TRY(hipMemsetAsync(b6 + 3, 0x80, sizeof(int) * 3, stream));  // -large: maxima
+    OT_HIP_TRY(hipMemsetAsync(b6 + 6, 0, sizeof(int), stream));         // error flag
+    if (n > 0)
+        hipLaunchKernelGGL(k_lattice_bounds, dim3((unsigned)std::min<int64_t>((n + 255) / 256, LB_BLOCKS)), dim3(256), 0,
+                           stream, new_xyz, n, voxel_size, origin[0], origin[1], origin[2], b6, b6 + 6);
+    if (m > 0)
+        hipLaunchKernelGGL(k_lattice_bounds, dim3((unsigned)std::min<int64_t>((m + 255) / 256, LB_BLOCKS)), dim3(256), 0,
+                           stream, old_xyz, m, voxel_size, origin[0], origin[1], origin[2], b6, b6 + 6);
+    OT_LAUNCH_CHECK();
+    int hb[7];
+    OT_HIP_TRY(hipMemcpyAsync(hb, b6, sizeof(hb), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    if (hb[6]) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] lattice key out of range (voxel_size too small)");
+    auto bits_for = [](long long v) {  // bits to represent 0..v
+        int b = 1;
+        while (b < 62 && (v >> b) != 0) ++b;
+        return b;
+    };
+    ObjLayout lay;
+    int bx[3];
+    for (int a = 0; a < 3; ++a) {
+        lay.mn[a] = hb[a];
+        bx[a] = bits_for((long long)hb[3 + a] - hb[a]);
+    }
+    lay.sy = bx[2];
+    lay.sx = bx[1] + bx[2];
+    lay.so = bx[0] + bx[1] + bx[2];
+    const int end_bit = lay.so + (n_objects > 1 ? bits_for(n_objects - 1) : 0);
+    if (end_bit > 64) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] lattice extent too large for 64-bit keys");
     int64_t na = 0, nb = 0;
-    ot_status st = unique_obj_keys(new_xyz, new_offsets, n_objects, voxel_size, origin, ua, &na, 33, stream);
+    ot_status st = unique_obj_keys(new_xyz, new_offsets, n_objects, voxel_size, origin, lay, end_bit, ua, &na, 33,
+                                   stream);
     if (st != OT_OK) return st;
-    st = unique_obj_keys(old_xyz, old_offsets, n_objects, voxel_size, origin, ub, &nb, 33, stream);
+    st = unique_obj_keys(old_xyz, old_offsets, n_objects, voxel_size, origin, lay, end_bit, ub, &nb, 33, stream);
     if (st != OT_OK) return st;
     if (na > 0) {
         if (!out_added) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] out_added is NULL");
-        st = compact(na, AbsentPred{ua, ub, nb}, ObjKeyEmit{ua, out_added}, stream, n_added_host, 35);
+        st = compact(na, AbsentPred{ua, ub, nb}, ObjKeyEmit{ua, out_added, lay}, stream, n_added_host, 35);
         if (st != OT_OK) return st;
     }
     if (nb > 0) {
         if (!out_removed) return fail(OT_ERR_INVALID_ARGUMENT, "[voxel_key_diff] out_removed is NULL");
-        st = compact(nb, AbsentPred{ub, ua, na}, ObjKeyEmit{ub, out_removed}, stream, n_removed_host, 36);
+        st = compact(nb, AbsentPred{ub, ua, na}, ObjKeyEmit{ub, out_removed, lay}, stream, n_removed_host, 36);
         if (st != OT_OK) return st;
     }
     return OT_OK;
