@@ -65,6 +65,24 @@ def test_unproject_bitexact(pkg, O, gpu, synth, seq16, posed):
     assert_bitwise(np.asarray(pcd.colors), rc, "unprojected rgb")
 
 
+def test_unproject_and_voxel_odd_resolution(pkg, O, gpu, synth):
+    """321x243 frame (odd sizes, off-centre principal point): unprojection order and values, then the voxel
+    downsample, bit-exact."""
+    intr_t = (321, 243, 283.1, 283.4, 161.7, 120.2)
+    depth, color, ext = synth.make_sequence(n_frames=8, frames=[3], intr=intr_t)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), depth_scale=1000.0, depth_trunc=5.0,
+        convert_rgb_to_intensity=False)
+    pcd = pkg.geometry.PointCloud.create_from_rgbd_image(rgbd, intr, ext[0])
+    rx, rc = O.unproject(O.depth_to_float(depth[0], 1000.0, 5.0), color[0], intr_t, ext[0])
+    assert len(pcd.points) == rx.shape[0] > 20000
+    assert_bitwise(np.asarray(pcd.points), rx, "unprojected xyz (odd size)")
+    ds = pcd.voxel_down_sample(0.005)
+    rv, rvc, _, _ = O.voxel_down_sample(rx, rc, 0.005)
+    assert_bitwise(np.asarray(ds.points), rv, "voxel averages (odd size)")
+
+
 def test_unproject_stride_and_empty(pkg, O, gpu, synth, seq16):
     depth = seq16[0][2]
     intr_t = ref_intr(synth)
@@ -77,9 +95,9 @@ def test_unproject_stride_and_empty(pkg, O, gpu, synth, seq16):
     assert len(empty.points) == 0
 
 
-def _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=None, trunc=3.0, float_path=False):
+def _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=None, trunc=3.0, float_path=False, intr_t=None):
     integ = _integration(pkg)
-    intr_t = ref_intr(synth)
+    intr_t = intr_t or ref_intr(synth)
     intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
     vol = integ.ScalableTSDFVolume(voxel_length=voxel, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
                                    batch_frames=batch)
@@ -115,6 +133,16 @@ def test_tsdf_integrate_bitexact(pkg, O, gpu, synth, seq16, voxel, batch):
     vol, ref = _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=batch)
     n = _compare_volumes(vol, ref)
     assert n > 300
+
+
+@pytest.mark.parametrize("batch", [1, None])
+def test_tsdf_odd_resolution(pkg, O, gpu, synth, batch):
+    """A 321x243 camera (width not a multiple of 4: the staging kernel's per-pixel path; odd sample grid at
+    stride 4) with an off-centre principal point: bit-exact like the reference resolution."""
+    intr_t = (321, 243, 283.1, 283.4, 161.7, 120.2)
+    depth, color, ext = synth.make_sequence(n_frames=12, frames=[0, 2, 5, 9], intr=intr_t)
+    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, batch=batch, intr_t=intr_t)
+    assert _compare_volumes(vol, ref) > 100
 
 
 def test_tsdf_float_path_batched(pkg, O, gpu, synth, seq16):
