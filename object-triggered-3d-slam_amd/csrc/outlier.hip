@@ -252,6 +252,10 @@ __device__ inline double block_guard(const GridDev& g, const double q[3], double
     return guard - 1e-6 * g.h;
 }
 
+#ifndef OT_SOR_SKIP
+#define OT_SOR_SKIP 1
+#endif
+
 // One lane per query (sorted order: a wave's queries share cells and candidate ranges).  Stage 1 scans the 9
 // ranges of the query's 3x3x3 block; the k-th distance is final when it does not exceed the distance from q to
 // the block's faces (>= h).  Stage 2 adds the rest of the 5x5x5 block (guard >= 2h).  Isolated points fall back.
@@ -266,12 +270,30 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     const int c = g.pcell[j];
     const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
     long long have = 0;
+#if OT_SOR_SKIP
+    // distances from q to its cell's faces in x and y (conservatively shrunk): a neighbouring column (dx, dy) lies
+    // at least sqrt(ex^2 + ey^2) away, so once that reaches the current k-th distance none of its points can enter
+    double lo[2], hi[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const double uu = (q[a] - g.origin[a]) / g.h;
+        const double fr = uu - floor(uu);
+        lo[a] = fmax(fr * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
+        hi[a] = fmax((1.0 - fr) * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
+    }
+#endif
     for (int u = 0; u < NBR3; ++u) {
         // own column, then the 4 face-adjacent columns, then the 4 diagonal ones: the k-th distance tightens
         // before the farthest candidates, so fewer of them pass the early-reject test into the insertion chain
         const int t = (int)((0x862075314ull >> (4 * u)) & 0xF);
         const int2 se = r3[t];
-        scan_range<KMAX>(g, q, se.x, se.y, best);
+#if OT_SOR_SKIP
+        const int dx = t / 3 - 1, dy = t % 3 - 1;
+        const double ex = dx < 0 ? lo[0] : (dx > 0 ? hi[0] : 0.0);
+        const double ey = dy < 0 ? lo[1] : (dy > 0 ? hi[1] : 0.0);
+        if (!(ex * ex + ey * ey >= best[KMAX - 1]))
+#endif
+            scan_range<KMAX>(g, q, se.x, se.y, best);
         have += se.y - se.x;
     }
     double guard = block_guard(g, q, 1.0);
