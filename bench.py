@@ -591,6 +591,12 @@ def filter_stream(args, L, lib, synth, torch, rank):
             "frames_per_s": round(args.filter_frames / dt, 2), "ms_per_frame": round(dt * 1e3 / args.filter_frames, 3),
             "points_per_frame": round(pts / args.filter_frames), "voxels_per_frame": round(vox / args.filter_frames),
             "kept_per_frame": round(kept / args.filter_frames),
+            # SURVEY 8(d) fused configs[2] pipeline bytes: 5*W*H (u16 depth + RGB8) + 15*K_kept per frame over the
+            # wall time; the chain is latency / VALU bound (host round trips, kNN selection), not HBM bound
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_frame": round(5.0 * W * H + 15.0 * kept / args.filter_frames),
+                         "achieved": round((5.0 * W * H * args.filter_frames + 15.0 * kept) / dt / 1e9, 2),
+                         "frac": round((5.0 * W * H * args.filter_frames + 15.0 * kept) / dt / 1e9 / HBM_PEAK_GBS, 5)},
             "cpu_baseline": {"mpoints_per_s": round(cpu_pts / cdt / 1e6, 3), "cores": cores, "kind": "port",
                              "sample": "2 frames of the same stream, CPU oracle chain"}}
 
