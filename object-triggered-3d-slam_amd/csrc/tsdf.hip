@@ -352,15 +352,19 @@ constexpr int TT = 16;          // tile edge in samples
 #define OT_TF 4
 #endif
 constexpr int TF = OT_TF;       // frames per workgroup
-constexpr int LTAB = 2048;      // LDS table entries (32 KiB)
+#ifndef OT_LTAB
+#define OT_LTAB 2048
+#endif
+constexpr int LTAB = OT_LTAB;   // LDS table entries (16 B each + a 4-B slot in the list of used entries)
 
-__device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* masks, unsigned long long key,
-                                 unsigned long long bit) {
+__device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* masks, int* used, int* nused,
+                                 unsigned long long key, unsigned long long bit) {
     unsigned h = (unsigned)mix64(key) & (LTAB - 1);
     for (int probe = 0; probe < 64; ++probe) {
         unsigned long long k = keys[h];
         if (k == KEY_EMPTY) {
             const unsigned long long old = atomicCAS(&keys[h], KEY_EMPTY, key);
+            if (old == KEY_EMPTY) used[atomicAdd(nused, 1)] = (int)h;  // the inserting lane lists the entry
             k = (old == KEY_EMPTY) ? key : old;
         }
         if (k == key) {
@@ -376,11 +380,14 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
                                                      TsdfDev d, int nframes) {
     __shared__ unsigned long long s_keys[LTAB];
     __shared__ unsigned long long s_masks[LTAB];
+    __shared__ int s_used[LTAB];
+    __shared__ int s_nused;
     const int tid = threadIdx.x;
     for (int e = tid; e < LTAB; e += 256) {
         s_keys[e] = KEY_EMPTY;
         s_masks[e] = 0ull;
     }
+    if (tid == 0) s_nused = 0;
     __syncthreads();
     const int tiles_x = (p.ws + TT - 1) / TT;
     const int sx = (blockIdx.x % tiles_x) * TT + (tid & (TT - 1));
@@ -419,14 +426,16 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
                         }
                         const unsigned long long key = pack_key(ux, uy, uz);
                         if (!unit_owned(d, key)) continue;
-                        if (!lds_merge(s_keys, s_masks, key, bit)) touch_unit_batch(d, f, p.slot_cap, ux, uy, uz);
+                        if (!lds_merge(s_keys, s_masks, s_used, &s_nused, key, bit)) touch_unit_batch(d, f, p.slot_cap, ux, uy, uz);
                     }
         }
     }
     __syncthreads();
-    for (int e = tid; e < LTAB; e += 256) {
+    // only the entries this tile filled (listed by their inserting lanes), not the whole table
+    const int nused = s_nused;
+    for (int t = tid; t < nused; t += 256) {
+        const int e = s_used[t];
         const unsigned long long key = s_keys[e];
-        if (key == KEY_EMPTY) continue;
         const int slot = hash_insert(d, key);
         if (slot < 0) {
             atomicOr(&d.counters[C_HASHERR], 1);

@@ -6,6 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mode=$1; shift
 if [ "$mode" = build ]; then
+  mkdir -p object-triggered-3d-slam_amd/variants
   for v in "$@"; do
     name=${v%%|*}; flags=${v#*|}
     make -j8 -C object-triggered-3d-slam_amd/csrc OUT=../variants/libotslam_$name.so BUILD=build_$name EXTRA="$flags" > /tmp/build_$name.log 2>&1 || { echo "$name build failed"; tail /tmp/build_$name.log; }
