@@ -248,7 +248,8 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
 
 // ============================================================================ batched (temporal blocking)
 // One launch per batch of F <= 64 frames:
-//   k_batch_prep      : per-pixel (depth, multiplier) float2 + packed colour for every frame (grid.y = frame)
+//   k_batch_prep      : per-pixel (depth, multiplier) float2 + packed colour for every frame (grid.y = frame);
+//                       by default fused into k_batch_touch (each touch workgroup stages a pixel chunk)
 //   k_batch_touch     : stride samples of every frame; a unit touched by frame f gets bit f in its slot's
 //                       fmask (64-bit atomicOr); the first bit set in a batch appends the slot to bslots
 //   k_batch_units     : per touched slot: allocate the unit if new, move its frame mask into a 32-B header
@@ -268,11 +269,7 @@ __device__ inline float prep_depth(const BatchFrame& fr, uint32_t raw16) {
 
 // 4 pixels per lane: 8-B depth load, 12-B colour load (3 aligned dwords), 16-B multiplier load,
 // 2 x 16-B (depth, multiplier) stores and one 16-B colour store.
-__global__ __launch_bounds__(256) void k_batch_prep(const BatchFrame* __restrict__ frames, const float* __restrict__ mult,
-                                                    int64_t npx) {
-    const BatchFrame& fr = frames[blockIdx.y];
-    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (i0 >= npx) return;
+__device__ inline void prep_quad(const BatchFrame& fr, const float* __restrict__ mult, int64_t i0, int64_t npx) {
     const bool aligned = ((reinterpret_cast<uintptr_t>(fr.depth16) & 7) == 0) &&
                          ((reinterpret_cast<uintptr_t>(fr.depthf) & 15) == 0) &&
                          ((reinterpret_cast<uintptr_t>(fr.color) & 3) == 0);
@@ -314,11 +311,19 @@ __global__ __launch_bounds__(256) void k_batch_prep(const BatchFrame* __restrict
     }
 }
 
+__global__ __launch_bounds__(256) void k_batch_prep(const BatchFrame* __restrict__ frames, const float* __restrict__ mult,
+                                                    int64_t npx) {
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 < npx) prep_quad(frames[blockIdx.y], mult, i0, npx);
+}
+
 struct BatchTouchParams {
     int W, stride, ws, hs;
     double fx, fy, cx, cy;
     double trunc, unit_len;
     int slot_cap;
+    const float* mult;  // fused staging (k_batch_touch stages the batch's pixels too): ray multipliers
+    int64_t npx;        // pixels per frame
 };
 
 __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int x, int y, int z) {
@@ -349,11 +354,11 @@ __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, i
 // not fit the LDS table falls back to the direct global path.
 constexpr int TT = 16;          // tile edge in samples
 #ifndef OT_TF
-#define OT_TF 4
+#define OT_TF 2
 #endif
 constexpr int TF = OT_TF;       // frames per workgroup
 #ifndef OT_LTAB
-#define OT_LTAB 2048
+#define OT_LTAB 1024
 #endif
 constexpr int LTAB = OT_LTAB;   // LDS table entries (16 B each + a 4-B slot in the list of used entries)
 
@@ -388,6 +393,17 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
         s_masks[e] = 0ull;
     }
     if (tid == 0) s_nused = 0;
+#ifndef OT_SPLIT_PREP
+    // Fused staging: this workgroup also stages a contiguous 1/gridDim.x of the pixels of each of its frames
+    // (k_batch_prep's work; the touch below reads raw depth itself, so nothing here waits on these stores).
+    {
+        const int64_t quads = (p.npx + 3) >> 2;
+        const int64_t per = (quads + gridDim.x - 1) / gridDim.x;
+        const int64_t q0 = (int64_t)blockIdx.x * per, q1 = q0 + per < quads ? q0 + per : quads;
+        for (int f = blockIdx.y * TF; f < blockIdx.y * TF + TF && f < nframes; ++f)
+            for (int64_t q = q0 + tid; q < q1; q += 256) prep_quad(frames[f], p.mult, q * 4, p.npx);
+    }
+#endif
     __syncthreads();
     const int tiles_x = (p.ws + TT - 1) / TT;
     const int sx = (blockIdx.x % tiles_x) * TT + (tid & (TT - 1));
@@ -397,7 +413,12 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
         const int r = sy * p.stride, c = sx * p.stride;
         for (int f = f0; f < f0 + TF && f < nframes; ++f) {
             const BatchFrame& fr = frames[f];
+#ifndef OT_SPLIT_PREP
+            const int64_t pix = (int64_t)r * p.W + c;  // the staged depth, computed as k_batch_prep does
+            const float df = fr.depth16 ? prep_depth(fr, fr.depth16[pix]) : fr.depthf[pix];
+#else
             const float df = fr.dm[(int64_t)r * p.W + c].x;
+#endif
             if (!(df > 0.0f)) continue;
             const double z = (double)df;
             const double x = ((double)c - p.cx) * z / p.fx;
@@ -979,9 +1000,13 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     // batch pair count and the integrate's queue heads
     OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, sizeof(int) * (N_COUNTERS - C_BATCH_PAIRS),
                               stream));
+#ifdef OT_SPLIT_PREP
     hipLaunchKernelGGL(k_batch_prep, dim3((unsigned)((npx / 4 + 255) / 256 + 1), n), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, (const float*)vol->mult, npx);
+#endif
     BatchTouchParams tp;
+    tp.mult = vol->mult;
+    tp.npx = npx;
     tp.W = in.width;
     tp.stride = vol->stride;
     tp.ws = (in.width + vol->stride - 1) / vol->stride;
