@@ -177,6 +177,9 @@ def main():
                 "algorithmic_bytes_per_launch": round(per_launch_bytes),
                 "effective": args.batch != 1,  # voxel state reused on chip across a batch
                 "voxel_updates_per_frame": round(upd.value / args.frames)}
+    if traffic and kernel_ms_avg > 0:  # measured HBM bytes (PMC, profiles/pmc_traffic.json) over the same launch time
+        roofline["traffic_gbs"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9, 1)
+        roofline["traffic_frac"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     if args.calib:  # a kernel with a known read byte count and the integrate kernel's pool access pattern
         nu = n_units.value

@@ -549,7 +549,13 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
     const int npx = p.W * p.H;
     unsigned upd = 0;  // per lane: <= BZ voxels x 64 frames x units per workgroup, far below 2^32
     {
-        for (int u = blockIdx.x; u < n; u += gridDim.x) {
+#ifdef OT_XCD_PERM  // within each grid-wide round, XCD x (blockIdx % 8) takes a contiguous 1/8 of the round's units
+        const int G = gridDim.x;
+        const int b = (G & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3));
+#else
+        const int b = blockIdx.x;
+#endif
+        for (int u = b; u < n; u += gridDim.x) {
             const UnitWork& w = work[u];
             const int ent = w.id;
             const unsigned long long mask = w.mask;
