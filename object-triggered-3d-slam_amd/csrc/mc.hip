@@ -5,7 +5,7 @@
 //   triangles : (unit key, voxel x*256+y*16+z, tri-table order), winding (e0, e2, e1) as Open3D.
 // Pipeline (one 256-lane workgroup per unit, units in key order from the rocPRIM sort):
 //   k_mc_prepare   : neighbour table (+x/+y/+z combos via the block hash), id->rank, clear edge bitmasks
-//   k_mc_classify  : 17^3 tsdf/weight tile of the unit and its +1 neighbours staged in LDS (39 KiB); per
+//   k_mc_classify  : 17^3 tile of (weight == 0, tsdf < 0) flag bytes of the unit and its +1 neighbours in LDS; per
 //                    voxel cube index (any weight == 0 => skipped, like Open3D); cut edges marked in the
 //                    owner unit's edge bitmask (atomicOr); per-unit triangle count
 //   k_mc_count     : per-unit popcount prefix over the 384 bitmask words => vertex ids without a hash map
@@ -26,6 +26,7 @@ __constant__ signed char c_tri[256][16];
 __constant__ int c_eshift[12][4];
 __constant__ int c_e2v[12][2];
 __constant__ int c_shift[8][3];
+__constant__ unsigned char c_ntri[256];  // triangles per cube configuration (from c_tri)
 
 constexpr int EWORDS = (UNIT_VOX * 3) / 32;  // 384 bitmask words per unit
 constexpr int T17 = 17;
@@ -74,61 +75,92 @@ __global__ __launch_bounds__(256) void k_mc_prepare(TsdfDev d, McDev m) {
 }
 
 __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
-    __shared__ float sF[T17 * T17 * T17];
-    __shared__ float sW[T17 * T17 * T17];
+    // Classification needs only two predicates per voxel (weight == 0, tsdf < 0): one flag byte each in LDS
+    // (4.9 KiB per 17^3 tile instead of 39 KiB of floats), so many more units are resident per CU.
+    __shared__ unsigned char sB[T17 * T17 * T17];
+    __shared__ unsigned sflags[EWORDS];  // this unit's own edge bits; edges owned by a +1 neighbour go to HBM directly
     __shared__ int snbr[8];
     __shared__ long long wsum[4];
     const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
     if (t < 8) snbr[t] = m.nbr[id * 8 + t];
+    for (int w = t; w < EWORDS; w += 256) sflags[w] = 0u;
     __syncthreads();
-    for (int c = t; c < T17 * T17 * T17; c += 256) {
-        const int lx = c / (T17 * T17), ly = (c / T17) % T17, lz = c % T17;
-        const int nid = snbr[((lx >> 4) << 2) | ((ly >> 4) << 1) | (lz >> 4)];
-        float f = 0.0f, w = 0.0f;
-        if (nid >= 0) {
-            const float* base = d.vox + (size_t)nid * UNIT_FLOATS;
-            const int vi = (lz & 15) * 256 + (lx & 15) * 16 + (ly & 15);
-            f = base[vi];
-            w = base[UNIT_VOX + vi];
+    // tile staging in the pool's memory order (z, x, y with y fastest), so a wave's loads are contiguous runs;
+    // all of a lane's loads are issued before any is consumed (the staging is latency-bound otherwise)
+    constexpr int NT = T17 * T17 * T17, NIT = (NT + 255) / 256;
+    float fv[NIT], wv[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int c = t + i * 256;
+        fv[i] = 0.0f;
+        wv[i] = 0.0f;
+        if (c < NT) {
+            const int lz = c / (T17 * T17), lx = (c / T17) % T17, ly = c % T17;
+            const int nid = snbr[((lx >> 4) << 2) | ((ly >> 4) << 1) | (lz >> 4)];
+            if (nid >= 0) {
+                const float* base = d.vox + (size_t)nid * UNIT_FLOATS;
+                const int vi = (lz & 15) * 256 + (lx & 15) * 16 + (ly & 15);
+                fv[i] = base[vi];
+                wv[i] = base[UNIT_VOX + vi];
+            }
         }
-        sF[c] = f;
-        sW[c] = w;
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+        const int c = t + i * 256;
+        if (c < NT) {
+            const int lz = c / (T17 * T17), lx = (c / T17) % T17, ly = c % T17;
+            sB[(lx * T17 + ly) * T17 + lz] = (unsigned char)((wv[i] == 0.0f ? 1 : 0) | (fv[i] < 0.0f ? 2 : 0));
+        }
     }
     __syncthreads();
     const int x = t >> 4, y = t & 15;
     long long ntri = 0;
-    unsigned char* cubes = m.cubes + (size_t)id * UNIT_VOX;
+    unsigned packed[4] = {0u, 0u, 0u, 0u};  // this lane's 16 cube bytes ([x][y][z] layout), one 16-B store
+#pragma unroll
     for (int z = 0; z < UNIT_RES; ++z) {
         int cube = 0;
         bool valid = true;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int c = ((x + c_shift[i][0]) * T17 + (y + c_shift[i][1])) * T17 + (z + c_shift[i][2]);
-            if (sW[c] == 0.0f) valid = false;
-            if (sF[c] < 0.0f) cube |= (1 << i);
+            const int b = sB[c];
+            if (b & 1) valid = false;
+            if (b & 2) cube |= (1 << i);
         }
         if (!valid) cube = 0;
         if (cube == 255) cube = 0;
-        cubes[t * 16 + z] = (unsigned char)cube;
+        packed[z >> 2] |= (unsigned)cube << ((z & 3) * 8);
         if (cube == 0) continue;
-        for (int k = 0; k < 15 && c_tri[cube][k] != -1; k += 3) ++ntri;
+        ntri += c_ntri[cube];
 #pragma unroll
         for (int e = 0; e < 12; ++e) {
             const int v0 = c_e2v[e][0], v1 = c_e2v[e][1];
             if (((cube >> v0) & 1) == ((cube >> v1) & 1)) continue;
             const int ox = x + c_eshift[e][0], oy = y + c_eshift[e][1], oz = z + c_eshift[e][2];
-            const int owner = snbr[((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4)];
+            const int nb = ((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4);
             const int local = (ox & 15) * 256 + (oy & 15) * 16 + (oz & 15);
             const int bit = local * 3 + c_eshift[e][3];
-            if (owner >= 0) atomicOr(&m.eflags[(size_t)owner * EWORDS + (bit >> 5)], 1u << (bit & 31));
+            if (nb == 0) {
+                atomicOr(&sflags[bit >> 5], 1u << (bit & 31));
+            } else {
+                const int owner = snbr[nb];
+                if (owner >= 0) atomicOr(&m.eflags[(size_t)owner * EWORDS + (bit >> 5)], 1u << (bit & 31));
+            }
         }
     }
+    *reinterpret_cast<uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
     ntri = wave_sum(ntri);
     if (lane_id() == 0) wsum[t >> 6] = ntri;
     __syncthreads();
     if (t == 0) m.tri_cnt[r] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    // neighbours' classify blocks may set bits of this unit's words too: merge, do not overwrite
+    for (int w = t; w < EWORDS; w += 256) {
+        const unsigned b = sflags[w];
+        if (b) atomicOr(&m.eflags[(size_t)id * EWORDS + w], b);
+    }
 }
 
 // per-unit exclusive popcount prefix of the 384 bitmask words (6 waves, one word per lane)
@@ -222,19 +254,17 @@ __global__ __launch_bounds__(256) void k_mc_triangles(McDev m, int32_t* T) {
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
     if (t < 8) snbr[t] = m.nbr[id * 8 + t];
-    const unsigned char* cubes = m.cubes + (size_t)id * UNIT_VOX + t * 16;
+    const uint4 q = *reinterpret_cast<const uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16);
+    const unsigned cw[4] = {q.x, q.y, q.z, q.w};
     int cnt = 0;
-    for (int z = 0; z < UNIT_RES; ++z) {
-        const int cube = cubes[z];
-        if (cube == 0) continue;
-        for (int k = 0; k < 15 && c_tri[cube][k] != -1; k += 3) ++cnt;
-    }
+#pragma unroll
+    for (int z = 0; z < UNIT_RES; ++z) cnt += c_ntri[(cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu];
     int total;
     const int pre = block_excl_scan_256(cnt, total);  // contains __syncthreads (snbr visible after)
     long long out = m.tri_base[r] + pre;
     const int x = t >> 4, y = t & 15;
     for (int z = 0; z < UNIT_RES; ++z) {
-        const int cube = cubes[z];
+        const int cube = (int)((cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu);
         if (cube == 0) continue;
         for (int k = 0; k < 15 && c_tri[cube][k] != -1; k += 3) {
             const int a = edge_vid(m, snbr, x, y, z, c_tri[cube][k]);
@@ -259,6 +289,13 @@ static ot_status upload_tables() {  // once per process (one process per GPU), s
     OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_eshift), OT_MC_EDGE_SHIFT, sizeof(OT_MC_EDGE_SHIFT)));
     OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_e2v), OT_MC_EDGE_TO_VERT, sizeof(OT_MC_EDGE_TO_VERT)));
     OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_shift), OT_MC_SHIFT, sizeof(OT_MC_SHIFT)));
+    unsigned char ntri[256];
+    for (int c = 0; c < 256; ++c) {
+        int n = 0;
+        for (int k = 0; k < 15 && OT_MC_TRI_TABLE[c][k] != -1; k += 3) ++n;
+        ntri[c] = (unsigned char)n;
+    }
+    OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_ntri), ntri, sizeof(ntri)));
     g_tables_uploaded.store(true, std::memory_order_release);
     return OT_OK;
 }
