@@ -28,7 +28,7 @@ constexpr int C_TOUCHED = 0;   // units touched by the current frame
 constexpr int C_UNITS = 1;     // units allocated
 constexpr int C_OVERFLOW = 2;  // pool exhausted (units dropped)
 constexpr int C_HASHERR = 3;   // hash full or key out of range
-constexpr int C_BATCH_PAIRS = 4;  // (frame, unit) pairs in the current batch
+constexpr int C_BATCH_PAIRS = 4;  // (frame, unit) pairs of a batch: counters[4 + parity] (batches alternate, see k_batch_units)
 constexpr int N_COUNTERS = 16;
 
 // stats[] slots (u64)
@@ -119,6 +119,7 @@ struct ot_tsdf {
     ot::BatchFrame* hbframes = nullptr;    // pinned host staging [2][MAX_BATCH]
     hipEvent_t hb_event[2] = {nullptr, nullptr};
     int hb_next = 0;
+    int batch_pc = ot::C_BATCH_PAIRS;      // pair counter of the next batch (alternates 4, 5)
     float2* bdm = nullptr;                 // device [batch][h][w] packed (depth, multiplier)
     uint32_t* brgba = nullptr;             // device [batch][h][w] packed colour
     int64_t bdepth_cap = 0;                // pixels (frames * h * w) the two buffers hold

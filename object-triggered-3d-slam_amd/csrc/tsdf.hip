@@ -324,9 +324,10 @@ struct BatchTouchParams {
     int slot_cap;
     const float* mult;  // fused staging (k_batch_touch stages the batch's pixels too): ray multipliers
     int64_t npx;        // pixels per frame
+    int pc;             // this batch's pair counter index
 };
 
-__device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int x, int y, int z) {
+__device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int pc, int x, int y, int z) {
     if (!key_in_range(x, y, z)) {
         atomicOr(&d.counters[C_HASHERR], 2);
         return;
@@ -342,7 +343,7 @@ __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, i
     if (d.fmask[slot] & bit) return;  // fast path; a stale read only costs the atomic below
     const unsigned long long old = atomicOr(&d.fmask[slot], bit);
     if (old == 0ull) {
-        const int pos = atomicAdd(&d.counters[C_BATCH_PAIRS], 1);
+        const int pos = atomicAdd(&d.counters[pc], 1);
         if (pos < slot_cap) d.bslots[pos] = slot;
         else atomicOr(&d.counters[C_HASHERR], 1);
     }
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
                         }
                         const unsigned long long key = pack_key(ux, uy, uz);
                         if (!unit_owned(d, key)) continue;
-                        if (!lds_merge(s_keys, s_masks, s_used, &s_nused, key, bit)) touch_unit_batch(d, f, p.slot_cap, ux, uy, uz);
+                        if (!lds_merge(s_keys, s_masks, s_used, &s_nused, key, bit)) touch_unit_batch(d, f, p.slot_cap, p.pc, ux, uy, uz);
                     }
         }
     }
@@ -466,7 +467,7 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
         if ((d.fmask[slot] & m) == m) continue;  // fast path; a stale read only costs the atomic below
         const unsigned long long old = atomicOr(&d.fmask[slot], m);
         if (old == 0ull) {
-            const int pos = atomicAdd(&d.counters[C_BATCH_PAIRS], 1);
+            const int pos = atomicAdd(&d.counters[p.pc], 1);
             if (pos < p.slot_cap) d.bslots[pos] = slot;
             else atomicOr(&d.counters[C_HASHERR], 1);
         }
@@ -493,9 +494,11 @@ struct UnitWork {
 };
 
 // Unit headers of the batch: allocate new units, move and clear the frame masks (ready for the next batch).
-__global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __restrict__ work) {
+__global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __restrict__ work, int pc) {
     __shared__ unsigned long long red[4];
-    const int n = d.counters[C_BATCH_PAIRS];
+    const int n = d.counters[pc];
+    // the other counter belongs to the next batch; the previous batch's integrate (its last reader) has finished
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.counters[pc ^ 1] = 0;
     unsigned long long pairs = 0;
     for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
         const int slot = d.bslots[t];
@@ -542,10 +545,10 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 // One workgroup of SLICES waves per unit, so a unit's frame footprint is gathered through one CU's L1; units are
 // assigned by a static grid stride that every wave derives on its own: no barriers, no LDS, no atomics.
 __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrate(
-    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work) {
+    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
     const int lane = threadIdx.x & 63;
     const int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // slice of this wave
-    const int n = d.counters[C_BATCH_PAIRS];
+    const int n = d.counters[pc];
     const int npx = p.W * p.H;
     unsigned upd = 0;  // per lane: <= BZ voxels x 64 frames x units per workgroup, far below 2^32
     {
@@ -1004,8 +1007,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     if (!vol->hb_event[hb]) OT_HIP_TRY(hipEventCreateWithFlags(&vol->hb_event[hb], hipEventDisableTiming));
     OT_HIP_TRY(hipEventRecord(vol->hb_event[hb], stream));
     // batch pair count and the integrate's queue heads
-    OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_BATCH_PAIRS, 0, sizeof(int) * (N_COUNTERS - C_BATCH_PAIRS),
-                              stream));
+    // this batch's pair counter: zeroed by reset, or by the previous batch's k_batch_units (no memset here)
+    const int pc = vol->batch_pc;
 #ifdef OT_SPLIT_PREP
     hipLaunchKernelGGL(k_batch_prep, dim3((unsigned)((npx / 4 + 255) / 256 + 1), n), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, (const float*)vol->mult, npx);
@@ -1013,6 +1016,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     BatchTouchParams tp;
     tp.mult = vol->mult;
     tp.npx = npx;
+    tp.pc = pc;
     tp.W = in.width;
     tp.stride = vol->stride;
     tp.ws = (in.width + vol->stride - 1) / vol->stride;
@@ -1027,7 +1031,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     const unsigned tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
     hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, tp, vol->dev, n);
-    hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work);
+    hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc);
     const int grid = integrate_grid();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
@@ -1036,7 +1040,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         OT_HIP_TRY(hipEventRecord(e0, stream));
     }
     hipLaunchKernelGGL(k_batch_integrate, dim3(grid), dim3(64 * SLICES), 0, stream, (const BatchFrame*)vol->bframes, ip0,
-                       vol->dev, (const UnitWork*)vol->dev.work);
+                       vol->dev, (const UnitWork*)vol->dev.work, pc);
+    vol->batch_pc ^= 1;  // only once this batch's kernels are queued (its units kernel zeroes the other counter)
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
         OT_HIP_TRY(hipEventRecord(e1, stream));
@@ -1222,6 +1227,7 @@ ot_status ot_tsdf_reset(ot_tsdf* v) {
     OT_HIP_TRY(hipMemset(d.counters, 0, sizeof(int) * N_COUNTERS));
     OT_HIP_TRY(hipMemset(d.stats, 0, sizeof(unsigned long long) * 4));
     OT_HIP_TRY(hipDeviceSynchronize());
+    v->batch_pc = C_BATCH_PAIRS;
     v->frame_id = 0;
     v->pending.clear();
     v->sorted_frame = -1;
@@ -1242,6 +1248,7 @@ ot_status ot_tsdf_reset_async(ot_tsdf* v, void* stream_) {
     OT_HIP_TRY(hipMemsetAsync(d.fmask, 0, sizeof(unsigned long long) * v->hash_cap, stream));
     OT_HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * N_COUNTERS, stream));
     OT_HIP_TRY(hipMemsetAsync(d.stats, 0, sizeof(unsigned long long) * 4, stream));
+    v->batch_pc = C_BATCH_PAIRS;
     v->frame_id = 0;
     v->sorted_frame = -1;
     v->sorted_units = -1;
