@@ -315,19 +315,23 @@ __device__ inline void prep_quad(const BatchFrame& fr, const float* __restrict__
 }
 
 // Quads [q, q1) with stride 256 (one lane's share of a chunk): on the common path (u16 depth, RGB8, aligned, W*H
-// a multiple of 4) two quads per step with all of their loads issued before any store.
+// a multiple of 4) PREP_K quads per step with all of their loads issued before any store.
+#ifndef OT_PREP_K
+#define OT_PREP_K 2
+#endif
+constexpr int PREP_K = OT_PREP_K;
 __device__ inline void prep_range(const BatchFrame& fr, const float* __restrict__ mult, int64_t q, int64_t q1,
                                   int64_t npx) {
     const bool fast = fr.depth16 && fr.color && (npx & 3) == 0 &&
                       ((reinterpret_cast<uintptr_t>(fr.depth16) & 7) == 0) &&
                       ((reinterpret_cast<uintptr_t>(fr.color) & 3) == 0);
     if (fast) {
-        for (; q + 256 < q1; q += 512) {
-            uint2 raw[2];
-            float4 m[2];
-            uint32_t w[2][3];
+        for (; q + 256 * (PREP_K - 1) < q1; q += 256 * PREP_K) {
+            uint2 raw[PREP_K];
+            float4 m[PREP_K];
+            uint32_t w[PREP_K][3];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < PREP_K; ++k) {
                 const int64_t i0 = (q + 256 * k) * 4;
                 raw[k] = *reinterpret_cast<const uint2*>(fr.depth16 + i0);
                 m[k] = *reinterpret_cast<const float4*>(mult + i0);
@@ -335,7 +339,7 @@ __device__ inline void prep_range(const BatchFrame& fr, const float* __restrict_
                 w[k][0] = c[0], w[k][1] = c[1], w[k][2] = c[2];
             }
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < PREP_K; ++k) {
                 const int64_t i0 = (q + 256 * k) * 4;
                 const float d0 = prep_depth(fr, raw[k].x & 0xFFFFu), d1 = prep_depth(fr, raw[k].x >> 16);
                 const float d2 = prep_depth(fr, raw[k].y & 0xFFFFu), d3 = prep_depth(fr, raw[k].y >> 16);
