@@ -76,6 +76,11 @@ struct UnprojEmit {
         const int r = (int)q * stride, c = (int)(su - q * (unsigned)ws) * stride;
         const int64_t pix = (int64_t)r * w + c;
         const double z = (double)depth[pix];
+        unsigned c0 = 0, c1 = 0, c2 = 0;  // colour loaded before the stores (byte data may alias them)
+        if (color) {
+            const uint8_t* p = color + pix * 3;
+            c0 = p[0], c1 = p[1], c2 = p[2];
+        }
         const double x = ((double)c - cx) * z / fx;
         const double y = ((double)r - cy) * z / fy;
         const double* m = pose.m;
@@ -87,10 +92,9 @@ struct UnprojEmit {
             xyz[pos * 3 + k] = ((a + b) + cc) + m[k * 4 + 3];
         }
         if (color) {
-            const uint8_t* p = color + pix * 3;
-            rgb[pos * 3 + 0] = (double)p[0] / 255.0;
-            rgb[pos * 3 + 1] = (double)p[1] / 255.0;
-            rgb[pos * 3 + 2] = (double)p[2] / 255.0;
+            rgb[pos * 3 + 0] = (double)c0 / 255.0;
+            rgb[pos * 3 + 1] = (double)c1 / 255.0;
+            rgb[pos * 3 + 2] = (double)c2 / 255.0;
         }
     }
 };
