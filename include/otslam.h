@@ -111,6 +111,40 @@ ot_status ot_gather_rows3(const double* in, const int64_t* idx, int64_t m, doubl
 ot_status ot_compute_point_cloud_distance(const double* src, int64_t n, const double* tgt, int64_t m,
                                           double* out, void* stream);
 
+/* The configs[2] filter chain for a batch of frames, device-resident end to end (not an Open3D API: the batch form
+ * of the per-frame calls below, results bit-identical to them).  Per frame f of a run:
+ *   create_from_color_and_depth(depth_scale, depth_trunc) -> PointCloud.create_from_rgbd_image(intrinsic,
+ *   extrinsic_f) -> voxel_down_sample(voxel_size) -> remove_statistical_outlier(nb_neighbors, std_ratio)
+ *   -> select_by_index(kept)
+ * i.e. check_one_frame.py:22-28 (with a pose) followed by the north_star's statistical filter.  A handle keeps its
+ * device buffers between runs (grow-only).  Not thread-safe per handle. */
+typedef struct ot_rgbd_filter ot_rgbd_filter;
+ot_status ot_rgbd_filter_create(const ot_intrinsics* intrinsic, int32_t max_frames, double depth_scale,
+                                double depth_trunc, double voxel_size, int32_t nb_neighbors, double std_ratio,
+                                ot_rgbd_filter** out);
+ot_status ot_rgbd_filter_destroy(ot_rgbd_filter* filter);
+/* depth: uint16 [n_frames][h][w], color: uint8 [n_frames][h][w][3] (device, contiguous); extrinsics_host:
+ * double [n_frames][16] row-major.  Synchronises `stream` (the result sizes come back to the host). */
+ot_status ot_rgbd_filter_run(ot_rgbd_filter* filter, int32_t n_frames, const uint16_t* depth, const uint8_t* color,
+                             const double* extrinsics_host, void* stream);
+/* Sizes of the last run: valid points, voxels and kept voxels in total, and (nullable) per-frame offsets
+ * [n_frames + 1] into the point / voxel / kept arrays. */
+ot_status ot_rgbd_filter_sizes(const ot_rgbd_filter* filter, int64_t* points_host, int64_t* voxels_host,
+                               int64_t* kept_host, int64_t* point_offsets_host, int64_t* voxel_offsets_host,
+                               int64_t* kept_offsets_host);
+/* Device arrays of the last run (valid until the next run / destroy; any out-pointer may be NULL): the kept
+ * points xyz / rgb f64 [kept][3] and their index inside their frame's voxel cloud (int64, ascending per frame: the
+ * indices remove_statistical_outlier returns), the voxel clouds xyz / rgb f64 [voxels][3] (per frame in key order,
+ * as ot_voxel_down_sample) and every voxel's mean kNN distance f64 [voxels]. */
+ot_status ot_rgbd_filter_outputs(const ot_rgbd_filter* filter, const double** kept_xyz, const double** kept_rgb,
+                                 const int64_t** kept_index, const double** voxel_xyz, const double** voxel_rgb,
+                                 const double** voxel_avg_dist);
+/* Copy frame `frame`'s results (or every frame's, frame = -1) of the last run into caller device buffers, ordered on
+ * `stream`; any pointer may be NULL.  Sizes: ot_rgbd_filter_sizes' offsets. */
+ot_status ot_rgbd_filter_copy(const ot_rgbd_filter* filter, int32_t frame, double* kept_xyz, double* kept_rgb,
+                              int64_t* kept_index, double* voxel_xyz, double* voxel_rgb, double* voxel_avg_dist,
+                              void* stream);
+
 /* ---------------------------------------------------------------------------------------------------
  * Scalable TSDF volume — pipelines.integration.ScalableTSDFVolume (reconstruct_rgbd_filter.py:81-85)
  * ------------------------------------------------------------------------------------------------- */

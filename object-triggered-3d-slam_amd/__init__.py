@@ -8,11 +8,11 @@ switches with one line:
 
     o3d.camera.PinholeCameraIntrinsic, o3d.io.read_image / read_point_cloud / write_point_cloud / ...,
     o3d.geometry.{Image, RGBDImage, PointCloud, TriangleMesh}, o3d.utility.Vector3dVector,
-    o3d.pipelines.integration.{ScalableTSDFVolume, TSDFVolumeColorType}
+    o3d.pipelines.integration.{ScalableTSDFVolume, TSDFVolumeColorType}, o3d.visualization.draw_geometries (headless)
 
 Every compute call goes through the C ABI in include/otslam.h (libotslam_hip.so, HIP kernels for gfx950).
 """
-from . import camera, change_detection, geometry, io, pipelines, utility  # noqa: F401
+from . import camera, change_detection, filters, geometry, io, pipelines, utility, visualization  # noqa: F401
 from ._lib import LIB_PATH, OTError  # noqa: F401
 
 __version__ = "0.1.0"

@@ -10,8 +10,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# OTSLAM_LIB selects an alternative in-tree build (kernel variants for A/B timing); default: the product library
-LIB_PATH = os.environ.get("OTSLAM_LIB") or os.path.join(_HERE, "libotslam_hip.so")
+# the product library; A/B timing of kernel variants goes through tools/with_variant.py (use_variant), never through
+# the product's environment
+LIB_PATH = os.path.join(_HERE, "libotslam_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "otslam.h")
 
 OT_OK = 0
@@ -89,6 +90,13 @@ SIGNATURES = {
     "ot_change_grid_destroy": [_p],
     "ot_change_grid_update": [_p, _p, _p, _i64, _d],
     "ot_change_grid_publish": [_p, _p, _i64, _pi64],
+    "ot_rgbd_filter_create": [_pint, _i32, _d, _d, _d, _i32, _d, C.POINTER(_p)],
+    "ot_rgbd_filter_destroy": [_p],
+    "ot_rgbd_filter_run": [_p, _i32, _p, _p, _p, _p],
+    "ot_rgbd_filter_sizes": [_p, _pi64, _pi64, _pi64, _p, _p, _p],
+    "ot_rgbd_filter_outputs": [_p, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p),
+                               C.POINTER(_p)],
+    "ot_rgbd_filter_copy": [_p, _i32, _p, _p, _p, _p, _p, _p, _p],
 }
 _RESTYPES = {"ot_last_error": C.c_char_p, "ot_version": C.c_char_p, "ot_abi_version": C.c_int32}
 
@@ -106,6 +114,18 @@ TEST_SIGNATURES = {
     "otx_tsdf_stats": [_p, _p],
     "otx_sort_pairs_u64_u32": [_p, _p, _p, _p, _i64, _i32, _p],
 }
+
+
+def use_variant(path: str) -> None:
+    """Test / tool hook: load a kernel-variant build from object-triggered-3d-slam_amd/variants/ instead of the
+    product library (A/B timing).  Must run before the first load(); the product never calls it."""
+    global LIB_PATH
+    path = os.path.abspath(path)
+    if os.path.dirname(path) != os.path.join(_HERE, "variants"):
+        raise RuntimeError(f"variant libraries live in {os.path.join(_HERE, 'variants')}: {path}")
+    if _lib is not None:
+        raise RuntimeError("use_variant() after the library was loaded")
+    LIB_PATH = path
 
 
 def load():

@@ -1,0 +1,44 @@
+// chain.h — exact parallel evaluation of Open3D's serial float64 sums (kernels in mesh_ops.hip).
+//
+// s = ((0 + x_0) + x_1) + ... for x_t >= 0 (any input is accepted: chunks the fast path cannot prove are walked
+// serially in the same order), bit-identical to the sequential loop.  Used by GetSurfaceArea / the sampling CDF
+// (reconstruct_rgbd_filter.py:123) and by RemoveStatisticalOutliers' cloud mean and squared-deviation sum
+// (std::accumulate / std::inner_product).
+#pragma once
+
+#include "common.h"
+
+namespace ot {
+
+constexpr int CHAIN_CH = 256;  // values per chunk: 64 lanes x 4
+
+struct ChainJob {
+    const double* x;  // input values (any alignment)
+    int64_t n;
+    double* out;      // CDF values (n), or the sum (out[0])
+    double* bsum;
+    int32_t* ex;
+    long long* msum;
+    int32_t* kind;    // 0 fast, 1 flagged by k_chain_chunk, 2 walked serially
+    double* start;    // exact s entering each fast chunk
+};
+
+// per-chain auxiliary arrays (bsum, start, msum, ex, kind)
+inline size_t chain_aux_bytes(int64_t n) { return (size_t)((n + CHAIN_CH - 1) / CHAIN_CH + 1) * 40 + 256; }
+
+inline char* chain_aux(char* cur, int64_t n, ChainJob& jb) {
+    const int64_t nb = (n + CHAIN_CH - 1) / CHAIN_CH + 1;
+    jb.bsum = (double*)cur;
+    jb.start = jb.bsum + nb;
+    jb.msum = (long long*)(jb.start + nb);
+    jb.ex = (int32_t*)(jb.msum + nb);
+    jb.kind = jb.ex + nb;
+    cur = (char*)(jb.kind + nb);
+    return (char*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
+}
+
+// sums (out[0]) of n_jobs independent chains whose job table is on the device; max_n bounds every job's n
+// (jobs with n == 0 write 0.0)
+void launch_sum_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream);
+
+}  // namespace ot

@@ -1,0 +1,651 @@
+// filter_batch.hip — the configs[2] filter chain for a batch of RGB-D frames in one device-resident pass.
+//
+// Per frame f (check_one_frame.py:22-28 with a pose, then the north_star's statistical filter):
+//   create_from_color_and_depth(depth_scale, depth_trunc) -> PointCloud.create_from_rgbd_image(intr, extrinsic_f)
+//   -> voxel_down_sample(voxel_size) -> remove_statistical_outlier(nb_neighbors, std_ratio) -> select_by_index
+// Results are bit-identical to that sequence of single calls (ot_depth_to_float, ot_unproject, ot_voxel_down_sample,
+// ot_remove_statistical_outlier, ot_gather_rows3) frame by frame; the frames never leave HBM and the whole batch
+// takes a fixed ~30 launches and 6 host synchronisations (sizes), instead of ~30 launches and 8 syncs per frame.
+//
+//   k_fb_pixels   tile of 2048 pixels of one frame: depth -> float (Open3D ConvertDepthToFloatImage), unprojection
+//                 of the valid pixels in float64 (camera_pose = inverse(extrinsic)), per-tile bounds + valid count
+//   k_fb_setup    per frame: bounds -> voxel origin (min - vs/2), key widths; one block scans the tile counts
+//   k_fb_keys     the same pixels again: voxel key (frame | kx | ky | kz), written by stable compaction in pixel
+//                 (= point index) order, value = global pixel index
+//   radix sort    stable => every voxel's points stay in point-index order
+//   heads         voxel segment starts (stable compaction)
+//   k_fb_reduce   one lane per voxel: its points re-unprojected from the depth (no xyz/rgb intermediates in HBM),
+//                 summed in index order, divided by the count (Open3D AccumulatedPoint)
+//   SOR           grid.h over all frames' voxel clouds at once (frame in the key's top bits) + sor_frames
+//   keep          stable compaction of avg > 0 && avg < threshold_f; rows gathered per frame
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "compact.h"
+#include "grid.h"
+#include "sort.h"
+
+namespace ot {
+
+constexpr int FB_THREADS = 256;
+constexpr int FB_PIX = 8;                        // consecutive pixels per lane (one 16-B depth load)
+constexpr int FB_TILE = FB_THREADS * FB_PIX;     // pixels per workgroup tile
+
+struct FbFrame {  // per-frame constants (device table)
+    double pose[16];    // inverse(extrinsic), row-major
+    double vmin[3];     // voxel grid origin: min_bound - vs / 2
+    int err;
+    int pad;
+};
+
+struct FbParams {
+    const uint16_t* depth;  // [F][h][w]
+    const uint8_t* color;   // [F][h][w][3]
+    int w, h, tpf;          // tiles per frame
+    float scale_f;
+    double trunc, fx, fy, cx, cy, vs;
+    FbFrame* frames;
+    int F;
+};
+
+// one pixel: Open3D's float depth, then (valid) the float64 point camera_pose * ((c-cx) z / fx, (r-cy) z / fy, z, 1)
+__device__ inline bool fb_point(const FbParams& p, const double* m, float d, int pix, double xyz[3]) {
+    if (!(d > 0.0f)) return false;
+    const unsigned pu = (unsigned)pix, rq = pu / (unsigned)p.w;
+    const int r = (int)rq, c = (int)(pu - rq * (unsigned)p.w);
+    const double z = (double)d;
+    const double x = ((double)c - p.cx) * z / p.fx;
+    const double y = ((double)r - p.cy) * z / p.fy;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double a = m[k * 4 + 0] * x;
+        const double b = m[k * 4 + 1] * y;
+        const double cc = m[k * 4 + 2] * z;
+        xyz[k] = ((a + b) + cc) + m[k * 4 + 3];
+    }
+    return true;
+}
+
+// the lane's 8 depth values as Open3D's float image: f = (float)u16 / (float)scale; 0 when f >= trunc
+__device__ inline void fb_depth8(const FbParams& p, const uint16_t* __restrict__ dep, int pix0, int npx, float f[8]) {
+    if (pix0 + FB_PIX <= npx && ((reinterpret_cast<uintptr_t>(dep + pix0) & 15) == 0)) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(dep + pix0);
+        const uint32_t wd[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f[2 * k] = (float)(wd[k] & 0xFFFFu);
+            f[2 * k + 1] = (float)(wd[k] >> 16);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < FB_PIX; ++k) f[k] = pix0 + k < npx ? (float)dep[pix0 + k] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < FB_PIX; ++k) {
+        f[k] = f[k] / p.scale_f;
+        if ((double)f[k] >= p.trunc) f[k] = 0.0f;
+    }
+}
+
+// per tile: valid count and bounds (order-preserving u64 encodings) of the valid pixels' points
+__global__ __launch_bounds__(FB_THREADS) void k_fb_pixels(FbParams p, int* __restrict__ tcount,
+                                                          unsigned long long* __restrict__ tbounds) {
+    const int f = blockIdx.y, tile = blockIdx.x;
+    const int npx = p.w * p.h;
+    const int pix0 = tile * FB_TILE + threadIdx.x * FB_PIX;
+    const uint16_t* dep = p.depth + (int64_t)f * npx;
+    double m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
+    float d[FB_PIX];
+    fb_depth8(p, dep, pix0, npx, d);
+    unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0, 0, 0};
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < FB_PIX; ++k) {
+        double xyz[3];
+        if (pix0 + k < npx && fb_point(p, m, d[k], pix0 + k, xyz)) {
+            ++c;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const unsigned long long o = dbl_to_ordered(xyz[a]);
+                mn[a] = o < mn[a] ? o : mn[a];
+                mx[a] = o > mx[a] ? o : mx[a];
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            unsigned long long t = __shfl_xor(mn[a], off, 64);
+            mn[a] = t < mn[a] ? t : mn[a];
+            t = __shfl_xor(mx[a], off, 64);
+            mx[a] = t > mx[a] ? t : mx[a];
+        }
+    }
+    c = wave_sum(c);
+    __shared__ unsigned long long s[4][6];
+    __shared__ int sc[4];
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+        for (int a = 0; a < 3; ++a) {
+            s[w][a] = mn[a];
+            s[w][3 + a] = mx[a];
+        }
+        sc[w] = c;
+    }
+    __syncthreads();
+    const int64_t t = (int64_t)f * p.tpf + tile;
+    if (threadIdx.x < 6) {
+        const int q = threadIdx.x;
+        unsigned long long v = s[0][q];
+        for (int k = 1; k < 4; ++k) v = q < 3 ? (s[k][q] < v ? s[k][q] : v) : (s[k][q] > v ? s[k][q] : v);
+        tbounds[t * 6 + q] = v;
+    }
+    if (threadIdx.x == 0) tcount[t] = sc[0] + sc[1] + sc[2] + sc[3];
+}
+
+// blocks 0..F-1: frame bounds -> voxel origin, per-axis key widths (atomicMax into kbits), Open3D's size check;
+// block F: exclusive scan of the F * tpf tile counts in place (-> output offsets), totals[0] = P
+__global__ __launch_bounds__(256) void k_fb_setup(FbParams p, int* __restrict__ tcount,
+                                                  const unsigned long long* __restrict__ tbounds,
+                                                  unsigned long long* __restrict__ fbounds, int* __restrict__ kbits,
+                                                  long long* __restrict__ totals, int* __restrict__ poff) {
+    const int f = blockIdx.x;
+    if (f == p.F) {  // scan
+        __shared__ int wsum[4];
+        __shared__ long long carry_s;
+        const int n = p.F * p.tpf;
+        const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+        if (threadIdx.x == 0) carry_s = 0;
+        __syncthreads();
+        for (int base = 0; base < n; base += 256) {
+            const int i = base + threadIdx.x;
+            const int x = i < n ? tcount[i] : 0;
+            int inc = x;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int tt = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += tt;
+            }
+            if (lane == 63) wsum[wid] = inc;
+            __syncthreads();
+            int off = 0, tot = 0;
+            for (int w = 0; w < 4; ++w) {
+                off += w < wid ? wsum[w] : 0;
+                tot += wsum[w];
+            }
+            const long long carry = carry_s;
+            if (i < n) tcount[i] = (int)(carry + off + inc - x);
+            __syncthreads();
+            if (threadIdx.x == 0) carry_s = carry + tot;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) totals[0] = carry_s;
+        __syncthreads();
+        for (int g = threadIdx.x; g < p.F; g += 256) poff[g] = tcount[g * p.tpf];  // frame g's first tile offset
+        return;
+    }
+    __shared__ unsigned long long s[256][6];
+    unsigned long long v[6] = {~0ull, ~0ull, ~0ull, 0, 0, 0};
+    for (int t = threadIdx.x; t < p.tpf; t += 256)
+        for (int q = 0; q < 6; ++q) {
+            const unsigned long long x = tbounds[((int64_t)f * p.tpf + t) * 6 + q];
+            v[q] = q < 3 ? (x < v[q] ? x : v[q]) : (x > v[q] ? x : v[q]);
+        }
+    for (int q = 0; q < 6; ++q) s[threadIdx.x][q] = v[q];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 256; ++i)
+            for (int q = 0; q < 6; ++q) v[q] = q < 3 ? (s[i][q] < v[q] ? s[i][q] : v[q]) : (s[i][q] > v[q] ? s[i][q] : v[q]);
+        for (int q = 0; q < 6; ++q) fbounds[f * 6 + q] = v[q];
+        FbFrame& fr = p.frames[f];
+        fr.err = 0;
+        if (v[0] == ~0ull) {  // no valid pixel: an empty frame
+            for (int a = 0; a < 3; ++a) fr.vmin[a] = 0.0;
+            return;
+        }
+        double ext = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            const double mnv = ordered_to_dbl(v[a]), mxv = ordered_to_dbl(v[3 + a]);
+            fr.vmin[a] = mnv - p.vs * 0.5;
+            const double vmax = mxv + p.vs * 0.5;
+            ext = fmax(ext, vmax - fr.vmin[a]);
+            const long long kmax = (long long)floor((vmax - fr.vmin[a]) / p.vs);
+            int b = 1;
+            while (b < 62 && (kmax >> b) != 0) ++b;
+            atomicMax(&kbits[a], b);
+        }
+        if (p.vs * 2147483647.0 < ext) fr.err = 1;  // Open3D: "voxel_size is too small."
+    }
+}
+
+struct FbKeys {
+    int bx, by, bz;
+};
+
+// the tile again: voxel keys of the valid pixels, emitted in pixel order at the tile's scanned offset
+__global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, const int* __restrict__ toff,
+                                                        unsigned long long* __restrict__ keys,
+                                                        unsigned* __restrict__ vals) {
+    const int f = blockIdx.y, tile = blockIdx.x;
+    const int npx = p.w * p.h;
+    const int pix0 = tile * FB_TILE + threadIdx.x * FB_PIX;
+    const uint16_t* dep = p.depth + (int64_t)f * npx;
+    double m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
+    const double vmin[3] = {p.frames[f].vmin[0], p.frames[f].vmin[1], p.frames[f].vmin[2]};
+    float d[FB_PIX];
+    fb_depth8(p, dep, pix0, npx, d);
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < FB_PIX; ++k) c += (pix0 + k < npx && d[k] > 0.0f) ? 1 : 0;
+    // exclusive prefix of the lanes' counts over the workgroup (lane-major = pixel order)
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    __shared__ int wsum[4];
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int pos = toff[(int64_t)f * p.tpf + tile] + inc - c;
+    for (int w = 0; w < wid; ++w) pos += wsum[w];
+    const unsigned long long fkey = (unsigned long long)f << (kb.bx + kb.by + kb.bz);
+#pragma unroll
+    for (int k = 0; k < FB_PIX; ++k) {
+        double xyz[3];
+        if (pix0 + k < npx && fb_point(p, m, d[k], pix0 + k, xyz)) {
+            long long kk[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor((xyz[a] - vmin[a]) / p.vs);
+            keys[pos] = fkey | ((unsigned long long)kk[0] << (kb.by + kb.bz)) | ((unsigned long long)kk[1] << kb.bz) |
+                        (unsigned long long)kk[2];
+            vals[pos] = (unsigned)((int64_t)f * npx + pix0 + k);
+            ++pos;
+        }
+    }
+}
+
+// one lane per voxel: its points (sorted values = global pixel indices, in index order) re-unprojected and summed
+__global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* __restrict__ sval,
+                                                   const int* __restrict__ heads, int64_t K, int64_t P,
+                                                   double* __restrict__ vx, double* __restrict__ vc) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= K) return;
+    const int64_t beg = heads[s], end = (s + 1 < K) ? heads[s + 1] : P;
+    const int npx = p.w * p.h;
+    const unsigned g0 = sval[beg];
+    const int f = (int)(g0 / (unsigned)npx);
+    double m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
+    const uint16_t* dep = p.depth + (int64_t)f * npx;
+    const uint8_t* col = p.color + (int64_t)f * npx * 3;
+    double sp[3] = {0, 0, 0}, sc[3] = {0, 0, 0};
+    for (int64_t j = beg; j < end; ++j) {
+        const int pix = (int)(sval[j] - (unsigned)f * (unsigned)npx);
+        float d = (float)dep[pix];
+        d = d / p.scale_f;  // valid by construction (d > 0, below trunc)
+        const uint8_t* cp = col + (int64_t)pix * 3;
+        const unsigned c0 = cp[0], c1 = cp[1], c2 = cp[2];
+        double xyz[3];
+        fb_point(p, m, d, pix, xyz);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) sp[a] += xyz[a];
+        sc[0] += (double)c0 / 255.0;
+        sc[1] += (double)c1 / 255.0;
+        sc[2] += (double)c2 / 255.0;
+    }
+    const double cnt = (double)(end - beg);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        vx[s * 3 + a] = sp[a] / cnt;
+        vc[s * 3 + a] = sc[a] / cnt;
+    }
+}
+
+// offs[f] = first segment whose frame is >= f (f = 0..F); segment frame = its key >> fshift
+__global__ void k_fb_frame_offsets(const unsigned long long* __restrict__ skeys, const int* __restrict__ heads,
+                                   int64_t K, int fshift, int F, int* __restrict__ offs) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f > F) return;
+    int64_t lo = 0, hi = K;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int)(skeys[heads[mid]] >> fshift) < f) lo = mid + 1;
+        else hi = mid;
+    }
+    offs[f] = (int)lo;
+}
+
+// kept_off[f] = first kept entry whose voxel index is >= voff[f]
+__global__ void k_fb_kept_offsets(const int64_t* __restrict__ kept, int64_t nk, const int* __restrict__ voff, int F,
+                                  int64_t* __restrict__ koff) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f > F) return;
+    int64_t lo = 0, hi = nk;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (kept[mid] < voff[f]) lo = mid + 1;
+        else hi = mid;
+    }
+    koff[f] = lo;
+}
+
+// kept rows: xyz / rgb of the kept voxels and their index inside their frame's voxel cloud
+__global__ __launch_bounds__(256) void k_fb_gather(const int64_t* __restrict__ kept, int64_t nk,
+                                                   const int* __restrict__ voff, int F, const double* __restrict__ vx,
+                                                   const double* __restrict__ vc, double* __restrict__ ox,
+                                                   double* __restrict__ oc, int64_t* __restrict__ oidx) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nk) return;
+    const int64_t i = kept[t];
+    int lo = 0, hi = F;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (voff[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        ox[t * 3 + a] = vx[i * 3 + a];
+        oc[t * 3 + a] = vc[i * 3 + a];
+    }
+    oidx[t] = i - voff[lo];
+}
+
+struct KeptEmit {
+    int64_t* out;
+    __device__ void operator()(int64_t i, int64_t pos) const { out[pos] = i; }
+};
+
+}  // namespace ot
+
+using namespace ot;
+
+// grow-only device buffers owned by a filter handle
+struct FbBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    void* get(size_t bytes) {
+        if (bytes <= n) return p;
+        if (p) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p);
+            p = nullptr;
+            n = 0;
+        }
+        const size_t nb = bytes + bytes / 8 + 256;
+        if (hipMalloc(&p, nb) != hipSuccess) return nullptr;
+        n = nb;
+        return p;
+    }
+    ~FbBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct ot_rgbd_filter {
+    ot_intrinsics intr;
+    int max_frames;
+    double depth_scale, depth_trunc, voxel_size, std_ratio;
+    int nb_neighbors;
+    // per-run state
+    int F = 0;
+    int64_t P = 0, K = 0, kept = 0;
+    std::vector<int64_t> poff, voff, koff;  // host offsets [F + 1]
+    FbBuf b_frames, b_tiles, b_keys, b_vals, b_heads, b_vox, b_avg, b_out, b_misc;
+    double* vx = nullptr;
+    double* vc = nullptr;
+    double* kx = nullptr;
+    double* kc = nullptr;
+    int64_t* kidx = nullptr;
+    double* avg = nullptr;
+    FbFrame* h_frames = nullptr;  // pinned
+};
+
+extern "C" {
+
+ot_status ot_rgbd_filter_create(const ot_intrinsics* intrinsic, int32_t max_frames, double depth_scale,
+                                double depth_trunc, double voxel_size, int32_t nb_neighbors, double std_ratio,
+                                ot_rgbd_filter** out) {
+    if (!out || !intrinsic || intrinsic->width <= 0 || intrinsic->height <= 0 || max_frames < 1 || max_frames > 1024)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[rgbd_filter] invalid arguments");
+    if (!(voxel_size > 0.0)) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel_size <= 0.");
+    if (nb_neighbors < 1 || !(std_ratio > 0))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[RemoveStatisticalOutliers] Illegal input parameters, the number of "
+                                             "neighbors and standard deviation ratio must be positive.");
+    if (nb_neighbors > 64)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[RemoveStatisticalOutliers] nb_neighbors > 64 is not supported");
+    const int64_t npx = (int64_t)intrinsic->width * intrinsic->height;
+    if (npx * max_frames > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[rgbd_filter] batch too large");
+    auto* f = new ot_rgbd_filter();
+    f->intr = *intrinsic;
+    f->max_frames = max_frames;
+    f->depth_scale = depth_scale;
+    f->depth_trunc = depth_trunc;
+    f->voxel_size = voxel_size;
+    f->nb_neighbors = nb_neighbors;
+    f->std_ratio = std_ratio;
+    if (hipHostMalloc((void**)&f->h_frames, sizeof(FbFrame) * max_frames, hipHostMallocDefault) != hipSuccess) {
+        delete f;
+        return fail(OT_ERR_HIP, "[rgbd_filter] pinned allocation failed");
+    }
+    *out = f;
+    return OT_OK;
+}
+
+ot_status ot_rgbd_filter_destroy(ot_rgbd_filter* f) {
+    if (!f) return OT_OK;
+    (void)hipDeviceSynchronize();
+    if (f->h_frames) (void)hipHostFree(f->h_frames);
+    delete f;
+    return OT_OK;
+}
+
+ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_t* depth, const uint8_t* color,
+                             const double* extrinsics_host, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!fl || n_frames < 0 || n_frames > fl->max_frames || (n_frames > 0 && (!depth || !color || !extrinsics_host)))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[rgbd_filter] invalid arguments");
+    const int F = n_frames;
+    fl->F = F;
+    fl->P = fl->K = fl->kept = 0;
+    fl->poff.assign(F + 1, 0);
+    fl->voff.assign(F + 1, 0);
+    fl->koff.assign(F + 1, 0);
+    if (F == 0) return OT_OK;
+    const int W = fl->intr.width, H = fl->intr.height, npx = W * H;
+    const int tpf = (npx + FB_TILE - 1) / FB_TILE;
+    const double vs = fl->voxel_size;
+    // ---- frame table: camera poses (Eigen 4x4 inverse of each extrinsic, as Open3D) ------------------------
+    // the pinned table is rewritten only after the previous run's copy has completed (every run synchronises)
+    for (int f = 0; f < F; ++f) inverse4(extrinsics_host + 16 * f, fl->h_frames[f].pose);
+    FbFrame* d_frames = (FbFrame*)fl->b_frames.get(sizeof(FbFrame) * F);
+    int* d_tc = (int*)fl->b_tiles.get((size_t)F * tpf * (4 + 48) + 1024 + (size_t)(F + 1) * 24);
+    if (!d_frames || !d_tc) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+    unsigned long long* d_tb = (unsigned long long*)(((uintptr_t)(d_tc + (size_t)F * tpf) + 63) & ~(uintptr_t)63);
+    unsigned long long* d_fb = d_tb + (size_t)F * tpf * 6;
+    int* d_kbits = (int*)(d_fb + (size_t)F * 6);
+    long long* d_tot = (long long*)(d_kbits + 4);
+    int* d_voff = (int*)(d_tot + 2);
+    int* d_poff = d_voff + (F + 1);
+    OT_HIP_TRY(hipMemcpyAsync(d_frames, fl->h_frames, sizeof(FbFrame) * F, hipMemcpyHostToDevice, stream));
+    OT_HIP_TRY(hipMemsetAsync(d_kbits, 0, sizeof(int) * 4, stream));
+    FbParams p;
+    p.depth = depth;
+    p.color = color;
+    p.w = W;
+    p.h = H;
+    p.tpf = tpf;
+    p.scale_f = (float)fl->depth_scale;
+    p.trunc = fl->depth_trunc;
+    p.fx = fl->intr.fx;
+    p.fy = fl->intr.fy;
+    p.cx = fl->intr.cx;
+    p.cy = fl->intr.cy;
+    p.vs = vs;
+    p.frames = d_frames;
+    p.F = F;
+    hipLaunchKernelGGL(k_fb_pixels, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, d_tc, d_tb);
+    hipLaunchKernelGGL(k_fb_setup, dim3(F + 1), dim3(256), 0, stream, p, d_tc, (const unsigned long long*)d_tb, d_fb,
+                       d_kbits, d_tot, d_poff);
+    OT_LAUNCH_CHECK();
+    // ---- sync 1: point count, key widths, frame bounds / origins -------------------------------------------
+    struct {
+        int kbits[4];
+        long long tot[2];
+    } hs;
+    std::vector<unsigned long long> hfb((size_t)F * 6);
+    std::vector<int> hpoff(F);
+    OT_HIP_TRY(hipMemcpyAsync(&hs, d_kbits, sizeof(hs), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipMemcpyAsync(hfb.data(), d_fb, sizeof(unsigned long long) * F * 6, hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipMemcpyAsync(fl->h_frames, d_frames, sizeof(FbFrame) * F, hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipMemcpyAsync(hpoff.data(), d_poff, sizeof(int) * F, hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    for (int f = 0; f < F; ++f) fl->poff[f] = hpoff[f];
+    for (int f = 0; f < F; ++f)
+        if (fl->h_frames[f].err) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel_size is too small.");
+    const int64_t P = hs.tot[0];
+    fl->P = P;
+    fl->poff[F] = P;
+    if (P == 0) return OT_OK;
+    FbKeys kb{std::max(hs.kbits[0], 1), std::max(hs.kbits[1], 1), std::max(hs.kbits[2], 1)};
+    int fbits = 0;
+    while ((1 << fbits) < F) ++fbits;
+    const int end_bit = kb.bx + kb.by + kb.bz + fbits;
+    if (end_bit > 64) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel grid exceeds 64-bit key packing");
+    // ---- voxel keys in point order, stable sort ------------------------------------------------------------
+    unsigned long long* kin = (unsigned long long*)fl->b_keys.get((size_t)P * 16 + 256);
+    unsigned* vin = (unsigned*)fl->b_vals.get((size_t)P * 8 + 256);
+    int* heads = (int*)fl->b_heads.get((size_t)P * 4 + 256);
+    if (!kin || !vin || !heads) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+    unsigned long long* kout = kin + P;
+    unsigned* vout = vin + P;
+    hipLaunchKernelGGL(k_fb_keys, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb, (const int*)d_tc, kin, vin);
+    OT_LAUNCH_CHECK();
+    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)P, end_bit, stream, 3);
+    if (st != OT_OK) return st;
+    int64_t K = 0;
+    st = compact(P, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises (sync 2)
+    if (st != OT_OK) return st;
+    fl->K = K;
+    // ---- voxel averages, frame offsets of the voxel clouds --------------------------------------------------
+    double* vox = (double*)fl->b_vox.get((size_t)K * 48 + 256);
+    if (!vox) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+    fl->vx = vox;
+    fl->vc = vox + K * 3;
+    hipLaunchKernelGGL(k_fb_reduce, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p, (const unsigned*)vout,
+                       (const int*)heads, K, P, fl->vx, fl->vc);
+    const int fshift = kb.bx + kb.by + kb.bz;
+    hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned long long*)kout,
+                       (const int*)heads, K, fshift, F, d_voff);
+    OT_LAUNCH_CHECK();
+    std::vector<int> hvoff(F + 1);
+    OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));
+    // ---- statistical outlier removal over all frames' voxel clouds at once ----------------------------------
+    // grid origin per frame = its voxel origin (every centroid lies above it); cell h from the voxel size
+    // (~target points per occupied cell of a surface sampled once per voxel: h = vs * sqrt(target))
+    double* d_org = (double*)fl->b_misc.get(sizeof(double) * 3 * F + 64);
+    if (!d_org) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+    const double hcell = vs * std::sqrt(sor_cell_target(fl->nb_neighbors));
+    std::vector<double> horg((size_t)F * 3);
+    int dims[3] = {1, 1, 1};
+    for (int f = 0; f < F; ++f)
+        for (int a = 0; a < 3; ++a) {
+            horg[f * 3 + a] = fl->h_frames[f].vmin[a];
+            if (hfb[f * 6] == ~0ull) continue;  // empty frame
+            const double span = ordered_to_dbl(hfb[f * 6 + 3 + a]) - horg[f * 3 + a];
+            dims[a] = std::max(dims[a], (int)std::floor(span / hcell) + 2);
+        }
+    OT_HIP_TRY(hipMemcpyAsync(d_org, horg.data(), sizeof(double) * 3 * F, hipMemcpyHostToDevice, stream));
+    GridBuild gb;
+    st = build_grid_frames(fl->vx, K, F, d_voff, d_org, hcell, dims, true, stream, gb, 25);  // synchronises
+    if (st != OT_OK) return st;
+    for (int f = 0; f <= F; ++f) fl->voff[f] = hvoff[f];
+    double* avg = (double*)fl->b_avg.get((size_t)K * 8 + (size_t)F * 32 + 256);
+    if (!avg) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+    fl->avg = avg;
+    double* stats = avg + K;
+    st = sor_frames(gb, K, hvoff.data(), fl->nb_neighbors, fl->std_ratio, avg, stats, stream, 28);
+    if (st != OT_OK) return st;
+    // ---- kept voxels: indices, per-frame offsets, rows ------------------------------------------------------
+    int64_t* kept = (int64_t*)fl->b_out.get((size_t)K * (8 + 8 + 48) + (size_t)(F + 1) * 8 + 512);
+    if (!kept) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+    int64_t nk = 0;
+    st = compact(K, SorKeep{avg, stats, d_voff, F}, KeptEmit{kept}, stream, &nk, 13);  // synchronises
+    if (st != OT_OK) return st;
+    fl->kept = nk;
+    int64_t* d_koff = kept + K;
+    fl->kidx = d_koff + (F + 1);
+    fl->kx = (double*)(fl->kidx + K);
+    fl->kc = fl->kx + K * 3;
+    hipLaunchKernelGGL(k_fb_kept_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const int64_t*)kept, nk,
+                       (const int*)d_voff, F, d_koff);
+    if (nk > 0)
+        hipLaunchKernelGGL(k_fb_gather, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, stream, (const int64_t*)kept,
+                           nk, (const int*)d_voff, F, (const double*)fl->vx, (const double*)fl->vc, fl->kx, fl->kc,
+                           fl->kidx);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipMemcpyAsync(fl->koff.data(), d_koff, sizeof(int64_t) * (F + 1), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
+}
+
+ot_status ot_rgbd_filter_sizes(const ot_rgbd_filter* fl, int64_t* points_host, int64_t* voxels_host,
+                               int64_t* kept_host, int64_t* point_offsets_host, int64_t* voxel_offsets_host,
+                               int64_t* kept_offsets_host) {
+    if (!fl) return fail(OT_ERR_INVALID_ARGUMENT, "[rgbd_filter] invalid handle");
+    if (points_host) *points_host = fl->P;
+    if (voxels_host) *voxels_host = fl->K;
+    if (kept_host) *kept_host = fl->kept;
+    for (int f = 0; f <= fl->F; ++f) {
+        if (point_offsets_host) point_offsets_host[f] = fl->poff[f];
+        if (voxel_offsets_host) voxel_offsets_host[f] = fl->voff[f];
+        if (kept_offsets_host) kept_offsets_host[f] = fl->koff[f];
+    }
+    return OT_OK;
+}
+
+ot_status ot_rgbd_filter_outputs(const ot_rgbd_filter* fl, const double** kept_xyz, const double** kept_rgb,
+                                 const int64_t** kept_index, const double** voxel_xyz, const double** voxel_rgb,
+                                 const double** voxel_avg_dist) {
+    if (!fl) return fail(OT_ERR_INVALID_ARGUMENT, "[rgbd_filter] invalid handle");
+    if (kept_xyz) *kept_xyz = fl->kx;
+    if (kept_rgb) *kept_rgb = fl->kc;
+    if (kept_index) *kept_index = fl->kidx;
+    if (voxel_xyz) *voxel_xyz = fl->vx;
+    if (voxel_rgb) *voxel_rgb = fl->vc;
+    if (voxel_avg_dist) *voxel_avg_dist = fl->avg;
+    return OT_OK;
+}
+
+ot_status ot_rgbd_filter_copy(const ot_rgbd_filter* fl, int32_t frame, double* kept_xyz, double* kept_rgb,
+                              int64_t* kept_index, double* voxel_xyz, double* voxel_rgb, double* voxel_avg_dist,
+                              void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!fl || frame < -1 || frame >= fl->F) return fail(OT_ERR_INVALID_ARGUMENT, "[rgbd_filter] invalid frame");
+    if (fl->F == 0) return OT_OK;
+    const int f0 = frame < 0 ? 0 : frame, f1 = frame < 0 ? fl->F : frame + 1;
+    const int64_t kb = fl->koff[f0], kn = fl->koff[f1] - kb, vb = fl->voff[f0], vn = fl->voff[f1] - vb;
+    if (kn > 0) {
+        if (kept_xyz) OT_HIP_TRY(hipMemcpyAsync(kept_xyz, fl->kx + kb * 3, kn * 24, hipMemcpyDeviceToDevice, stream));
+        if (kept_rgb) OT_HIP_TRY(hipMemcpyAsync(kept_rgb, fl->kc + kb * 3, kn * 24, hipMemcpyDeviceToDevice, stream));
+        if (kept_index) OT_HIP_TRY(hipMemcpyAsync(kept_index, fl->kidx + kb, kn * 8, hipMemcpyDeviceToDevice, stream));
+    }
+    if (vn > 0) {
+        if (voxel_xyz) OT_HIP_TRY(hipMemcpyAsync(voxel_xyz, fl->vx + vb * 3, vn * 24, hipMemcpyDeviceToDevice, stream));
+        if (voxel_rgb) OT_HIP_TRY(hipMemcpyAsync(voxel_rgb, fl->vc + vb * 3, vn * 24, hipMemcpyDeviceToDevice, stream));
+        if (voxel_avg_dist)
+            OT_HIP_TRY(hipMemcpyAsync(voxel_avg_dist, fl->avg + vb, vn * 8, hipMemcpyDeviceToDevice, stream));
+    }
+    return OT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,81 @@
+// grid.h — multi-frame neighbour grid shared by outlier.hip (single clouds) and filter_batch.hip (frame batches).
+//
+// A cloud of n points grouped in F frames (frame f = point indices [foff[f], foff[f+1])) is binned into cubic cells
+// of size h anchored at a per-frame origin.  Keys pack (frame, x, y, z) with z in the low bits, so a frame's points
+// stay one contiguous range of the sorted order and cells (x', y', z-R .. z+R) of one frame are ONE contiguous range
+// whichever of them are occupied.  Per occupied cell the 3x3 (and optionally 5x5) z-column ranges of its block are
+// precomputed.  The grid only decides which candidates a query scans, never a result.
+#pragma once
+
+#include "common.h"
+
+namespace ot {
+
+constexpr int NBR3 = 9;   // 3x3 columns, z-1 .. z+1
+constexpr int NBR5 = 25;  // 5x5 columns, z-2 .. z+2
+
+// SOR: radius (in cells) of the block a query scans first, and the matching cell occupancy target (points per
+// occupied cell of a surface-like cloud); both only change speed, never a result
+#ifndef OT_SOR_R
+#define OT_SOR_R 1
+#endif
+constexpr int SOR_BLOCK_R = OT_SOR_R;
+inline double sor_cell_target(int nb_neighbors) {
+    const double t = (SOR_BLOCK_R == 1 ? 0.7 : 0.25) * (double)nb_neighbors;
+    return t > 2.0 ? t : 2.0;
+}
+
+struct GridDev {
+    const double* sxyz;        // [n][3] points in sorted (frame, cell) order
+    const unsigned* sidx;      // sorted position -> point index
+    const int* pcell;          // sorted position -> cell (position in the sorted cell list)
+    const int2* nbr3;          // per cell: NBR3 column ranges
+    const int2* nbr5;          // per cell: NBR5 column ranges (nullptr unless built)
+    unsigned long long* hkeys; // cell hash: keys (KEY_EMPTY = free)
+    int2* hval;                // cell hash: [start, end) in the sorted order
+    int hash_mask;
+    int dim[3];                // cells per axis (every frame's cells lie in [0, dim))
+    int sy, sx, sf;            // key = f << sf | x << sx | y << sy | z
+    const double* origin;      // [F][3] per-frame grid origins (device)
+    const int* foff;           // [F + 1] frame offsets (device; the same in input and sorted order)
+    int nframes;
+    double h;
+};
+
+struct GridBuild {
+    GridDev g;
+    int64_t ncells = 0;
+};
+
+// Build the grid of n points (xyz device [n][3]) grouped in nframes frames.  d_foff / d_origin: device arrays
+// ([F+1] ints, [F][3] doubles) that must outlive the grid; dims: cells per axis covering every frame.  Scratch
+// slots slot0 .. slot0 + 2.  Synchronises (cell count).
+ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int* d_foff, const double* d_origin,
+                            double h, const int dims[3], bool with5, hipStream_t stream, GridBuild& out, int slot0);
+
+// Statistical outlier removal over a built grid (Open3D RemoveStatisticalOutliers per frame):
+// avg[i] = mean kNN distance of point i (-1 when none); per frame the cloud mean and squared-deviation sum are
+// Open3D's sequential float64 accumulations (exact chains), stats[f] = {mean, std, valid, threshold}.
+// h_foff: host copy of the frame offsets.  Scratch slots slot0 .. slot0 + 1.  Does not synchronise.
+ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_neighbors, double std_ratio,
+                     double* avg, double* stats, hipStream_t stream, int slot0);
+
+// keep predicate of frame f's points: avg > 0 && avg < stats[f].threshold
+struct SorKeep {
+    const double* avg;
+    const double* stats;  // [F][4]
+    const int* foff;
+    int nframes;
+    __device__ inline bool operator()(int64_t i) const {
+        int lo = 0, hi = nframes;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (foff[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        const double a = avg[i];
+        return a > 0 && a < stats[lo * 4 + 3];
+    }
+};
+
+}  // namespace ot

@@ -12,6 +12,7 @@
 // a = 1 - sqrt(r1), b = sqrt(r1)(1 - r2), c = sqrt(r1) r2.
 #include <vector>
 
+#include "chain.h"
 #include "compact.h"
 #include "sort.h"
 
@@ -117,20 +118,9 @@ __global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V,
 //   k_chain_emit   (CDF) every accepted chunk's values (N_b + prefix_t) * u_b, exact integers times 2^k
 // The guesses only decide which chunks take the fast path; every accepted value is proven exact by the walk's
 // check, so any input (zeros, ties, NaN, huge ranges) gives the serial chain's bits.
-constexpr int CH = 256;                // values per chunk: 64 lanes x 4
+constexpr int CH = CHAIN_CH;
 constexpr int EX_NONE = -100000;       // no usable binade guess
 constexpr long long R_MAX = 1ll << 53;
-
-struct ChainJob {
-    const double* x;  // 16-B aligned input
-    int64_t n;
-    double* out;  // CDF values (n), or the sum (out[0])
-    double* bsum;
-    int32_t* ex;
-    long long* msum;
-    int32_t* kind;  // 0 fast, 1 flagged by k_chain_chunk, 2 walked serially
-    double* start;  // exact s entering each fast chunk
-};
 
 __device__ inline double pow2(int k) { return __longlong_as_double((long long)(k + 1023) << 52); }
 
@@ -143,7 +133,7 @@ __device__ inline int binade(double s) {
 
 __device__ inline void chunk_load4(const double* __restrict__ x, int64_t n, int64_t base, int lane, double v[4]) {
     const int64_t i = base + 4 * lane;
-    if (i + 3 < n) {
+    if (i + 3 < n && ((reinterpret_cast<uintptr_t>(x) & 15) == 0)) {  // base is a multiple of 4: x's alignment decides
         const double2 p = *reinterpret_cast<const double2*>(x + i);
         const double2 q = *reinterpret_cast<const double2*>(x + i + 2);
         v[0] = p.x, v[1] = p.y, v[2] = q.x, v[3] = q.y;
@@ -376,18 +366,8 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
     if (CDF) hipLaunchKernelGGL(k_chain_emit, grid, dim3(256), 0, stream, djobs);
 }
 
-// per-chain auxiliary arrays (reused by the sum and the CDF chains, which run one after the other)
-inline size_t chain_aux_bytes(int64_t n) { return (size_t)((n + CH - 1) / CH + 1) * 40 + 256; }
-
-inline char* chain_aux(char* cur, int64_t n, ChainJob& jb) {
-    const int64_t nb = (n + CH - 1) / CH + 1;
-    jb.bsum = (double*)cur;
-    jb.start = jb.bsum + nb;
-    jb.msum = (long long*)(jb.start + nb);
-    jb.ex = (int32_t*)(jb.msum + nb);
-    jb.kind = jb.ex + nb;
-    cur = (char*)(jb.kind + nb);
-    return (char*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
+void launch_sum_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream) {
+    launch_chains<false>(djobs, n_jobs, max_n > 0 ? max_n : 1, stream);
 }
 
 __global__ __launch_bounds__(256) void k_area_div(const double* __restrict__ area, int64_t nt,

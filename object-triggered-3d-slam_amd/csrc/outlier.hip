@@ -1,54 +1,50 @@
-// outlier.hip — PointCloud::RemoveStatisticalOutliers / RemoveRadiusOutliers on MI355X.
+// outlier.hip — PointCloud::RemoveStatisticalOutliers / RemoveRadiusOutliers / ComputePointCloudDistance on
+// MI355X (eval_cone.py:99-110).
 //
-// Neighbour search uses a uniform cell grid instead of Open3D's KD-tree (the results are defined by the
+// Neighbour search uses a uniform cell grid (grid.h) instead of Open3D's KD-tree (the results are defined by the
 // distances, not by the search structure):
-//   grid build : cell key per point -> stable radix sort (cell, index) -> cell heads -> open-addressing hash
-//                (cell key -> [start, end) in the sorted order); points are re-laid out in sorted order so a
-//                cell's points are contiguous in HBM.
+//   grid build : (frame, cell) key per point -> stable radix sort -> cell heads -> open-addressing hash (cell key ->
+//                [start, end) in the sorted order) -> per cell the z-column ranges of its 3x3 / 5x5 block; points
+//                are re-laid out in sorted order so a cell's points are contiguous in HBM.
 //   ROR        : cell = radius; count |{j : d2(i, j) < r^2}| over the 27 neighbour cells (exact integers).
-//   SOR        : exact k nearest neighbours by shell expansion: cells at Chebyshev ring 0, 1, 2, ... are
-//                scanned into a register-resident sorted top-k list until the k-th distance is provably
-//                inside the scanned cube.  Distances d2 = ((dx*dx + dy*dy) + dz*dz) (nanoflann L2 order),
-//                sqrt'ed and summed in ascending order, divided by the count (std::accumulate in Open3D).
-//                Cloud mean / std use a fixed-order two-level reduction in float64.
-// Queries run in sorted (cell) order, so a wave's neighbourhoods overlap and stay in L2.
+//   SOR        : exact k nearest neighbours: the columns of the query's block are scanned nearest-first into a
+//                register-resident sorted top-k list (columns that cannot hold a closer point are skipped) until the
+//                k-th distance is provably inside the scanned block, else Chebyshev rings continue it.  Distances
+//                d2 = ((dx*dx + dy*dy) + dz*dz) (nanoflann L2 order), sqrt'ed and summed in ascending order, divided
+//                by the count (std::accumulate).  The cloud mean and squared-deviation sum are Open3D's sequential
+//                float64 accumulations, computed exactly by the chain kernels (chain.h); `valid` counts every point
+//                with a non-empty neighbour list (Open3D: valid_distances), the sums take only avg > 0.
+// Queries run in sorted (cell) order, so a wave's neighbourhoods overlap and stay in L1/L2.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <vector>
 
+#include "chain.h"
 #include "compact.h"
+#include "grid.h"
 #include "sort.h"
 
 namespace ot {
 
-struct GridDev {
-    const double* sxyz;           // points in sorted (cell) order [n][3]
-    const unsigned* sidx;         // sorted position -> original index
-    const int* pcell;             // sorted position -> cell index (position in the sorted cell list)
-    const int2* nbr3;             // per cell: 9 merged z-column ranges covering its 3x3x3 cell block
-    const int2* nbr5;             // per cell: 25 merged z-column ranges covering its 5x5x5 block (SOR only)
-    unsigned long long* hkeys;    // cell hash keys (compact keys, KEY_EMPTY = free)
-    int2* hval;                   // cell hash values: [start, end) in the sorted order
-    int hash_mask;
-    int dim[3];                   // cells per axis (cell coordinates are >= 0: origin = the cloud's minimum)
-    int sy, sx;                   // key = x << sx | y << sy | z  (z in the low bits)
-    double origin[3];
-    double h;
-};
-
-// A block of cells around a cell as z-columns: cells (x', y', z-R .. z+R) have consecutive keys, so their points
-// are ONE contiguous range of the sorted order whichever of those cells are occupied.  The 3x3x3 block is 9
-// ranges, the 5x5x5 block 25; a 5-column minus its 3-column is the two ranges on either side.
-constexpr int NBR3 = 9;
-constexpr int NBR5 = 25;
+__device__ inline int frame_of(const int* __restrict__ foff, int nframes, int64_t i) {
+    int lo = 0, hi = nframes;  // last f with foff[f] <= i (empty frames are skipped over)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (foff[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
 
 __device__ inline int cell_coord(double v, double origin, double h) { return (int)floor((v - origin) / h); }
 
 __device__ inline bool cell_valid(const GridDev& g, int x, int y, int z) {
     return x >= 0 && x < g.dim[0] && y >= 0 && y < g.dim[1] && z >= 0 && z < g.dim[2];
 }
-__device__ inline unsigned long long cell_key(const GridDev& g, int x, int y, int z) {
-    return ((unsigned long long)x << g.sx) | ((unsigned long long)y << g.sy) | (unsigned long long)z;
+__device__ inline unsigned long long cell_key(const GridDev& g, int f, int x, int y, int z) {
+    return ((unsigned long long)f << g.sf) | ((unsigned long long)x << g.sx) | ((unsigned long long)y << g.sy) |
+           (unsigned long long)z;
 }
 
 __device__ inline int2 grid_probe(const GridDev& g, unsigned long long key, unsigned slot) {
@@ -61,9 +57,9 @@ __device__ inline int2 grid_probe(const GridDev& g, unsigned long long key, unsi
     return make_int2(0, 0);
 }
 
-__device__ inline int2 grid_find(const GridDev& g, int x, int y, int z) {
+__device__ inline int2 grid_find(const GridDev& g, int f, int x, int y, int z) {
     if (!cell_valid(g, x, y, z)) return make_int2(0, 0);
-    const unsigned long long key = cell_key(g, x, y, z);
+    const unsigned long long key = cell_key(g, f, x, y, z);
     return grid_probe(g, key, (unsigned)mix64(key) & (unsigned)g.hash_mask);
 }
 
@@ -71,11 +67,14 @@ __global__ __launch_bounds__(256) void k_cell_keys(const double* __restrict__ xy
                                                    unsigned long long* keys, unsigned* idx, int* err) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const int x = cell_coord(xyz[i * 3 + 0], g.origin[0], g.h);
-    const int y = cell_coord(xyz[i * 3 + 1], g.origin[1], g.h);
-    const int z = cell_coord(xyz[i * 3 + 2], g.origin[2], g.h);
-    if (!cell_valid(g, x, y, z)) *err = 1;
-    keys[i] = cell_valid(g, x, y, z) ? cell_key(g, x, y, z) : 0ull;
+    const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, i) : 0;
+    const double* o = g.origin + 3 * f;
+    const int x = cell_coord(xyz[i * 3 + 0], o[0], g.h);
+    const int y = cell_coord(xyz[i * 3 + 1], o[1], g.h);
+    const int z = cell_coord(xyz[i * 3 + 2], o[2], g.h);
+    const bool ok = cell_valid(g, x, y, z);
+    if (!ok) *err = 1;
+    keys[i] = ok ? cell_key(g, f, x, y, z) : 0ull;
     idx[i] = (unsigned)i;
 }
 
@@ -112,9 +111,10 @@ __global__ __launch_bounds__(256) void k_cell_nbr(const unsigned long long* __re
     const int t = (int)(gid - c * COLS);
     const int dx = t / W - R, dy = t % W - R;
     const unsigned long long key = skeys[heads[c]];
+    const int f = (int)(key >> g.sf);
     const int z = (int)(key & ((1ull << g.sy) - 1));
     const int y = (int)((key >> g.sy) & ((1ull << (g.sx - g.sy)) - 1)) + dy;
-    const int x = (int)(key >> g.sx) + dx;
+    const int x = (int)((key >> g.sx) & ((1ull << (g.sf - g.sx)) - 1)) + dx;
     unsigned long long kq[W];
     unsigned slot[W];
     unsigned long long k0[W];
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_cell_nbr(const unsigned long long* __re
 #pragma unroll
     for (int i = 0; i < W; ++i) {
         valid[i] = cell_valid(g, x, y, z + i - R);
-        kq[i] = valid[i] ? cell_key(g, x, y, z + i - R) : 0ull;
+        kq[i] = valid[i] ? cell_key(g, f, x, y, z + i - R) : 0ull;
         slot[i] = (unsigned)mix64(kq[i]) & (unsigned)g.hash_mask;
     }
 #pragma unroll
@@ -194,10 +194,20 @@ __device__ inline void topk_insert(double (&best)[KMAX], double d) {
     }
 }
 
+// candidates [beg, end) of the sorted points, two per step with both rows loaded before either is tested
 template <int KMAX>
-__device__ inline void scan_range(const GridDev& g, const double q[3], int beg, int end, double (&best)[KMAX]) {
-    for (int m = beg; m < end; ++m) {
-        const double d = d2_l2(q, g.sxyz + (int64_t)m * 3);
+__device__ inline void scan_range(const double* __restrict__ P, const double q[3], int beg, int end,
+                                  double (&best)[KMAX]) {
+    int m = beg;
+    for (; m + 2 <= end; m += 2) {
+        const double* p = P + (int64_t)m * 3;
+        const double a[3] = {p[0], p[1], p[2]}, b[3] = {p[3], p[4], p[5]};
+        const double da = d2_l2(q, a), db = d2_l2(q, b);
+        if (da < best[KMAX - 1]) topk_insert<KMAX>(best, da);
+        if (db < best[KMAX - 1]) topk_insert<KMAX>(best, db);
+    }
+    if (m < end) {
+        const double d = d2_l2(q, P + (int64_t)m * 3);
         if (d < best[KMAX - 1]) topk_insert<KMAX>(best, d);
     }
 }
@@ -208,124 +218,111 @@ __device__ inline void topk_reset(double (&best)[KMAX], int kk) {
     for (int i = 0; i < KMAX; ++i) best[i] = (i < KMAX - kk) ? -INFINITY : INFINITY;
 }
 
-constexpr int SOR_RMAX = 8;  // beyond this ring a query falls back to an exact scan of every point
-
-// Exact kNN for a query the 5x5x5 block does not settle (isolated points): Chebyshev shell expansion through the
-// hash until the k-th distance lies inside the scanned cube, else a scan of the whole cloud.
-template <int KMAX>
-__device__ inline void sor_fallback(const GridDev& g, const double q[3], int64_t n, int kk,
-                                                       double (&best)[KMAX]) {
-    const int cx = cell_coord(q[0], g.origin[0], g.h), cy = cell_coord(q[1], g.origin[1], g.h),
-              cz = cell_coord(q[2], g.origin[2], g.h);
-    topk_reset<KMAX>(best, kk);
-    long long have = 0;
-    for (int r = 0; r <= SOR_RMAX; ++r) {
-        for (int dx = -r; dx <= r; ++dx)
-            for (int dy = -r; dy <= r; ++dy) {
-                const bool face = (dx == -r || dx == r || dy == -r || dy == r);
-                for (int dz = -r; dz <= r; dz += (face || r == 0) ? 1 : 2 * r) {
-                    const int2 se = grid_find(g, cx + dx, cy + dy, cz + dz);
-                    scan_range<KMAX>(g, q, se.x, se.y, best);
-                    have += se.y - se.x;
-                }
-            }
-        if (have >= kk) {
-            const double kth = best[KMAX - 1];
-            // every point within distance (r - margin) * h of q lies in rings 0..r
-            const double guard = (r > 0 ? (double)r - 0.01 : 0.0) * g.h;
-            if (kth <= guard * guard || have >= n) return;
-        }
-    }
-    topk_reset<KMAX>(best, kk);
-    scan_range<KMAX>(g, q, 0, (int)n, best);
-}
+constexpr int SOR_RMAX = 8;  // beyond this ring a query falls back to an exact scan of its frame
 
 // distance from q to the faces of its (2R+1)^3 cell block, minus a rounding margin
-__device__ inline double block_guard(const GridDev& g, const double q[3], double R) {
+__device__ inline double block_guard(const GridDev& g, const double q[3], const double* o, double R) {
     double guard = (R + 1.0) * g.h;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const double u = (q[a] - g.origin[a]) / g.h;
+        const double u = (q[a] - o[a]) / g.h;
         const double f = u - floor(u);
         guard = fmin(guard, fmin(R + f, R + 1.0 - f) * g.h);
     }
     return guard - 1e-6 * g.h;
 }
 
-#ifndef OT_SOR_SKIP
-#define OT_SOR_SKIP 1
-#endif
-
-// One lane per query (sorted order: a wave's queries share cells and candidate ranges).  Stage 1 scans the 9
-// ranges of the query's 3x3x3 block; the k-th distance is final when it does not exceed the distance from q to
-// the block's faces (>= h).  Stage 2 adds the rest of the 5x5x5 block (guard >= 2h).  Isolated points fall back.
+// Continue an unsettled query through the Chebyshev rings r0 .. SOR_RMAX of its cell (rings < r0 are already in the
+// list) until the k-th distance lies inside the scanned cube, else scan the whole frame from scratch.
 template <int KMAX>
+__device__ inline void sor_rings(const GridDev& g, const double q[3], const double* o, int f, int r0, int64_t fbeg,
+                                 int64_t fend, int kk, long long have, double (&best)[KMAX]) {
+    const int cx = cell_coord(q[0], o[0], g.h), cy = cell_coord(q[1], o[1], g.h), cz = cell_coord(q[2], o[2], g.h);
+    for (int r = r0; r <= SOR_RMAX; ++r) {
+        for (int dx = -r; dx <= r; ++dx)
+            for (int dy = -r; dy <= r; ++dy) {
+                const bool face = (dx == -r || dx == r || dy == -r || dy == r);
+                for (int dz = -r; dz <= r; dz += (face || r == 0) ? 1 : 2 * r) {
+                    const int2 se = grid_find(g, f, cx + dx, cy + dy, cz + dz);
+                    scan_range<KMAX>(g.sxyz, q, se.x, se.y, best);
+                    have += se.y - se.x;
+                }
+            }
+        const double guard = block_guard(g, q, o, (double)r);
+        if (have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard)) return;
+    }
+    topk_reset<KMAX>(best, kk);
+    scan_range<KMAX>(g.sxyz, q, (int)fbeg, (int)fend, best);
+}
+
+// column visiting order of a (2R+1)^2 block, nearest first (t = (dx + R) * (2R + 1) + dy + R)
+__constant__ unsigned char c_cols3[NBR3] = {4, 1, 3, 5, 7, 0, 2, 6, 8};
+__constant__ unsigned char c_cols5[NBR5] = {12, 7, 11, 13, 17, 6, 8, 16, 18, 2, 10, 14, 22,
+                                            1, 3, 5, 9, 15, 19, 21, 23, 0, 4, 20, 24};
+
+// One lane per query (sorted order: a wave's queries share cells and candidate ranges).  Stage 1 scans the columns
+// of the query's (2R+1)^3 block nearest-first, skipping a column once the distance from q to it reaches the current
+// k-th distance; the k-th distance is final when it does not exceed the distance from q to the block's faces.  With
+// R = 1 an unsettled query completes the 5x5x5 block; then the rings continue.
+template <int KMAX, int R>
 __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, double* avg) {
+    constexpr int W = 2 * R + 1;
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
+    const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, j) : 0;
+    const int64_t fbeg = g.foff[f], fend = g.foff[f + 1];
+    const double* o = g.origin + 3 * f;
     const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
-    const int kk = (int)((int64_t)k < n ? k : n);
+    const int kk = (int)((int64_t)k < fend - fbeg ? k : fend - fbeg);
     double best[KMAX];
     topk_reset<KMAX>(best, kk);
     const int c = g.pcell[j];
-    const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
-    long long have = 0;
-#if OT_SOR_SKIP
-    // distances from q to its cell's faces in x and y (conservatively shrunk): a neighbouring column (dx, dy) lies
-    // at least sqrt(ex^2 + ey^2) away, so once that reaches the current k-th distance none of its points can enter
+    const int2* rr = (R == 1 ? g.nbr3 + (int64_t)c * NBR3 : g.nbr5 + (int64_t)c * NBR5);
+    // distances from q to its cell's faces in x and y (conservatively shrunk): column (dx, dy) lies at least
+    // sqrt(ex^2 + ey^2) away, so once that reaches the current k-th distance none of its points can enter
     double lo[2], hi[2];
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-        const double uu = (q[a] - g.origin[a]) / g.h;
+        const double uu = (q[a] - o[a]) / g.h;
         const double fr = uu - floor(uu);
         lo[a] = fmax(fr * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
         hi[a] = fmax((1.0 - fr) * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
     }
-#endif
-    for (int u = 0; u < NBR3; ++u) {
-        // own column, then the 4 face-adjacent columns, then the 4 diagonal ones: the k-th distance tightens
-        // before the farthest candidates, so fewer of them pass the early-reject test into the insertion chain
-        const int t = (int)((0x862075314ull >> (4 * u)) & 0xF);
-        const int2 se = r3[t];
-#if OT_SOR_SKIP
-        const int dx = t / 3 - 1, dy = t % 3 - 1;
-        const double ex = dx < 0 ? lo[0] : (dx > 0 ? hi[0] : 0.0);
-        const double ey = dy < 0 ? lo[1] : (dy > 0 ? hi[1] : 0.0);
-        if (!(ex * ex + ey * ey >= best[KMAX - 1]))
-#endif
-            scan_range<KMAX>(g, q, se.x, se.y, best);
+    long long have = 0;
+    for (int u = 0; u < W * W; ++u) {
+        const int t = R == 1 ? c_cols3[u] : c_cols5[u];
+        const int dx = t / W - R, dy = t % W - R;
+        const int2 se = rr[t];
+        const double ex = dx < 0 ? lo[0] + (double)(-dx - 1) * g.h : (dx > 0 ? hi[0] + (double)(dx - 1) * g.h : 0.0);
+        const double ey = dy < 0 ? lo[1] + (double)(-dy - 1) * g.h : (dy > 0 ? hi[1] + (double)(dy - 1) * g.h : 0.0);
+        if (!(ex * ex + ey * ey >= best[KMAX - 1])) scan_range<KMAX>(g.sxyz, q, se.x, se.y, best);
         have += se.y - se.x;
     }
-    double guard = block_guard(g, q, 1.0);
-    bool settled = have >= n || (have >= kk && best[KMAX - 1] <= guard * guard);
-    int stage = 1;
-    if (!settled) {
-        stage = 2;
+    double guard = block_guard(g, q, o, (double)R);
+    bool settled = have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard);
+    int rnext = R + 1;
+    if (!settled && R == 1 && g.nbr5) {  // complete the 5x5x5 block from the precomputed ranges
         const int2* r5 = g.nbr5 + (int64_t)c * NBR5;
         for (int t = 0; t < NBR5; ++t) {
             const int dx = t / 5 - 2, dy = t % 5 - 2;
-            const int2 o = r5[t];
+            const int2 o5 = r5[t];
             if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1) {
-                const int2 i3 = r3[(dx + 1) * 3 + (dy + 1)];
+                const int2 i3 = rr[(dx + 1) * 3 + (dy + 1)];
                 if (i3.y > i3.x) {  // the column's cells at z-2 and z+2 only
-                    scan_range<KMAX>(g, q, o.x, i3.x, best);
-                    scan_range<KMAX>(g, q, i3.y, o.y, best);
-                    have += (o.y - o.x) - (i3.y - i3.x);
+                    scan_range<KMAX>(g.sxyz, q, o5.x, i3.x, best);
+                    scan_range<KMAX>(g.sxyz, q, i3.y, o5.y, best);
+                    have += (o5.y - o5.x) - (i3.y - i3.x);
                     continue;
                 }
             }
-            scan_range<KMAX>(g, q, o.x, o.y, best);
-            have += o.y - o.x;
+            scan_range<KMAX>(g.sxyz, q, o5.x, o5.y, best);
+            have += o5.y - o5.x;
         }
-        guard = block_guard(g, q, 2.0);
-        settled = have >= n || (have >= kk && best[KMAX - 1] <= guard * guard);
-        if (!settled) {
-            stage = 3;
-#ifndef OT_SOR_NOFB  // timing-only ablation build: isolated queries skip the exact fallback (results wrong)
-            sor_fallback<KMAX>(g, q, n, kk, best);
-#endif
-        }
+        guard = block_guard(g, q, o, 2.0);
+        settled = have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard);
+        rnext = 3;
     }
+    if (!settled) sor_rings<KMAX>(g, q, o, f, rnext, fbeg, fend, kk, have, best);
     double s = 0.0;
     int cnt = 0;
 #pragma unroll
@@ -334,12 +331,7 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
             s += sqrt(best[i]);
             ++cnt;
         }
-#ifdef OT_SOR_DIAG  // diagnostic build (tools/sor_work.py): (sorted position, stage, candidates scanned)
-    avg[g.sidx[j]] = (double)((j << 26) | ((long long)stage << 24) | (have < (1 << 24) ? have : (1 << 24) - 1));
-#else
-    (void)stage;
     avg[g.sidx[j]] = cnt > 0 ? s / (double)cnt : -1.0;
-#endif
 }
 
 // ------------------------------------------------------------------------------------ cross-cloud 1-NN distance
@@ -351,7 +343,7 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
 constexpr int NN_RMAX = 6;
 
 __device__ inline int2 grid_cell_range(const GridDev& g, int x, int y, int z, int& cell) {
-    const int2 se = grid_find(g, x, y, z);
+    const int2 se = grid_find(g, 0, x, y, z);
     cell = se.y > se.x ? g.pcell[se.x] : -1;
     return se;
 }
@@ -389,7 +381,7 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
                 const int2 se = r3[(u + 4) % NBR3];
                 nn_range(g, q, se.x, se.y, best);
             }
-            double guard = block_guard(g, q, 1.0);
+            double guard = block_guard(g, q, g.origin, 1.0);
             settled = best <= guard * guard;
             if (!settled) {
                 const int2* r5 = g.nbr5 + (int64_t)c * NBR5;
@@ -406,7 +398,7 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
                     }
                     nn_range(g, q, o.x, o.y, best);
                 }
-                guard = block_guard(g, q, 2.0);
+                guard = block_guard(g, q, g.origin, 2.0);
                 settled = best <= guard * guard;
             }
         }
@@ -419,7 +411,7 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
                 for (int dy = -r; dy <= r; ++dy) {
                     const bool face = (dx == -r || dx == r || dy == -r || dy == r);
                     for (int dz = -r; dz <= r; dz += (face || r == 0) ? 1 : 2 * r) {
-                        const int2 se = grid_find(g, cx + dx, cy + dy, cz + dz);
+                        const int2 se = grid_find(g, 0, cx + dx, cy + dy, cz + dz);
                         nn_range(g, q, se.x, se.y, best);
                         have += se.y - se.x;
                     }
@@ -435,82 +427,67 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
     out[i] = sqrt(best);
 }
 
-// fixed-order two-level reduction: blocks reduce contiguous chunks in a fixed tree, then one block reduces
-// the block partials in the same fixed order.  mode 0: sum of avg > 0 and count; mode 1: sum of (avg-mean)^2
-__global__ __launch_bounds__(256) void k_sor_partial(const double* __restrict__ avg, int64_t n, int mode,
-                                                     const double* __restrict__ stats, double* partial,
-                                                     long long* pcount) {
-    __shared__ double sd[256];
-    __shared__ long long sc[256];
-    const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t beg = (int64_t)blockIdx.x * chunk, end = beg + chunk < n ? beg + chunk : n;
-    double acc = 0.0;
-    long long c = 0;
-    const double mean = mode == 1 ? stats[0] : 0.0;
-    for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
+// ---- cloud statistics per frame (RemoveStatisticalOutliers after the kNN loop) -----------------------------------
+// mode 0: x[i] = avg > 0 ? avg : 0 (the accumulate's lambda) and valid[f] += (avg has neighbours, i.e. avg >= 0)
+// mode 1: x[i] = avg > 0 ? (avg - mean)^2 : 0 with mean = sum1[f] / valid[f] (the inner_product's op2)
+// grid (chunks, frames): a workgroup stays inside one frame, so the valid count is one exact integer atomic per block
+__global__ __launch_bounds__(256) void k_sor_values(const double* __restrict__ avg, const int* __restrict__ foff,
+                                                    int mode, const double* __restrict__ stats, double* __restrict__ x,
+                                                    unsigned long long* __restrict__ valid) {
+    const int f = blockIdx.y;
+    const int64_t beg = foff[f], end = foff[f + 1];
+    const int64_t i = beg + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    double mean = 0.0;
+    if (mode == 1) {
+        const double v = stats[f * 4 + 2];
+        mean = stats[f * 4 + 0] / v;
+    }
+    int c = 0;
+    if (i < end) {
         const double a = avg[i];
-        if (a > 0) {
-            acc += mode == 0 ? a : (a - mean) * (a - mean);
-            ++c;
-        }
-    }
-    sd[threadIdx.x] = acc;
-    sc[threadIdx.x] = c;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            sd[threadIdx.x] += sd[threadIdx.x + s];
-            sc[threadIdx.x] += sc[threadIdx.x + s];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        partial[blockIdx.x] = sd[0];
-        pcount[blockIdx.x] = sc[0];
-    }
-}
-
-__global__ __launch_bounds__(256) void k_sor_final(const double* partial, const long long* pcount, int nb, int mode,
-                                                   double std_ratio, double* stats) {
-    __shared__ double sd[256];
-    __shared__ long long sc[256];
-    double acc = 0.0;
-    long long c = 0;
-    for (int i = threadIdx.x; i < nb; i += 256) {
-        acc += partial[i];
-        c += pcount[i];
-    }
-    sd[threadIdx.x] = acc;
-    sc[threadIdx.x] = c;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            sd[threadIdx.x] += sd[threadIdx.x + s];
-            sc[threadIdx.x] += sc[threadIdx.x + s];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
         if (mode == 0) {
-            stats[2] = (double)sc[0];                  // valid
-            stats[0] = sc[0] > 0 ? sd[0] / (double)sc[0] : 0.0;  // cloud mean
+            x[i] = a > 0 ? a : 0.0;
+            c = a >= 0 ? 1 : 0;
         } else {
-            const double valid = stats[2];
-            const double sdv = sqrt(sd[0] / (valid - 1.0));
-            stats[1] = sdv;
-            stats[3] = stats[0] + std_ratio * sdv;  // threshold
+            x[i] = a > 0 ? (a - mean) * (a - mean) : 0.0;
+        }
+    }
+    if (mode == 0 && (int64_t)blockIdx.x * 256 < end - beg) {
+        c = wave_sum(c);
+        __shared__ int ws[4];
+        if (lane_id() == 0) ws[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int t = ws[0] + ws[1] + ws[2] + ws[3];
+            if (t) atomicAdd(&valid[f], (unsigned long long)t);
         }
     }
 }
 
-struct SorPred {
-    const double* avg;
-    const double* stats;
-    __device__ bool operator()(int64_t i) const {
-        const double a = avg[i];
-        return a > 0 && a < stats[3];
+// stats[f] = {cloud_mean (sum until mode 1), std, valid, threshold} (Bessel-corrected std)
+__global__ void k_sor_stats(int nframes, int mode, const double* __restrict__ sums,
+                            const unsigned long long* __restrict__ valid, double std_ratio, double* __restrict__ stats) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    if (mode == 0) {
+        stats[f * 4 + 0] = sums[f];  // the sum; k_sor_values divides it by valid exactly as cloud_mean /= valid
+        stats[f * 4 + 2] = (double)valid[f];
+        return;
     }
-};
+    const unsigned long long v = valid[f];
+    if (v == 0) {  // Open3D returns an empty cloud
+        stats[f * 4 + 0] = 0.0;
+        stats[f * 4 + 1] = 0.0;
+        stats[f * 4 + 3] = -INFINITY;
+        return;
+    }
+    const double mean = stats[f * 4 + 0] / (double)v;
+    const double sd = sqrt(sums[f] / (double)(v - 1));
+    stats[f * 4 + 0] = mean;
+    stats[f * 4 + 1] = sd;
+    stats[f * 4 + 3] = mean + std_ratio * sd;
+}
+
 struct RorPred {
     const unsigned char* keep;
     __device__ bool operator()(int64_t i) const { return keep[i] != 0; }
@@ -521,36 +498,32 @@ struct IndexEmit {
 };
 
 // ------------------------------------------------------------------------------------ grid builder (host)
-struct GridBuild {
-    GridDev g;
-    int64_t ncells = 0;
-};
-
 static int bits_for_host(int64_t v) {  // bits to represent 0..v
     int b = 1;
     while (b < 62 && (v >> b) != 0) ++b;
     return b;
 }
 
-// Cell grid of size h anchored at the cloud's minimum corner (mn, mx: exact bounds on the host).  Keys are
-// compact (only the bits the extent needs), so the stable radix sort runs ceil(bits / 8) passes.  with5: also
-// build the 5x5x5 ranges (SOR).
-static ot_status build_grid(const double* xyz, int64_t n, double h, const double mn[3], const double mx[3], bool with5,
-                            hipStream_t stream, GridBuild& out) {
+ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int* d_foff, const double* d_origin,
+                            double h, const int dims[3], bool with5, hipStream_t stream, GridBuild& out, int slot0) {
     GridDev& g = out.g;
     g.h = h;
+    g.origin = d_origin;
+    g.foff = d_foff;
+    g.nframes = nframes;
     int bits[3];
     for (int a = 0; a < 3; ++a) {
-        g.origin[a] = mn[a];
-        const double span = std::floor((mx[a] - mn[a]) / h);
-        if (!(span < 1.0e6)) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (radius too small for the extent)");
-        g.dim[a] = (int)span + 1;
+        if (dims[a] < 1 || dims[a] > 1000000)
+            return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (radius too small for the extent)");
+        g.dim[a] = dims[a];
         bits[a] = bits_for_host(g.dim[a] - 1);
     }
     g.sy = bits[2];
     g.sx = bits[1] + bits[2];
-    const int end_bit = bits[0] + bits[1] + bits[2];
-    char* ws = (char*)scratch(256 + (size_t)n * (8 + 8 + 4 + 4 + 4 + 4 + 24), 8);
+    g.sf = bits[0] + bits[1] + bits[2];
+    const int end_bit = g.sf + (nframes > 1 ? bits_for_host(nframes - 1) : 0);
+    if (end_bit > 64) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid keys exceed 64 bits");
+    char* ws = (char*)scratch(256 + (size_t)n * (8 + 8 + 4 + 4 + 4 + 4 + 24), slot0);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
     int* err = (int*)ws;
     unsigned long long* kin = (unsigned long long*)(ws + 256);
@@ -563,10 +536,10 @@ static ot_status build_grid(const double* xyz, int64_t n, double h, const double
     OT_HIP_TRY(hipMemsetAsync(err, 0, sizeof(int), stream));
     hipLaunchKernelGGL(k_cell_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, xyz, n, g, kin, vin, err);
     OT_LAUNCH_CHECK();
-    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, end_bit, stream, 3);
+    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, std::max(end_bit, 1), stream, 3);
     if (st != OT_OK) return st;
     int64_t ncells = 0;
-    st = compact_segments(n, kout, heads, pcell, stream, &ncells, 9);  // synchronises
+    st = compact_segments(n, kout, heads, pcell, stream, &ncells, slot0 + 1);  // synchronises
     if (st != OT_OK) return st;
     int e = 0;
     OT_HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, stream));
@@ -574,7 +547,7 @@ static ot_status build_grid(const double* xyz, int64_t n, double h, const double
     if (e) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (non-finite point coordinates)");
     int64_t cap = 1;
     while (cap < 2 * ncells + 2) cap <<= 1;
-    char* hs = (char*)scratch((size_t)cap * (8 + 8) + (size_t)ncells * (NBR3 + (with5 ? NBR5 : 0)) * 8 + 64, 10);
+    char* hs = (char*)scratch((size_t)cap * (8 + 8) + (size_t)ncells * (NBR3 + (with5 ? NBR5 : 0)) * 8 + 64, slot0 + 2);
     if (!hs) return fail(OT_ERR_HIP, "scratch allocation failed");
     g.hkeys = (unsigned long long*)hs;
     g.hval = (int2*)(g.hkeys + cap);
@@ -601,6 +574,65 @@ static ot_status build_grid(const double* xyz, int64_t n, double h, const double
     return OT_OK;
 }
 
+ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_neighbors, double std_ratio,
+                     double* avg, double* stats, hipStream_t stream, int slot0) {
+    const int F = gb.g.nframes;
+    int64_t max_n = 0;
+    for (int f = 0; f < F; ++f) max_n = std::max<int64_t>(max_n, h_foff[f + 1] - h_foff[f]);
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    const int kk = (int)std::min<int64_t>(nb_neighbors, std::max<int64_t>(max_n, 1));  // list length actually needed
+#define OT_SOR_LAUNCH(KM) \
+    hipLaunchKernelGGL((k_sor_knn<KM, SOR_BLOCK_R>), dim3(grid), dim3(256), 0, stream, gb.g, n, (int)nb_neighbors, avg)
+    if (kk <= 4) OT_SOR_LAUNCH(4);
+    else if (kk <= 8) OT_SOR_LAUNCH(8);
+    else if (kk <= 12) OT_SOR_LAUNCH(12);
+    else if (kk <= 16) OT_SOR_LAUNCH(16);
+    else if (kk <= 20) OT_SOR_LAUNCH(20);
+    else if (kk <= 24) OT_SOR_LAUNCH(24);
+    else if (kk <= 32) OT_SOR_LAUNCH(32);
+    else if (kk <= 48) OT_SOR_LAUNCH(48);
+    else OT_SOR_LAUNCH(64);
+#undef OT_SOR_LAUNCH
+    OT_LAUNCH_CHECK();
+    // the two sequential float64 sums per frame (exact chains): x values, chain jobs, valid counts, sums
+    size_t aux = 0;
+    for (int f = 0; f < F; ++f) aux += chain_aux_bytes(h_foff[f + 1] - h_foff[f]);
+    const size_t bytes = (size_t)n * 8 + 256 + aux + (sizeof(ChainJob) + 32) * (size_t)F + 256;
+    char* ws = (char*)scratch(bytes, slot0);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    double* x = (double*)ws;
+    unsigned long long* valid = (unsigned long long*)(((uintptr_t)(x + n) + 63) & ~(uintptr_t)63);
+    double* sums = (double*)(valid + F);
+    char* cur = (char*)(((uintptr_t)(sums + F) + 63) & ~(uintptr_t)63);
+    std::vector<ChainJob> jobs((size_t)F);
+    for (int f = 0; f < F; ++f) {
+        ChainJob& jb = jobs[f];
+        jb.x = x + h_foff[f];
+        jb.n = h_foff[f + 1] - h_foff[f];
+        jb.out = sums + f;
+        cur = chain_aux(cur, jb.n, jb);
+    }
+    ChainJob* djobs = (ChainJob*)cur;
+    OT_HIP_TRY(hipMemcpyAsync(djobs, jobs.data(), sizeof(ChainJob) * F, hipMemcpyHostToDevice, stream));
+    OT_HIP_TRY(hipMemsetAsync(valid, 0, sizeof(unsigned long long) * F, stream));
+    const dim3 vgrid((unsigned)std::max<int64_t>((max_n + 255) / 256, 1), (unsigned)F);
+    hipLaunchKernelGGL(k_sor_values, vgrid, dim3(256), 0, stream, (const double*)avg, gb.g.foff, 0,
+                       (const double*)stats, x, valid);
+    launch_sum_chains(djobs, F, max_n, stream);
+    const unsigned sgrid = (unsigned)((F + 63) / 64);
+    hipLaunchKernelGGL(k_sor_stats, dim3(sgrid), dim3(64), 0, stream, F, 0, (const double*)sums,
+                       (const unsigned long long*)valid, std_ratio, stats);
+    hipLaunchKernelGGL(k_sor_values, vgrid, dim3(256), 0, stream, (const double*)avg, gb.g.foff, 1,
+                       (const double*)stats, x, valid);
+    launch_sum_chains(djobs, F, max_n, stream);
+    hipLaunchKernelGGL(k_sor_stats, dim3(sgrid), dim3(64), 0, stream, F, 1, (const double*)sums,
+                       (const unsigned long long*)valid, std_ratio, stats);
+    OT_LAUNCH_CHECK();
+    // the host job table is consumed by the copy above before the caller's next synchronisation point returns
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
+}
+
 }  // namespace ot
 
 using namespace ot;
@@ -622,6 +654,26 @@ static ot_status bounds_host(const double* xyz, int64_t n, hipStream_t stream, d
     return OT_OK;
 }
 
+// one frame: origin = the cloud's minimum corner, cells per axis from the extent.  frame_dev receives the device
+// origin [3] and offsets {0, n} (scratch slot 20).
+static ot_status single_frame_grid(const double* xyz, int64_t n, double h, const double mn[3], const double mx[3],
+                                   bool with5, hipStream_t stream, GridBuild& gb) {
+    int dims[3];
+    for (int a = 0; a < 3; ++a) {
+        const double span = std::floor((mx[a] - mn[a]) / h);
+        if (!(span < 1.0e6)) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (radius too small for the extent)");
+        dims[a] = (int)span + 1;
+    }
+    char* fr = (char*)scratch(64, 20);
+    if (!fr) return fail(OT_ERR_HIP, "scratch allocation failed");
+    const double org[4] = {mn[0], mn[1], mn[2], 0.0};
+    const int off[2] = {0, (int)n};
+    OT_HIP_TRY(hipMemcpyAsync(fr, org, sizeof(org), hipMemcpyHostToDevice, stream));
+    OT_HIP_TRY(hipMemcpyAsync(fr + 32, off, sizeof(off), hipMemcpyHostToDevice, stream));
+    // build_grid_frames synchronises the stream before returning, so org / off outlive their copies
+    return build_grid_frames(xyz, n, 1, (const int*)(fr + 32), (const double*)fr, h, dims, with5, stream, gb, 22);
+}
+
 extern "C" {
 
 ot_status ot_remove_radius_outlier(const double* xyz, int64_t n, int32_t nb_points, double radius,
@@ -638,7 +690,7 @@ ot_status ot_remove_radius_outlier(const double* xyz, int64_t n, int32_t nb_poin
     ot_status st = bounds_host(xyz, n, stream, mn, mx);
     if (st != OT_OK) return st;
     GridBuild gb;
-    st = build_grid(xyz, n, radius, mn, mx, false, stream, gb);
+    st = single_frame_grid(xyz, n, radius, mn, mx, false, stream, gb);
     if (st != OT_OK) return st;
     unsigned char* keep = (unsigned char*)scratch((size_t)n + 64, 12);
     if (!keep) return fail(OT_ERR_HIP, "scratch allocation failed");
@@ -665,59 +717,33 @@ ot_status ot_remove_statistical_outlier(const double* xyz, int64_t n, int32_t nb
     double mn[3], mx[3];
     ot_status st = bounds_host(xyz, n, stream, mn, mx);
     if (st != OT_OK) return st;
-    // Cell size: the grid only changes speed, never the result.  Aim for ~occ_target points per occupied cell
-    // of a surface-like cloud (0.7 k: the k-th neighbour then lies ~0.7 h away, inside the 3x3x3 block that settles
-    // most queries).  First guess: the points cover half of the bounding box's largest face; refined once from the
-    // measured occupancy (2-D scaling) when it is off by more than 2.5x.
-    const double k = (double)nb_neighbors;
-    static const double occ_env = [] {
-        const char* e = std::getenv("OT_SOR_OCC");
-        return e ? std::atof(e) : 0.0;
-    }();
-    const double target = occ_env > 0.0 ? occ_env : std::max(0.7 * k, 2.0);
+    // Cell size: the grid only changes speed, never the result.  Aim for ~target points per occupied cell of a
+    // surface-like cloud.  First guess: the points cover half of the bounding box's largest face; refined once from
+    // the measured occupancy (2-D scaling) when it is off by more than 2.5x.
+    const double target = sor_cell_target(nb_neighbors);
     double ext[3];
     for (int a = 0; a < 3; ++a) ext[a] = std::max(mx[a] - mn[a], 1e-9);
     std::sort(ext, ext + 3);
     const double hmin = ext[2] / 5.0e5;
     double h = std::max(std::sqrt(0.5 * ext[2] * ext[1] * target / (double)n), hmin);
     GridBuild gb;
-    st = build_grid(xyz, n, h, mn, mx, true, stream, gb);
+    st = single_frame_grid(xyz, n, h, mn, mx, true, stream, gb);
     if (st != OT_OK) return st;
     const double occ = (double)n / (double)std::max<int64_t>(gb.ncells, 1);
     if (occ > 2.5 * target || occ < 0.4 * target) {
         h = std::max(h * std::sqrt(target / occ), hmin);
-        st = build_grid(xyz, n, h, mn, mx, true, stream, gb);
+        st = single_frame_grid(xyz, n, h, mn, mx, true, stream, gb);
         if (st != OT_OK) return st;
     }
-    char* ws = (char*)scratch((size_t)n * 8 + 1024 * 16 + 256, 12);
+    char* ws = (char*)scratch((size_t)n * 8 + 256, 12);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-    double* stats = (double*)ws;                  // [0] mean [1] std [2] valid [3] threshold
-    double* partial = (double*)(ws + 64);         // 1024
-    long long* pcount = (long long*)(ws + 64 + 1024 * 8);
-    double* avg = out_avg_dist ? out_avg_dist : (double*)(ws + 256 + 1024 * 16);
-    const unsigned grid = (unsigned)((n + 255) / 256);
-    const int kk = (int)std::min<int64_t>(nb_neighbors, n);  // list length actually needed
-#define OT_SOR_LAUNCH(KM) \
-    hipLaunchKernelGGL(k_sor_knn<KM>, dim3(grid), dim3(256), 0, stream, gb.g, n, (int)nb_neighbors, avg)
-    if (kk <= 4) OT_SOR_LAUNCH(4);
-    else if (kk <= 8) OT_SOR_LAUNCH(8);
-    else if (kk <= 12) OT_SOR_LAUNCH(12);
-    else if (kk <= 16) OT_SOR_LAUNCH(16);
-    else if (kk <= 20) OT_SOR_LAUNCH(20);
-    else if (kk <= 24) OT_SOR_LAUNCH(24);
-    else if (kk <= 32) OT_SOR_LAUNCH(32);
-    else if (kk <= 48) OT_SOR_LAUNCH(48);
-    else OT_SOR_LAUNCH(64);
-#undef OT_SOR_LAUNCH
-    const int nb = (int)std::min<int64_t>(1024, (n + 255) / 256);
-    hipLaunchKernelGGL(k_sor_partial, dim3(nb), dim3(256), 0, stream, avg, n, 0, stats, partial, pcount);
-    hipLaunchKernelGGL(k_sor_final, dim3(1), dim3(256), 0, stream, partial, pcount, nb, 0, std_ratio, stats);
-    hipLaunchKernelGGL(k_sor_partial, dim3(nb), dim3(256), 0, stream, avg, n, 1, stats, partial, pcount);
-    hipLaunchKernelGGL(k_sor_final, dim3(1), dim3(256), 0, stream, partial, pcount, nb, 1, std_ratio, stats);
-    OT_LAUNCH_CHECK();
-    return compact(n, SorPred{avg, stats}, IndexEmit{out_indices}, stream, n_kept_host, 13);
+    double* stats = (double*)ws;  // [mean, std, valid, threshold]
+    double* avg = out_avg_dist ? out_avg_dist : (double*)(ws + 256);
+    const int foff[2] = {0, (int)n};
+    st = sor_frames(gb, n, foff, nb_neighbors, std_ratio, avg, stats, stream, 21);
+    if (st != OT_OK) return st;
+    return compact(n, SorKeep{avg, stats, gb.g.foff, 1}, IndexEmit{out_indices}, stream, n_kept_host, 13);
 }
-
 
 ot_status ot_compute_point_cloud_distance(const double* src, int64_t n, const double* tgt, int64_t m, double* out,
                                           void* stream_) {
@@ -742,12 +768,12 @@ ot_status ot_compute_point_cloud_distance(const double* src, int64_t n, const do
     const double hmin = ext[2] / 5.0e5;
     double h = std::max(std::sqrt(0.5 * ext[2] * ext[1] * target / (double)m), hmin);
     GridBuild gb;
-    st = build_grid(tgt, m, h, mn, mx, true, stream, gb);
+    st = single_frame_grid(tgt, m, h, mn, mx, true, stream, gb);
     if (st != OT_OK) return st;
     const double occ = (double)m / (double)std::max<int64_t>(gb.ncells, 1);
     if (occ > 2.5 * target || occ < 0.4 * target) {
         h = std::max(h * std::sqrt(target / occ), hmin);
-        st = build_grid(tgt, m, h, mn, mx, true, stream, gb);
+        st = single_frame_grid(tgt, m, h, mn, mx, true, stream, gb);
         if (st != OT_OK) return st;
     }
     hipLaunchKernelGGL(k_nn_dist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, gb.g, src, n, m, mn[0],

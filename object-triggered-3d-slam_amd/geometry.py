@@ -514,6 +514,9 @@ class TriangleMesh:
             raise RuntimeError("[SamplePointsUniformly] number_of_points <= 0")
         if len(self._t) == 0:
             raise RuntimeError("[SamplePointsUniformly] Input mesh has no triangles.")
+        if use_triangle_normal:  # the reference never asks for it (reconstruct_rgbd_filter.py:123)
+            raise NotImplementedError("[SamplePointsUniformly] use_triangle_normal=True is not implemented by this "
+                                      "build (interpolated vertex normals only)")
         n = int(number_of_points)
         P = D.empty((n, 3), "float64")
         PN = D.empty((n, 3), "float64") if self.has_vertex_normals() else None

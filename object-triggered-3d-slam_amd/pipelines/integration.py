@@ -33,7 +33,8 @@ class ScalableTSDFVolume:
         D.require_gpu()
         ct = int(color_type)
         if ct == TSDFVolumeColorType.Gray32:
-            raise RuntimeError("[ScalableTSDFVolume] Gray32 color type is not supported by this build")
+            raise NotImplementedError("[ScalableTSDFVolume] TSDFVolumeColorType.Gray32 is not implemented by this build "
+                                      "(the reference uses RGB8: reconstruct_rgbd_filter.py:81-85)")
         self.voxel_length = float(voxel_length)
         self.sdf_trunc = float(sdf_trunc)
         self.color_type = TSDFVolumeColorType(ct)

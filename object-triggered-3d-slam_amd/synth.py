@@ -156,6 +156,28 @@ def make_sequence(scene: Scene | None = None, n_frames: int = 16, intr=REF_INTRI
     return np.stack(depths), np.stack(colors), np.stack(exts)
 
 
+def render_frames(job):
+    """Picklable worker for process pools: job = (scene, n_frames, intr, frame indices) -> make_sequence(...)."""
+    scene, n_frames, intr, frames = job
+    return make_sequence(scene, n_frames=n_frames, intr=intr, frames=frames)
+
+
+def make_sequence_parallel(scene: Scene | None = None, n_frames: int = 16, intr=REF_INTRINSICS_640, frames=None,
+                           workers: int = 16, chunk: int = 4):
+    """make_sequence over a fork process pool (identical arrays; call before the process initialises the GPU)."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+
+    scene = scene or Scene()
+    ks = list(range(n_frames) if frames is None else frames)
+    jobs = [(scene, n_frames, intr, ks[i:i + chunk]) for i in range(0, len(ks), chunk)]
+    if len(jobs) <= 1 or workers <= 1:
+        return make_sequence(scene, n_frames=n_frames, intr=intr, frames=ks)
+    with ProcessPoolExecutor(max_workers=min(workers, len(jobs)), mp_context=mp.get_context("fork")) as ex:
+        parts = list(ex.map(render_frames, jobs))
+    return tuple(np.concatenate([p[i] for p in parts]) for i in range(3))
+
+
 def write_dataset(base_dir: str, label: str, depth, color, poses_ros, start_index: int = 1):
     """Write the reference dataset layout (scanner_node.cpp:260-302): color/<label>_<n>.jpg,
     depth/<label>_<n>.png (uint16 mm), poses/<label>_<n>.txt (4x4, %.6f).  Counter starts at 1."""

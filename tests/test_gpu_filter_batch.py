@@ -1,0 +1,119 @@
+"""GPU parity of the configs[2] filter chain (BASELINE.json configs[2]: 1280x720, unproject -> voxel_down_sample(0.005)
+-> remove_statistical_outlier(20, 2.0)), per frame as Open3D would run it (check_one_frame.py:22-28 + SURVEY A.7).
+
+* the per-call HIP chain on one full 1280x720 frame vs the CPU oracle (bit-exact voxels, mean kNN distances, kept);
+* the batched device-resident chain (ot_rgbd_filter_run) on several distinct full-size frames vs the oracle, and vs
+  the per-call HIP chain, including an empty frame and ragged frame sizes;
+* the Open3D-shaped facade (filters.RGBDFilterBatch.frame) returns what remove_statistical_outlier returns.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_chain(O, depth, color, ext, intr_t, trunc=5.0, vs=0.005, k=20, ratio=2.0):
+    xyz, rgb = O.unproject(O.depth_to_float(depth, 1000.0, trunc), color, intr_t, ext)
+    v, vc, _, _ = O.voxel_down_sample(xyz, rgb, vs)
+    idx, avg = O.remove_statistical_outlier(v, k, ratio)
+    return xyz.shape[0], v, vc, avg, idx
+
+
+@pytest.fixture(scope="module")
+def hd_frames(synth):
+    """3 distinct frames of a 512-frame 1280x720 ring stream (frames 0, 171, 342)."""
+    return synth.make_sequence(synth.Scene(seed=0), n_frames=512, intr=synth.REF_INTRINSICS_1280, frames=[0, 171, 342])
+
+
+@pytest.fixture(scope="module")
+def hd_oracle(O, synth, hd_frames):
+    depth, color, ext = hd_frames
+    return [_oracle_chain(O, depth[f], color[f], ext[f], synth.REF_INTRINSICS_1280) for f in range(depth.shape[0])]
+
+
+def test_hd_chain_per_call_bitexact(pkg, synth, hd_frames, hd_oracle, gpu):
+    """VERDICT r1 'Next' 1: the HIP unproject -> voxel -> SOR chain on one full 1280x720 frame, Open3D-shaped calls."""
+    depth, color, ext = hd_frames
+    intr = pkg.camera.PinholeCameraIntrinsic(*synth.REF_INTRINSICS_1280)
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), depth_scale=1000.0, depth_trunc=5.0,
+        convert_rgb_to_intensity=False)
+    pcd = pkg.geometry.PointCloud.create_from_rgbd_image(rgbd, intr, ext[0])
+    down = pcd.voxel_down_sample(0.005)
+    kept, ind = down.remove_statistical_outlier(20, 2.0)
+    P, v, vc, avg, idx = hd_oracle[0]
+    assert len(pcd.points) == P
+    assert_bitwise(np.asarray(down.points), v, "voxel averages (1280x720)")
+    assert_bitwise(np.asarray(down.colors), vc, "voxel colours (1280x720)")
+    assert_bitwise(np.asarray(ind, np.int64), idx, "SOR kept indices (1280x720)")
+    assert_bitwise(np.asarray(kept.points), v[idx], "kept points (1280x720)")
+    assert_bitwise(np.asarray(kept.colors), vc[idx], "kept colours (1280x720)")
+
+
+def _run_batch(pkg, intr_t, depth, color, ext, max_frames=None, trunc=5.0):
+    flt = pkg.filters.RGBDFilterBatch(pkg.camera.PinholeCameraIntrinsic(*intr_t), max_frames=max_frames or depth.shape[0],
+                                      depth_trunc=trunc)
+    return flt.run(depth, color, ext)
+
+
+def test_hd_batch_bitexact(pkg, synth, hd_frames, hd_oracle, gpu):
+    depth, color, ext = hd_frames
+    flt = _run_batch(pkg, synth.REF_INTRINSICS_1280, depth, color, ext)
+    assert flt.points == sum(o[0] for o in hd_oracle)
+    for f, (P, v, vc, avg, idx) in enumerate(hd_oracle):
+        assert flt.point_offsets[f + 1] - flt.point_offsets[f] == P
+        down, davg = flt.voxel_cloud(f)
+        assert_bitwise(np.asarray(down.points), v, f"batch voxel averages (frame {f})")
+        assert_bitwise(np.asarray(down.colors), vc, f"batch voxel colours (frame {f})")
+        assert_bitwise(davg, avg, f"batch mean kNN distances (frame {f})")
+        kept, ind = flt.frame(f)
+        assert_bitwise(np.asarray(ind, np.int64), idx, f"batch SOR kept indices (frame {f})")
+        assert_bitwise(np.asarray(kept.points), v[idx], f"batch kept points (frame {f})")
+        assert_bitwise(np.asarray(kept.colors), vc[idx], f"batch kept colours (frame {f})")
+
+
+def test_batch_matches_per_call_ragged(pkg, O, synth, gpu):
+    """640x480 frames incl. an all-invalid frame (empty cloud) and one truncated by depth_trunc: the batch equals
+    the per-frame Open3D-shaped calls, frame by frame; the batch buffers are reused by a second, smaller run."""
+    intr_t = synth.REF_INTRINSICS_640
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=3), n_frames=64, frames=[1, 9, 17, 40, 63])
+    depth = depth.copy()
+    depth[2] = 0                        # no valid pixel
+    depth[3][depth[3] > 1500] = 4000    # beyond depth_trunc (3 m) -> invalid
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    flt = _run_batch(pkg, intr_t, depth, color, ext, max_frames=8, trunc=3.0)
+    for f in range(depth.shape[0]):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[f]), pkg.geometry.Image(depth[f]), depth_scale=1000.0, depth_trunc=3.0,
+            convert_rgb_to_intensity=False)
+        down = pkg.geometry.PointCloud.create_from_rgbd_image(rgbd, intr, ext[f]).voxel_down_sample(0.005)
+        kept, ind = down.remove_statistical_outlier(20, 2.0)
+        bdown, _ = flt.voxel_cloud(f)
+        bkept, bind = flt.frame(f)
+        assert_bitwise(np.asarray(bdown.points), np.asarray(down.points).reshape(-1, 3), f"ragged voxels (frame {f})")
+        assert bind == ind, f"ragged kept indices (frame {f})"
+        assert_bitwise(np.asarray(bkept.points), np.asarray(kept.points).reshape(-1, 3), f"ragged kept (frame {f})")
+    assert flt.voxel_offsets[3] == flt.voxel_offsets[2]  # the empty frame
+    # a second run on 2 frames reuses the handle
+    flt.run(depth[:2], color[:2], ext[:2])
+    assert flt.n_frames == 2 and flt.kept_offsets[2] == flt.kept
+
+
+def test_batch_errors(pkg, synth, gpu):
+    intr = pkg.camera.PinholeCameraIntrinsic(*synth.REF_INTRINSICS_640)
+    with pytest.raises(RuntimeError, match="voxel_size"):
+        pkg.filters.RGBDFilterBatch(intr, voxel_size=0.0)
+    with pytest.raises(RuntimeError, match="Illegal input"):
+        pkg.filters.RGBDFilterBatch(intr, nb_neighbors=0)
+    flt = pkg.filters.RGBDFilterBatch(intr, max_frames=2)
+    d = np.zeros((3, 480, 640), np.uint16)
+    c = np.zeros((3, 480, 640, 3), np.uint8)
+    with pytest.raises(RuntimeError):
+        flt.run(d, c, np.stack([np.eye(4)] * 3))           # more frames than max_frames
+    with pytest.raises(RuntimeError, match="Unsupported image format"):
+        flt.run(d[:1, :100], c[:1, :100], np.eye(4)[None])  # wrong image size

@@ -1,9 +1,9 @@
 """GPU parity: voxel_down_sample, remove_statistical_outlier, remove_radius_outlier, Z-mask, occupancy points.
 
 Bit-exact: voxel key set, per-voxel averaged xyz/colour (sums in index order), ROR kept indices, Z-mask
-compaction, occupancy points.  SOR: per-point mean kNN distance bit-exact; kept indices bit-exact (the cloud
-mean/std are float64 reductions in a different association than Open3D's sequential std::accumulate — the
-test asserts no point lies within 1e-9 relative of the threshold, where that could matter).
+compaction, occupancy points, SOR mean kNN distances and kept indices.  The SOR cloud mean and squared-deviation
+sum are Open3D's sequential float64 accumulations (exact chains on the GPU): test_sor_threshold_exact puts points
+exactly ON the threshold, where any other summation order moves the kept set.
 """
 import ctypes as C
 
@@ -91,12 +91,83 @@ def test_sor_bitexact(pkg, O, frame_cloud, k, ratio):
            C.c_void_p(idx.data_ptr()), C.c_void_p(avg.data_ptr()), C.byref(n), None)
     ridx, ravg = O.remove_statistical_outlier(ds, k, ratio)
     assert_bitwise(avg.cpu().numpy(), ravg, "SOR mean kNN distance")
-    valid = ravg[ravg > 0]
-    mean = valid.sum() / valid.size
-    thr = mean + ratio * np.sqrt(((valid - mean) ** 2).sum() / (valid.size - 1))
-    assert np.min(np.abs(valid - thr) / thr) > 1e-9
     assert_bitwise(idx[:n.value].cpu().numpy(), ridx, "SOR kept indices")
     assert not set(range(ds.shape[0] - 50, ds.shape[0])) <= set(ridx.tolist())
+
+
+def _sor_gpu(pkg, pts, k, ratio):
+    L = pkg._lib
+    d = torch.from_numpy(np.ascontiguousarray(pts)).cuda()
+    idx = torch.empty(pts.shape[0], dtype=torch.int64, device="cuda")
+    avg = torch.empty(pts.shape[0], dtype=torch.float64, device="cuda")
+    n = C.c_int64(0)
+    L.call("ot_remove_statistical_outlier", C.c_void_p(d.data_ptr()), pts.shape[0], k, ratio,
+           C.c_void_p(idx.data_ptr()), C.c_void_p(avg.data_ptr()), C.byref(n), None)
+    return idx[:n.value].cpu().numpy(), avg.cpu().numpy()
+
+
+def _seq_stats(avg):
+    """RemoveStatisticalOutliers' cloud statistics in Open3D's order (std::accumulate / std::inner_product)."""
+    valid = int((avg >= 0).sum())
+    s = 0.0
+    for a in avg.tolist():
+        s = s + a if a > 0 else s
+    mean = s / valid
+    q = 0.0
+    for a in avg.tolist():
+        q = q + ((a - mean) * (a - mean) if a > 0 else 0.0)
+    return mean, float(np.sqrt(q / (valid - 1)))
+
+
+def test_sor_threshold_exact(pkg, O, gpu):
+    """Points exactly ON the threshold: k = 2 on isolated pairs makes every mean kNN distance an exact dyadic
+    s_j / 2; std_ratio is solved so that mean + ratio * std == one pair's distance bit for bit.  That pair must be
+    dropped (strict <) and the pairs one step below kept.  The values span 2^20 in magnitude, so a pairwise or tree
+    summation gives a different mean / std than Open3D's sequential one (asserted) — only the exact sequential
+    chains reproduce the kept set."""
+    for seed in range(64):
+        rng = np.random.default_rng(seed)
+        m = 12 ** 3  # pairs on a 12^3 lattice of spacing 10 (the partner is every point's only close neighbour)
+        s = rng.integers(1, 1 << 20, size=m).astype(np.float64) * 2.0 ** -24
+        p0 = np.stack(np.meshgrid(*([np.arange(12, dtype=np.float64) * 10.0] * 3), indexing="ij"), -1).reshape(-1, 3)
+        p1 = p0 + np.stack([s, np.zeros(m), np.zeros(m)], 1)
+        pts = np.stack([p0, p1], 1).reshape(-1, 3)
+        avg = np.repeat(s / 2.0, 2)
+        mean, sd = _seq_stats(avg)
+        if np.sum(avg) / avg.size == mean and np.sqrt(np.sum((avg - mean) ** 2) / (avg.size - 1)) == sd:
+            continue  # pairwise summation happens to agree: not adversarial
+        t = float(np.quantile(avg, 0.9, method="higher"))
+        r = (t - mean) / sd
+        for _ in range(4000):
+            thr = mean + r * sd
+            if thr == t:
+                break
+            r = np.nextafter(r, np.inf if thr < t else -np.inf)
+        if mean + r * sd != t:
+            continue
+        ridx, ravg = O.remove_statistical_outlier(pts, 2, float(r))
+        assert_bitwise(ravg, avg, "oracle mean distances of the pair cloud")
+        gidx, gavg = _sor_gpu(pkg, pts, 2, float(r))
+        assert_bitwise(gavg, avg, "SOR mean distances (pairs)")
+        on = np.nonzero(avg == t)[0]
+        assert on.size >= 2 and not set(on.tolist()) & set(ridx.tolist()), "points on the threshold are dropped"
+        assert_bitwise(gidx, ridx, "SOR kept indices at the exact threshold")
+        return
+    pytest.fail("no adversarial configuration found")
+
+
+def test_sor_coincident_points(pkg, O, frame_cloud):
+    """More than k coincident points: their mean kNN distance is 0 — counted in `valid` but not summed (Open3D's
+    valid_distances vs the accumulate's avg > 0 lambda); they are never kept."""
+    xyz, rgb = frame_cloud
+    ds = O.voxel_down_sample(xyz, rgb, 0.01)[0]
+    dup = np.concatenate([ds, np.repeat(ds[:1], 30, 0), np.repeat(ds[500:501], 25, 0)])
+    for k, ratio in ((20, 2.0), (8, 0.7)):
+        ridx, ravg = O.remove_statistical_outlier(dup, k, ratio)
+        gidx, gavg = _sor_gpu(pkg, dup, k, ratio)
+        assert (ravg == 0).sum() >= 55
+        assert_bitwise(gavg, ravg, f"SOR mean distances with coincident points (k={k})")
+        assert_bitwise(gidx, ridx, f"SOR kept with coincident points (k={k})")
 
 
 def test_sor_small_and_errors(pkg, O, gpu):

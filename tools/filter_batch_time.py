@@ -1,0 +1,68 @@
+"""Time the batched configs[2] chain (ot_rgbd_filter_run) on distinct 1280x720 frames: per-frame ms for a few
+batch sizes (and the kernel breakdown when run under rocprofv3 --kernel-trace --stats)."""
+import argparse
+import ctypes as C
+import importlib
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "object-triggered-3d-slam_amd"
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--frames", type=int, default=64)
+ap.add_argument("--batches", default="8,16,32,64")
+ap.add_argument("--reps", type=int, default=3)
+a = ap.parse_args()
+synth = importlib.import_module(PKG + ".synth")
+from concurrent.futures import ProcessPoolExecutor
+import multiprocessing as mp
+
+intr_t = synth.REF_INTRINSICS_1280
+t0 = time.time()
+with ProcessPoolExecutor(max_workers=16, mp_context=mp.get_context("fork")) as ex:
+    parts = list(ex.map(synth.render_frames, [(synth.Scene(seed=0), 512, intr_t, list(range(i, min(i + 4, a.frames))))
+                                               for i in range(0, a.frames, 4)]))
+depth = np.concatenate([p[0] for p in parts])
+color = np.concatenate([p[1] for p in parts])
+ext = np.concatenate([p[2] for p in parts])
+print(f"rendered {a.frames} frames in {time.time() - t0:.1f} s", flush=True)
+import torch
+
+L = importlib.import_module(PKG + "._lib")
+L.load()
+d = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
+c = torch.from_numpy(color).cuda().contiguous()
+W, H = intr_t[0], intr_t[1]
+intr = L.ot_intrinsics(W, H, *intr_t[2:])
+stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+npx = W * H
+for B in [int(x) for x in a.batches.split(",")]:
+    h = C.c_void_p()
+    L.call("ot_rgbd_filter_create", C.byref(intr), B, 1000.0, 5.0, 0.005, 20, 2.0, C.byref(h))
+    def run_all():
+        pts = kept = 0
+        for f0 in range(0, a.frames, B):
+            n = min(B, a.frames - f0)
+            e = np.ascontiguousarray(ext[f0:f0 + n])
+            L.call("ot_rgbd_filter_run", h, n, C.c_void_p(d.data_ptr() + f0 * npx * 2), C.c_void_p(c.data_ptr() + f0 * npx * 3),
+                   e.ctypes.data_as(C.c_void_p), stream)
+            P, K, KK = C.c_int64(), C.c_int64(), C.c_int64()
+            L.call("ot_rgbd_filter_sizes", h, C.byref(P), C.byref(K), C.byref(KK), None, None, None)
+            pts += P.value
+            kept += KK.value
+        return pts, kept
+    run_all()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(a.reps):
+        pts, kept = run_all()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t1) / a.reps
+    print(f"batch {B}: {dt * 1e3 / a.frames:.4f} ms/frame, {pts / dt / 1e6:.1f} Mpoints/s, kept/frame {kept / a.frames:.0f}",
+          flush=True)
+    L.call("ot_rgbd_filter_destroy", h)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Diagnostic PMC passes for k_batch_integrate (KPREFIX selects other kernels; OTSLAM_LIB a variant library) (one rocprofv3 run per pass; --pmc never combined with tracing
+# Diagnostic PMC passes for k_batch_integrate (KPREFIX selects other kernels; VARIANT a variant library) (one rocprofv3 run per pass; --pmc never combined with tracing
 # domains other than --kernel-trace).  Output: gpurun_out/diag_<i>/ and a per-kernel summary on stdout.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -13,7 +13,7 @@ PASSES=(
 dirs=()
 for i in "${!PASSES[@]}"; do
   timeout -k 10 240 rocprofv3 --pmc ${PASSES[$i]} --kernel-trace --output-format csv -d gpurun_out/diag_$i -o run -- \
-      python3 bench.py $ARGS > gpurun_out/diag_$i.log 2>&1
+      python3 tools/with_variant.py ${VARIANT:-base} bench.py $ARGS > gpurun_out/diag_$i.log 2>&1
   dirs+=("gpurun_out/diag_$i")
 done
 python3 - "${dirs[@]}" <<'PY'

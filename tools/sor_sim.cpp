@@ -1,0 +1,184 @@
+// sor_sim.cpp — CPU model of k_sor_knn's lockstep work (design tool, not product code).
+// Loads a float64 [n][3] .npy cloud, builds the cell grid (cell h, x-major keys, points in cell order) and
+// simulates waves of 64 consecutive sorted queries scanning their candidate ranges in lockstep: per range slot the
+// wave runs max-lane-length steps, and a step executes the top-k insertion chain when ANY lane inserts.
+// Reports candidates per query, per-lane insertions, and wave-level step / insertion-step counts.
+//   g++ -O2 -std=c++17 -o /tmp/sor_sim tools/sor_sim.cpp && /tmp/sor_sim cloud.npy k h_mult [order]
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <unordered_map>
+#include <vector>
+
+static std::vector<double> load_npy(const char* path, size_t& n) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { perror(path); exit(1); }
+    char magic[10];
+    fread(magic, 1, 10, f);
+    unsigned short hl = (unsigned char)magic[8] | ((unsigned char)magic[9] << 8);
+    std::vector<char> hdr(hl);
+    fread(hdr.data(), 1, hl, f);
+    fseek(f, 0, SEEK_END);
+    long sz = ftell(f) - 10 - hl;
+    fseek(f, 10 + hl, SEEK_SET);
+    n = sz / 24;
+    std::vector<double> v(n * 3);
+    fread(v.data(), 8, n * 3, f);
+    fclose(f);
+    return v;
+}
+
+int main(int argc, char** argv) {
+    size_t n;
+    auto P = load_npy(argv[1], n);
+    const int K = atoi(argv[2]);
+    const double hm = atof(argv[3]);  // cell = hm * 5 mm
+    const int R = argc > 4 ? atoi(argv[4]) : 1;  // stage-1 block radius in cells
+    const int zorder = argc > 5 ? atoi(argv[5]) : 0;  // 1: own z-cell first inside a column
+    const double h = hm * 0.005;
+    double mn[3] = {1e30, 1e30, 1e30};
+    for (size_t i = 0; i < n; ++i)
+        for (int a = 0; a < 3; ++a) mn[a] = std::min(mn[a], P[i * 3 + a]);
+    auto cc = [&](size_t i, int a) { return (long long)std::floor((P[i * 3 + a] - mn[a]) / h); };
+    auto key = [](long long x, long long y, long long z) { return (x << 42) | (y << 21) | z; };
+    std::vector<std::pair<long long, size_t>> ord(n);
+    for (size_t i = 0; i < n; ++i) ord[i] = {key(cc(i, 0), cc(i, 1), cc(i, 2)), i};
+    std::stable_sort(ord.begin(), ord.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    std::unordered_map<long long, std::pair<int, int>> cells;
+    for (size_t s = 0; s < n;) {
+        size_t e = s;
+        while (e < n && ord[e].first == ord[s].first) ++e;
+        cells[ord[s].first] = {(int)s, (int)e};
+        s = e;
+    }
+    std::vector<double> S(n * 3);
+    for (size_t s = 0; s < n; ++s)
+        for (int a = 0; a < 3; ++a) S[s * 3 + a] = P[ord[s].second * 3 + a];
+    auto find = [&](long long x, long long y, long long z) -> std::pair<int, int> {
+        if (x < 0 || y < 0 || z < 0) return {0, 0};
+        auto it = cells.find(key(x, y, z));
+        return it == cells.end() ? std::pair<int, int>{0, 0} : it->second;
+    };
+    // per query: list of ranges (slots), columns ordered by distance class; a column = cells z-R..z+R
+    const int W = 2 * R + 1;
+    std::vector<std::pair<int, int>> cols;  // (dx, dy) ordered: centre, faces, rest by squared distance
+    for (int dx = -R; dx <= R; ++dx)
+        for (int dy = -R; dy <= R; ++dy) cols.push_back({dx, dy});
+    std::stable_sort(cols.begin(), cols.end(), [](auto a, auto b) {
+        return a.first * a.first + a.second * a.second < b.first * b.first + b.second * b.second;
+    });
+    const int nslot = (int)cols.size() * (zorder ? W : 1);
+    long long stage2_steps = 0, tot_cand = 0, tot_ins = 0, wave_steps = 0, wave_ins_steps = 0, unsettled = 0;
+    std::vector<std::vector<std::pair<int, int>>> plan(64, std::vector<std::pair<int, int>>(nslot));
+    std::vector<std::vector<double>> best(64, std::vector<double>(K));
+    std::vector<double> lo(64 * 2), hi(64 * 2), lz(64), hz(64);
+    for (size_t w0 = 0; w0 < n; w0 += 64) {
+        const int nl = (int)std::min<size_t>(64, n - w0);
+        for (int l = 0; l < nl; ++l) {
+            const size_t j = w0 + l;
+            long long x = (long long)std::floor((S[j * 3] - mn[0]) / h), y = (long long)std::floor((S[j * 3 + 1] - mn[1]) / h),
+                      z = (long long)std::floor((S[j * 3 + 2] - mn[2]) / h);
+            int u = 0;
+            for (auto [dx, dy] : cols) {
+                if (!zorder) {
+                    int b = 1 << 30, e = 0;
+                    for (int dz = -R; dz <= R; ++dz) {
+                        auto se = find(x + dx, y + dy, z + dz);
+                        if (se.second > se.first) b = std::min(b, se.first), e = std::max(e, se.second);
+                    }
+                    plan[l][u++] = e > 0 ? std::pair<int, int>{b, e} : std::pair<int, int>{0, 0};
+                } else {
+                    plan[l][u++] = find(x + dx, y + dy, z);
+                    for (int r = 1; r <= R; ++r) {
+                        plan[l][u++] = find(x + dx, y + dy, z - r);
+                        plan[l][u++] = find(x + dx, y + dy, z + r);
+                    }
+                }
+            }
+            for (int a = 0; a < 2; ++a) {
+                const double uu = (S[j * 3 + a] - mn[a]) / h, fr = uu - std::floor(uu);
+                lo[l * 2 + a] = fr * h, hi[l * 2 + a] = (1 - fr) * h;
+            }
+            {
+                const double uu = (S[j * 3 + 2] - mn[2]) / h, fr = uu - std::floor(uu);
+                lz[l] = fr * h, hz[l] = (1 - fr) * h;
+            }
+            std::fill(best[l].begin(), best[l].end(), INFINITY);
+        }
+        for (int u = 0; u < nslot; ++u) {
+            const int ci = zorder ? u / W : u;
+            const int dx = cols[ci].first, dy = cols[ci].second;
+            int maxlen = 0;
+            std::vector<char> act(nl);
+            for (int l = 0; l < nl; ++l) {
+                // column cull (distance to the column's near face vs the current k-th distance)
+                double ex = dx < 0 ? lo[l * 2] + (-dx - 1) * h : (dx > 0 ? hi[l * 2] + (dx - 1) * h : 0.0);
+                double ey = dy < 0 ? lo[l * 2 + 1] + (-dy - 1) * h : (dy > 0 ? hi[l * 2 + 1] + (dy - 1) * h : 0.0);
+                double ez = 0.0;
+                if (zorder) {
+                    const int dz = (u % W) == 0 ? 0 : (((u % W) - 1) % 2 == 0 ? -((u % W) + 1) / 2 : ((u % W) + 1) / 2);
+                    ez = dz < 0 ? lz[l] + (-dz - 1) * h : (dz > 0 ? hz[l] + (dz - 1) * h : 0.0);
+                }
+                act[l] = ex * ex + ey * ey + ez * ez < best[l][K - 1];
+                if (act[l]) maxlen = std::max(maxlen, plan[l][u].second - plan[l][u].first);
+            }
+            for (int s = 0; s < maxlen; ++s) {
+                bool any = false;
+                for (int l = 0; l < nl; ++l) {
+                    if (!act[l] || s >= plan[l][u].second - plan[l][u].first) continue;
+                    const size_t j = w0 + l, m = plan[l][u].first + s;
+                    const double d0 = S[j * 3] - S[m * 3], d1 = S[j * 3 + 1] - S[m * 3 + 1], d2 = S[j * 3 + 2] - S[m * 3 + 2];
+                    const double d = (d0 * d0 + d1 * d1) + d2 * d2;
+                    ++tot_cand;
+                    if (d < best[l][K - 1]) {
+                        any = true;
+                        ++tot_ins;
+                        auto& b = best[l];
+                        b[K - 1] = d;
+                        for (int i = K - 1; i > 0 && b[i] < b[i - 1]; --i) std::swap(b[i], b[i - 1]);
+                    }
+                }
+                ++wave_steps;
+                wave_ins_steps += any;
+            }
+        }
+        long long wmax2 = 0;
+        for (int l = 0; l < nl; ++l) {
+            // settled if k-th <= distance to the block faces
+            const size_t j = w0 + l;
+            double g = 1e30;
+            for (int a = 0; a < 3; ++a) {
+                const double uu = (S[j * 3 + a] - mn[a]) / h, fr = uu - std::floor(uu);
+                g = std::min(g, std::min(R + fr, R + 1 - fr) * h);
+            }
+            const bool un = !(best[l][K - 1] <= g * g);
+            unsettled += un;
+            if (un) {
+                long long x = (long long)std::floor((S[j * 3] - mn[0]) / h), y = (long long)std::floor((S[j * 3 + 1] - mn[1]) / h),
+                          z = (long long)std::floor((S[j * 3 + 2] - mn[2]) / h);
+                long long c = 0;
+                const int R2 = R + 1;
+                for (int dx = -R2; dx <= R2; ++dx)
+                    for (int dy = -R2; dy <= R2; ++dy)
+                        for (int dz = -R2; dz <= R2; ++dz) {
+                            if (std::max(std::abs(dx), std::max(std::abs(dy), std::abs(dz))) != R2) continue;
+                            auto se = find(x + dx, y + dy, z + dz);
+                            c += se.second - se.first;
+                        }
+                wmax2 = std::max(wmax2, c);
+            }
+        }
+        stage2_steps += wmax2;
+    }
+    const double nq = (double)n, nw = std::ceil(nq / 64);
+    printf("n %zu h %.4f R %d zorder %d cells %zu (%.1f pts/cell): cand/query %.1f ins/query %.1f | per wave: steps %.1f "
+           "ins-steps %.1f (%.0f%%) | unsettled %.2f%% | VALU model (12/step + 42/ins-step) per query %.1f\n",
+           n, h, R, zorder, cells.size(), nq / cells.size(), tot_cand / nq, tot_ins / nq, wave_steps / nw,
+           wave_ins_steps / nw, 100.0 * wave_ins_steps / std::max<long long>(wave_steps, 1), 100.0 * unsettled / nq,
+           (12.0 * wave_steps + 42.0 * wave_ins_steps) / nq);
+    printf("   stage-2 wave steps per wave %.1f -> model incl. stage 2 (54/step) per query %.1f\n", stage2_steps / nw,
+           (12.0 * wave_steps + 42.0 * wave_ins_steps + 54.0 * stage2_steps) / nq);
+}

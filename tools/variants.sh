@@ -14,9 +14,7 @@ if [ "$mode" = build ]; then
   exit 0
 fi
 for name in "$@"; do
-  lib=$PWD/object-triggered-3d-slam_amd/variants/libotslam_$name.so
-  [ "$name" = base ] && lib=$PWD/object-triggered-3d-slam_amd/libotslam_hip.so
-  OTSLAM_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_tsdf.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/vtest_$name.log 2>&1 || { echo "$name TESTS FAILED"; tail -20 gpurun_out/vtest_$name.log; exit 1; }
-  OTSLAM_LIB=$lib timeout -k 10 200 python3 bench.py --steps 5 --warmup 1 --cpu-frames 0 --filter-frames 0 > gpurun_out/vbench_$name.log 2>&1 || { echo "$name bench failed"; tail -3 gpurun_out/vbench_$name.log; exit 1; }
+    timeout -k 10 300 python -u tools/with_variant.py $name -m pytest tests/test_gpu_tsdf.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/vtest_$name.log 2>&1 || { echo "$name TESTS FAILED"; tail -20 gpurun_out/vtest_$name.log; exit 1; }
+  timeout -k 10 200 python3 tools/with_variant.py $name bench.py --steps 5 --warmup 1 --cpu-frames 0 --filter-frames 0 > gpurun_out/vbench_$name.log 2>&1 || { echo "$name bench failed"; tail -3 gpurun_out/vbench_$name.log; exit 1; }
   python3 -c "import json;d=json.loads(open('gpurun_out/vbench_$name.log').read().strip().splitlines()[-1]);r=d['roofline'];print('$name', d['value'], d['ms_per_step'], r['kernel_ms_avg'], r['launches_per_step'])"
 done
