@@ -9,9 +9,16 @@ timing.  Prints ONE JSON line on rank 0.
 
 Also reported:
   roofline     — dominant kernel (k_batch_integrate): algorithmic bytes per launch (5*W*H + 40*U_f)
-                 over its mean device time measured with HIP events on the launch stream;
+                 over its mean device time measured with HIP events on the launch stream (`frac` = `frac_effective`:
+                 temporal blocking keeps voxel state on chip across a batch, so it may exceed 1), and the measured HBM
+                 bytes per launch from rocprofv3 PMC counters (profiles/pmc_traffic.json, used only when its source
+                 hash and workload match this build) over the same time (`hbm_frac`);
   cpu_baseline — the CPU oracle (strict-IEEE restatement of Open3D's ScalableTSDFVolume, OpenMP where Open3D
-                 places it) on a bounded sample of the same frames, rank 0 only.
+                 places it) on a bounded sample of the same frames, rank 0 only: 1 warm-up, median of 5 passes;
+  sustained    — the headline step repeated for >= 1.5 s after the timed steps (corroborates `value`);
+  filtered     — configs[2]: 512 distinct 1280x720 frames through the batched device-resident chain
+                 (ot_rgbd_filter_run), Mpoints/s;
+  objects / hybrid_map / single_frame / spatial — configs[3], [4], [0] and single-object sharding (N > 1).
 """
 from __future__ import annotations
 
@@ -37,22 +44,24 @@ COLL_DEV = "cuda"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--voxel", type=float, default=0.005)
     ap.add_argument("--sdf-trunc", type=float, default=0.04)
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
-    ap.add_argument("--cpu-frames", type=int, default=64, help="frames in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=32, help="frames in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--sustain", type=float, default=1.5, help="seconds of sustained headline steps (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--calib", action="store_true", help="after timing, run export_units once (PMC calibration)")
-    ap.add_argument("--filter-frames", type=int, default=64,
-                    help="configs[2] stream length (1280x720 unproject + 5 mm voxel + SOR); 0 = skip")
+    ap.add_argument("--filter-frames", type=int, default=512,
+                    help="configs[2] stream length, distinct frames (1280x720 unproject + 5 mm voxel + SOR); 0 = skip")
+    ap.add_argument("--filter-batch", type=int, default=32, help="configs[2]: frames per batched chain call")
     ap.add_argument("--objects", type=int, default=8,
                     help="configs[3]: object scans shared by all ranks (full per-object pipeline + RCCL merge); 0 = skip")
     ap.add_argument("--object-frames", type=int, default=64, help="configs[3]: frames per object scan")
-    ap.add_argument("--filter-streams", type=int, default=6,
-                    help="configs[2]: frames filtered concurrently (host threads x HIP streams)")
+    ap.add_argument("--filter-streams", type=int, default=2,
+                    help="configs[2]: batches filtered concurrently (host threads x HIP streams)")
     ap.add_argument("--object-streams", type=int, default=2,
                     help="configs[3]: objects reconstructed concurrently per GPU (host threads x HIP streams)")
     ap.add_argument("--spatial", type=int, default=1,
@@ -74,6 +83,12 @@ def main():
     synth0 = importlib.import_module(PKG + ".synth")
     obj_ids = list(range(args.objects))[(args.objects * rank) // world:(args.objects * (rank + 1)) // world]
     obj_scans = _render_objects(synth0, obj_ids, args.object_frames) if args.objects > 0 else None
+    # every scan is rendered by forked workers before this process touches the GPU
+    head_scan = synth0.make_sequence_parallel(synth0.Scene(seed=rank), n_frames=args.frames,
+                                              intr=synth0.REF_INTRINSICS_640)
+    filt_frames = synth0.make_sequence_parallel(synth0.Scene(seed=rank), n_frames=args.filter_frames,
+                                                intr=synth0.REF_INTRINSICS_1280) \
+        if (args.filter_frames > 0 and rank == 0) else None
     # OT_BENCH_BACKEND=gloo + OT_BENCH_SHARE_GPU=1 rehearse the N-rank path on a one-GPU box (every rank on
     # device 0, collectives through host memory); the driver's runs use RCCL ("nccl"), one GPU per rank.
     backend = os.environ.get("OT_BENCH_BACKEND", "nccl")
@@ -97,8 +112,7 @@ def main():
     # ---- synthetic object scan for this rank (same geometry, rank-seeded noise) ----
     intr_t = synth.REF_INTRINSICS_640
     W, H = intr_t[0], intr_t[1]
-    scene = synth.Scene(seed=rank)
-    depth, color, ext = synth.make_sequence(scene, n_frames=args.frames, intr=intr_t)
+    depth, color, ext = head_scan
     d_depth = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
     d_color = torch.from_numpy(color).cuda().contiguous()
     ext = np.ascontiguousarray(ext, dtype=np.float64)
@@ -143,6 +157,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # ---- sustained: the same step back to back for >= args.sustain seconds (corroborates value over a long window) ----
+    sustained = None
+    if args.sustain > 0:
+        n_s, t_s = 0, time.perf_counter()
+        while time.perf_counter() - t_s < args.sustain:
+            step()
+            n_s += 1
+            if n_s % 8 == 0:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        dt_s = time.perf_counter() - t_s
+        sustained = {"steps": n_s, "seconds": round(dt_s, 3), "frames_per_s": round(world * n_s * args.frames / dt_s, 1)}
+
     # ---- per-step accounting: exact voxel updates (U_f summed over frames) ----
     upd, unit_int = C.c_int64(0), C.c_int64(0)
     L.call("ot_tsdf_counters", vol, C.byref(upd), C.byref(unit_int))
@@ -163,23 +190,19 @@ def main():
     per_launch_bytes = algo_bytes_step / max(klaunch.value, 1)
     kernel_ms_avg = kms.value / max(klaunch.value, 1)
     achieved = per_launch_bytes / (kernel_ms_avg * 1e-3) / 1e9 if kernel_ms_avg > 0 else 0.0
-    traffic = None
-    try:
-        with open(args.traffic) as f:
-            tr = json.load(f)
-        if tr.get("kernel") and tr.get("bytes_per_launch"):
-            traffic = tr["bytes_per_launch"]
-    except Exception:
-        traffic = None
+    traffic, traffic_note = _traffic(args, L, "k_batch_integrate", {"voxel": args.voxel, "frames": args.frames,
+                                                                    "batch": args.batch})
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_integrate" if args.batch == 1 else "k_batch_integrate", "kernel_ms_avg": round(kernel_ms_avg, 5), "launches_per_step": klaunch.value,
-                "algorithmic_bytes_per_launch": round(per_launch_bytes),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "frac_effective": round(achieved / HBM_PEAK_GBS, 4),
                 "effective": args.batch != 1,  # voxel state reused on chip across a batch
+                "traffic": traffic, "traffic_source": traffic_note,
+                "kernel": "k_integrate" if args.batch == 1 else "k_batch_integrate",
+                "kernel_ms_avg": round(kernel_ms_avg, 5), "launches_per_step": klaunch.value,
+                "algorithmic_bytes_per_launch": round(per_launch_bytes),
                 "voxel_updates_per_frame": round(upd.value / args.frames)}
-    if traffic and kernel_ms_avg > 0:  # measured HBM bytes (PMC, profiles/pmc_traffic.json) over the same launch time
-        roofline["traffic_gbs"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9, 1)
-        roofline["traffic_frac"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if traffic and kernel_ms_avg > 0:  # measured HBM bytes per launch over the same launch time
+        roofline["hbm_achieved"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9, 1)
+        roofline["hbm_frac"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     if args.calib:  # a kernel with a known read byte count and the integrate kernel's pool access pattern
         nu = n_units.value
@@ -187,11 +210,13 @@ def main():
         L.call("ot_tsdf_export_units", vol, None, *[C.c_void_p(b.data_ptr()) for b in bufs], stream)
         torch.cuda.synchronize()
 
-    # configs[2] runs before configs[3]: after the objects leg the filtered stream measures ~0.44 instead of
-    # ~0.38 ms/frame (cause not isolated); each leg is timed on its own either way
-    filt = filter_stream(args, L, lib, synth, torch, rank) if (args.filter_frames > 0 and rank == 0) else None
-    objects = objects_pipeline(args, L, lib, synth, torch, dist, rank, world, obj_ids, obj_scans) \
-        if args.objects > 0 else None
+    order = os.environ.get("OT_BENCH_ORDER", "filtered,objects").split(",")  # leg-order check
+    filt = objects = None
+    for leg in order:
+        if leg == "filtered" and args.filter_frames > 0 and rank == 0:
+            filt = filter_stream(args, L, synth, torch, rank, filt_frames)
+        if leg == "objects" and args.objects > 0:
+            objects = objects_pipeline(args, L, lib, synth, torch, dist, rank, world, obj_ids, obj_scans)
     hybrid = hybrid_fusion(args, L, synth, torch, dist, rank, world) if args.hybrid_objects > 0 else None
 
     spatial = spatial_shard(args, L, lib, synth, torch, dist, rank, world, n_units.value) \
@@ -211,8 +236,8 @@ def main():
                       "frames_per_step": args.frames, "width": W, "height": H, "voxel_length": args.voxel,
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
-           "roofline": roofline, "cpu_baseline": cpu, "filtered": filt, "objects": objects, "hybrid_map": hybrid,
-           "single_frame": single, "spatial": spatial}
+           "roofline": roofline, "cpu_baseline": cpu, "sustained": sustained, "filtered": filt, "objects": objects,
+           "hybrid_map": hybrid, "single_frame": single, "spatial": spatial, "source_hash": L.source_hash()}
     if rank == 0:
         print(json.dumps(out), flush=True)
     L.call("ot_tsdf_destroy", vol)
@@ -433,12 +458,43 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
 
     dt, merged = _timed(torch, dist, world, run, 3)
     pool.shutdown()
+
+    # one object end to end on one stream (integrate -> mesh -> normals -> 100k samples -> z mask): the latency that
+    # bounds the objects-over-GPUs time from below (8 objects on 8 GPUs cannot finish faster than one object)
+    single = None
+    if dev:
+        vol, (d16, col, ext) = vols[0], dev[0]
+        s_ = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+        def one():
+            vol.reset()
+            for k in range(ext.shape[0]):
+                if lib.ot_tsdf_integrate_u16(vol._h, C.c_void_p(d16.data_ptr() + k * npx * 2),
+                                             C.c_void_p(col.data_ptr() + k * npx * 3), C.byref(intr),
+                                             ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, s_):
+                    raise RuntimeError(lib.ot_last_error().decode())
+            mesh = vol.extract_triangle_mesh()
+            mesh.compute_vertex_normals()
+            return mesh.sample_points_uniformly(number_of_points=100000).filter_min_z(0.03)
+
+        one()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            t1 = time.perf_counter()
+            one()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t1)
+        single = round(float(np.median(ts)) * 1e3, 3)
+    merge = "RCCL all-gather over xGMI" if (world > 1 and COLL_DEV == "cuda") else \
+        ("gloo all-gather" if world > 1 else "local concatenation (N=1: no process group, no collective)")
     return {"workload": f"configs[3]: {args.objects} object scans x {args.object_frames} 640x480 frames, "
                         f"{args.voxel * 1000:g} mm TSDF -> mesh -> normals -> 100k samples -> z mask per object, "
-                        f"contiguous object shards over {world} GPU(s) ({T} concurrent streams per GPU), "
-                        f"RCCL all-gather merge",
+                        f"contiguous object shards over {world} GPU(s) ({T} concurrent streams per GPU), merge: {merge}",
             "frames_per_s": round(args.objects * args.object_frames / dt, 1), "ms": round(dt * 1e3, 3),
-            "objects_per_rank": len(ids), "merged_points": int(merged.shape[0])}
+            "objects_per_rank": len(ids), "merged_points": int(merged.shape[0]), "merge": merge,
+            "single_object_ms": single,
+            "single_object_note": "median of 5, object 0 of this rank on one stream, same pipeline, no merge"}
 
 
 def hybrid_fusion(args, L, synth, torch, dist, rank, world):
@@ -510,120 +566,147 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
             "removed_keys_rank0": stats.get("removed")}
 
 
-def filter_stream(args, L, lib, synth, torch, rank):
-    """configs[2]: 1280x720 RGB-D stream, per frame unproject (depth_trunc 5 m) -> voxel_down_sample(0.005) ->
-    remove_statistical_outlier(20, 2.0) -> gather kept points, all through the C ABI on device buffers.
-    16 distinct synthetic frames are cycled to the requested stream length.  Mpoints/s counts valid input
-    points per second; the CPU oracle runs the same chain on 2 frames for the baseline."""
+def filter_stream(args, L, synth, torch, rank, frames):
+    """configs[2]: a 1280x720 RGB-D stream of --filter-frames DISTINCT frames (rendered before GPU init, resident in
+    HBM: 512 x 4.6 MB), per frame create_from_color_and_depth(depth_trunc 5 m) -> create_from_rgbd_image ->
+    voxel_down_sample(0.005) -> remove_statistical_outlier(20, 2.0) -> select_by_index (check_one_frame.py:22-28 +
+    SURVEY A.7), through the batched device-resident chain ot_rgbd_filter_run: --filter-batch frames per call,
+    --filter-streams calls in flight (one host thread + HIP stream + handle each).  Mpoints/s counts valid input
+    points per second.  The CPU oracle runs the same chain on 2 of the frames (1 warm-up, median of 5)."""
+    depth, color, ext = frames
     intr_t = synth.REF_INTRINSICS_1280
     W, H = intr_t[0], intr_t[1]
-    nuniq = 16
-    depth, color, ext = synth.make_sequence(synth.Scene(seed=rank), n_frames=nuniq, intr=intr_t)
+    npx = W * H
+    nf = depth.shape[0]
     d16 = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
     col = torch.from_numpy(color).cuda().contiguous()
-    npx = W * H
+    exts = np.ascontiguousarray(ext, dtype=np.float64).reshape(nf, 16)
     intr = L.ot_intrinsics(W, H, *intr_t[2:])
-    exts = np.ascontiguousarray(ext)
-    ptr = lambda t: C.c_void_p(t.data_ptr())
-    # frames are independent: T host threads, each with its own HIP stream and buffers, take frames round-robin,
-    # so one frame's host round trips (each Open3D-shaped call returns its size) overlap another's kernels
+    B, T = max(1, args.filter_batch), max(1, args.filter_streams)
+    nb = (nf + B - 1) // B
+    handles = []
+    for _ in range(T):
+        h = C.c_void_p()
+        L.call("ot_rgbd_filter_create", C.byref(intr), B, 1000.0, 5.0, 0.005, 20, 2.0, C.byref(h))
+        handles.append(h)
+    streams = [torch.cuda.Stream() for _ in range(T)]
     from concurrent.futures import ThreadPoolExecutor
 
-    T = max(1, args.filter_streams)
-    streams = [torch.cuda.Stream() for _ in range(T)]
-
-    def buffers():
-        f64 = lambda: torch.empty((npx, 3), dtype=torch.float64, device="cuda")
-        return {"df": torch.empty((H, W), dtype=torch.float32, device="cuda"), "xyz": f64(), "rgb": f64(),
-                "vx": f64(), "vc": f64(), "out": f64(), "idx": torch.empty((npx,), dtype=torch.int64, device="cuda")}
-
-    bufs = []
-    for t in range(T):
-        with torch.cuda.stream(streams[t]):
-            bufs.append(buffers())
-
-    def frame(k, t):
-        f = k % nuniq
-        b, stream = bufs[t], C.c_void_p(streams[t].cuda_stream)
-        P, K, Kk = C.c_int64(0), C.c_int64(0), C.c_int64(0)
-        L.call("ot_depth_to_float", C.c_void_p(d16.data_ptr() + f * npx * 2), ptr(b["df"]), npx, 1000.0, 5.0, stream)
-        L.call("ot_unproject", ptr(b["df"]), C.c_void_p(col.data_ptr() + f * npx * 3), C.byref(intr),
-               exts[f].ctypes.data_as(C.c_void_p), 1, ptr(b["xyz"]), ptr(b["rgb"]), npx, C.byref(P), stream)
-        L.call("ot_voxel_down_sample", ptr(b["xyz"]), ptr(b["rgb"]), None, P.value, 0.005, ptr(b["vx"]), ptr(b["vc"]),
-               None, None, C.byref(K), stream)
-        L.call("ot_remove_statistical_outlier", ptr(b["vx"]), K.value, 20, 2.0, ptr(b["idx"]), None, C.byref(Kk),
-               stream)
-        L.call("ot_gather_rows3", ptr(b["vx"]), ptr(b["idx"]), Kk.value, ptr(b["out"]), stream)
-        return P.value, K.value, Kk.value
-
-    def worker(t, frames):
+    def worker(t, batches):
         tot = [0, 0, 0]
         with torch.cuda.stream(streams[t]):
-            for k in range(t, frames, T):
-                r = frame(k, t)
-                tot = [a + b for a, b in zip(tot, r)]
+            s_ = C.c_void_p(streams[t].cuda_stream)
+            for b in batches:
+                f0 = b * B
+                n = min(B, nf - f0)
+                L.call("ot_rgbd_filter_run", handles[t], n, C.c_void_p(d16.data_ptr() + f0 * npx * 2),
+                       C.c_void_p(col.data_ptr() + f0 * npx * 3), exts[f0:f0 + n].ctypes.data_as(C.c_void_p), s_)
+                P, K, KK = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+                L.call("ot_rgbd_filter_sizes", handles[t], C.byref(P), C.byref(K), C.byref(KK), None, None, None)
+                tot = [tot[0] + P.value, tot[1] + K.value, tot[2] + KK.value]
             streams[t].synchronize()
         return tot
 
     pool = ThreadPoolExecutor(max_workers=T)
-    for _ in pool.map(lambda t: worker(t, 4 * T), range(T)):
+    for _ in pool.map(lambda t: worker(t, [t % nb]), range(T)):  # warm-up: grows every handle's buffers
         pass
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     pts = vox = kept = 0
-    for p_, v_, k_ in pool.map(lambda t: worker(t, args.filter_frames), range(T)):
+    for p_, v_, k_ in pool.map(lambda t: worker(t, list(range(t, nb, T))), range(T)):
         pts, vox, kept = pts + p_, vox + v_, kept + k_
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     pool.shutdown()
-    # CPU oracle on 2 frames of the same stream
+    for h in handles:
+        L.call("ot_rgbd_filter_destroy", h)
+    del d16, col
+    torch.cuda.empty_cache()
+    # CPU oracle: the same chain on frames 0 and nf // 2 (1 warm-up pass, median of 5 timed passes)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
-    t1 = time.perf_counter()
-    cpu_pts = 0
-    for f in range(2):
-        dff = O.depth_to_float(depth[f], 1000.0, 5.0)
-        x, c = O.unproject(dff, color[f], intr_t, ext[f])
-        v, vcc, _, _ = O.voxel_down_sample(x, c, 0.005)
-        O.remove_statistical_outlier(v, 20, 2.0)
-        cpu_pts += x.shape[0]
-    cdt = time.perf_counter() - t1
+    sample = [0, nf // 2]
+
+    def cpu_pass():
+        n_pts = 0
+        for f in sample:
+            x, c = O.unproject(O.depth_to_float(depth[f], 1000.0, 5.0), color[f], intr_t, ext[f])
+            v = O.voxel_down_sample(x, c, 0.005)[0]
+            O.remove_statistical_outlier(v, 20, 2.0)
+            n_pts += x.shape[0]
+        return n_pts
+
+    cpu_pass()
+    times = []
+    for _ in range(5):
+        t1 = time.perf_counter()
+        cpu_pts = cpu_pass()
+        times.append(time.perf_counter() - t1)
+    cdt = float(np.median(times))
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    return {"workload": f"configs[2]: 1280x720 RGB-D stream ({T} concurrent streams), unproject + voxel_down_sample(0.005) + "
-                        "remove_statistical_outlier(20, 2.0) per frame",
-            "frames": args.filter_frames, "mpoints_per_s": round(pts / dt / 1e6, 2),
-            "frames_per_s": round(args.filter_frames / dt, 2), "ms_per_frame": round(dt * 1e3 / args.filter_frames, 3),
-            "points_per_frame": round(pts / args.filter_frames), "voxels_per_frame": round(vox / args.filter_frames),
-            "kept_per_frame": round(kept / args.filter_frames),
+    bytes_frame = 5.0 * W * H + 15.0 * kept / nf
+    return {"workload": f"configs[2]: {nf} distinct 1280x720 RGB-D frames, create_from_rgbd_image (depth_trunc 5 m) + "
+                        f"voxel_down_sample(0.005) + remove_statistical_outlier(20, 2.0) + select_by_index per frame; "
+                        f"batched device-resident chain, {B} frames per call, {T} calls in flight",
+            "frames": nf, "distinct_frames": nf, "batch": B, "streams": T,
+            "mpoints_per_s": round(pts / dt / 1e6, 2), "frames_per_s": round(nf / dt, 2),
+            "ms_per_frame": round(dt * 1e3 / nf, 4), "points_per_frame": round(pts / nf),
+            "voxels_per_frame": round(vox / nf), "kept_per_frame": round(kept / nf),
             # SURVEY 8(d) fused configs[2] pipeline bytes: 5*W*H (u16 depth + RGB8) + 15*K_kept per frame over the
-            # wall time; the chain is latency / VALU bound (host round trips, kNN selection), not HBM bound
+            # wall time (intermediates not counted; the chain is sort / kNN bound, DESIGN.md §4)
             "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                         "algorithmic_bytes_per_frame": round(5.0 * W * H + 15.0 * kept / args.filter_frames),
-                         "achieved": round((5.0 * W * H * args.filter_frames + 15.0 * kept) / dt / 1e9, 2),
-                         "frac": round((5.0 * W * H * args.filter_frames + 15.0 * kept) / dt / 1e9 / HBM_PEAK_GBS, 5)},
+                         "algorithmic_bytes_per_frame": round(bytes_frame),
+                         "achieved": round(bytes_frame * nf / dt / 1e9, 2),
+                         "frac": round(bytes_frame * nf / dt / 1e9 / HBM_PEAK_GBS, 5)},
             "cpu_baseline": {"mpoints_per_s": round(cpu_pts / cdt / 1e6, 3), "cores": cores, "kind": "port",
-                             "sample": "2 frames of the same stream, CPU oracle chain"}}
+                             "sample": f"frames {sample} of the same stream, CPU oracle chain, 1 warm-up + median of 5"}}
+
+
+def _traffic(args, L, kernel, config):
+    """Measured HBM bytes per launch of `kernel` from profiles/pmc_traffic.json -- only when the file was taken on
+    this build (source hash) and the same workload; else (None, reason)."""
+    try:
+        with open(args.traffic) as f:
+            tr = json.load(f)
+    except Exception:
+        return None, "no PMC file"
+    ent = tr.get("kernels_traffic", {}).get(kernel)
+    if not ent:
+        return None, f"no PMC entry for {kernel}"
+    if tr.get("source_hash") != L.source_hash():
+        return None, f"stale PMC file (source hash {tr.get('source_hash')} != {L.source_hash()})"
+    if any(tr.get("config", {}).get(k) != v for k, v in config.items()):
+        return None, f"PMC file workload {tr.get('config')} != {config}"
+    return ent["bytes_per_launch"], f"{os.path.relpath(args.traffic, ROOT)} (source hash {tr['source_hash']})"
 
 
 def cpu_baseline(depth, color, ext, intr_t, args):
-    """CPU oracle (kind "port") on the first --cpu-frames frames of the same scan."""
+    """CPU oracle (kind "port") on the first --cpu-frames frames of the same scan: 1 warm-up pass, then the median
+    of 5 timed passes (BASELINE.md / SURVEY 8(d) method), each into a fresh volume."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
     O.lib()
     n = min(args.cpu_frames, depth.shape[0])
     dfs = [O.depth_to_float(depth[k], 1000.0, 3.0) for k in range(n)]
-    vol = O.TSDF(args.voxel, args.sdf_trunc, 1, 4)
-    t0 = time.perf_counter()
-    for k in range(n):
-        vol.integrate(dfs[k], color[k], intr_t, ext[k])
-    dt = time.perf_counter() - t0
+
+    def one_pass():
+        vol = O.TSDF(args.voxel, args.sdf_trunc, 1, 4)
+        t0 = time.perf_counter()
+        for k in range(n):
+            vol.integrate(dfs[k], color[k], intr_t, ext[k])
+        return time.perf_counter() - t0
+
+    one_pass()
+    times = [one_pass() for _ in range(5)]
+    dt = float(np.median(times))
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     return {"value": round(n / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} of the {args.frames} frames, same synthetic scan, one fresh volume, "
-                      f"depth->float excluded (done before timing), OMP_NUM_THREADS={cores}",
-            "seconds": round(dt, 2)}
+            "sample": f"first {n} of the {args.frames} frames, same synthetic scan, one fresh volume per pass, "
+                      f"1 warm-up + median of 5 passes, depth->float excluded (done before timing), "
+                      f"OMP_NUM_THREADS={cores}",
+            "pass_seconds": [round(t, 3) for t in times]}
 
 
 if __name__ == "__main__":

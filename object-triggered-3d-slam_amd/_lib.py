@@ -167,3 +167,21 @@ def call(name, *args):
 def intrinsics_struct(intr) -> ot_intrinsics:
     return ot_intrinsics(int(intr.width), int(intr.height), float(intr.fx), float(intr.fy), float(intr.cx),
                          float(intr.cy))
+
+
+def source_hash() -> str:
+    """sha256 (16 hex) over the HIP sources, headers and Makefile the library is built from: tags measurements
+    (profiles/pmc_traffic.json) with the build they were taken on, independent of compiler output bytes."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(_HERE, "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h")) or f == "Makefile")
+    inc = os.path.join(os.path.dirname(_HERE), "include")
+    paths = [os.path.join(csrc, f) for f in files] + sorted(os.path.join(inc, f) for f in os.listdir(inc)
+                                                            if f.endswith(".h"))
+    for p in paths:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]

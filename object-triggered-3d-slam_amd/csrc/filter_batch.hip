@@ -44,7 +44,7 @@ struct FbParams {
     const uint8_t* color;   // [F][h][w][3]
     int w, h, tpf;          // tiles per frame
     float scale_f;
-    double trunc, fx, fy, cx, cy, vs;
+    double trunc, fx, fy, cx, cy, vs, inv_vs;
     FbFrame* frames;
     int F;
 };
@@ -65,6 +65,18 @@ __device__ inline bool fb_point(const FbParams& p, const double* m, float d, int
         xyz[k] = ((a + b) + cc) + m[k * 4 + 3];
     }
     return true;
+}
+
+// floor(fl(a / b)) (Open3D's voxel index) without the division when it cannot matter: q = fl(a * fl(1/b)) and
+// fl(a / b) both lie within 2^-52 (a/b) of a / b (a >= 0 here), so |q - fl(a/b)| < 2.3e-16 q; when q's distance to
+// the nearest integer exceeds 1e-15 q both floor the same, otherwise the exact quotient decides
+__device__ inline double floor_div(double a, double b, double inv_b) {
+    const double q = a * inv_b;
+    const double fq = floor(q);
+    const double fr = q - fq;  // exact (Sterbenz)
+    const double eps = 1e-15 * q;
+    if (fr > eps && fr < 1.0 - eps) return fq;
+    return floor(a / b);
 }
 
 // the lane's 8 depth values as Open3D's float image: f = (float)u16 / (float)scale; 0 when f >= trunc
@@ -147,7 +159,8 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_pixels(FbParams p, int* __res
     if (threadIdx.x == 0) tcount[t] = sc[0] + sc[1] + sc[2] + sc[3];
 }
 
-// blocks 0..F-1: frame bounds -> voxel origin, per-axis key widths (atomicMax into kbits), Open3D's size check;
+// blocks 0..F-1: frame bounds -> voxel origin, per-axis largest voxel index (atomicMax into kbits), Open3D's size
+// check;
 // block F: exclusive scan of the F * tpf tile counts in place (-> output offsets), totals[0] = P
 __global__ __launch_bounds__(256) void k_fb_setup(FbParams p, int* __restrict__ tcount,
                                                   const unsigned long long* __restrict__ tbounds,
@@ -214,16 +227,17 @@ __global__ __launch_bounds__(256) void k_fb_setup(FbParams p, int* __restrict__ 
             const double vmax = mxv + p.vs * 0.5;
             ext = fmax(ext, vmax - fr.vmin[a]);
             const long long kmax = (long long)floor((vmax - fr.vmin[a]) / p.vs);
-            int b = 1;
-            while (b < 62 && (kmax >> b) != 0) ++b;
-            atomicMax(&kbits[a], b);
+            atomicMax(&kbits[a], (int)(kmax < 0x3FFFFFFF ? kmax : 0x3FFFFFFF));  // voxels per axis - 1
         }
         if (p.vs * 2147483647.0 < ext) fr.err = 1;  // Open3D: "voxel_size is too small."
     }
 }
 
+// voxel key = frame << vbits | (kx * ny + ky) * nz + kz: mixed radix (lexicographic (kx, ky, kz) order) over the
+// batch's largest per-axis ranges, so the radix sort runs over as few bits as the extents need
 struct FbKeys {
-    int bx, by, bz;
+    unsigned long long ny, nz;
+    int vbits;
 };
 
 // the tile again: voxel keys of the valid pixels, emitted in pixel order at the tile's scanned offset
@@ -256,16 +270,16 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
     __syncthreads();
     int pos = toff[(int64_t)f * p.tpf + tile] + inc - c;
     for (int w = 0; w < wid; ++w) pos += wsum[w];
-    const unsigned long long fkey = (unsigned long long)f << (kb.bx + kb.by + kb.bz);
+    const unsigned long long fkey = (unsigned long long)f << kb.vbits;
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
         double xyz[3];
         if (pix0 + k < npx && fb_point(p, m, d[k], pix0 + k, xyz)) {
             long long kk[3];
 #pragma unroll
-            for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor((xyz[a] - vmin[a]) / p.vs);
-            keys[pos] = fkey | ((unsigned long long)kk[0] << (kb.by + kb.bz)) | ((unsigned long long)kk[1] << kb.bz) |
-                        (unsigned long long)kk[2];
+            for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
+            keys[pos] = fkey | (((unsigned long long)kk[0] * kb.ny + (unsigned long long)kk[1]) * kb.nz +
+                                (unsigned long long)kk[2]);
             vals[pos] = (unsigned)((int64_t)f * npx + pix0 + k);
             ++pos;
         }
@@ -288,19 +302,31 @@ __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* _
     const uint16_t* dep = p.depth + (int64_t)f * npx;
     const uint8_t* col = p.color + (int64_t)f * npx * 3;
     double sp[3] = {0, 0, 0}, sc[3] = {0, 0, 0};
-    for (int64_t j = beg; j < end; ++j) {
-        const int pix = (int)(sval[j] - (unsigned)f * (unsigned)npx);
-        float d = (float)dep[pix];
-        d = d / p.scale_f;  // valid by construction (d > 0, below trunc)
-        const uint8_t* cp = col + (int64_t)pix * 3;
-        const unsigned c0 = cp[0], c1 = cp[1], c2 = cp[2];
-        double xyz[3];
-        fb_point(p, m, d, pix, xyz);
+    // points in batches of 4: the batch's index, depth and colour loads are all issued before its in-order sums
+    constexpr int VB = 4;
+    for (int64_t j0 = beg; j0 < end; j0 += VB) {
+        int pix[VB];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) sp[a] += xyz[a];
-        sc[0] += (double)c0 / 255.0;
-        sc[1] += (double)c1 / 255.0;
-        sc[2] += (double)c2 / 255.0;
+        for (int k = 0; k < VB; ++k) pix[k] = (int)(sval[j0 + k < end ? j0 + k : j0] - (unsigned)f * (unsigned)npx);
+        float dd[VB];
+        unsigned cc[VB][3];
+#pragma unroll
+        for (int k = 0; k < VB; ++k) {
+            dd[k] = (float)dep[pix[k]];
+            const uint8_t* cp = col + (int64_t)pix[k] * 3;
+            cc[k][0] = cp[0], cc[k][1] = cp[1], cc[k][2] = cp[2];
+        }
+#pragma unroll
+        for (int k = 0; k < VB; ++k) {
+            if (j0 + k >= end) break;
+            double xyz[3];
+            fb_point(p, m, dd[k] / p.scale_f, pix[k], xyz);  // valid by construction (d > 0, below trunc)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) sp[a] += xyz[a];
+            sc[0] += (double)cc[k][0] / 255.0;
+            sc[1] += (double)cc[k][1] / 255.0;
+            sc[2] += (double)cc[k][2] / 255.0;
+        }
     }
     const double cnt = (double)(end - beg);
 #pragma unroll
@@ -491,6 +517,7 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     p.cx = fl->intr.cx;
     p.cy = fl->intr.cy;
     p.vs = vs;
+    p.inv_vs = 1.0 / vs;
     p.frames = d_frames;
     p.F = F;
     hipLaunchKernelGGL(k_fb_pixels, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, d_tc, d_tb);
@@ -516,11 +543,16 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     fl->P = P;
     fl->poff[F] = P;
     if (P == 0) return OT_OK;
-    FbKeys kb{std::max(hs.kbits[0], 1), std::max(hs.kbits[1], 1), std::max(hs.kbits[2], 1)};
+    const unsigned long long nx = (unsigned long long)hs.kbits[0] + 1, ny = (unsigned long long)hs.kbits[1] + 1,
+                             nz = (unsigned long long)hs.kbits[2] + 1;
     int fbits = 0;
     while ((1 << fbits) < F) ++fbits;
-    const int end_bit = kb.bx + kb.by + kb.bz + fbits;
-    if (end_bit > 64) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel grid exceeds 64-bit key packing");
+    const double cells = (double)nx * (double)ny * (double)nz;
+    int vbits = 1;
+    while (vbits < 64 && std::ldexp(1.0, vbits) < cells) ++vbits;
+    const int end_bit = vbits + fbits;
+    if (end_bit > 63) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel grid exceeds 64-bit key packing");
+    const FbKeys kb{ny, nz, vbits};
     // ---- voxel keys in point order, stable sort ------------------------------------------------------------
     unsigned long long* kin = (unsigned long long*)fl->b_keys.get((size_t)P * 16 + 256);
     unsigned* vin = (unsigned*)fl->b_vals.get((size_t)P * 8 + 256);
@@ -535,17 +567,16 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     int64_t K = 0;
     st = compact(P, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises (sync 2)
     if (st != OT_OK) return st;
+    hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned long long*)kout,
+                       (const int*)heads, K, vbits, F, d_voff);
     fl->K = K;
-    // ---- voxel averages, frame offsets of the voxel clouds --------------------------------------------------
+    // ---- voxel averages (frame-major, key order inside a frame) ----------------------------------------------
     double* vox = (double*)fl->b_vox.get((size_t)K * 48 + 256);
     if (!vox) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
     fl->vx = vox;
     fl->vc = vox + K * 3;
     hipLaunchKernelGGL(k_fb_reduce, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p, (const unsigned*)vout,
                        (const int*)heads, K, P, fl->vx, fl->vc);
-    const int fshift = kb.bx + kb.by + kb.bz;
-    hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned long long*)kout,
-                       (const int*)heads, K, fshift, F, d_voff);
     OT_LAUNCH_CHECK();
     std::vector<int> hvoff(F + 1);
     OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));
@@ -566,7 +597,7 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
         }
     OT_HIP_TRY(hipMemcpyAsync(d_org, horg.data(), sizeof(double) * 3 * F, hipMemcpyHostToDevice, stream));
     GridBuild gb;
-    st = build_grid_frames(fl->vx, K, F, d_voff, d_org, hcell, dims, true, stream, gb, 25);  // synchronises
+    st = build_grid_frames(fl->vx, K, F, d_voff, d_org, hcell, dims, SOR_WITH5, stream, gb, 25);  // synchronises
     if (st != OT_OK) return st;
     for (int f = 0; f <= F; ++f) fl->voff[f] = hvoff[f];
     double* avg = (double*)fl->b_avg.get((size_t)K * 8 + (size_t)F * 32 + 256);

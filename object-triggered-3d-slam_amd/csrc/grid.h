@@ -3,8 +3,10 @@
 // A cloud of n points grouped in F frames (frame f = point indices [foff[f], foff[f+1])) is binned into cubic cells
 // of size h anchored at a per-frame origin.  Keys pack (frame, x, y, z) with z in the low bits, so a frame's points
 // stay one contiguous range of the sorted order and cells (x', y', z-R .. z+R) of one frame are ONE contiguous range
-// whichever of them are occupied.  Per occupied cell the 3x3 (and optionally 5x5) z-column ranges of its block are
-// precomputed.  The grid only decides which candidates a query scans, never a result.
+// whichever of them are occupied.  The hash is over COLUMNS (frame, x, y) -> the column's run of occupied cells in
+// the sorted cell list, so any z-range of a column costs one probe plus a short scan of the column's cells.  Per
+// occupied cell the 3x3 (and optionally 5x5) column ranges of its block are precomputed.  The grid only decides
+// which candidates a query scans, never a result.
 #pragma once
 
 #include "common.h"
@@ -19,9 +21,16 @@ constexpr int NBR5 = 25;  // 5x5 columns, z-2 .. z+2
 #ifndef OT_SOR_R
 #define OT_SOR_R 1
 #endif
+#ifndef OT_SOR_OCC
+#define OT_SOR_OCC (OT_SOR_R == 1 ? 0.9 : 0.45)
+#endif
+#ifndef OT_SOR_NBR5
+#define OT_SOR_NBR5 0  // R = 1: precompute the 5x5 column ranges of every cell for stage 2 (default: probe on the fly)
+#endif
 constexpr int SOR_BLOCK_R = OT_SOR_R;
+constexpr bool SOR_WITH5 = OT_SOR_R == 2 || OT_SOR_NBR5;
 inline double sor_cell_target(int nb_neighbors) {
-    const double t = (SOR_BLOCK_R == 1 ? 0.7 : 0.25) * (double)nb_neighbors;
+    const double t = (OT_SOR_OCC) * (double)nb_neighbors;
     return t > 2.0 ? t : 2.0;
 }
 
@@ -31,9 +40,11 @@ struct GridDev {
     const int* pcell;          // sorted position -> cell (position in the sorted cell list)
     const int2* nbr3;          // per cell: NBR3 column ranges
     const int2* nbr5;          // per cell: NBR5 column ranges (nullptr unless built)
-    unsigned long long* hkeys; // cell hash: keys (KEY_EMPTY = free)
-    int2* hval;                // cell hash: [start, end) in the sorted order
+    unsigned long long* hkeys; // column hash: keys (cell key >> sy; KEY_EMPTY = free)
+    int2* hval;                // column hash: {first cell, number of cells} (cells sorted by z inside a column)
     int hash_mask;
+    int2* crange;              // per cell: [start, end) in the sorted order
+    int* cz;                   // per cell: z
     int dim[3];                // cells per axis (every frame's cells lie in [0, dim))
     int sy, sx, sf;            // key = f << sf | x << sx | y << sy | z
     const double* origin;      // [F][3] per-frame grid origins (device)
@@ -56,7 +67,7 @@ ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int
 // Statistical outlier removal over a built grid (Open3D RemoveStatisticalOutliers per frame):
 // avg[i] = mean kNN distance of point i (-1 when none); per frame the cloud mean and squared-deviation sum are
 // Open3D's sequential float64 accumulations (exact chains), stats[f] = {mean, std, valid, threshold}.
-// h_foff: host copy of the frame offsets.  Scratch slots slot0 .. slot0 + 1.  Does not synchronise.
+// h_foff: host copy of the frame offsets.  Scratch slots slot0 .. slot0 + 1.  Synchronises once (job table).
 ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_neighbors, double std_ratio,
                      double* avg, double* stats, hipStream_t stream, int slot0);
 

@@ -57,14 +57,37 @@ __device__ inline int2 grid_probe(const GridDev& g, unsigned long long key, unsi
     return make_int2(0, 0);
 }
 
-__device__ inline int2 grid_find(const GridDev& g, int f, int x, int y, int z) {
-    if (!cell_valid(g, x, y, z)) return make_int2(0, 0);
-    const unsigned long long key = cell_key(g, f, x, y, z);
+// the occupied cells of column (f, x, y): {first cell, count}
+__device__ inline int2 grid_column(const GridDev& g, int f, int x, int y) {
+    if (x < 0 || x >= g.dim[0] || y < 0 || y >= g.dim[1]) return make_int2(0, 0);
+    const unsigned long long key = cell_key(g, f, x, y, 0) >> g.sy;
     return grid_probe(g, key, (unsigned)mix64(key) & (unsigned)g.hash_mask);
 }
 
-__global__ __launch_bounds__(256) void k_cell_keys(const double* __restrict__ xyz, int64_t n, GridDev g,
-                                                   unsigned long long* keys, unsigned* idx, int* err) {
+// points of the column's cells with zlo <= z <= zhi: one contiguous range of the sorted order (or empty)
+__device__ inline int2 column_range(const GridDev& g, int2 col, int zlo, int zhi) {
+    int b = 0, e = 0;
+    bool any = false;
+    for (int i = 0; i < col.y; ++i) {
+        const int z = g.cz[col.x + i];
+        if (z > zhi) break;
+        if (z >= zlo) {
+            const int2 r = g.crange[col.x + i];
+            if (!any) b = r.x;
+            e = r.y;
+            any = true;
+        }
+    }
+    return any ? make_int2(b, e) : make_int2(0, 0);
+}
+
+__device__ inline int2 grid_find(const GridDev& g, int f, int x, int y, int z) {
+    return column_range(g, grid_column(g, f, x, y), z, z);
+}
+
+template <typename KeyT>
+__global__ __launch_bounds__(256) void k_cell_keys(const double* __restrict__ xyz, int64_t n, GridDev g, KeyT* keys,
+                                                   unsigned* idx, int* err) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, i) : 0;
@@ -74,11 +97,17 @@ __global__ __launch_bounds__(256) void k_cell_keys(const double* __restrict__ xy
     const int z = cell_coord(xyz[i * 3 + 2], o[2], g.h);
     const bool ok = cell_valid(g, x, y, z);
     if (!ok) *err = 1;
-    keys[i] = ok ? cell_key(g, f, x, y, z) : 0ull;
+    keys[i] = ok ? (KeyT)cell_key(g, f, x, y, z) : (KeyT)0;
     idx[i] = (unsigned)i;
 }
 
-// per occupied cell: hash insert of [start, end)
+__global__ __launch_bounds__(256) void k_widen_keys(const unsigned* __restrict__ in, int64_t n,
+                                                    unsigned long long* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+// per occupied cell: its range and z; a column's first cell also inserts the column (its run of cells) into the hash
 __global__ __launch_bounds__(256) void k_grid_insert(const unsigned long long* __restrict__ skeys,
                                                      const int* __restrict__ heads, int64_t ncells, int64_t n,
                                                      GridDev g) {
@@ -87,19 +116,25 @@ __global__ __launch_bounds__(256) void k_grid_insert(const unsigned long long* _
     const int beg = heads[c];
     const int end = (c + 1 < ncells) ? heads[c + 1] : (int)n;
     const unsigned long long key = skeys[beg];
-    unsigned slot = (unsigned)mix64(key) & (unsigned)g.hash_mask;
-    while (true) {  // capacity >= 2 * ncells: always terminates
-        const unsigned long long old = atomicCAS(&g.hkeys[slot], KEY_EMPTY, key);
+    g.crange[c] = make_int2(beg, end);
+    g.cz[c] = (int)(key & ((1ull << g.sy) - 1));
+    const unsigned long long col = key >> g.sy;
+    if (c > 0 && (skeys[heads[c - 1]] >> g.sy) == col) return;
+    int cnt = 1;
+    while (c + cnt < ncells && (skeys[heads[c + cnt]] >> g.sy) == col) ++cnt;
+    unsigned slot = (unsigned)mix64(col) & (unsigned)g.hash_mask;
+    while (true) {  // capacity >= 2 * ncells >= 2 * columns: always terminates
+        const unsigned long long old = atomicCAS(&g.hkeys[slot], KEY_EMPTY, col);
         if (old == KEY_EMPTY) {
-            g.hval[slot] = make_int2(beg, end);
+            g.hval[slot] = make_int2((int)c, cnt);
             return;
         }
         slot = (slot + 1) & (unsigned)g.hash_mask;
     }
 }
 
-// One lane per (cell, z-column of its (2R+1)^2 neighbourhood): 2R+1 hash lookups whose first probes are issued
-// together, merged into the column's range over z-R..z+R (and, R = 2, over z-1..z+1 for the inner 3x3 columns).
+// One lane per (cell, column of its (2R+1)^2 neighbourhood): one column probe, then the column's cells in
+// z-R..z+R (and, R = 2, z-1..z+1 for the inner 3x3 columns) as contiguous point ranges.
 template <int R>
 __global__ __launch_bounds__(256) void k_cell_nbr(const unsigned long long* __restrict__ skeys,
                                                   const int* __restrict__ heads, int64_t ncells, GridDev g,
@@ -115,40 +150,10 @@ __global__ __launch_bounds__(256) void k_cell_nbr(const unsigned long long* __re
     const int z = (int)(key & ((1ull << g.sy) - 1));
     const int y = (int)((key >> g.sy) & ((1ull << (g.sx - g.sy)) - 1)) + dy;
     const int x = (int)((key >> g.sx) & ((1ull << (g.sf - g.sx)) - 1)) + dx;
-    unsigned long long kq[W];
-    unsigned slot[W];
-    unsigned long long k0[W];
-    bool valid[W];
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        valid[i] = cell_valid(g, x, y, z + i - R);
-        kq[i] = valid[i] ? cell_key(g, f, x, y, z + i - R) : 0ull;
-        slot[i] = (unsigned)mix64(kq[i]) & (unsigned)g.hash_mask;
-    }
-#pragma unroll
-    for (int i = 0; i < W; ++i) k0[i] = valid[i] ? g.hkeys[slot[i]] : KEY_EMPTY;
-    int2 se[W];
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        se[i] = make_int2(0, 0);
-        if (valid[i] && k0[i] != KEY_EMPTY)
-            se[i] = (k0[i] == kq[i]) ? g.hval[slot[i]] : grid_probe(g, kq[i], (slot[i] + 1) & (unsigned)g.hash_mask);
-    }
-    int b5 = 0x7FFFFFFF, e5 = 0, b3 = 0x7FFFFFFF, e3 = 0;
-#pragma unroll
-    for (int i = 0; i < W; ++i)
-        if (se[i].y > se[i].x) {
-            b5 = min(b5, se[i].x);
-            e5 = max(e5, se[i].y);
-            if (i >= R - 1 && i <= R + 1) {
-                b3 = min(b3, se[i].x);
-                e3 = max(e3, se[i].y);
-            }
-        }
-    const int2 r5 = e5 > 0 ? make_int2(b5, e5) : make_int2(0, 0);
-    const int2 r3 = e3 > 0 ? make_int2(b3, e3) : make_int2(0, 0);
-    if (R == 2) nbr5[c * NBR5 + t] = r5;
-    if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1) nbr3[c * NBR3 + (dx + 1) * 3 + (dy + 1)] = r3;
+    const int2 col = grid_column(g, f, x, y);
+    if (R == 2) nbr5[c * NBR5 + t] = column_range(g, col, z - 2, z + 2);
+    if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1)
+        nbr3[c * NBR3 + (dx + 1) * 3 + (dy + 1)] = column_range(g, col, z - 1, z + 1);
 }
 
 __global__ __launch_bounds__(256) void k_gather_sorted(const double* __restrict__ xyz, const unsigned* __restrict__ sidx,
@@ -181,17 +186,29 @@ __global__ __launch_bounds__(256) void k_ror(GridDev g, int64_t n, double r2, in
 
 // ------------------------------------------------------------------------------------------------ SOR
 // Register top-k list, RIGHT-aligned ascending: best[KMAX-kk .. KMAX-1] hold the kk smallest squared distances
-// and best[0 .. KMAX-kk-1] = -inf.  Insertion is a branch-free min/max exchange chain, skipped for a whole wave
-// when no lane's candidate beats its current k-th distance best[KMAX-1]; lanes whose candidate does not enter
-// leave the list unchanged (their d is >= every entry).  NaN never enters (d < kth is false).
+// and best[0 .. KMAX-kk-1] = -inf.  Inserting d (< best[KMAX-1]) keeps the kk smallest of the list and d: entry i
+// becomes max(best[i-1], min(best[i], d)) -- i < p keeps best[i], i == p takes d, i > p takes best[i-1] for the
+// insertion position p -- so every entry is two independent min/max (no serial dependency through the list).
+// Skipped for a whole wave when no lane's candidate beats its k-th distance; NaN never enters (d < kth is false).
+// fmin / fmax in IEEE mode cost a v_max_f64 canonicalisation of each operand the compiler cannot prove canonical (the
+// loop-carried list): one extra instruction per min/max.  Every operand here is a product of arithmetic or of these
+// selections (canonical, never NaN), so the bare instructions give the same values.
+__device__ inline double dmin(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline double dmax(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 template <int KMAX>
 __device__ inline void topk_insert(double (&best)[KMAX], double d) {
 #pragma unroll
-    for (int i = 0; i < KMAX; ++i) {
-        const double lo = fmin(best[i], d);
-        d = fmax(best[i], d);
-        best[i] = lo;
-    }
+    for (int i = KMAX - 1; i > 0; --i) best[i] = dmax(best[i - 1], dmin(best[i], d));
+    best[0] = dmin(best[0], d);
 }
 
 // candidates [beg, end) of the sorted points, two per step with both rows loaded before either is tested
@@ -260,12 +277,49 @@ __constant__ unsigned char c_cols3[NBR3] = {4, 1, 3, 5, 7, 0, 2, 6, 8};
 __constant__ unsigned char c_cols5[NBR5] = {12, 7, 11, 13, 17, 6, 8, 16, 18, 2, 10, 14, 22,
                                             1, 3, 5, 9, 15, 19, 21, 23, 0, 4, 20, 24};
 
-// One lane per query (sorted order: a wave's queries share cells and candidate ranges).  Stage 1 scans the columns
-// of the query's (2R+1)^3 block nearest-first, skipping a column once the distance from q to it reaches the current
-// k-th distance; the k-th distance is final when it does not exceed the distance from q to the block's faces.  With
-// R = 1 an unsettled query completes the 5x5x5 block; then the rings continue.
+// Queries stage 1 could not settle, deferred to a second launch so that its waves are full of them (a wave runs a
+// stage for all its lanes when one lane needs it): sorted position, candidates counted, the top-k list (SoA).
+struct SorPend {
+    int* count;
+    int* j;
+    long long* have;
+    double* best;  // best[i * cap + slot]
+    int64_t cap;
+};
+
+template <int KMAX>
+__device__ inline double sor_mean(const double (&best)[KMAX], int kk) {
+    double s = 0.0;
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i)
+        if (i >= KMAX - kk && best[i] < INFINITY) {
+            s += sqrt(best[i]);
+            ++cnt;
+        }
+    return cnt > 0 ? s / (double)cnt : -1.0;
+}
+
+// distance from q to the near face of the column / cell at signed offset d (0: q's own), conservatively shrunk
+__device__ inline double face_gap(double lo, double hi, int d, double h) {
+    return d < 0 ? lo + (double)(-d - 1) * h : (d > 0 ? hi + (double)(d - 1) * h : 0.0);
+}
+__device__ inline void cell_fracs(const GridDev& g, const double q[3], const double* o, double lo[3], double hi[3]) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double uu = (q[a] - o[a]) / g.h;
+        const double fr = uu - floor(uu);
+        lo[a] = fmax(fr * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
+        hi[a] = fmax((1.0 - fr) * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
+    }
+}
+
+// Stage 1, one lane per query (sorted order: a wave's queries share cells and candidate ranges): the columns of the
+// query's (2R+1)^3 block nearest-first, a column skipped once its distance from q reaches the current k-th distance;
+// the k-th distance is final when it does not exceed the distance from q to the block's faces.  Unsettled queries
+// go to the pending list.
 template <int KMAX, int R>
-__global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, double* avg) {
+__global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, double* avg, SorPend pd) {
     constexpr int W = 2 * R + 1;
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= n) return;
@@ -278,60 +332,92 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     topk_reset<KMAX>(best, kk);
     const int c = g.pcell[j];
     const int2* rr = (R == 1 ? g.nbr3 + (int64_t)c * NBR3 : g.nbr5 + (int64_t)c * NBR5);
-    // distances from q to its cell's faces in x and y (conservatively shrunk): column (dx, dy) lies at least
-    // sqrt(ex^2 + ey^2) away, so once that reaches the current k-th distance none of its points can enter
-    double lo[2], hi[2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        const double uu = (q[a] - o[a]) / g.h;
-        const double fr = uu - floor(uu);
-        lo[a] = fmax(fr * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
-        hi[a] = fmax((1.0 - fr) * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
-    }
+    double lo[3], hi[3];
+    cell_fracs(g, q, o, lo, hi);
     long long have = 0;
     for (int u = 0; u < W * W; ++u) {
         const int t = R == 1 ? c_cols3[u] : c_cols5[u];
         const int dx = t / W - R, dy = t % W - R;
         const int2 se = rr[t];
-        const double ex = dx < 0 ? lo[0] + (double)(-dx - 1) * g.h : (dx > 0 ? hi[0] + (double)(dx - 1) * g.h : 0.0);
-        const double ey = dy < 0 ? lo[1] + (double)(-dy - 1) * g.h : (dy > 0 ? hi[1] + (double)(dy - 1) * g.h : 0.0);
+        const double ex = face_gap(lo[0], hi[0], dx, g.h), ey = face_gap(lo[1], hi[1], dy, g.h);
         if (!(ex * ex + ey * ey >= best[KMAX - 1])) scan_range<KMAX>(g.sxyz, q, se.x, se.y, best);
         have += se.y - se.x;
     }
-    double guard = block_guard(g, q, o, (double)R);
-    bool settled = have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard);
-    int rnext = R + 1;
-    if (!settled && R == 1 && g.nbr5) {  // complete the 5x5x5 block from the precomputed ranges
-        const int2* r5 = g.nbr5 + (int64_t)c * NBR5;
-        for (int t = 0; t < NBR5; ++t) {
-            const int dx = t / 5 - 2, dy = t % 5 - 2;
-            const int2 o5 = r5[t];
-            if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1) {
-                const int2 i3 = rr[(dx + 1) * 3 + (dy + 1)];
-                if (i3.y > i3.x) {  // the column's cells at z-2 and z+2 only
-                    scan_range<KMAX>(g.sxyz, q, o5.x, i3.x, best);
-                    scan_range<KMAX>(g.sxyz, q, i3.y, o5.y, best);
-                    have += (o5.y - o5.x) - (i3.y - i3.x);
-                    continue;
+    const double guard = block_guard(g, q, o, (double)R);
+    if (have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard)) {
+        avg[g.sidx[j]] = sor_mean<KMAX>(best, kk);
+        return;
+    }
+    const unsigned long long m = __ballot(1);  // the wave's unsettled lanes: one atomic per wave
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(pd.count, __popcll(m));
+    base = __shfl(base, leader);
+    const int slot = base + __popcll(m & ((1ull << lane_id()) - 1));
+    pd.j[slot] = (int)j;
+    pd.have[slot] = have;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) pd.best[(int64_t)i * pd.cap + slot] = best[i];
+}
+
+// Stage 2 for the pending queries (grid-stride over the device count): R = 1 completes the 5x5x5 block (the inner
+// columns' cells at z-2 / z+2 and the 16 outer columns, each skipped when provably too far), then Chebyshev rings.
+template <int KMAX, int R>
+__global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* avg, SorPend pd) {
+    const int cnt = *pd.count;
+    for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < cnt; s += (int64_t)gridDim.x * 256) {
+        const int64_t j = pd.j[s];
+        const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, j) : 0;
+        const int64_t fbeg = g.foff[f], fend = g.foff[f + 1];
+        const double* o = g.origin + 3 * f;
+        const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
+        const int kk = (int)((int64_t)k < fend - fbeg ? k : fend - fbeg);
+        double best[KMAX];
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) best[i] = pd.best[(int64_t)i * pd.cap + s];
+        long long have = pd.have[s];
+        bool settled = false;
+        int rnext = R + 1;
+        if (R == 1) {
+            const int c = g.pcell[j];
+            const int cx = cell_coord(q[0], o[0], g.h), cy = cell_coord(q[1], o[1], g.h), cz = g.cz[c];
+            double lo[3], hi[3];
+            cell_fracs(g, q, o, lo, hi);
+            const int2* r5 = g.nbr5 ? g.nbr5 + (int64_t)c * NBR5 : nullptr;
+            const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
+            for (int u = 0; u < NBR5; ++u) {
+                const int t = c_cols5[u];
+                const int dx = t / 5 - 2, dy = t % 5 - 2;
+                const bool inner = dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1;
+                const double ex = face_gap(lo[0], hi[0], dx, g.h), ey = face_gap(lo[1], hi[1], dy, g.h);
+                const double e2 = ex * ex + ey * ey;
+                int2 full, mid = make_int2(0, 0);
+                if (r5) {
+                    full = r5[t];
+                    if (inner) mid = r3[(dx + 1) * 3 + (dy + 1)];
+                } else {
+                    const int2 col = grid_column(g, f, cx + dx, cy + dy);
+                    full = column_range(g, col, cz - 2, cz + 2);
+                    if (inner) mid = column_range(g, col, cz - 1, cz + 1);
+                }
+                if (inner && mid.y > mid.x) {  // the column's cells at z-2 and z+2 only
+                    const double ez = face_gap(lo[2], hi[2], 2, g.h);  // both are >= one cell plus q's gap away
+                    const double ezl = face_gap(lo[2], hi[2], -2, g.h);
+                    if (!(e2 + ezl * ezl >= best[KMAX - 1])) scan_range<KMAX>(g.sxyz, q, full.x, mid.x, best);
+                    if (!(e2 + ez * ez >= best[KMAX - 1])) scan_range<KMAX>(g.sxyz, q, mid.y, full.y, best);
+                    have += (full.y - full.x) - (mid.y - mid.x);
+                } else {
+                    if (!(e2 >= best[KMAX - 1])) scan_range<KMAX>(g.sxyz, q, full.x, full.y, best);
+                    have += full.y - full.x;
                 }
             }
-            scan_range<KMAX>(g.sxyz, q, o5.x, o5.y, best);
-            have += o5.y - o5.x;
+            const double guard = block_guard(g, q, o, 2.0);
+            settled = have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard);
+            rnext = 3;
         }
-        guard = block_guard(g, q, o, 2.0);
-        settled = have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard);
-        rnext = 3;
+        if (!settled) sor_rings<KMAX>(g, q, o, f, rnext, fbeg, fend, kk, have, best);
+        avg[g.sidx[j]] = sor_mean<KMAX>(best, kk);
     }
-    if (!settled) sor_rings<KMAX>(g, q, o, f, rnext, fbeg, fend, kk, have, best);
-    double s = 0.0;
-    int cnt = 0;
-#pragma unroll
-    for (int i = 0; i < KMAX; ++i)
-        if (i >= KMAX - kk && best[i] < INFINITY) {
-            s += sqrt(best[i]);
-            ++cnt;
-        }
-    avg[g.sidx[j]] = cnt > 0 ? s / (double)cnt : -1.0;
 }
 
 // ------------------------------------------------------------------------------------ cross-cloud 1-NN distance
@@ -384,19 +470,19 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
             double guard = block_guard(g, q, g.origin, 1.0);
             settled = best <= guard * guard;
             if (!settled) {
-                const int2* r5 = g.nbr5 + (int64_t)c * NBR5;
+                const int czc = g.cz[c];
                 for (int t = 0; t < NBR5; ++t) {
                     const int dx = t / 5 - 2, dy = t % 5 - 2;
-                    const int2 o = r5[t];
+                    const int2 col = grid_column(g, 0, cx + dx, cy + dy);
+                    if (col.y == 0) continue;
                     if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1) {
-                        const int2 i3 = r3[(dx + 1) * 3 + (dy + 1)];
-                        if (i3.y > i3.x) {
-                            nn_range(g, q, o.x, i3.x, best);
-                            nn_range(g, q, i3.y, o.y, best);
-                            continue;
-                        }
+                        const int2 a = column_range(g, col, czc - 2, czc - 2), b = column_range(g, col, czc + 2, czc + 2);
+                        nn_range(g, q, a.x, a.y, best);
+                        nn_range(g, q, b.x, b.y, best);
+                    } else {
+                        const int2 r = column_range(g, col, czc - 2, czc + 2);
+                        nn_range(g, q, r.x, r.y, best);
                     }
-                    nn_range(g, q, o.x, o.y, best);
                 }
                 guard = block_guard(g, q, g.origin, 2.0);
                 settled = best <= guard * guard;
@@ -428,20 +514,22 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
 }
 
 // ---- cloud statistics per frame (RemoveStatisticalOutliers after the kNN loop) -----------------------------------
-// mode 0: x[i] = avg > 0 ? avg : 0 (the accumulate's lambda) and valid[f] += (avg has neighbours, i.e. avg >= 0)
+// mode 0: x[i] = avg > 0 ? avg : 0 (the accumulate's lambda) and the block's count of points with neighbours
+//         (avg >= 0: Open3D's valid_distances) -> vpart[f][block]
 // mode 1: x[i] = avg > 0 ? (avg - mean)^2 : 0 with mean = sum1[f] / valid[f] (the inner_product's op2)
-// grid (chunks, frames): a workgroup stays inside one frame, so the valid count is one exact integer atomic per block
+// grid (chunks, frames): a workgroup stays inside one frame
 __global__ __launch_bounds__(256) void k_sor_values(const double* __restrict__ avg, const int* __restrict__ foff,
                                                     int mode, const double* __restrict__ stats, double* __restrict__ x,
-                                                    unsigned long long* __restrict__ valid) {
+                                                    int* __restrict__ vpart) {
     const int f = blockIdx.y;
     const int64_t beg = foff[f], end = foff[f + 1];
     const int64_t i = beg + (int64_t)blockIdx.x * 256 + threadIdx.x;
-    double mean = 0.0;
-    if (mode == 1) {
-        const double v = stats[f * 4 + 2];
-        mean = stats[f * 4 + 0] / v;
+    if ((int64_t)blockIdx.x * 256 >= end - beg) {
+        if (mode == 0 && threadIdx.x == 0) vpart[(int64_t)f * gridDim.x + blockIdx.x] = 0;
+        return;
     }
+    double mean = 0.0;
+    if (mode == 1) mean = stats[f * 4 + 0] / stats[f * 4 + 2];
     int c = 0;
     if (i < end) {
         const double a = avg[i];
@@ -452,37 +540,44 @@ __global__ __launch_bounds__(256) void k_sor_values(const double* __restrict__ a
             x[i] = a > 0 ? (a - mean) * (a - mean) : 0.0;
         }
     }
-    if (mode == 0 && (int64_t)blockIdx.x * 256 < end - beg) {
+    if (mode == 0) {
         c = wave_sum(c);
         __shared__ int ws[4];
         if (lane_id() == 0) ws[threadIdx.x >> 6] = c;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const int t = ws[0] + ws[1] + ws[2] + ws[3];
-            if (t) atomicAdd(&valid[f], (unsigned long long)t);
-        }
+        if (threadIdx.x == 0) vpart[(int64_t)f * gridDim.x + blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
     }
 }
 
-// stats[f] = {cloud_mean (sum until mode 1), std, valid, threshold} (Bessel-corrected std)
-__global__ void k_sor_stats(int nframes, int mode, const double* __restrict__ sums,
-                            const unsigned long long* __restrict__ valid, double std_ratio, double* __restrict__ stats) {
+// one workgroup per frame: valid = sum of the block counts; stats[f] = {sum (mean after mode 1), -, valid, -}
+__global__ __launch_bounds__(256) void k_sor_valid(const int* __restrict__ vpart, int nblocks,
+                                                   const double* __restrict__ sums, double* __restrict__ stats) {
+    const int f = blockIdx.x;
+    long long c = 0;
+    for (int b = threadIdx.x; b < nblocks; b += 256) c += vpart[(int64_t)f * nblocks + b];
+    c = wave_sum(c);
+    __shared__ long long ws[4];
+    if (lane_id() == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        stats[f * 4 + 0] = sums[f];  // the sum; mode 1 divides it by valid exactly as cloud_mean /= valid
+        stats[f * 4 + 2] = (double)(ws[0] + ws[1] + ws[2] + ws[3]);
+    }
+}
+
+// stats[f] = {cloud_mean, std, valid, threshold} (Bessel-corrected std)
+__global__ void k_sor_stats(int nframes, const double* __restrict__ sums, double std_ratio, double* __restrict__ stats) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
-    if (mode == 0) {
-        stats[f * 4 + 0] = sums[f];  // the sum; k_sor_values divides it by valid exactly as cloud_mean /= valid
-        stats[f * 4 + 2] = (double)valid[f];
-        return;
-    }
-    const unsigned long long v = valid[f];
-    if (v == 0) {  // Open3D returns an empty cloud
+    const double v = stats[f * 4 + 2];
+    if (v == 0.0) {  // Open3D returns an empty cloud
         stats[f * 4 + 0] = 0.0;
         stats[f * 4 + 1] = 0.0;
         stats[f * 4 + 3] = -INFINITY;
         return;
     }
-    const double mean = stats[f * 4 + 0] / (double)v;
-    const double sd = sqrt(sums[f] / (double)(v - 1));
+    const double mean = stats[f * 4 + 0] / v;
+    const double sd = sqrt(sums[f] / (v - 1.0));  // valid - 1 exactly (valid < 2^53)
     stats[f * 4 + 0] = mean;
     stats[f * 4 + 1] = sd;
     stats[f * 4 + 3] = mean + std_ratio * sd;
@@ -534,10 +629,24 @@ ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int
     int* pcell = heads + n;
     double* sxyz = (double*)(((uintptr_t)(pcell + n) + 15) & ~(uintptr_t)15);
     OT_HIP_TRY(hipMemsetAsync(err, 0, sizeof(int), stream));
-    hipLaunchKernelGGL(k_cell_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, xyz, n, g, kin, vin, err);
-    OT_LAUNCH_CHECK();
-    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, std::max(end_bit, 1), stream, 3);
-    if (st != OT_OK) return st;
+    ot_status st;
+    if (end_bit <= 32 && n > (int64_t)(1 << 21)) {  // large sorts on 32-bit keys: 8 B per pair per pass, not 12
+        unsigned* k32 = (unsigned*)kin;
+        unsigned* k32o = k32 + n;
+        hipLaunchKernelGGL(k_cell_keys<unsigned>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, xyz, n, g,
+                           k32, vin, err);
+        OT_LAUNCH_CHECK();
+        st = sort_pairs_u32_u32(k32, k32o, vin, vout, (size_t)n, std::max(end_bit, 1), stream, 3);
+        if (st != OT_OK) return st;
+        hipLaunchKernelGGL(k_widen_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const unsigned*)k32o,
+                           n, kout);
+    } else {
+        hipLaunchKernelGGL(k_cell_keys<unsigned long long>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                           xyz, n, g, kin, vin, err);
+        OT_LAUNCH_CHECK();
+        st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)n, std::max(end_bit, 1), stream, 3);
+        if (st != OT_OK) return st;
+    }
     int64_t ncells = 0;
     st = compact_segments(n, kout, heads, pcell, stream, &ncells, slot0 + 1);  // synchronises
     if (st != OT_OK) return st;
@@ -547,16 +656,19 @@ ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int
     if (e) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (non-finite point coordinates)");
     int64_t cap = 1;
     while (cap < 2 * ncells + 2) cap <<= 1;
-    char* hs = (char*)scratch((size_t)cap * (8 + 8) + (size_t)ncells * (NBR3 + (with5 ? NBR5 : 0)) * 8 + 64, slot0 + 2);
+    char* hs = (char*)scratch((size_t)cap * (8 + 8) + (size_t)ncells * ((NBR3 + (with5 ? NBR5 : 0)) * 8 + 12) + 128,
+                              slot0 + 2);
     if (!hs) return fail(OT_ERR_HIP, "scratch allocation failed");
     g.hkeys = (unsigned long long*)hs;
     g.hval = (int2*)(g.hkeys + cap);
     int2* nbr3 = g.hval + cap;
     int2* nbr5 = with5 ? nbr3 + ncells * NBR3 : nullptr;
+    g.crange = (with5 ? nbr5 + ncells * NBR5 : nbr3 + ncells * NBR3);
+    g.cz = (int*)(g.crange + ncells);
     g.hash_mask = (int)(cap - 1);
     OT_HIP_TRY(hipMemsetAsync(g.hkeys, 0xFF, sizeof(unsigned long long) * cap, stream));
     hipLaunchKernelGGL(k_grid_insert, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, stream, kout, heads,
-                       ncells, n, g);
+                       ncells, n, g);  // cell ranges / z and the column hash, read by k_cell_nbr
     if (with5)
         hipLaunchKernelGGL(k_cell_nbr<2>, dim3((unsigned)((ncells * NBR5 + 255) / 256)), dim3(256), 0, stream, kout,
                            heads, ncells, g, nbr3, nbr5);
@@ -581,8 +693,26 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
     for (int f = 0; f < F; ++f) max_n = std::max<int64_t>(max_n, h_foff[f + 1] - h_foff[f]);
     const unsigned grid = (unsigned)((n + 255) / 256);
     const int kk = (int)std::min<int64_t>(nb_neighbors, std::max<int64_t>(max_n, 1));  // list length actually needed
-#define OT_SOR_LAUNCH(KM) \
-    hipLaunchKernelGGL((k_sor_knn<KM, SOR_BLOCK_R>), dim3(grid), dim3(256), 0, stream, gb.g, n, (int)nb_neighbors, avg)
+    // pending list of stage-1 misses (device count; capacity n)
+    const int km = kk <= 4 ? 4 : kk <= 8 ? 8 : kk <= 12 ? 12 : kk <= 16 ? 16 : kk <= 20 ? 20 : kk <= 24 ? 24
+                 : kk <= 32 ? 32 : kk <= 48 ? 48 : 64;
+    char* pw = (char*)scratch((size_t)n * (4 + 8 + 8 * (size_t)km) + 512, slot0 + 1);
+    if (!pw) return fail(OT_ERR_HIP, "scratch allocation failed");
+    SorPend pd;
+    pd.count = (int*)pw;
+    pd.j = (int*)(pw + 256);
+    pd.have = (long long*)(((uintptr_t)(pd.j + n) + 15) & ~(uintptr_t)15);
+    pd.best = (double*)(pd.have + n);
+    pd.cap = n;
+    OT_HIP_TRY(hipMemsetAsync(pd.count, 0, sizeof(int), stream));
+    const unsigned rgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid / 4, 1), 2048);
+#define OT_SOR_LAUNCH(KM)                                                                                           \
+    do {                                                                                                            \
+        hipLaunchKernelGGL((k_sor_knn<KM, SOR_BLOCK_R>), dim3(grid), dim3(256), 0, stream, gb.g, n,                 \
+                           (int)nb_neighbors, avg, pd);                                                             \
+        hipLaunchKernelGGL((k_sor_knn_rest<KM, SOR_BLOCK_R>), dim3(rgrid), dim3(256), 0, stream, gb.g,              \
+                           (int)nb_neighbors, avg, pd);                                                             \
+    } while (0)
     if (kk <= 4) OT_SOR_LAUNCH(4);
     else if (kk <= 8) OT_SOR_LAUNCH(8);
     else if (kk <= 12) OT_SOR_LAUNCH(12);
@@ -595,15 +725,16 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
 #undef OT_SOR_LAUNCH
     OT_LAUNCH_CHECK();
     // the two sequential float64 sums per frame (exact chains): x values, chain jobs, valid counts, sums
+    const int nvb = (int)std::max<int64_t>((max_n + 255) / 256, 1);
     size_t aux = 0;
     for (int f = 0; f < F; ++f) aux += chain_aux_bytes(h_foff[f + 1] - h_foff[f]);
-    const size_t bytes = (size_t)n * 8 + 256 + aux + (sizeof(ChainJob) + 32) * (size_t)F + 256;
+    const size_t bytes = (size_t)n * 8 + 256 + aux + (sizeof(ChainJob) + 32) * (size_t)F + (size_t)F * nvb * 4 + 512;
     char* ws = (char*)scratch(bytes, slot0);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
     double* x = (double*)ws;
-    unsigned long long* valid = (unsigned long long*)(((uintptr_t)(x + n) + 63) & ~(uintptr_t)63);
-    double* sums = (double*)(valid + F);
-    char* cur = (char*)(((uintptr_t)(sums + F) + 63) & ~(uintptr_t)63);
+    double* sums = (double*)(((uintptr_t)(x + n) + 63) & ~(uintptr_t)63);
+    int* vpart = (int*)(sums + F);
+    char* cur = (char*)(((uintptr_t)(vpart + (size_t)F * nvb) + 63) & ~(uintptr_t)63);
     std::vector<ChainJob> jobs((size_t)F);
     for (int f = 0; f < F; ++f) {
         ChainJob& jb = jobs[f];
@@ -614,19 +745,16 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
     }
     ChainJob* djobs = (ChainJob*)cur;
     OT_HIP_TRY(hipMemcpyAsync(djobs, jobs.data(), sizeof(ChainJob) * F, hipMemcpyHostToDevice, stream));
-    OT_HIP_TRY(hipMemsetAsync(valid, 0, sizeof(unsigned long long) * F, stream));
-    const dim3 vgrid((unsigned)std::max<int64_t>((max_n + 255) / 256, 1), (unsigned)F);
+    const dim3 vgrid((unsigned)nvb, (unsigned)F);
     hipLaunchKernelGGL(k_sor_values, vgrid, dim3(256), 0, stream, (const double*)avg, gb.g.foff, 0,
-                       (const double*)stats, x, valid);
+                       (const double*)stats, x, vpart);
     launch_sum_chains(djobs, F, max_n, stream);
-    const unsigned sgrid = (unsigned)((F + 63) / 64);
-    hipLaunchKernelGGL(k_sor_stats, dim3(sgrid), dim3(64), 0, stream, F, 0, (const double*)sums,
-                       (const unsigned long long*)valid, std_ratio, stats);
+    hipLaunchKernelGGL(k_sor_valid, dim3(F), dim3(256), 0, stream, (const int*)vpart, nvb, (const double*)sums, stats);
     hipLaunchKernelGGL(k_sor_values, vgrid, dim3(256), 0, stream, (const double*)avg, gb.g.foff, 1,
-                       (const double*)stats, x, valid);
+                       (const double*)stats, x, vpart);
     launch_sum_chains(djobs, F, max_n, stream);
-    hipLaunchKernelGGL(k_sor_stats, dim3(sgrid), dim3(64), 0, stream, F, 1, (const double*)sums,
-                       (const unsigned long long*)valid, std_ratio, stats);
+    hipLaunchKernelGGL(k_sor_stats, dim3((unsigned)((F + 63) / 64)), dim3(64), 0, stream, F, (const double*)sums,
+                       std_ratio, stats);
     OT_LAUNCH_CHECK();
     // the host job table is consumed by the copy above before the caller's next synchronisation point returns
     OT_HIP_TRY(hipStreamSynchronize(stream));
@@ -727,12 +855,12 @@ ot_status ot_remove_statistical_outlier(const double* xyz, int64_t n, int32_t nb
     const double hmin = ext[2] / 5.0e5;
     double h = std::max(std::sqrt(0.5 * ext[2] * ext[1] * target / (double)n), hmin);
     GridBuild gb;
-    st = single_frame_grid(xyz, n, h, mn, mx, true, stream, gb);
+    st = single_frame_grid(xyz, n, h, mn, mx, SOR_WITH5, stream, gb);
     if (st != OT_OK) return st;
     const double occ = (double)n / (double)std::max<int64_t>(gb.ncells, 1);
     if (occ > 2.5 * target || occ < 0.4 * target) {
         h = std::max(h * std::sqrt(target / occ), hmin);
-        st = single_frame_grid(xyz, n, h, mn, mx, true, stream, gb);
+        st = single_frame_grid(xyz, n, h, mn, mx, SOR_WITH5, stream, gb);
         if (st != OT_OK) return st;
     }
     char* ws = (char*)scratch((size_t)n * 8 + 256, 12);
@@ -740,7 +868,7 @@ ot_status ot_remove_statistical_outlier(const double* xyz, int64_t n, int32_t nb
     double* stats = (double*)ws;  // [mean, std, valid, threshold]
     double* avg = out_avg_dist ? out_avg_dist : (double*)(ws + 256);
     const int foff[2] = {0, (int)n};
-    st = sor_frames(gb, n, foff, nb_neighbors, std_ratio, avg, stats, stream, 21);
+    st = sor_frames(gb, n, foff, nb_neighbors, std_ratio, avg, stats, stream, 41);
     if (st != OT_OK) return st;
     return compact(n, SorKeep{avg, stats, gb.g.foff, 1}, IndexEmit{out_indices}, stream, n_kept_host, 13);
 }
@@ -768,12 +896,12 @@ ot_status ot_compute_point_cloud_distance(const double* src, int64_t n, const do
     const double hmin = ext[2] / 5.0e5;
     double h = std::max(std::sqrt(0.5 * ext[2] * ext[1] * target / (double)m), hmin);
     GridBuild gb;
-    st = single_frame_grid(tgt, m, h, mn, mx, true, stream, gb);
+    st = single_frame_grid(tgt, m, h, mn, mx, false, stream, gb);
     if (st != OT_OK) return st;
     const double occ = (double)m / (double)std::max<int64_t>(gb.ncells, 1);
     if (occ > 2.5 * target || occ < 0.4 * target) {
         h = std::max(h * std::sqrt(target / occ), hmin);
-        st = single_frame_grid(tgt, m, h, mn, mx, true, stream, gb);
+        st = single_frame_grid(tgt, m, h, mn, mx, false, stream, gb);
         if (st != OT_OK) return st;
     }
     hipLaunchKernelGGL(k_nn_dist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, gb.g, src, n, m, mn[0],

@@ -15,6 +15,16 @@ namespace ot {
 // below 2^20 items, ~10 launches per sort independent of how few key bits are in use.
 using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                               rocprim::default_config, 0>;
+// large (u64 key, u32 value) sorts: 8-bit digits with a 256-thread histogram kernel (measured: 10-bit digits, 4 passes
+// instead of 5 for a 33-bit key, are slower; 11 bits do not fit the onesweep histograms of a 64-bit key in LDS)
+#ifndef OT_SORT_BITS
+#define OT_SORT_BITS 8
+#endif
+using BigSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 16>, rocprim::kernel_config<512, 16>, OT_SORT_BITS,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
 
 // ------------------------------------------------------------------------------------------------------------
 // Own stable LSD radix sort (8-bit digits), P + 2 launches for P passes:
@@ -261,12 +271,25 @@ ot_status sort_pairs_u64_u32(const unsigned long long* kin, unsigned long long* 
 #endif
     {
     size_t tmp = 0;
+    OT_HIP_TRY(rocprim::radix_sort_pairs<BigSortConfig>(nullptr, tmp, kin, kout, vin, vout, n, 0u, (unsigned)end_bit,
+                                                        stream));
+    void* ws = scratch(tmp + 16, scratch_slot);
+    if (!ws) return fail(OT_ERR_HIP, "sort scratch allocation failed");
+    OT_HIP_TRY(rocprim::radix_sort_pairs<BigSortConfig>(ws, tmp, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, stream));
+    return OT_OK;
+    }
+}
+
+ot_status sort_pairs_u32_u32(const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout, size_t n,
+                             int end_bit, hipStream_t stream, int scratch_slot) {
+    if (n == 0) return OT_OK;
+    if (end_bit < 1) end_bit = 1;
+    size_t tmp = 0;
     OT_HIP_TRY(rocprim::radix_sort_pairs<SortConfig>(nullptr, tmp, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, stream));
     void* ws = scratch(tmp + 16, scratch_slot);
     if (!ws) return fail(OT_ERR_HIP, "sort scratch allocation failed");
     OT_HIP_TRY(rocprim::radix_sort_pairs<SortConfig>(ws, tmp, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, stream));
     return OT_OK;
-    }
 }
 
 }  // namespace ot

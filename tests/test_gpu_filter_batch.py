@@ -104,6 +104,25 @@ def test_batch_matches_per_call_ragged(pkg, O, synth, gpu):
     assert flt.n_frames == 2 and flt.kept_offsets[2] == flt.kept
 
 
+def test_batch_wide_keys_match_per_call(pkg, synth, gpu):
+    """A 0.4 mm voxel makes the voxel key wider than 32 bits: the batch takes its 64-bit-key path (frame in the
+    key) and must still equal the per-frame calls."""
+    intr_t = synth.REF_INTRINSICS_640
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=16, frames=[2, 11])
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    flt = pkg.filters.RGBDFilterBatch(intr, max_frames=2, depth_trunc=5.0, voxel_size=0.0004).run(depth, color, ext)
+    for f in range(2):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[f]), pkg.geometry.Image(depth[f]), depth_scale=1000.0, depth_trunc=5.0,
+            convert_rgb_to_intensity=False)
+        down = pkg.geometry.PointCloud.create_from_rgbd_image(rgbd, intr, ext[f]).voxel_down_sample(0.0004)
+        kept, ind = down.remove_statistical_outlier(20, 2.0)
+        bdown, _ = flt.voxel_cloud(f)
+        bkept, bind = flt.frame(f)
+        assert_bitwise(np.asarray(bdown.points), np.asarray(down.points), f"wide-key voxels (frame {f})")
+        assert bind == ind, f"wide-key kept indices (frame {f})"
+
+
 def test_batch_errors(pkg, synth, gpu):
     intr = pkg.camera.PinholeCameraIntrinsic(*synth.REF_INTRINSICS_640)
     with pytest.raises(RuntimeError, match="voxel_size"):
