@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
     ap.add_argument("--cpu-frames", type=int, default=32, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--sustain", type=float, default=1.5, help="seconds of sustained headline steps (0 = skip)")
+    ap.add_argument("--color64", type=int, default=1, help="also time the headline at float64 colour precision")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--calib", action="store_true", help="after timing, run export_units once (PMC calibration)")
     ap.add_argument("--filter-frames", type=int, default=512,
@@ -131,7 +132,7 @@ def main():
     pintr = C.byref(intr)
 
     def step():
-        L.call("ot_tsdf_reset", vol)
+        L.call("ot_tsdf_reset_async", vol, stream)  # stream-ordered: no device-wide synchronisation per step
         for k in range(args.frames):
             st = integrate(vol, dptrs[k], cptrs[k], pintr, eptrs[k], 1000.0, 3.0, stream)
             if st:
@@ -172,9 +173,9 @@ def main():
 
     # ---- per-step accounting: exact voxel updates (U_f summed over frames) ----
     upd, unit_int = C.c_int64(0), C.c_int64(0)
-    L.call("ot_tsdf_counters", vol, C.byref(upd), C.byref(unit_int))
+    L.call("ot_tsdf_counters", vol, C.byref(upd), C.byref(unit_int), stream)
     n_units = C.c_int64(0)
-    L.call("ot_tsdf_num_units", vol, C.byref(n_units))
+    L.call("ot_tsdf_num_units", vol, C.byref(n_units), stream)
 
     # ---- roofline: one extra (untimed) step with HIP events around every dominant-kernel launch ----
     L.call("ot_tsdf_set_profiling", vol, 1)
@@ -207,8 +208,11 @@ def main():
     if args.calib:  # a kernel with a known read byte count and the integrate kernel's pool access pattern
         nu = n_units.value
         bufs = [torch.empty((nu, 4096, k), dtype=torch.float32, device="cuda") for k in (1, 1, 3)]
-        L.call("ot_tsdf_export_units", vol, None, *[C.c_void_p(b.data_ptr()) for b in bufs], stream)
+        L.call("ot_tsdf_export_units", vol, nu, None, *[C.c_void_p(b.data_ptr()) for b in bufs], stream)
         torch.cuda.synchronize()
+
+    color64 = headline_color64(args, L, lib, torch, dist, world, d_depth, d_color, ext, intr, stream, upd.value) \
+        if args.color64 else None
 
     order = os.environ.get("OT_BENCH_ORDER", "filtered,objects").split(",")  # leg-order check
     filt = objects = None
@@ -236,7 +240,8 @@ def main():
                       "frames_per_step": args.frames, "width": W, "height": H, "voxel_length": args.voxel,
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
-           "roofline": roofline, "cpu_baseline": cpu, "sustained": sustained, "filtered": filt, "objects": objects,
+           "roofline": roofline, "cpu_baseline": cpu, "sustained": sustained, "color64": color64,
+           "filtered": filt, "objects": objects,
            "hybrid_map": hybrid, "single_frame": single, "spatial": spatial, "source_hash": L.source_hash()}
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -244,6 +249,46 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def headline_color64(args, L, lib, torch, dist, world, d_depth, d_color, ext, intr, stream, updates_f32):
+    """The configs[1] workload with the voxel colour state at Open3D's precision (float64, exact division:
+    ot_tsdf_set_color_precision(64), bit-exact colours) -- what reference precision costs next to the float32
+    headline.  Same frames, same timing method (K steps between barrier + synchronize, max over ranks)."""
+    vol = C.c_void_p()
+    L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
+    L.call("ot_tsdf_set_color_precision", vol, 64)
+    if args.batch > 0:
+        L.call("ot_tsdf_set_batch", vol, args.batch)
+    W, H = intr.width, intr.height
+    npx = W * H
+    integrate, pintr = lib.ot_tsdf_integrate_u16, C.byref(intr)
+    dptrs = [C.c_void_p(d_depth.data_ptr() + k * npx * 2) for k in range(args.frames)]
+    cptrs = [C.c_void_p(d_color.data_ptr() + k * npx * 3) for k in range(args.frames)]
+    eptrs = [ext[k].ctypes.data_as(C.c_void_p) for k in range(args.frames)]
+
+    def step():
+        L.call("ot_tsdf_reset_async", vol, stream)
+        for k in range(args.frames):
+            if integrate(vol, dptrs[k], cptrs[k], pintr, eptrs[k], 1000.0, 3.0, stream):
+                raise RuntimeError(lib.ot_last_error().decode())
+        L.call("ot_tsdf_flush", vol, stream)
+
+    for _ in range(2):
+        step()
+    steps = max(1, min(args.steps, 50))
+    dt, _ = _timed(torch, dist, world, step, steps)
+    upd = C.c_int64(0)
+    L.call("ot_tsdf_counters", vol, C.byref(upd), None, stream)
+    L.call("ot_tsdf_set_profiling", vol, 1)
+    step()
+    kms, kl = C.c_double(0.0), C.c_int64(0)
+    L.call("ot_tsdf_kernel_time", vol, C.byref(kms), C.byref(kl))
+    L.call("ot_tsdf_destroy", vol)
+    return {"workload": "configs[1] with colour precision 64 (float64 running colour mean, exact division: Open3D's "
+                        "TSDFVoxel::color_)", "steps": steps, "frames_per_s": round(world * args.frames / dt, 1),
+            "ms_per_step": round(dt * 1e3, 3), "kernel_ms_avg": round(kms.value / max(kl.value, 1), 5),
+            "voxel_updates_match_f32": upd.value == updates_f32}
 
 
 def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
@@ -276,7 +321,7 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
     integrate, pintr = lib.ot_tsdf_integrate_u16, C.byref(intr)
 
     def step():
-        L.call("ot_tsdf_reset", vol)
+        L.call("ot_tsdf_reset_async", vol, stream)
         for k in range(args.frames):
             if integrate(vol, dptrs[k], cptrs[k], pintr, eptrs[k], 1000.0, 3.0, stream):
                 raise RuntimeError(lib.ot_last_error().decode())
@@ -284,14 +329,14 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
 
     dt, _ = _timed(torch, dist, world, step, args.steps)
     nu = C.c_int64(0)
-    L.call("ot_tsdf_num_units", vol, C.byref(nu))
+    L.call("ot_tsdf_num_units", vol, C.byref(nu), stream)
     cnt = Dm.all_gather_rows(torch.tensor([[nu.value]], dtype=torch.int64, device=COLL_DEV)).flatten().tolist()
 
     def assemble():
         n = nu.value
         keys = torch.empty((n, 3), dtype=torch.int32, device="cuda")
         f = [torch.empty((n, 4096, k), dtype=torch.float32, device="cuda") for k in (1, 1, 3)]
-        L.call("ot_tsdf_export_units", vol, C.c_void_p(keys.data_ptr()), *[C.c_void_p(t.data_ptr()) for t in f],
+        L.call("ot_tsdf_export_units", vol, n, C.c_void_p(keys.data_ptr()), *[C.c_void_p(t.data_ptr()) for t in f],
                stream)
         rows = Dm.pack_units(keys, *f)
         rows = Dm.all_gather_rows(rows if COLL_DEV == "cuda" else rows.cpu())
@@ -303,7 +348,7 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
         L.call("ot_tsdf_import_units", merged, rows.shape[0], C.c_void_p(k2.data_ptr()), C.c_void_p(t2.data_ptr()),
                C.c_void_p(w2.data_ptr()), C.c_void_p(c2.data_ptr()), stream)
         total = C.c_int64(0)
-        L.call("ot_tsdf_num_units", merged, C.byref(total))
+        L.call("ot_tsdf_num_units", merged, C.byref(total), stream)
         L.call("ot_tsdf_destroy", merged)
         return total.value
 

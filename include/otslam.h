@@ -178,10 +178,16 @@ ot_status ot_tsdf_flush(ot_tsdf* vol, void* stream);
 /* Batch size used by ot_tsdf_integrate_u16 (1 = integrate immediately, default 32). */
 ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames);
 
-/* Number of allocated volume units (synchronises). */
-ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n_units_host);
-/* Cumulative voxel updates and volume-unit integrations since create/reset (synchronises). */
-ot_status ot_tsdf_counters(ot_tsdf* vol, int64_t* voxel_updates_host, int64_t* unit_integrations_host);
+/* Number of allocated volume units.  Queued frames are integrated first, on `stream`; synchronises `stream`. */
+ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n_units_host, void* stream);
+/* Cumulative voxel updates and volume-unit integrations since create/reset (flushes on `stream`, synchronises it). */
+ot_status ot_tsdf_counters(ot_tsdf* vol, int64_t* voxel_updates_host, int64_t* unit_integrations_host,
+                           void* stream);
+/* Colour state precision: 64 keeps each voxel's running colour mean in float64 with exact IEEE division, as Open3D's
+ * TSDFVoxel::color_ (Eigen::Vector3d; reconstruct_rgbd_filter.py:81-85 -> SURVEY A.3(iv)) -- bit-exact colours;
+ * 32 (default of the C ABI) keeps float32 with one hardware reciprocal per update (|rel| <= 1e-4, faster).  Call
+ * before the first integrate. */
+ot_status ot_tsdf_set_color_precision(ot_tsdf* vol, int32_t bits);
 
 /* Kernel timing for roofline reporting: when enabled, HIP events bracket every launch of the dominant
  * integration kernel on the caller's stream; ot_tsdf_kernel_time returns the summed device time (ms) and the
@@ -191,15 +197,21 @@ ot_status ot_tsdf_kernel_time(ot_tsdf* vol, double* total_ms_host, int64_t* laun
 
 /* Dump every unit sorted by key (kx, ky, kz): keys int32 [U][3]; per unit 4096 voxels in Open3D
  * IndexOf order (x*256 + y*16 + z): tsdf f32, weight f32, color f32 [3] (0..255).  Any pointer may be
- * NULL.  Device pointers. */
-ot_status ot_tsdf_export_units(ot_tsdf* vol, int32_t* keys, float* tsdf, float* weight, float* color,
-                               void* stream);
+ * NULL.  Device pointers; every output holds `capacity` units. */
+ot_status ot_tsdf_export_units(ot_tsdf* vol, int64_t capacity, int32_t* keys, float* tsdf, float* weight,
+                               float* color, void* stream);
+/* The float64 colours of a colour-precision-64 volume, [U][4096][3] in export_units' order.  Both exports fail with
+ * OT_ERR_CAPACITY when the volume holds more than `capacity` units (outputs sized from an older unit count). */
+ot_status ot_tsdf_export_color64(ot_tsdf* vol, int64_t capacity, double* color, void* stream);
 
 /* The inverse of ot_tsdf_export_units (same layouts): insert n units, overwriting any unit with the same key;
  * keys must be unique within one call.  color may be NULL (zeros).  Used to assemble a spatially sharded volume
  * on one GPU before extract_triangle_mesh.  Device pointers. */
 ot_status ot_tsdf_import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf, const float* weight,
                                const float* color, void* stream);
+/* The same for a colour-precision-64 volume (float64 colours, export_color64's layout). */
+ot_status ot_tsdf_import_units_color64(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf,
+                                       const float* weight, const double* color, void* stream);
 
 /* Spatial sharding of ONE object's volume over `world` GPUs (not an Open3D API): this volume
  * allocates and integrates only the units whose owner hash(key) mod world == rank.  Every rank integrates every

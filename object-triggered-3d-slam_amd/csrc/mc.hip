@@ -183,13 +183,23 @@ __global__ __launch_bounds__(EWORDS) void k_mc_count(McDev m) {
     if (t == 0) m.vert_cnt[r] = tot;
 }
 
-__device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z, float& f, float c[3]) {
+// tsdf and colour of one voxel; colour from the float64 pool when the volume keeps it (exact: a float colour widens
+// to double exactly, as Open3D's float-to-double promotion)
+__device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z, float& f, double c[3]) {
     const float* base = d.vox + (size_t)id * UNIT_FLOATS;
     const int vi = z * 256 + x * 16 + y;
     f = base[vi];
-    c[0] = base[2 * UNIT_VOX + vi];
-    c[1] = base[3 * UNIT_VOX + vi];
-    c[2] = base[4 * UNIT_VOX + vi];
+    if (d.vcol) {
+        const double* cb = color_base<double>(d, id);
+        c[0] = cb[vi];
+        c[1] = cb[UNIT_VOX + vi];
+        c[2] = cb[2 * UNIT_VOX + vi];
+    } else {
+        const float* cb = color_base<float>(d, id);
+        c[0] = (double)cb[vi];
+        c[1] = (double)cb[UNIT_VOX + vi];
+        c[2] = (double)cb[2 * UNIT_VOX + vi];
+    }
 }
 
 __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, double vl, double* V, double* VC) {
@@ -207,7 +217,8 @@ __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, doub
         const int gbit = w * 32 + b;
         const int local = gbit / 3, axis = gbit % 3;
         const int x = local >> 8, y = (local >> 4) & 15, z = local & 15;
-        float f0f, f1f, c0[3], c1[3];
+        float f0f, f1f;
+        double c0[3], c1[3];
         voxel_value(d, id, x, y, z, f0f, c0);
         int x1 = x + (axis == 0), y1 = y + (axis == 1), z1 = z + (axis == 2);
         const int nid = m.nbr[id * 8 + (((x1 >> 4) << 2) | ((y1 >> 4) << 1) | (z1 >> 4))];
@@ -228,7 +239,7 @@ __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, doub
         if (VC) {
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const double a0 = (double)c0[a] / 255.0, a1 = (double)c1[a] / 255.0;
+                const double a0 = c0[a] / 255.0, a1 = c1[a] / 255.0;
                 VC[vid * 3 + a] = (f1 * a0 + f0 * a1) / (f0 + f1);
             }
         }

@@ -44,6 +44,7 @@ struct TsdfDev {
     unsigned long long* stats;
     int* unit_keys;
     float* vox;
+    double* vcol;               // float64 colour pool [id][3][4096] (colour precision 64), else nullptr
     unsigned long long* fmask;  // per hash slot: frames of the current batch that touch the unit (bit f)
     int* bslots;                // hash slots touched by the current batch (first-touch order)
     void* work;                 // per touched slot of the batch: unit header (UnitWork, 32 B) for the integrate
@@ -58,6 +59,19 @@ struct TsdfDev {
 __host__ __device__ inline bool unit_owned(const TsdfDev& d, unsigned long long key) {
     if (d.shard_world <= 1) return true;
     return (int)((unsigned)(mix64(key + 0x9E3779B97F4A7C15ull) >> 32) % (unsigned)d.shard_world) == d.shard_rank;
+}
+
+// a unit's colour planes r, g, b (4096 each, voxel vi = z*256 + x*16 + y): the float planes inside the voxel
+// record, or the float64 pool when the volume keeps colour at Open3D's precision
+template <typename CT>
+__device__ inline CT* color_base(const TsdfDev& d, int id);
+template <>
+__device__ inline float* color_base<float>(const TsdfDev& d, int id) {
+    return d.vox + (size_t)id * UNIT_FLOATS + 2 * UNIT_VOX;
+}
+template <>
+__device__ inline double* color_base<double>(const TsdfDev& d, int id) {
+    return d.vcol + (size_t)id * 3 * UNIT_VOX;
 }
 
 constexpr int MAX_BATCH = 64;  // frames per fused launch (one bit each in fmask)
@@ -99,6 +113,7 @@ struct ot_tsdf {
     int device = 0;
     double voxel_length = 0.0, sdf_trunc = 0.0, unit_length = 0.0;
     int color_type = 1, stride = 4;
+    bool color64 = false;  // colour state in float64 (Open3D's Vector3d) instead of float32
     int64_t max_units = 0;
     int64_t hash_cap = 0;
     ot::TsdfDev dev{};

@@ -17,6 +17,7 @@
 //                 written whole (no pool memset); old units read/write only the voxels that update.
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 #include "sort.h"
 #include "tsdf.h"
@@ -52,6 +53,18 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // return 0 instead of faulting.
 __device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+
+// element i of a float64 array behind a buffer resource (32-bit offsets: no per-lane 64-bit address registers)
+__device__ inline double ld_f64(__amdgpu_buffer_rsrc_t r, int i) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8, 0, 0);
+    return __hiloint2double((int)v.y, (int)v.x);
+}
+__device__ inline void st_f64(__amdgpu_buffer_rsrc_t r, int i, double x) {
+    u32x2 v;
+    v.x = (unsigned)__double2loint(x);
+    v.y = (unsigned)__double2hiint(x);
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, i * 8, 0, 0);
 }
 
 __device__ inline int hash_insert(const TsdfDev& d, unsigned long long key) {
@@ -176,7 +189,9 @@ __device__ inline bool voxel_sample(const IntegrateParams& p, const float pc[3],
     return true;
 }
 
+template <bool C64>
 __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d) {
+    using CT = typename std::conditional<C64, double, float>::type;
     const int n = d.counters[C_TOUCHED];
     const int tid = threadIdx.x;
     const int x = tid >> 4, y = tid & 15;
@@ -188,6 +203,7 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
         const bool fresh = ent < 0;
         const int kx = d.unit_keys[id * 3 + 0], ky = d.unit_keys[id * 3 + 1], kz = d.unit_keys[id * 3 + 2];
         float* base = d.vox + (size_t)id * UNIT_FLOATS;
+        CT* cbase = color_base<CT>(d, id);
         float pc[3];
         column_origin(p, kx, ky, kz, x, y, pc);
         ++units;
@@ -197,34 +213,36 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
             int pix = 0;
             const bool hit = voxel_sample(p, pc, tn, pix);
             if (fresh) {
-                float ts = 0.0f, w = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f;
+                float ts = 0.0f, w = 0.0f;
+                CT cr = 0, cg = 0, cb = 0;
                 if (hit) {
                     ts = tn;  // (0*0 + t) / (0 + 1)
                     w = 1.0f;
-                    if (use_color) {
+                    if (use_color) {  // (0 * 0 + c) / (0 + 1) = c exactly
                         const uint8_t* c = p.color + (int64_t)pix * 3;
-                        cr = (float)c[0];
-                        cg = (float)c[1];
-                        cb = (float)c[2];
+                        cr = (CT)c[0];
+                        cg = (CT)c[1];
+                        cb = (CT)c[2];
                     }
                     ++upd;
                 }
                 base[vi] = ts;
                 base[UNIT_VOX + vi] = w;
-                base[2 * UNIT_VOX + vi] = cr;
-                base[3 * UNIT_VOX + vi] = cg;
-                base[4 * UNIT_VOX + vi] = cb;
+                cbase[vi] = cr;
+                cbase[UNIT_VOX + vi] = cg;
+                cbase[2 * UNIT_VOX + vi] = cb;
             } else if (hit) {
                 const float w = base[UNIT_VOX + vi];
                 const float ts = base[vi];
                 const float w1 = w + 1.0f;
                 base[vi] = (ts * w + tn) / w1;
-                if (use_color) {
+                if (use_color) {  // C64: Open3D's float64 expression; else its float32 rounding
                     const uint8_t* c = p.color + (int64_t)pix * 3;
-                    const float cr = base[2 * UNIT_VOX + vi], cg = base[3 * UNIT_VOX + vi], cb = base[4 * UNIT_VOX + vi];
-                    base[2 * UNIT_VOX + vi] = (cr * w + (float)c[0]) / w1;
-                    base[3 * UNIT_VOX + vi] = (cg * w + (float)c[1]) / w1;
-                    base[4 * UNIT_VOX + vi] = (cb * w + (float)c[2]) / w1;
+                    const CT wc = (CT)w, w1c = (CT)w1;
+                    const CT cr = cbase[vi], cg = cbase[UNIT_VOX + vi], cb = cbase[2 * UNIT_VOX + vi];
+                    cbase[vi] = (cr * wc + (CT)c[0]) / w1c;
+                    cbase[UNIT_VOX + vi] = (cg * wc + (CT)c[1]) / w1c;
+                    cbase[2 * UNIT_VOX + vi] = (cb * wc + (CT)c[2]) / w1c;
                 }
                 base[UNIT_VOX + vi] = w1;
                 ++upd;
@@ -585,25 +603,29 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
     }
 }
 
+// occupancy floor the integrate is compiled for: the float32-colour kernel allocates 64 VGPRs (8 waves
+// per SIMD) on its own; the float64-colour state and its IEEE f64 divides need 106 (4 waves per SIMD, no scratch —
+// forcing 5 or 6 waves spills)
 #ifndef OT_WAVES_PER_EU
 #define OT_WAVES_PER_EU 4
 #endif
+#ifndef OT_WAVES_PER_EU_C64
+#define OT_WAVES_PER_EU_C64 4
+#endif
 // One workgroup of SLICES waves per unit, so a unit's frame footprint is gathered through one CU's L1; units are
 // assigned by a static grid stride that every wave derives on its own: no barriers, no LDS, no atomics.
-__global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrate(
+// C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the separate pool d.vcol
+template <bool C64>
+__global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
+    using CT = typename std::conditional<C64, double, float>::type;
     const int lane = threadIdx.x & 63;
     const int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // slice of this wave
     const int n = d.counters[pc];
     const int npx = p.W * p.H;
     unsigned upd = 0;  // per lane: <= BZ voxels x 64 frames x units per workgroup, far below 2^32
     {
-#ifdef OT_XCD_PERM  // within each grid-wide round, XCD x (blockIdx % 8) takes a contiguous 1/8 of the round's units
-        const int G = gridDim.x;
-        const int b = (G & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3));
-#else
         const int b = blockIdx.x;
-#endif
         for (int u = b; u < n; u += gridDim.x) {
             const UnitWork& w = work[u];
             const int ent = w.id;
@@ -611,31 +633,35 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
             if (ent != -1) {
                 const int id = ent & 0x7FFFFFFF;
                 const bool fresh = ent < 0;
-#ifndef OT_MAP416  // wave = 8 x 8 columns: a square patch of the unit's xy plane projects to fewer pixel rows
+                // wave = 8 x 8 columns: a square patch of the unit's xy plane projects to fewer pixel rows
                 const int x = (s & 2) * 4 + (lane >> 3), y = (s & 1) * 8 + (lane & 7);
                 const int col = x * 16 + y;
-#else  // wave = 4 x 16 columns (4 whole x rows: 1-KiB coalesced state rows)
-                const int col = (s & 3) * 64 + lane;
-                const int x = col >> 4, y = col & 15;
-#endif
                 const int z0 = (s >> 2) * BZ;
                 float* base = d.vox + (size_t)id * UNIT_FLOATS;
-                float ts[BZ], wt[BZ], cr[BZ], cg[BZ], cb[BZ];
+                // colour plane c of voxel vi: float32 planes addressed from base (one address register for the
+                // whole record: a separate colour pointer costs ~34 VGPRs in this kernel), float64 from the pool
+                const __amdgpu_buffer_rsrc_t col64 =
+                    make_rsrc(C64 ? (const void*)color_base<double>(d, id) : (const void*)base, 3 * UNIT_VOX * 8);
+                float ts[BZ], wt[BZ];
+                CT cr[BZ], cg[BZ], cb[BZ];
 #pragma unroll
                 for (int k = 0; k < BZ; ++k) {
                     const int vi = (z0 + k) * 256 + col;
-#ifdef OT_ABL_NOSTATE  // timing-only ablation build: no voxel-state traffic (results are wrong)
-                    if (true) {
-#else
                     if (fresh) {
-#endif
-                        ts[k] = wt[k] = cr[k] = cg[k] = cb[k] = 0.0f;
+                        ts[k] = wt[k] = 0.0f;
+                        cr[k] = cg[k] = cb[k] = (CT)0;
                     } else {
                         ts[k] = base[vi];
                         wt[k] = base[UNIT_VOX + vi];
-                        cr[k] = base[2 * UNIT_VOX + vi];
-                        cg[k] = base[3 * UNIT_VOX + vi];
-                        cb[k] = base[4 * UNIT_VOX + vi];
+                        if constexpr (C64) {
+                            cr[k] = ld_f64(col64, vi);
+                            cg[k] = ld_f64(col64, UNIT_VOX + vi);
+                            cb[k] = ld_f64(col64, 2 * UNIT_VOX + vi);
+                        } else {
+                            cr[k] = base[2 * UNIT_VOX + vi];
+                            cg[k] = base[3 * UNIT_VOX + vi];
+                            cb[k] = base[4 * UNIT_VOX + vi];
+                        }
                     }
                 }
                 const float ox = (float)((double)w.kx * p.unit_len);
@@ -670,7 +696,6 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
 #pragma unroll
                     for (int k = 0; k < BZ; ++k) {
                         const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
-#ifndef OT_EXACTPROJ
                         // Certified fast projection.  Only floor(u), floor(v) and the bound tests are used, so
                         // u = nu * rcp(z) decides them exactly unless u lies within proj_eps of an integer (the
                         // bound tests 0.0001 and W - 0.0001 sit 1e-4 from integers); those rare waves redo the
@@ -685,10 +710,6 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
                             u_f = ((nu / pc[2]) + p.cx) + 0.5f;
                             v_f = ((nv / pc[2]) + p.cy) + 0.5f;
                         }
-#else
-                        const float u_f = ((nu / pc[2]) + p.cx) + 0.5f;
-                        const float v_f = ((nv / pc[2]) + p.cy) + 0.5f;
-#endif
                         // non-short-circuit test keeps all BZ projections in one basic block
                         const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) &
                                         (v_f < p.safe_h);
@@ -719,15 +740,6 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
                         cv[k] = 0u;
                         if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
                     }
-#ifdef OT_COUNT_IDLE  // diagnostic build: wave-frames with no updating lane (stats[2]) of all wave-frames (stats[3])
-                    if (lane == 0) atomicAdd(&d.stats[3], 1ull);
-                    {
-                        bool any = false;
-#pragma unroll
-                        for (int k = 0; k < BZ; ++k) any |= doitv[k];
-                        if (__ballot(any) == 0ull && lane == 0) atomicAdd(&d.stats[2], 1ull);
-                    }
-#endif
                     // phase D: updates in frame order (select form: identical values, no exec-mask branches)
 #pragma unroll
                     for (int k = 0; k < BZ; ++k) {
@@ -739,12 +751,18 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
                         const float tsn = (ts[k] * wv + tn) / w1;  // exact IEEE quotient: tsdf bit-exact
                         ts[k] = doit ? tsn : ts[k];
                         if (use_color) {
-                            // colour running mean: one reciprocal for the three channels — within the 1e-4 colour
-                            // contract (Open3D keeps colour in f64)
-                            const float rw = __builtin_amdgcn_rcpf(w1);
-                            const float nr = (cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
-                            const float ng = (cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
-                            const float nb = (cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                            CT nr, ng, nb;
+                            if (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
+                                const double wd = (double)wv, w1d = (double)w1;
+                                nr = (CT)(((double)cr[k] * wd + (double)(cv[k] & 0xFFu)) / w1d);
+                                ng = (CT)(((double)cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu)) / w1d);
+                                nb = (CT)(((double)cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu)) / w1d);
+                            } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
+                                const float rw = __builtin_amdgcn_rcpf(w1);
+                                nr = (CT)(((float)cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw);
+                                ng = (CT)(((float)cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw);
+                                nb = (CT)(((float)cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw);
+                            }
                             cr[k] = doit ? nr : cr[k];
                             cg[k] = doit ? ng : cg[k];
                             cb[k] = doit ? nb : cb[k];
@@ -753,20 +771,21 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
                         upd += doit ? 1u : 0u;
                     }
                 }
-#ifdef OT_ABL_NOSTATE  // keep every result live without storing it
-#pragma unroll
-                for (int k = 0; k < BZ; ++k) asm volatile("" ::"v"(ts[k]), "v"(wt[k]), "v"(cr[k]), "v"(cg[k]), "v"(cb[k]));
-#else
 #pragma unroll
                 for (int k = 0; k < BZ; ++k) {
                     const int vi = (z0 + k) * 256 + col;
                     base[vi] = ts[k];
                     base[UNIT_VOX + vi] = wt[k];
-                    base[2 * UNIT_VOX + vi] = cr[k];
-                    base[3 * UNIT_VOX + vi] = cg[k];
-                    base[4 * UNIT_VOX + vi] = cb[k];
+                    if constexpr (C64) {
+                        st_f64(col64, vi, cr[k]);
+                        st_f64(col64, UNIT_VOX + vi, cg[k]);
+                        st_f64(col64, 2 * UNIT_VOX + vi, cb[k]);
+                    } else {
+                        base[2 * UNIT_VOX + vi] = cr[k];
+                        base[3 * UNIT_VOX + vi] = cg[k];
+                        base[4 * UNIT_VOX + vi] = cb[k];
+                    }
                 }
-#endif
             }
         }
     }
@@ -774,13 +793,16 @@ __global__ __launch_bounds__(64 * SLICES, OT_WAVES_PER_EU) void k_batch_integrat
     if (lane == 0 && tot) atomicAdd(&d.stats[S_UPDATES], tot);
 }
 
-// export: units in sorted order, voxels transposed to Open3D IndexOf order (x*256 + y*16 + z)
+// export: units in sorted order, voxels transposed to Open3D IndexOf order (x*256 + y*16 + z); colour as CT
+// (float export of a float64 volume rounds to nearest)
+template <typename CT, typename OT>
 __global__ __launch_bounds__(256) void k_export(TsdfDev d, const unsigned* sorted_ids, int32_t* keys, float* tsdf,
-                                                float* weight, float* color) {
+                                                float* weight, OT* color) {
     const int r = blockIdx.x;
     const int id = (int)sorted_ids[r];
     const int tid = threadIdx.x;
     const float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    const CT* cbase = color_base<CT>(d, id);
     if (keys && tid < 3) keys[(int64_t)r * 3 + tid] = d.unit_keys[id * 3 + tid];
     for (int z = 0; z < UNIT_RES; ++z) {
         const int vi = z * 256 + tid;
@@ -788,17 +810,19 @@ __global__ __launch_bounds__(256) void k_export(TsdfDev d, const unsigned* sorte
         if (tsdf) tsdf[o] = base[vi];
         if (weight) weight[o] = base[UNIT_VOX + vi];
         if (color) {
-            color[o * 3 + 0] = base[2 * UNIT_VOX + vi];
-            color[o * 3 + 1] = base[3 * UNIT_VOX + vi];
-            color[o * 3 + 2] = base[4 * UNIT_VOX + vi];
+            color[o * 3 + 0] = (OT)cbase[vi];
+            color[o * 3 + 1] = (OT)cbase[UNIT_VOX + vi];
+            color[o * 3 + 2] = (OT)cbase[2 * UNIT_VOX + vi];
         }
     }
 }
 
-// import: the inverse of k_export (keys unique within one call; an existing unit is overwritten)
+// import: the inverse of k_export (keys unique within one call; an existing unit is overwritten); colour as the
+// volume keeps it (CT)
+template <typename CT>
 __global__ __launch_bounds__(256) void k_import(TsdfDev d, const int32_t* __restrict__ keys,
                                                 const float* __restrict__ tsdf, const float* __restrict__ weight,
-                                                const float* __restrict__ color) {
+                                                const CT* __restrict__ color) {
     __shared__ int s_id;
     const int r = blockIdx.x;
     const int tid = threadIdx.x;
@@ -833,14 +857,15 @@ __global__ __launch_bounds__(256) void k_import(TsdfDev d, const int32_t* __rest
     const int id = s_id;
     if (id < 0) return;
     float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    CT* cbase = color_base<CT>(d, id);
     for (int z = 0; z < UNIT_RES; ++z) {
         const int vi = z * 256 + tid;
         const int64_t o = (int64_t)r * UNIT_VOX + tid * 16 + z;
         base[vi] = tsdf[o];
         base[UNIT_VOX + vi] = weight[o];
-        base[2 * UNIT_VOX + vi] = color ? color[o * 3 + 0] : 0.0f;
-        base[3 * UNIT_VOX + vi] = color ? color[o * 3 + 1] : 0.0f;
-        base[4 * UNIT_VOX + vi] = color ? color[o * 3 + 2] : 0.0f;
+        cbase[vi] = color ? color[o * 3 + 0] : (CT)0;
+        cbase[UNIT_VOX + vi] = color ? color[o * 3 + 1] : (CT)0;
+        cbase[2 * UNIT_VOX + vi] = color ? color[o * 3 + 2] : (CT)0;
     }
 }
 
@@ -975,7 +1000,8 @@ static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t
         OT_HIP_TRY(hipEventCreate(&e1));
         OT_HIP_TRY(hipEventRecord(e0, stream));
     }
-    hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, stream, ip, vol->dev);
+    if (vol->color64) hipLaunchKernelGGL(k_integrate<true>, dim3(grid), dim3(256), 0, stream, ip, vol->dev);
+    else hipLaunchKernelGGL(k_integrate<false>, dim3(grid), dim3(256), 0, stream, ip, vol->dev);
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
         OT_HIP_TRY(hipEventRecord(e1, stream));
@@ -990,19 +1016,21 @@ static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t
 #endif
 // Grid of k_batch_integrate: OT_GRID_MULT x the co-resident workgroups (cached per device; a benign race at worst
 // computes the same value twice).
-static int integrate_grid() {
-    static int cache[64] = {0};
+static int integrate_grid(bool c64) {
+    static int cache[2][64] = {{0}};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 4096;
-    if (!cache[dev]) {
+    int* cache_c = cache[c64 ? 1 : 0];
+    if (!cache_c[dev]) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_batch_integrate, 64 * SLICES, 0) != hipSuccess ||
+        const void* kern = c64 ? (const void*)k_batch_integrate<true> : (const void*)k_batch_integrate<false>;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * SLICES, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 ||
             cus <= 0)
             return 4096;
-        cache[dev] = per_cu * cus * OT_GRID_MULT;
+        cache_c[dev] = per_cu * cus * OT_GRID_MULT;
     }
-    return cache[dev];
+    return cache_c[dev];
 }
 
 static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n, hipStream_t stream) {
@@ -1078,15 +1106,19 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, tp, vol->dev, n);
     hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc);
-    const int grid = integrate_grid();
+    const int grid = integrate_grid(vol->color64);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
         OT_HIP_TRY(hipEventCreate(&e0));
         OT_HIP_TRY(hipEventCreate(&e1));
         OT_HIP_TRY(hipEventRecord(e0, stream));
     }
-    hipLaunchKernelGGL(k_batch_integrate, dim3(grid), dim3(64 * SLICES), 0, stream, (const BatchFrame*)vol->bframes, ip0,
-                       vol->dev, (const UnitWork*)vol->dev.work, pc);
+    if (vol->color64)
+        hipLaunchKernelGGL(k_batch_integrate<true>, dim3(grid), dim3(64 * SLICES), 0, stream,
+                           (const BatchFrame*)vol->bframes, ip0, vol->dev, (const UnitWork*)vol->dev.work, pc);
+    else
+        hipLaunchKernelGGL(k_batch_integrate<false>, dim3(grid), dim3(64 * SLICES), 0, stream,
+                           (const BatchFrame*)vol->bframes, ip0, vol->dev, (const UnitWork*)vol->dev.work, pc);
     vol->batch_pc ^= 1;  // only once this batch's kernels are queued (its units kernel zeroes the other counter)
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
@@ -1251,7 +1283,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     (void)hipDeviceSynchronize();
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
-    void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, v->mult,
+    void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, d.vcol, v->mult,
                     v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, d.fmask, d.bslots, d.work,
                     v->bframes, v->bdm, v->brgba};
     for (void* p : ptrs)
@@ -1347,24 +1379,46 @@ ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames) {
     return OT_OK;
 }
 
-ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n) {
+ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n, void* stream_) {
     if (!vol || !n) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
-    ot_status st = tsdf_flush(vol, nullptr);
+    hipStream_t stream = S(stream_);
+    ot_status st = tsdf_flush(vol, stream);  // queued frames, on the caller's stream
     if (st != OT_OK) return st;
     int nu = 0;
-    OT_HIP_TRY(hipMemcpy(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost));
+    OT_HIP_TRY(hipMemcpyAsync(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
     *n = std::min<int64_t>(nu, vol->max_units);
     return OT_OK;
 }
 
-ot_status ot_tsdf_counters(ot_tsdf* vol, int64_t* updates, int64_t* unit_integrations) {
+ot_status ot_tsdf_counters(ot_tsdf* vol, int64_t* updates, int64_t* unit_integrations, void* stream_) {
     if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
-    ot_status st = tsdf_flush(vol, nullptr);
+    hipStream_t stream = S(stream_);
+    ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
     unsigned long long s[4];
-    OT_HIP_TRY(hipMemcpy(s, vol->dev.stats, sizeof(s), hipMemcpyDeviceToHost));
+    OT_HIP_TRY(hipMemcpyAsync(s, vol->dev.stats, sizeof(s), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
     if (updates) *updates = (int64_t)s[S_UPDATES];
     if (unit_integrations) *unit_integrations = (int64_t)s[S_UNIT_INTEGRATIONS];
+    return OT_OK;
+}
+
+ot_status ot_tsdf_set_color_precision(ot_tsdf* vol, int32_t bits) {
+    if (!vol || (bits != 32 && bits != 64))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] colour precision must be 32 or 64 bits");
+    int nu = 0;
+    OT_HIP_TRY(hipMemcpy(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost));
+    if (nu != 0 || !vol->pending.empty())
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] set the colour precision before the first integrate");
+    if (bits == 64 && !vol->dev.vcol)
+        OT_HIP_TRY(hipMalloc(&vol->dev.vcol, sizeof(double) * 3 * (size_t)UNIT_VOX * vol->max_units));
+    if (bits == 32 && vol->dev.vcol) {  // kernels take the float64 pool whenever it exists
+        OT_HIP_TRY(hipDeviceSynchronize());
+        OT_HIP_TRY(hipFree(vol->dev.vcol));
+        vol->dev.vcol = nullptr;
+    }
+    vol->color64 = bits == 64;
     return OT_OK;
 }
 
@@ -1400,21 +1454,42 @@ ot_status ot_tsdf_kernel_time(ot_tsdf* vol, double* total_ms, int64_t* launches)
     return OT_OK;
 }
 
-ot_status ot_tsdf_export_units(ot_tsdf* vol, int32_t* keys, float* tsdf, float* weight, float* color, void* stream) {
+ot_status ot_tsdf_export_units(ot_tsdf* vol, int64_t capacity, int32_t* keys, float* tsdf, float* weight, float* color,
+                               void* stream) {
     if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     int64_t nu = 0;
     ot_status st = tsdf_sorted_units(vol, S(stream), &nu);
     if (st != OT_OK) return st;
+    if (nu > capacity) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] export: more units than the output capacity");
     if (nu == 0) return OT_OK;
-    hipLaunchKernelGGL(k_export, dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev, vol->sorted_ids, keys, tsdf,
-                       weight, color);
+    if (vol->color64)
+        hipLaunchKernelGGL((k_export<double, float>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev,
+                           vol->sorted_ids, keys, tsdf, weight, color);
+    else
+        hipLaunchKernelGGL((k_export<float, float>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev,
+                           vol->sorted_ids, keys, tsdf, weight, color);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(S(stream)));
+    return OT_OK;
+}
+
+ot_status ot_tsdf_export_color64(ot_tsdf* vol, int64_t capacity, double* color, void* stream) {
+    if (!vol || !color) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    if (!vol->color64) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] export_color64 needs colour precision 64");
+    int64_t nu = 0;
+    ot_status st = tsdf_sorted_units(vol, S(stream), &nu);
+    if (st != OT_OK) return st;
+    if (nu > capacity) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] export: more units than the output capacity");
+    if (nu == 0) return OT_OK;
+    hipLaunchKernelGGL((k_export<double, double>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev,
+                       vol->sorted_ids, nullptr, nullptr, nullptr, color);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(S(stream)));
     return OT_OK;
 }
 
 // test / diagnostic hook (not part of the drop-in boundary): the volume's raw u64 stats[4] (0 voxel updates,
-// 1 unit integrations; 2, 3 filled by -DOT_COUNT_IDLE builds)
+// 1 unit integrations; 2, 3 unused)
 ot_status otx_tsdf_stats(ot_tsdf* vol, uint64_t* out4) {
     if (!vol || !out4) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     ot_status st = tsdf_flush(vol, nullptr);
@@ -1435,22 +1510,40 @@ ot_status ot_tsdf_set_shard(ot_tsdf* vol, int32_t rank, int32_t world) {
     return OT_OK;
 }
 
-ot_status ot_tsdf_import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf, const float* weight,
-                               const float* color, void* stream) {
+}  // extern "C"
+
+template <typename CT>
+static ot_status import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf, const float* weight,
+                              const CT* color, hipStream_t stream) {
     if (!vol || n < 0 || (n > 0 && (!keys || !tsdf || !weight)))
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: invalid arguments");
     if (n > vol->max_units) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: more units than max_units");
-    ot_status st = tsdf_flush(vol, S(stream));
+    if (vol->color64 != (sizeof(CT) == 8))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: colour dtype does not match the volume's "
+                                             "colour precision");
+    ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
     if (n == 0) return OT_OK;
-    hipLaunchKernelGGL(k_import, dim3((unsigned)n), dim3(256), 0, S(stream), vol->dev, keys, tsdf, weight,
+    hipLaunchKernelGGL(k_import<CT>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf, weight,
                        vol->color_type == OT_COLOR_RGB8 ? color : nullptr);
     OT_LAUNCH_CHECK();
     vol->sorted_units = -1;  // the sorted-unit cache no longer matches
-    st = check_errors(vol, S(stream));
+    st = check_errors(vol, stream);
     if (st != OT_OK) return st;
-    OT_HIP_TRY(hipStreamSynchronize(S(stream)));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
+}
+
+extern "C" {
+
+ot_status ot_tsdf_import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf, const float* weight,
+                               const float* color, void* stream) {
+    return import_units<float>(vol, n, keys, tsdf, weight, color, S(stream));
+}
+
+ot_status ot_tsdf_import_units_color64(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf,
+                                       const float* weight, const double* color, void* stream) {
+    return import_units<double>(vol, n, keys, tsdf, weight, color, S(stream));
 }
 
 }  // extern "C"

@@ -53,6 +53,7 @@ def all_gather_rows(local, group=None):
 
 
 UNIT_WORDS = 3 + 4096 * 5  # packed unit row: key int3 | tsdf f32 | weight f32 | colour f32 x3 (bit patterns)
+UNIT_WORDS_C64 = 3 + 4096 * 8  # the same with float64 colours (colour precision 64)
 
 
 def pack_units(keys, tsdf, weight, color):
@@ -66,12 +67,14 @@ def pack_units(keys, tsdf, weight, color):
 
 
 def unpack_units(rows):
+    """Inverse of pack_units; the row width tells float32 from float64 colours."""
     import torch
 
     n = rows.shape[0]
     f = rows[:, 3:].contiguous().view(torch.float32)
-    return (rows[:, :3].contiguous(), f[:, :4096].contiguous(), f[:, 4096:8192].contiguous(),
-            f[:, 8192:].contiguous().view(n, 4096, 3))
+    c = rows[:, 3 + 8192:].contiguous()
+    c = c.view(torch.float64) if rows.shape[1] == UNIT_WORDS_C64 else c.view(torch.float32)
+    return rows[:, :3].contiguous(), f[:, :4096].contiguous(), f[:, 4096:8192].contiguous(), c.view(n, 4096, 3)
 
 
 def assemble_sharded_volume(volume, group=None):
@@ -85,7 +88,7 @@ def assemble_sharded_volume(volume, group=None):
     merged = ScalableTSDFVolume(volume.voxel_length, volume.sdf_trunc, color_type=volume.color_type,
                                 volume_unit_resolution=volume.volume_unit_resolution,
                                 depth_sampling_stride=volume.depth_sampling_stride,
-                                max_units=max(32768, int(rows.shape[0])))
+                                max_units=max(32768, int(rows.shape[0])), color_precision=volume.color_precision)
     merged.import_units(*unpack_units(rows))
     return merged
 

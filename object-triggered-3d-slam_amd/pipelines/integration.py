@@ -24,12 +24,14 @@ class ScalableTSDFVolume:
     """pipelines.integration.ScalableTSDFVolume(voxel_length, sdf_trunc, color_type=NoColor,
     volume_unit_resolution=16, depth_sampling_stride=4).
 
-    Extra keyword arguments (not in Open3D): `max_units` (block-pool capacity in HBM) and `batch_frames`
-    (frames queued per fused integration launch, default 32, max 64; 1 = integrate immediately).  Results
-    are bit-identical for any value: a batch applies its frames to each voxel in call order."""
+    Extra keyword arguments (not in Open3D): `max_units` (block-pool capacity in HBM), `batch_frames`
+    (frames queued per fused integration launch, default 32, max 64; 1 = integrate immediately; results are
+    bit-identical for any value: a batch applies its frames to each voxel in call order) and `color_precision`
+    (64, the default: the running colour mean in float64 with exact division, Open3D's TSDFVoxel::color_ --
+    bit-exact colours; 32: float32 state with one reciprocal per update, |rel| <= 1e-4, faster)."""
 
     def __init__(self, voxel_length, sdf_trunc, color_type=TSDFVolumeColorType.NoColor, volume_unit_resolution=16,
-                 depth_sampling_stride=4, max_units=0, batch_frames=None):
+                 depth_sampling_stride=4, max_units=0, batch_frames=None, color_precision=64):
         D.require_gpu()
         ct = int(color_type)
         if ct == TSDFVolumeColorType.Gray32:
@@ -44,9 +46,12 @@ class ScalableTSDFVolume:
         L.call("ot_tsdf_create", self.voxel_length, self.sdf_trunc, ct, self.volume_unit_resolution,
                self.depth_sampling_stride, int(max_units), C.byref(h))
         self._h = h
-        self._keep = []  # frames queued for a batched launch stay referenced until the flush
+        self._keep = []  # frames queued for a batched launch stay referenced until the C side integrates them
+        self._batch = 32
         if batch_frames is not None:
             self.set_batch(batch_frames)
+        self.color_precision = int(color_precision)
+        L.call("ot_tsdf_set_color_precision", self._h, self.color_precision)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -59,6 +64,14 @@ class ScalableTSDFVolume:
 
     def set_batch(self, frames):
         L.call("ot_tsdf_set_batch", self._h, int(frames))
+        self._batch = int(frames)
+
+    def _queued(self, item):
+        """Keep a queued frame's device images alive while the C side holds it; the C side integrates its queue
+        (asynchronously, on the caller's stream, which orders any reuse of the freed memory) when it is full."""
+        self._keep.append(item)
+        if len(self._keep) >= min(self._batch, 64):
+            self._keep.clear()
 
     def reset(self):
         """ScalableTSDFVolume::Reset, ordered on the current stream (no device-wide synchronisation)."""
@@ -82,12 +95,12 @@ class ScalableTSDFVolume:
         raw = getattr(image, "_raw_depth", None)
         if raw is not None:
             d16, scale, trunc = raw
-            self._keep.append((d16, cdev))
+            self._queued((d16, cdev))
             L.call("ot_tsdf_integrate_u16", self._h, D.ptr(d16), D.ptr(cdev), C.byref(intr),
                    ext.ctypes.data_as(C.c_void_p), scale, trunc, D.stream_ptr())
         else:
             ddev = depth.dev()
-            self._keep.append((ddev, cdev))
+            self._queued((ddev, cdev))
             L.call("ot_tsdf_integrate", self._h, D.ptr(ddev), D.ptr(cdev), C.byref(intr),
                    ext.ctypes.data_as(C.c_void_p), D.stream_ptr())
 
@@ -98,27 +111,36 @@ class ScalableTSDFVolume:
     # ---- readers (each flushes queued frames first) ----
     def num_units(self):
         n = C.c_int64(0)
-        L.call("ot_tsdf_num_units", self._h, C.byref(n))
+        L.call("ot_tsdf_num_units", self._h, C.byref(n), D.stream_ptr())
         self._keep.clear()
         return n.value
 
     def counters(self):
         """(voxel_updates, unit_integrations) since create/reset."""
         u, k = C.c_int64(0), C.c_int64(0)
-        L.call("ot_tsdf_counters", self._h, C.byref(u), C.byref(k))
+        L.call("ot_tsdf_counters", self._h, C.byref(u), C.byref(k), D.stream_ptr())
         self._keep.clear()
         return u.value, k.value
 
-    def export_units(self):
-        """All units sorted by key: keys (U,3) int32, tsdf/weight (U,4096) f32, color (U,4096,3) f32
-        (voxels in Open3D IndexOf order x*256 + y*16 + z)."""
+    def export_units(self, color_dtype=None):
+        """All units sorted by key: keys (U,3) int32, tsdf/weight (U,4096) f32, color (U,4096,3) (voxels in Open3D
+        IndexOf order x*256 + y*16 + z).  Colour comes out as float64 for a colour-precision-64 volume (exact) and
+        float32 otherwise, unless color_dtype ("float32" / "float64") asks for another."""
         n = self.num_units()
         keys = D.empty((n, 3), "int32")
         tsdf = D.empty((n, 4096), "float32")
         weight = D.empty((n, 4096), "float32")
-        color = D.empty((n, 4096, 3), "float32")
-        L.call("ot_tsdf_export_units", self._h, D.ptr(keys), D.ptr(tsdf), D.ptr(weight), D.ptr(color),
-               D.stream_ptr())
+        cdt = color_dtype or ("float64" if self.color_precision == 64 else "float32")
+        color = D.empty((n, 4096, 3), cdt)
+        L.call("ot_tsdf_export_units", self._h, n, D.ptr(keys), D.ptr(tsdf), D.ptr(weight),
+               D.ptr(color) if cdt == "float32" else None, D.stream_ptr())
+        if cdt == "float64":
+            if self.color_precision == 64:
+                L.call("ot_tsdf_export_color64", self._h, n, D.ptr(color), D.stream_ptr())
+            else:
+                c32 = D.empty((n, 4096, 3), "float32")
+                L.call("ot_tsdf_export_units", self._h, n, None, None, None, D.ptr(c32), D.stream_ptr())
+                color.copy_(c32)
         return keys, tsdf, weight, color
 
     def import_units(self, keys, tsdf, weight, color=None):
@@ -127,12 +149,13 @@ class ScalableTSDFVolume:
         n = int(keys.shape[0])
         tsdf = D.to_device(tsdf, "float32")
         weight = D.to_device(weight, "float32")
-        color = D.to_device(color, "float32") if color is not None else None
+        c64 = self.color_precision == 64
+        color = D.to_device(color, "float64" if c64 else "float32") if color is not None else None
         if tuple(tsdf.shape[-1:]) != (4096,) or tsdf.shape[0] != n or weight.shape[0] != n or (
                 color is not None and color.shape[0] != n):
             raise RuntimeError("[ScalableTSDFVolume] import_units: shapes do not match export_units")
-        L.call("ot_tsdf_import_units", self._h, n, D.ptr(keys), D.ptr(tsdf), D.ptr(weight), D.ptr(color),
-               D.stream_ptr())
+        L.call("ot_tsdf_import_units_color64" if c64 else "ot_tsdf_import_units", self._h, n, D.ptr(keys),
+               D.ptr(tsdf), D.ptr(weight), D.ptr(color), D.stream_ptr())
 
     def set_shard(self, rank, world):
         """Keep only the units owned by `rank` of `world` (spatial sharding of one object)."""

@@ -1,7 +1,8 @@
 """GPU parity at the benchmark's full size (BASELINE.json configs[1]): the 256-frame 640x480 synthetic scan bench.py
 times, integrated at 5 mm through the same C-ABI entry point (ot_tsdf_integrate_u16, 32-frame fused batches), is
-bit-exact against the CPU oracle on every unit key, voxel weight and tsdf value; colours within 1e-4; and the
-exact voxel-update / unit-integration counters agree (they are the `roofline` accounting's inputs).
+bit-exact against the CPU oracle on every unit key, voxel weight and tsdf value, and the exact voxel-update /
+unit-integration counters agree (they are the `roofline` accounting's inputs).  Colours: bit-exact in float64 with
+colour precision 64 (Open3D's TSDFVoxel::color_), within 1e-4 with the float32 headline setting.
 The oracle takes ~5-10 s with OpenMP here."""
 import ctypes as C
 
@@ -14,12 +15,27 @@ from conftest import assert_bitwise
 pytestmark = pytest.mark.gpu
 
 
-def test_bench_workload_bitexact(pkg, O, synth, gpu):
+@pytest.fixture(scope="module")
+def scan(synth):
+    return synth.make_sequence(synth.Scene(seed=0), n_frames=256, intr=synth.REF_INTRINSICS_640)
+
+
+@pytest.fixture(scope="module")
+def oracle_volume(O, synth, scan):
+    depth, color, ext = scan
+    ref = O.TSDF(0.005, 0.04, 1, 4)
+    for k in range(256):
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], synth.REF_INTRINSICS_640, ext[k])
+    return ref.export(), ref.total_updates(), ref.unit_integrations()
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+def test_bench_workload_bitexact(pkg, synth, scan, oracle_volume, gpu, bits):
     L = pkg._lib
     lib = L.load()
     intr_t = synth.REF_INTRINSICS_640
     W, H = intr_t[0], intr_t[1]
-    depth, color, ext = synth.make_sequence(synth.Scene(seed=0), n_frames=256, intr=intr_t)
+    depth, color, ext = scan
     d16 = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
     col = torch.from_numpy(color).cuda().contiguous()
     ext = np.ascontiguousarray(ext, dtype=np.float64)
@@ -28,6 +44,7 @@ def test_bench_workload_bitexact(pkg, O, synth, gpu):
     vol = C.c_void_p()
     L.call("ot_tsdf_create", 0.005, 0.04, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
     try:
+        L.call("ot_tsdf_set_color_precision", vol, bits)
         npx = W * H
         for k in range(256):
             st = lib.ot_tsdf_integrate_u16(vol, C.c_void_p(d16.data_ptr() + k * npx * 2),
@@ -35,25 +52,29 @@ def test_bench_workload_bitexact(pkg, O, synth, gpu):
                                            ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
             assert st == 0, lib.ot_last_error()
         nu = C.c_int64(0)
-        L.call("ot_tsdf_num_units", vol, C.byref(nu))
+        L.call("ot_tsdf_num_units", vol, C.byref(nu), stream)
         keys = torch.empty((nu.value, 3), dtype=torch.int32, device="cuda")
         tsdf = torch.empty((nu.value, 4096), dtype=torch.float32, device="cuda")
         weight = torch.empty((nu.value, 4096), dtype=torch.float32, device="cuda")
-        colr = torch.empty((nu.value, 4096, 3), dtype=torch.float32, device="cuda")
-        L.call("ot_tsdf_export_units", vol, C.c_void_p(keys.data_ptr()), C.c_void_p(tsdf.data_ptr()),
-               C.c_void_p(weight.data_ptr()), C.c_void_p(colr.data_ptr()), stream)
+        colr = torch.empty((nu.value, 4096, 3), dtype=torch.float32 if bits == 32 else torch.float64, device="cuda")
+        L.call("ot_tsdf_export_units", vol, nu.value, C.c_void_p(keys.data_ptr()), C.c_void_p(tsdf.data_ptr()),
+               C.c_void_p(weight.data_ptr()), C.c_void_p(colr.data_ptr()) if bits == 32 else None, stream)
+        if bits == 64:
+            L.call("ot_tsdf_export_color64", vol, nu.value, C.c_void_p(colr.data_ptr()), stream)
+        with pytest.raises(RuntimeError, match="capacity"):  # outputs sized from an older unit count
+            L.call("ot_tsdf_export_units", vol, nu.value - 1, None, None, None, None, stream)
         upd, units = C.c_int64(0), C.c_int64(0)
-        L.call("ot_tsdf_counters", vol, C.byref(upd), C.byref(units))
+        L.call("ot_tsdf_counters", vol, C.byref(upd), C.byref(units), stream)
     finally:
         L.call("ot_tsdf_destroy", vol)
-    ref = O.TSDF(0.005, 0.04, 1, 4)
-    for k in range(256):
-        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
-    rk, rt, rw, rc = ref.export()
+    (rk, rt, rw, rc), r_upd, r_units = oracle_volume
     assert nu.value == rk.shape[0] > 5000
     assert_bitwise(keys.cpu().numpy(), rk, "unit keys (bench workload)")
     assert_bitwise(weight.cpu().numpy(), rw, "voxel weights (bench workload)")
     assert_bitwise(tsdf.cpu().numpy(), rt, "voxel tsdf (bench workload)")
-    np.testing.assert_allclose(colr.cpu().numpy(), rc, rtol=1e-4, atol=1e-4 * 255)
-    assert upd.value == ref.total_updates()
-    assert units.value == ref.unit_integrations()
+    if bits == 64:
+        assert_bitwise(colr.cpu().numpy(), rc, "float64 voxel colours (bench workload)")
+    else:
+        np.testing.assert_allclose(colr.cpu().numpy(), rc, rtol=1e-4, atol=1e-4 * 255)
+    assert upd.value == r_upd
+    assert units.value == r_units

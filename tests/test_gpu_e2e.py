@@ -53,8 +53,8 @@ def test_reconstruct_object_end_to_end(pkg, O, synth, gpu, scan_dir):
     rx, rc = _oracle_object(O, synth, scan_dir, "Object_0", cfg)
     assert 1000 < len(got.points) < cfg.n_samples
     assert_bitwise(np.asarray(got.points), rx, "reconstructed points (PLY float64)")
-    c8 = np.asarray(got.colors) * 255.0
-    assert np.abs(c8 - np.round(np.clip(rc, 0, 1) * 255.0)).max() <= 1.0
+    c8 = np.asarray(got.colors) * 255.0  # float64 colour state: the PLY's uchar colours equal the oracle's exactly
+    assert np.array_equal(c8, np.round(np.clip(rc, 0, 1) * 255.0))
 
 
 def test_merge_driver_single_rank(pkg, O, synth, gpu, scan_dir, tmp_path):

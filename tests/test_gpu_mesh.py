@@ -41,7 +41,7 @@ def test_marching_cubes_bitexact(meshes):
     assert len(mesh.vertices) == V.shape[0] and len(mesh.triangles) == T.shape[0]
     assert_bitwise(np.asarray(mesh.triangles), T, "triangles")
     assert_bitwise(np.asarray(mesh.vertices), V, "vertices")
-    np.testing.assert_allclose(np.asarray(mesh.vertex_colors), VC, rtol=1e-4, atol=1e-6)
+    assert_bitwise(np.asarray(mesh.vertex_colors), VC, "vertex colours (float64 colour state)")
 
 
 def test_marching_cubes_5mm(pkg, O, synth, seq16):
@@ -75,7 +75,7 @@ def test_sampling_bitexact(O, meshes):
         P, PN, PC = O.sample_points_uniformly(V, T, n_pts, seed, VN=N, VC=VC)
         assert_bitwise(np.asarray(pcd.points), P, "sampled points")
         assert_bitwise(np.asarray(pcd.normals), PN, "sampled normals")
-        np.testing.assert_allclose(np.asarray(pcd.colors), PC, rtol=1e-4, atol=1e-6)
+        assert_bitwise(np.asarray(pcd.colors), PC, "sampled colours")
 
 
 def test_z_filter_tail(O, meshes):

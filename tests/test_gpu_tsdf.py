@@ -95,12 +95,13 @@ def test_unproject_stride_and_empty(pkg, O, gpu, synth, seq16):
     assert len(empty.points) == 0
 
 
-def _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=None, trunc=3.0, float_path=False, intr_t=None):
+def _run_pair(pkg, O, synth, depth, color, ext, voxel, batch=None, trunc=3.0, float_path=False, intr_t=None,
+              color_precision=64):
     integ = _integration(pkg)
     intr_t = intr_t or ref_intr(synth)
     intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
     vol = integ.ScalableTSDFVolume(voxel_length=voxel, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
-                                   batch_frames=batch)
+                                   batch_frames=batch, color_precision=color_precision)
     ref = O.TSDF(voxel, 0.04, 1, 4)
     for k in range(depth.shape[0]):
         rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
@@ -119,7 +120,10 @@ def _compare_volumes(vol, ref):
     assert_bitwise(keys, rk, "unit keys")
     assert_bitwise(weight, rw, "voxel weights")
     assert_bitwise(tsdf, rt, "voxel tsdf")
-    np.testing.assert_allclose(col, rc, rtol=1e-4, atol=1e-4 * 255)
+    if vol.color_precision == 64:  # Open3D's float64 colour state: bit-exact
+        assert_bitwise(col, rc, "voxel colours (float64)")
+    else:  # float32 state with one reciprocal per update
+        np.testing.assert_allclose(col, rc, rtol=1e-4, atol=1e-4 * 255)
     upd, units = vol.counters()
     assert upd == ref.total_updates()
     assert units == ref.unit_integrations()
@@ -210,3 +214,14 @@ def test_tsdf_capacity_error(pkg, gpu, synth, seq16):
     vol.integrate(rgbd, intr, ext[0])
     with pytest.raises(RuntimeError, match="pool exhausted"):
         vol.export_units()
+
+
+@pytest.mark.parametrize("batch", [1, 32])
+def test_float32_colour_mode(pkg, O, synth, seq16, gpu, batch):
+    """colour precision 32 (the C ABI default, the headline's setting): tsdf / weight still bit-exact, colour within
+    1e-4; both the per-frame (batch 1) and the fused kernel."""
+    depth, color, ext = seq16
+    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, batch=batch, color_precision=32)
+    _compare_volumes(vol, ref)
+    with pytest.raises(RuntimeError, match="colour precision"):  # float64 colours into a float32 volume
+        pkg._lib.call("ot_tsdf_import_units_color64", vol._h, 0, None, None, None, None, None)
