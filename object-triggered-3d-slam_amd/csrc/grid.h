@@ -16,8 +16,8 @@ namespace ot {
 constexpr int NBR3 = 9;   // 3x3 columns, z-1 .. z+1
 constexpr int NBR5 = 25;  // 5x5 columns, z-2 .. z+2
 
-// SOR: radius (in cells) of the block a query scans first, and the matching cell occupancy target (points per
-// occupied cell of a surface-like cloud); both only change speed, never a result
+// SOR (outlier.hip): radius (in cells) of the block a query scans first, and the matching cell occupancy target
+// (points per occupied cell of a surface-like cloud); both only change speed, never a result.
 #ifndef OT_SOR_R
 #define OT_SOR_R 1
 #endif
@@ -28,11 +28,14 @@ constexpr int NBR5 = 25;  // 5x5 columns, z-2 .. z+2
 #define OT_SOR_NBR5 0  // R = 1: precompute the 5x5 column ranges of every cell for stage 2 (default: probe on the fly)
 #endif
 constexpr int SOR_BLOCK_R = OT_SOR_R;
-constexpr bool SOR_WITH5 = OT_SOR_R == 2 || OT_SOR_NBR5;
 inline double sor_cell_target(int nb_neighbors) {
     const double t = (OT_SOR_OCC) * (double)nb_neighbors;
     return t > 2.0 ? t : 2.0;
 }
+
+// neighbour structures a grid build can precompute (bit mask)
+enum { GRID_NBR3 = 1, GRID_NBR5 = 2 };
+constexpr int SOR_GRID_NBR = GRID_NBR3 | ((OT_SOR_R == 2 || OT_SOR_NBR5) ? GRID_NBR5 : 0);
 
 struct GridDev {
     const double* sxyz;        // [n][3] points in sorted (frame, cell) order
@@ -59,10 +62,11 @@ struct GridBuild {
 };
 
 // Build the grid of n points (xyz device [n][3]) grouped in nframes frames.  d_foff / d_origin: device arrays
-// ([F+1] ints, [F][3] doubles) that must outlive the grid; dims: cells per axis covering every frame.  Scratch
+// ([F+1] ints, [F][3] doubles) that must outlive the grid; dims: cells per axis covering every frame; nbr: the
+// GRID_* structures to precompute.  Scratch
 // slots slot0 .. slot0 + 2.  Synchronises (cell count).
 ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int* d_foff, const double* d_origin,
-                            double h, const int dims[3], bool with5, hipStream_t stream, GridBuild& out, int slot0);
+                            double h, const int dims[3], int nbr, hipStream_t stream, GridBuild& out, int slot0);
 
 // Statistical outlier removal over a built grid (Open3D RemoveStatisticalOutliers per frame):
 // avg[i] = mean kNN distance of point i (-1 when none); per frame the cloud mean and squared-deviation sum are

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_cell_nbr(const unsigned long long* __re
     const int x = (int)((key >> g.sx) & ((1ull << (g.sf - g.sx)) - 1)) + dx;
     const int2 col = grid_column(g, f, x, y);
     if (R == 2) nbr5[c * NBR5 + t] = column_range(g, col, z - 2, z + 2);
-    if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1)
+    if (nbr3 && dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1)
         nbr3[c * NBR3 + (dx + 1) * 3 + (dy + 1)] = column_range(g, col, z - 1, z + 1);
 }
 
@@ -315,13 +315,23 @@ __device__ inline void cell_fracs(const GridDev& g, const double q[3], const dou
 }
 
 // Stage 1, one lane per query (sorted order: a wave's queries share cells and candidate ranges): the columns of the
-// query's (2R+1)^3 block nearest-first, a column skipped once its distance from q reaches the current k-th distance;
-// the k-th distance is final when it does not exceed the distance from q to the block's faces.  Unsettled queries
-// go to the pending list.
+// query's (2R+1)^3 block nearest-first into the register top-k list, a column skipped once its distance from q
+// reaches the current k-th distance; the k-th distance is final when it does not exceed the distance from q to the
+// block's faces.  Unsettled queries go to the pending list.
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2): XCD x runs the blocks b = x mod 8.
+// Block b is remapped so that XCD x takes one contiguous range of the sorted queries instead, keeping a query's
+// neighbourhood in the L2 that the neighbouring workgroups (the neighbouring cells) just filled (a bijection of
+// [0, G); configs[2] SOR -2 %).
+__device__ inline int64_t xcd_block() {
+    const int64_t b = blockIdx.x, G = gridDim.x;
+    const int64_t x = b & 7, per = G >> 3, rem = G & 7;
+    return x * per + (x < rem ? x : rem) + (b >> 3);
+}
+
 template <int KMAX, int R>
 __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, double* avg, SorPend pd) {
     constexpr int W = 2 * R + 1;
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t j = xcd_block() * 256 + threadIdx.x;
     if (j >= n) return;
     const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, j) : 0;
     const int64_t fbeg = g.foff[f], fend = g.foff[f + 1];
@@ -600,7 +610,7 @@ static int bits_for_host(int64_t v) {  // bits to represent 0..v
 }
 
 ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int* d_foff, const double* d_origin,
-                            double h, const int dims[3], bool with5, hipStream_t stream, GridBuild& out, int slot0) {
+                            double h, const int dims[3], int nbr, hipStream_t stream, GridBuild& out, int slot0) {
     GridDev& g = out.g;
     g.h = h;
     g.origin = d_origin;
@@ -656,23 +666,27 @@ ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int
     if (e) return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (non-finite point coordinates)");
     int64_t cap = 1;
     while (cap < 2 * ncells + 2) cap <<= 1;
-    char* hs = (char*)scratch((size_t)cap * (8 + 8) + (size_t)ncells * ((NBR3 + (with5 ? NBR5 : 0)) * 8 + 12) + 128,
-                              slot0 + 2);
+    const bool w3 = nbr & GRID_NBR3, w5 = nbr & GRID_NBR5;
+    const size_t per_cell = (w3 ? NBR3 * 8 : 0) + (w5 ? NBR5 * 8 : 0) + 12;
+    char* hs = (char*)scratch((size_t)cap * (8 + 8) + (size_t)ncells * per_cell + 128, slot0 + 2);
     if (!hs) return fail(OT_ERR_HIP, "scratch allocation failed");
     g.hkeys = (unsigned long long*)hs;
     g.hval = (int2*)(g.hkeys + cap);
-    int2* nbr3 = g.hval + cap;
-    int2* nbr5 = with5 ? nbr3 + ncells * NBR3 : nullptr;
-    g.crange = (with5 ? nbr5 + ncells * NBR5 : nbr3 + ncells * NBR3);
+    int2* cur = g.hval + cap;
+    int2* nbr3 = w3 ? cur : nullptr;
+    cur += w3 ? ncells * NBR3 : 0;
+    int2* nbr5 = w5 ? cur : nullptr;
+    cur += w5 ? ncells * NBR5 : 0;
+    g.crange = cur;
     g.cz = (int*)(g.crange + ncells);
     g.hash_mask = (int)(cap - 1);
     OT_HIP_TRY(hipMemsetAsync(g.hkeys, 0xFF, sizeof(unsigned long long) * cap, stream));
     hipLaunchKernelGGL(k_grid_insert, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, stream, kout, heads,
                        ncells, n, g);  // cell ranges / z and the column hash, read by k_cell_nbr
-    if (with5)
+    if (w5)
         hipLaunchKernelGGL(k_cell_nbr<2>, dim3((unsigned)((ncells * NBR5 + 255) / 256)), dim3(256), 0, stream, kout,
                            heads, ncells, g, nbr3, nbr5);
-    else
+    else if (w3)
         hipLaunchKernelGGL(k_cell_nbr<1>, dim3((unsigned)((ncells * NBR3 + 255) / 256)), dim3(256), 0, stream, kout,
                            heads, ncells, g, nbr3, nbr5);
     hipLaunchKernelGGL(k_gather_sorted, dim3((unsigned)((n * 3 + 255) / 256)), dim3(256), 0, stream, xyz, vout, n, sxyz);
@@ -785,7 +799,7 @@ static ot_status bounds_host(const double* xyz, int64_t n, hipStream_t stream, d
 // one frame: origin = the cloud's minimum corner, cells per axis from the extent.  frame_dev receives the device
 // origin [3] and offsets {0, n} (scratch slot 20).
 static ot_status single_frame_grid(const double* xyz, int64_t n, double h, const double mn[3], const double mx[3],
-                                   bool with5, hipStream_t stream, GridBuild& gb) {
+                                   int nbr, hipStream_t stream, GridBuild& gb) {
     int dims[3];
     for (int a = 0; a < 3; ++a) {
         const double span = std::floor((mx[a] - mn[a]) / h);
@@ -799,7 +813,7 @@ static ot_status single_frame_grid(const double* xyz, int64_t n, double h, const
     OT_HIP_TRY(hipMemcpyAsync(fr, org, sizeof(org), hipMemcpyHostToDevice, stream));
     OT_HIP_TRY(hipMemcpyAsync(fr + 32, off, sizeof(off), hipMemcpyHostToDevice, stream));
     // build_grid_frames synchronises the stream before returning, so org / off outlive their copies
-    return build_grid_frames(xyz, n, 1, (const int*)(fr + 32), (const double*)fr, h, dims, with5, stream, gb, 22);
+    return build_grid_frames(xyz, n, 1, (const int*)(fr + 32), (const double*)fr, h, dims, nbr, stream, gb, 22);
 }
 
 extern "C" {
@@ -818,7 +832,7 @@ ot_status ot_remove_radius_outlier(const double* xyz, int64_t n, int32_t nb_poin
     ot_status st = bounds_host(xyz, n, stream, mn, mx);
     if (st != OT_OK) return st;
     GridBuild gb;
-    st = single_frame_grid(xyz, n, radius, mn, mx, false, stream, gb);
+    st = single_frame_grid(xyz, n, radius, mn, mx, GRID_NBR3, stream, gb);
     if (st != OT_OK) return st;
     unsigned char* keep = (unsigned char*)scratch((size_t)n + 64, 12);
     if (!keep) return fail(OT_ERR_HIP, "scratch allocation failed");
@@ -855,12 +869,12 @@ ot_status ot_remove_statistical_outlier(const double* xyz, int64_t n, int32_t nb
     const double hmin = ext[2] / 5.0e5;
     double h = std::max(std::sqrt(0.5 * ext[2] * ext[1] * target / (double)n), hmin);
     GridBuild gb;
-    st = single_frame_grid(xyz, n, h, mn, mx, SOR_WITH5, stream, gb);
+    st = single_frame_grid(xyz, n, h, mn, mx, SOR_GRID_NBR, stream, gb);
     if (st != OT_OK) return st;
     const double occ = (double)n / (double)std::max<int64_t>(gb.ncells, 1);
     if (occ > 2.5 * target || occ < 0.4 * target) {
         h = std::max(h * std::sqrt(target / occ), hmin);
-        st = single_frame_grid(xyz, n, h, mn, mx, SOR_WITH5, stream, gb);
+        st = single_frame_grid(xyz, n, h, mn, mx, SOR_GRID_NBR, stream, gb);
         if (st != OT_OK) return st;
     }
     char* ws = (char*)scratch((size_t)n * 8 + 256, 12);
@@ -896,12 +910,12 @@ ot_status ot_compute_point_cloud_distance(const double* src, int64_t n, const do
     const double hmin = ext[2] / 5.0e5;
     double h = std::max(std::sqrt(0.5 * ext[2] * ext[1] * target / (double)m), hmin);
     GridBuild gb;
-    st = single_frame_grid(tgt, m, h, mn, mx, false, stream, gb);
+    st = single_frame_grid(tgt, m, h, mn, mx, GRID_NBR3, stream, gb);
     if (st != OT_OK) return st;
     const double occ = (double)m / (double)std::max<int64_t>(gb.ncells, 1);
     if (occ > 2.5 * target || occ < 0.4 * target) {
         h = std::max(h * std::sqrt(target / occ), hmin);
-        st = single_frame_grid(tgt, m, h, mn, mx, false, stream, gb);
+        st = single_frame_grid(tgt, m, h, mn, mx, GRID_NBR3, stream, gb);
         if (st != OT_OK) return st;
     }
     hipLaunchKernelGGL(k_nn_dist, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, gb.g, src, n, m, mn[0],
