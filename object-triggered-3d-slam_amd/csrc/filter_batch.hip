@@ -240,10 +240,11 @@ struct FbKeys {
     int vbits;
 };
 
-// the tile again: voxel keys of the valid pixels, emitted in pixel order at the tile's scanned offset
+// the tile again: voxel keys of the valid pixels, emitted in pixel order at the tile's scanned offset.  KeyT = u64:
+// the frame in the key's top bits (one sort over the batch); u32: the voxel index only (segmented sort by frame)
+template <typename KeyT>
 __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, const int* __restrict__ toff,
-                                                        unsigned long long* __restrict__ keys,
-                                                        unsigned* __restrict__ vals) {
+                                                        KeyT* __restrict__ keys, unsigned* __restrict__ vals) {
     const int f = blockIdx.y, tile = blockIdx.x;
     const int npx = p.w * p.h;
     const int pix0 = tile * FB_TILE + threadIdx.x * FB_PIX;
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
     __syncthreads();
     int pos = toff[(int64_t)f * p.tpf + tile] + inc - c;
     for (int w = 0; w < wid; ++w) pos += wsum[w];
-    const unsigned long long fkey = (unsigned long long)f << kb.vbits;
+    const unsigned long long fkey = sizeof(KeyT) == 8 ? (unsigned long long)f << kb.vbits : 0ull;
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
         double xyz[3];
@@ -278,8 +279,8 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
             long long kk[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
-            keys[pos] = fkey | (((unsigned long long)kk[0] * kb.ny + (unsigned long long)kk[1]) * kb.nz +
-                                (unsigned long long)kk[2]);
+            keys[pos] = (KeyT)(fkey | (((unsigned long long)kk[0] * kb.ny + (unsigned long long)kk[1]) * kb.nz +
+                                       (unsigned long long)kk[2]));
             vals[pos] = (unsigned)((int64_t)f * npx + pix0 + k);
             ++pos;
         }
@@ -336,15 +337,15 @@ __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* _
     }
 }
 
-// offs[f] = first segment whose frame is >= f (f = 0..F); segment frame = its key >> fshift
-__global__ void k_fb_frame_offsets(const unsigned long long* __restrict__ skeys, const int* __restrict__ heads,
-                                   int64_t K, int fshift, int F, int* __restrict__ offs) {
+// offs[f] = first voxel whose frame is >= f (f = 0..F); a voxel's frame = its first point's global pixel / npx
+__global__ void k_fb_frame_offsets(const unsigned* __restrict__ sval, const int* __restrict__ heads, int64_t K,
+                                   int npx, int F, int* __restrict__ offs) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f > F) return;
     int64_t lo = 0, hi = K;
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
-        if ((int)(skeys[heads[mid]] >> fshift) < f) lo = mid + 1;
+        if ((int)(sval[heads[mid]] / (unsigned)npx) < f) lo = mid + 1;
         else hi = mid;
     }
     offs[f] = (int)lo;
@@ -385,6 +386,16 @@ __global__ __launch_bounds__(256) void k_fb_gather(const int64_t* __restrict__ k
     }
     oidx[t] = i - voff[lo];
 }
+
+// voxel heads of the segmented (u32-key) sort: a new key, or the first point of a frame
+struct SegHeadPred32 {
+    const unsigned* keys;
+    const unsigned* vals;
+    unsigned npx;
+    __device__ bool operator()(int64_t i) const {
+        return i == 0 || keys[i] != keys[i - 1] || vals[i] / npx != vals[i - 1] / npx;
+    }
+};
 
 struct KeptEmit {
     int64_t* out;
@@ -560,15 +571,28 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     if (!kin || !vin || !heads) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
     unsigned long long* kout = kin + P;
     unsigned* vout = vin + P;
-    hipLaunchKernelGGL(k_fb_keys, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb, (const int*)d_tc, kin, vin);
-    OT_LAUNCH_CHECK();
-    ot_status st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)P, end_bit, stream, 3);
-    if (st != OT_OK) return st;
+    ot_status st;
     int64_t K = 0;
-    st = compact(P, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises (sync 2)
+    if (vbits <= 32 && F <= 64) {  // 32-bit voxel keys, one sort segment per frame: 8 B per pair per pass
+        unsigned* k32 = (unsigned*)kin;
+        unsigned* k32o = k32 + P;
+        hipLaunchKernelGGL(k_fb_keys<unsigned>, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb, (const int*)d_tc,
+                           k32, vin);
+        OT_LAUNCH_CHECK();
+        st = sort_segments_u32_u32(k32, k32o, vin, vout, fl->poff.data(), F, vbits, stream, 3);
+        if (st != OT_OK) return st;
+        st = compact(P, SegHeadPred32{k32o, vout, (unsigned)npx}, SegHeadEmit{heads}, stream, &K, 7);  // sync 2
+    } else {
+        hipLaunchKernelGGL(k_fb_keys<unsigned long long>, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb,
+                           (const int*)d_tc, kin, vin);
+        OT_LAUNCH_CHECK();
+        st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)P, end_bit, stream, 3);
+        if (st != OT_OK) return st;
+        st = compact(P, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises (sync 2)
+    }
     if (st != OT_OK) return st;
-    hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned long long*)kout,
-                       (const int*)heads, K, vbits, F, d_voff);
+    hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)vout,
+                       (const int*)heads, K, npx, F, d_voff);
     fl->K = K;
     // ---- voxel averages (frame-major, key order inside a frame) ----------------------------------------------
     double* vox = (double*)fl->b_vox.get((size_t)K * 48 + 256);

@@ -53,3 +53,27 @@ def test_sort_presorted_and_reversed(pkg, gpu):
         k, v = _sort(pkg, keys, 20)
         order = np.argsort(keys, kind="stable")
         assert_bitwise(v, order.astype(np.uint32), "sort order (structured input)")
+
+
+@pytest.mark.parametrize("sizes,end_bit", [
+    ([0, 1, 2047, 2048, 2049, 0, 5], 12), ([812746, 810001, 0, 799999], 28), ([100000] * 33, 32), ([3] * 64, 2),
+])
+def test_segmented_sort_bitexact(pkg, gpu, sizes, end_bit):
+    """sort_segments_u32_u32 (the batched configs[2] voxel sort): every segment sorted stably on its own, nothing
+    crosses a boundary; vs numpy's stable argsort per segment."""
+    L = pkg._lib
+    rng = np.random.default_rng(sum(sizes) + end_bit)
+    n = int(sum(sizes))
+    seg = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    keys = rng.integers(0, 1 << end_bit, max(n, 1), dtype=np.uint64).astype(np.uint32)[:n]
+    keys[: n // 3] = keys[: n // 3] % 7  # duplicates: stability
+    kin = torch.from_numpy(keys.view(np.int32)).cuda()
+    vin = torch.arange(n, dtype=torch.int32, device="cuda")
+    kout = torch.empty_like(kin)
+    vout = torch.empty_like(vin)
+    L.call("otx_sort_segments_u32_u32", C.c_void_p(kin.data_ptr()), C.c_void_p(kout.data_ptr()),
+           C.c_void_p(vin.data_ptr()), C.c_void_p(vout.data_ptr()), seg.ctypes.data_as(C.c_void_p), len(sizes),
+           end_bit, C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    order = np.concatenate([seg[s] + np.argsort(keys[seg[s]:seg[s + 1]], kind="stable") for s in range(len(sizes))])
+    assert_bitwise(vout.cpu().numpy().view(np.uint32), order.astype(np.uint32), "segmented sort order")
+    assert_bitwise(kout.cpu().numpy().view(np.uint32), keys[order], "segmented sorted keys")

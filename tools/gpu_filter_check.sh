@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${TAG:-r02f}
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-timeout -k 10 900 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_filter_batch.py tests/test_gpu_eval.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_ftests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${TAG}_ftests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_filter_batch.py tests/test_gpu_eval.py tests/test_gpu_sort.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_ftests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${TAG}_ftests.log; exit 1; }
 tail -2 gpurun_out/${TAG}_ftests.log
 fi
 for v in base ${VARIANTS:-}; do
