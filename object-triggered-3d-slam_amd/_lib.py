@@ -101,7 +101,8 @@ SIGNATURES = {
                                C.POINTER(_p)],
     "ot_rgbd_filter_copy": [_p, _i32, _p, _p, _p, _p, _p, _p, _p],
 }
-_RESTYPES = {"ot_last_error": C.c_char_p, "ot_version": C.c_char_p, "ot_abi_version": C.c_int32}
+_RESTYPES = {"ot_last_error": C.c_char_p, "ot_version": C.c_char_p, "ot_abi_version": C.c_int32,
+             "otx_alloc_count": C.c_longlong}
 
 _lib = None
 _lock = threading.Lock()
@@ -117,6 +118,7 @@ TEST_SIGNATURES = {
     "otx_tsdf_stats": [_p, _p],
     "otx_sort_pairs_u64_u32": [_p, _p, _p, _p, _i64, _i32, _p],
     "otx_sort_segments_u32_u32": [_p, _p, _p, _p, _p, _i32, _i32, _p],
+    "otx_alloc_count": [],
 }
 
 
@@ -166,6 +168,11 @@ def call(name, *args):
         msg = lib.ot_last_error().decode(errors="replace")
         raise OTError(msg or f"{name} failed with status {st}")
     return st
+
+
+def alloc_count() -> int:
+    """Device allocations made so far by the library's grow-only buffers (test / bench hook)."""
+    return int(load().otx_alloc_count())
 
 
 def intrinsics_struct(intr) -> ot_intrinsics:

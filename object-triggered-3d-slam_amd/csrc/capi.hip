@@ -1,6 +1,7 @@
 // capi.hip — C-ABI plumbing: error reporting, version, scratch arena, host-side 4x4 inverse.
 #include "common.h"
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -24,6 +25,10 @@ struct Arena {
     std::vector<size_t> size;
 };
 static thread_local std::vector<Arena> g_arena;
+static std::atomic<long long> g_allocs{0};
+
+void note_alloc() { g_allocs.fetch_add(1, std::memory_order_relaxed); }
+long long g_allocs_count() { return g_allocs.load(std::memory_order_relaxed); }
 
 void* scratch(size_t bytes, int slot) {
     int dev = 0;
@@ -48,6 +53,7 @@ void* scratch(size_t bytes, int slot) {
         }
         a.ptr[slot] = p;
         a.size[slot] = nb;
+        note_alloc();
     }
     return a.ptr[slot];
 }
@@ -89,3 +95,6 @@ const char* ot_version(void) { return "otslam-mi355x 0.1.0 (gfx950)"; }
 int32_t ot_abi_version(void) { return 1; }
 
 }  // extern "C"
+
+// test hook (not part of the drop-in boundary): allocations made by the library's grow-only buffers
+extern "C" long long otx_alloc_count(void) { return ot::g_allocs_count(); }

@@ -31,6 +31,10 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // Grow-only scratch arena (one per device).  Not thread-safe: the facade is single-threaded per process
 // (Open3D's calls are synchronous from one Python thread, SURVEY.md §8(b) Threading).
 void* scratch(size_t bytes, int slot);
+// device allocations made by the library's grow-only buffers so far (scratch arenas, filter handles): a timed
+// region that allocates shows up as a change (bench.py reports it; test hook otx_alloc_count)
+void note_alloc();
+long long g_allocs_count();
 
 // --------------------------------------------------------------------------------- math helpers
 struct Mat4d {

@@ -421,6 +421,7 @@ struct FbBuf {
         const size_t nb = bytes + bytes / 8 + 256;
         if (hipMalloc(&p, nb) != hipSuccess) return nullptr;
         n = nb;
+        note_alloc();
         return p;
     }
     ~FbBuf() {

@@ -133,8 +133,10 @@ def reconstruct_and_merge(cfg, yaml_file=None, pgm_file=None, save_path=None, ob
     else:
         from concurrent.futures import ThreadPoolExecutor
 
+        streams_ = importlib.import_module(pkg + ".streams").worker_streams(T)
+
         def work(t):
-            s = torch.cuda.Stream()
+            s = streams_[t]
             out = {}
             with torch.cuda.stream(s):
                 for j in range(t, len(mine), T):

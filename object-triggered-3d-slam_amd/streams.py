@@ -1,0 +1,26 @@
+"""Worker streams for concurrent independent work inside one process (objects of a rank, frames of a filter stream).
+
+HIP maps every stream onto one of GPU_MAX_HW_QUEUES hardware queues (4 by default) in creation order, and
+torch.cuda.Stream() hands out the next stream of torch's pool.  Streams created ad hoc by successive phases of a
+program therefore land on queues that depend on how many streams were created before: two "concurrent" streams can
+share one hardware queue and run serially (measured: the configs[3] objects leg 19 -> 24 ms, the configs[2] stream
+0.16 -> 0.20 ms/frame, depending on which leg created its streams first).  worker_streams(n) returns the same n
+streams every time (created once, consecutively, per device), so concurrent workers always sit on distinct queues.
+"""
+from __future__ import annotations
+
+import threading
+
+_lock = threading.Lock()
+_streams: dict = {}
+
+
+def worker_streams(n: int) -> list:
+    import torch
+
+    dev = torch.cuda.current_device()
+    with _lock:
+        lst = _streams.setdefault(dev, [])
+        while len(lst) < n:
+            lst.append(torch.cuda.Stream(device=dev))
+        return lst[:n]
