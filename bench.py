@@ -313,12 +313,15 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
     """ONE object's scan (seed 0) on every rank, its volume spatially sharded (ot_tsdf_set_shard:
     rank r keeps the units with owner(key) == r), so N GPUs integrate one object together (strong scaling; at
     N = 1 this is the headline itself).  Timed like the headline (reset + all frames + flush, max over ranks).
-    Then the shards are assembled into one volume (all-gather of packed unit rows + import) -- timed apart as
-    the per-object cost before marching cubes; its unit count must equal the unsharded volume's (rank 0's
-    headline volume is the same seed-0 scan)."""
+    Then marching cubes over the shards with a border halo (distributed.extract_sharded_mesh: all-gather of the
+    units' 721 low-face voxels, halo import, own-unit extraction, all-gather + merge of the partial meshes) -- timed
+    apart as the per-object cost before normals / sampling; assemble_bytes = border rows each rank receives (the
+    old whole-unit all-gather's bytes beside it), and the merged mesh must equal rank 0's unsharded mesh."""
     import importlib
 
+    pkg = importlib.import_module(PKG)
     Dm = importlib.import_module(PKG + ".distributed")
+    integ = pkg.pipelines.integration
     intr_t = synth.REF_INTRINSICS_640
     W, H = intr_t[0], intr_t[1]
     depth, color, ext = synth.make_sequence(synth.Scene(seed=0), n_frames=args.frames, intr=intr_t)
@@ -327,57 +330,55 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
     ext = np.ascontiguousarray(ext, dtype=np.float64)
     intr = L.ot_intrinsics(W, H, *intr_t[2:])
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    vol = C.c_void_p()
-    L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
-    L.call("ot_tsdf_set_shard", vol, rank, world)
-    if args.batch > 0:
-        L.call("ot_tsdf_set_batch", vol, args.batch)
+
+    def make(shard):
+        v = integ.ScalableTSDFVolume(voxel_length=args.voxel, sdf_trunc=args.sdf_trunc,
+                                     color_type=integ.TSDFVolumeColorType.RGB8)
+        if shard:
+            v.set_shard(rank, world)
+        if args.batch > 0:
+            v.set_batch(args.batch)
+        return v
+
+    vol = make(True)
     npx = W * H
     dptrs = [C.c_void_p(d_depth.data_ptr() + k * npx * 2) for k in range(args.frames)]
     cptrs = [C.c_void_p(d_color.data_ptr() + k * npx * 3) for k in range(args.frames)]
     eptrs = [ext[k].ctypes.data_as(C.c_void_p) for k in range(args.frames)]
     integrate, pintr = lib.ot_tsdf_integrate_u16, C.byref(intr)
 
-    def step():
-        L.call("ot_tsdf_reset_async", vol, stream)
+    def step(v=vol):
+        L.call("ot_tsdf_reset_async", v._h, stream)
         for k in range(args.frames):
-            if integrate(vol, dptrs[k], cptrs[k], pintr, eptrs[k], 1000.0, 3.0, stream):
+            if integrate(v._h, dptrs[k], cptrs[k], pintr, eptrs[k], 1000.0, 3.0, stream):
                 raise RuntimeError(lib.ot_last_error().decode())
-        L.call("ot_tsdf_flush", vol, stream)
+        L.call("ot_tsdf_flush", v._h, stream)
 
     dt, _ = _timed(torch, dist, world, step, args.steps)
-    nu = C.c_int64(0)
-    L.call("ot_tsdf_num_units", vol, C.byref(nu), stream)
-    cnt = Dm.all_gather_rows(torch.tensor([[nu.value]], dtype=torch.int64, device=COLL_DEV)).flatten().tolist()
+    nu = vol.num_units()
+    cnt = Dm.all_gather_rows(torch.tensor([[nu]], dtype=torch.int64, device=COLL_DEV)).flatten().tolist()
+    group = None
 
     def assemble():
-        n = nu.value
-        keys = torch.empty((n, 3), dtype=torch.int32, device="cuda")
-        f = [torch.empty((n, 4096, k), dtype=torch.float32, device="cuda") for k in (1, 1, 3)]
-        L.call("ot_tsdf_export_units", vol, n, C.c_void_p(keys.data_ptr()), *[C.c_void_p(t.data_ptr()) for t in f],
-               stream)
-        rows = Dm.pack_units(keys, *f)
-        rows = Dm.all_gather_rows(rows if COLL_DEV == "cuda" else rows.cpu())
-        rows = rows.cuda()
-        merged = C.c_void_p()
-        L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, max(32768, rows.shape[0]),
-               C.byref(merged))
-        k2, t2, w2, c2 = Dm.unpack_units(rows)
-        L.call("ot_tsdf_import_units", merged, rows.shape[0], C.c_void_p(k2.data_ptr()), C.c_void_p(t2.data_ptr()),
-               C.c_void_p(w2.data_ptr()), C.c_void_p(c2.data_ptr()), stream)
-        total = C.c_int64(0)
-        L.call("ot_tsdf_num_units", merged, C.byref(total), stream)
-        L.call("ot_tsdf_destroy", merged)
-        return total.value
+        return Dm.extract_sharded_mesh(vol, group)
 
-    t_asm, merged_units = _timed(torch, dist, world, assemble, 1)
-    L.call("ot_tsdf_destroy", vol)
+    t_asm, (mesh, border_bytes) = _timed(torch, dist, world, assemble, 1)
+    whole = sum(cnt) * (3 + 4096 * (2 + 6)) * 4  # the whole-unit all-gather (f64 colour rows) it replaces
+    match = None
+    if rank == 0:  # the unsharded volume of the same scan, extracted on rank 0 (untimed)
+        ref = make(False)
+        step(ref)
+        m0 = ref.extract_triangle_mesh()
+        match = bool(torch.equal(mesh._v.dev(), m0._v.dev()) and torch.equal(mesh._t.dev(), m0._t.dev()) and
+                     torch.equal(mesh._vc.dev(), m0._vc.dev()))
+        del ref
     return {"workload": f"configs[1] scan (seed 0) as ONE object spatially sharded over {world} GPU(s): unit owner = "
-                        f"hash(key) mod {world}, every rank integrates every frame into its own units",
+                        f"hash(key) mod {world}, every rank integrates every frame into its own units; marching "
+                        "cubes with a border halo",
             "scaling": "strong", "frames_per_s": round(args.frames * 1.0 / dt, 1), "ms_per_step": round(dt * 1e3, 3),
             "units_per_rank_min": min(cnt), "units_per_rank_max": max(cnt), "assemble_ms": round(t_asm * 1e3, 2),
-            "assembled_units": merged_units, "units_match_unsharded": merged_units == units_rank0 if rank == 0
-            else None}
+            "assemble_bytes": border_bytes, "whole_unit_bytes": whole,
+            "mesh_vertices": int(mesh._v.dev().shape[0]), "mesh_matches_unsharded": match}
 
 
 def single_frame(L, synth, torch, depth, color, ext, intr_t, reps=50):

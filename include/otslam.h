@@ -219,6 +219,20 @@ ot_status ot_tsdf_import_units_color64(ot_tsdf* vol, int64_t n, const int32_t* k
  * to one unsharded volume.  Call before the first integrate. */
 ot_status ot_tsdf_set_shard(ot_tsdf* vol, int32_t rank, int32_t world);
 
+/* Border halo of a spatially sharded volume (SURVEY §8(e) "all-gather of border faces"; not an Open3D API).
+ * export_border: per OWN unit (sorted key order; halo units are not exported) its 721 low-face voxels (x == 0 ||
+ * y == 0 || z == 0, increasing x*256 + y*16 + z): keys int32 [n][3], tsdf / weight f32 [n][721], colour
+ * [n][721][3] in the volume's colour precision (f32, or f64 after ot_tsdf_set_color_precision(64); NULL to skip);
+ * the row count to *n_exported_host (capacity: rows the buffers hold, ot_tsdf_num_units is enough).
+ * import_border: rows of other shards; a row becomes a halo unit when its key is not owned by this shard and one of
+ * its -x/-y/-z neighbours is (marching cubes of the own units reads exactly these voxels); other rows are skipped.
+ * Marching cubes of a sharded volume then emits only the own units' cubes; ot_tsdf_fetch_mesh_keys gives the keys
+ * that merge the shards' meshes into the unsharded mesh (distributed.extract_sharded_mesh). */
+ot_status ot_tsdf_export_border(ot_tsdf* vol, int64_t capacity, int32_t* keys, float* tsdf, float* weight, void* color,
+                                int64_t* n_exported_host, void* stream);
+ot_status ot_tsdf_import_border(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf, const float* weight,
+                                const void* color, void* stream);
+
 /* volume.extract_triangle_mesh() — reconstruct_rgbd_filter.py:112 (marching cubes, Appendix A.4).
  * Runs the extraction and stores the mesh inside the handle; returns its sizes.  Vertices are ordered by
  * (unit key, local voxel, edge) — a canonical order; Open3D's is hash order. */
@@ -228,6 +242,10 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices_host, 
  * triangles int32 [T][3].  Device pointers. */
 ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors,
                                       int32_t* triangles, void* stream);
+/* Merge keys of the extracted mesh (device pointers, NULL to skip): per vertex int32 [V][4] = owner unit key
+ * (x, y, z) and edge bit (local voxel x*256+y*16+z times 3 plus axis) -- the canonical vertex order; per triangle
+ * int32 [T][3] = the unit key of its cube. */
+ot_status ot_tsdf_fetch_mesh_keys(ot_tsdf* vol, int32_t* vertex_keys, int32_t* triangle_units, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------
  * Triangle meshes

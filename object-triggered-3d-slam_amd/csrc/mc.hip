@@ -42,6 +42,8 @@ struct McDev {
     long long* vert_cnt;         // [rank]
     long long* tri_base;         // [rank]
     long long* vert_base;        // [rank]
+    int4* vk;                    // per vertex: owner unit key + edge bit (the merge key of a sharded extraction)
+    int32_t* tk;                 // per triangle: its cube's unit key
 };
 
 __device__ inline int find_unit(const TsdfDev& d, int x, int y, int z) {
@@ -84,6 +86,14 @@ __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
     const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
+    // a spatially sharded volume emits only its own units' cubes; its halo units (other ranks' border voxels,
+    // ot_tsdf_import_border) are read as neighbours and own the vertices of the edges on them
+    if (d.shard_world > 1 &&
+        !unit_owned(d, pack_key(d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]))) {
+        *reinterpret_cast<uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16) = make_uint4(0u, 0u, 0u, 0u);
+        if (t == 0) m.tri_cnt[r] = 0;
+        return;
+    }
     if (t < 8) snbr[t] = m.nbr[id * 8 + t];
     for (int w = t; w < EWORDS; w += 256) sflags[w] = 0u;
     __syncthreads();
@@ -236,6 +246,7 @@ __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, doub
         pt[axis] += f0 * vl / (f0 + f1);
 #pragma unroll
         for (int a = 0; a < 3; ++a) V[vid * 3 + a] = pt[a];
+        if (m.vk) m.vk[vid] = make_int4(kx, ky, kz, gbit);
         if (VC) {
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -259,11 +270,12 @@ __device__ inline int edge_vid(const McDev& m, const int* snbr, int x, int y, in
     return (int)(m.vert_base[m.rank_of[owner]] + m.wprefix[(size_t)owner * EWORDS + word] + __popc(below));
 }
 
-__global__ __launch_bounds__(256) void k_mc_triangles(McDev m, int32_t* T) {
+__global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_t* T) {
     __shared__ int snbr[8];
     const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
+    const int ukey[3] = {d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]};
     if (t < 8) snbr[t] = m.nbr[id * 8 + t];
     const uint4 q = *reinterpret_cast<const uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16);
     const unsigned cw[4] = {q.x, q.y, q.z, q.w};
@@ -284,6 +296,11 @@ __global__ __launch_bounds__(256) void k_mc_triangles(McDev m, int32_t* T) {
             T[out * 3 + 0] = a;
             T[out * 3 + 1] = c;
             T[out * 3 + 2] = b;
+            if (m.tk) {
+                m.tk[out * 3 + 0] = ukey[0];
+                m.tk[out * 3 + 1] = ukey[1];
+                m.tk[out * 3 + 2] = ukey[2];
+            }
             ++out;
         }
     }
@@ -345,6 +362,8 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
     McDev m;
     m.sorted_ids = vol->sorted_ids;
+    m.vk = nullptr;
+    m.tk = nullptr;
     char* p = ws;
     auto take = [&](size_t n) {
         char* q = p;
@@ -386,9 +405,15 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     if (st != OT_OK) return st;
     st = grow(mb.t, mb.cap_t, nt * 3);
     if (st != OT_OK) return st;
+    st = grow(mb.vk, mb.cap_vk, nv);  // merge keys: 16 B per vertex, 12 B per triangle
+    if (st != OT_OK) return st;
+    st = grow(mb.tk, mb.cap_tk, nt * 3);
+    if (st != OT_OK) return st;
+    m.vk = mb.vk;
+    m.tk = mb.tk;
     hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, stream, vol->dev, m, vol->voxel_length, mb.v,
                        vol->color_type == OT_COLOR_RGB8 ? mb.c : nullptr);
-    hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, m, mb.t);
+    hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, mb.t);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(stream));
     mb.nv = nv;
@@ -413,6 +438,20 @@ ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* ve
     }
     if (mb.nt > 0 && triangles)
         OT_HIP_TRY(hipMemcpyAsync(triangles, mb.t, sizeof(int32_t) * 3 * mb.nt, hipMemcpyDefault, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
+}
+
+// merge keys of the extracted mesh: per vertex (owner unit x, y, z, edge bit = local voxel * 3 + axis), per
+// triangle its cube's unit key (x, y, z).  Device pointers; either may be NULL.
+ot_status ot_tsdf_fetch_mesh_keys(ot_tsdf* vol, int32_t* vertex_keys, int32_t* triangle_units, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    const MeshBuffers& mb = vol->mesh;
+    if (mb.nv > 0 && vertex_keys)
+        OT_HIP_TRY(hipMemcpyAsync(vertex_keys, mb.vk, sizeof(int4) * mb.nv, hipMemcpyDefault, stream));
+    if (mb.nt > 0 && triangle_units)
+        OT_HIP_TRY(hipMemcpyAsync(triangle_units, mb.tk, sizeof(int32_t) * 3 * mb.nt, hipMemcpyDefault, stream));
     OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
 }

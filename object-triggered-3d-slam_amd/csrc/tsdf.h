@@ -74,6 +74,21 @@ __device__ inline double* color_base<double>(const TsdfDev& d, int id) {
     return d.vcol + (size_t)id * 3 * UNIT_VOX;
 }
 
+// Border voxels of a unit: every voxel with x == 0, y == 0 or z == 0 (3 * 256 - 3 * 16 + 1 = 721), the only
+// voxels of a unit that marching cubes reads from its -x/-y/-z neighbours (the 17^3 tile of a unit is the unit plus
+// the low faces of its +1 neighbours).  Order: increasing Open3D index x*256 + y*16 + z.
+constexpr int BORDER_VOX = 721;
+__host__ __device__ inline void border_voxel(int b, int& x, int& y, int& z) {
+    if (b < 256) {
+        x = 0, y = b >> 4, z = b & 15;
+        return;
+    }
+    const int c = b - 256, r = c % 31;
+    x = 1 + c / 31;
+    if (r < 16) y = 0, z = r;
+    else y = r - 15, z = 0;
+}
+
 constexpr int MAX_BATCH = 64;  // frames per fused launch (one bit each in fmask)
 
 // per-frame parameters of a batch (device resident)
@@ -103,8 +118,10 @@ struct MeshBuffers {
     double* v = nullptr;
     double* c = nullptr;
     int32_t* t = nullptr;
+    int4* vk = nullptr;     // per vertex: owner unit key (x, y, z) and edge bit (local voxel * 3 + axis)
+    int32_t* tk = nullptr;  // per triangle: its cube's unit key (x, y, z)
     int64_t nv = 0, nt = 0;
-    int64_t cap_v = 0, cap_t = 0;
+    int64_t cap_v = 0, cap_t = 0, cap_vk = 0, cap_tk = 0;
 };
 
 }  // namespace ot

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <type_traits>
 
+#include "compact.h"
 #include "sort.h"
 #include "tsdf.h"
 
@@ -817,6 +818,132 @@ __global__ __launch_bounds__(256) void k_export(TsdfDev d, const unsigned* sorte
     }
 }
 
+// border export: the BORDER_VOX low-face voxels of every unit, units in sorted order; colour as the volume keeps it
+template <typename CT>
+__global__ __launch_bounds__(256) void k_export_border(TsdfDev d, const unsigned* sorted_ids, int32_t* keys,
+                                                       float* tsdf, float* weight, CT* color) {
+    const int r = blockIdx.x;
+    const int id = (int)sorted_ids[r];
+    const float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    const CT* cbase = color_base<CT>(d, id);
+    if (threadIdx.x < 3) keys[(int64_t)r * 3 + threadIdx.x] = d.unit_keys[id * 3 + threadIdx.x];
+    for (int b = threadIdx.x; b < BORDER_VOX; b += 256) {
+        int x, y, z;
+        border_voxel(b, x, y, z);
+        const int vi = z * 256 + x * 16 + y;
+        const int64_t o = (int64_t)r * BORDER_VOX + b;
+        tsdf[o] = base[vi];
+        weight[o] = base[UNIT_VOX + vi];
+        if (color) {
+            color[o * 3 + 0] = cbase[vi];
+            color[o * 3 + 1] = cbase[UNIT_VOX + vi];
+            color[o * 3 + 2] = cbase[2 * UNIT_VOX + vi];
+        }
+    }
+}
+
+__device__ inline int find_unit_id(const TsdfDev& d, int x, int y, int z) {
+    if (!key_in_range(x, y, z)) return -1;
+    const unsigned long long key = pack_key(x, y, z);
+    unsigned slot = (unsigned)mix64(key) & (unsigned)d.hash_mask;
+    for (int probe = 0; probe <= d.hash_mask; ++probe) {
+        const unsigned long long k = d.hkeys[slot];
+        if (k == key) {
+            const int id = d.hvals[slot];
+            return id < d.max_units ? id : -1;
+        }
+        if (k == KEY_EMPTY) return -1;
+        slot = (slot + 1) & (unsigned)d.hash_mask;
+    }
+    return -1;
+}
+
+// border import (halo): a row becomes a halo unit of this volume when its key is not owned here and one of its
+// -x/-y/-z neighbours (the units whose marching cubes read it) is; a new halo unit is zeroed (weight 0 = unobserved)
+// and receives the border voxels.  Rows of owned or unneeded units are skipped.
+template <typename CT>
+__global__ __launch_bounds__(256) void k_import_border(TsdfDev d, const int32_t* __restrict__ keys,
+                                                       const float* __restrict__ tsdf, const float* __restrict__ weight,
+                                                       const CT* __restrict__ color) {
+    __shared__ int s_id, s_fresh;
+    const int r = blockIdx.x;
+    if (threadIdx.x == 0) {
+        const int x = keys[(int64_t)r * 3], y = keys[(int64_t)r * 3 + 1], z = keys[(int64_t)r * 3 + 2];
+        int id = -1, fresh = 0;
+        bool needed = false;
+        if (key_in_range(x, y, z) && !unit_owned(d, pack_key(x, y, z))) {
+            for (int t = 1; t < 8 && !needed; ++t) {
+                const int nx = x - ((t >> 2) & 1), ny = y - ((t >> 1) & 1), nz = z - (t & 1);
+                needed = key_in_range(nx, ny, nz) && unit_owned(d, pack_key(nx, ny, nz)) &&
+                         find_unit_id(d, nx, ny, nz) >= 0;
+            }
+        }
+        if (needed) {
+            const int slot = hash_insert(d, pack_key(x, y, z));
+            if (slot < 0) {
+                atomicOr(&d.counters[C_HASHERR], 1);
+            } else {
+                id = d.hvals[slot];
+                if (id < 0) {
+                    id = atomicAdd(&d.counters[C_UNITS], 1);
+                    if (id >= d.max_units) {
+                        atomicOr(&d.counters[C_OVERFLOW], 1);
+                        id = -1;
+                    } else {
+                        d.hvals[slot] = id;
+                        d.unit_keys[id * 3 + 0] = x;
+                        d.unit_keys[id * 3 + 1] = y;
+                        d.unit_keys[id * 3 + 2] = z;
+                        fresh = 1;
+                    }
+                }
+            }
+        }
+        s_id = id;
+        s_fresh = fresh;
+    }
+    __syncthreads();
+    const int id = s_id;
+    if (id < 0) return;
+    float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    CT* cbase = color_base<CT>(d, id);
+    if (s_fresh) {
+        for (int vi = threadIdx.x; vi < UNIT_VOX; vi += 256) {
+            base[vi] = 0.0f;
+            base[UNIT_VOX + vi] = 0.0f;
+            cbase[vi] = cbase[UNIT_VOX + vi] = cbase[2 * UNIT_VOX + vi] = (CT)0;
+        }
+        __syncthreads();
+    }
+    for (int b = threadIdx.x; b < BORDER_VOX; b += 256) {
+        int x, y, z;
+        border_voxel(b, x, y, z);
+        const int vi = z * 256 + x * 16 + y;
+        const int64_t o = (int64_t)r * BORDER_VOX + b;
+        base[vi] = tsdf[o];
+        base[UNIT_VOX + vi] = weight[o];
+        cbase[vi] = color ? color[o * 3 + 0] : (CT)0;
+        cbase[UNIT_VOX + vi] = color ? color[o * 3 + 1] : (CT)0;
+        cbase[2 * UNIT_VOX + vi] = color ? color[o * 3 + 2] : (CT)0;
+    }
+}
+
+// owned units of the sorted order (a sharded volume's own units; every unit when unsharded)
+struct OwnedPred {
+    TsdfDev d;
+    const unsigned* sorted_ids;
+    __device__ bool operator()(int64_t r) const {
+        const int id = (int)sorted_ids[r];
+        return d.shard_world <= 1 ||
+               unit_owned(d, pack_key(d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]));
+    }
+};
+struct OwnedEmit {
+    const unsigned* sorted_ids;
+    unsigned* out;
+    __device__ void operator()(int64_t r, int64_t pos) const { out[pos] = sorted_ids[r]; }
+};
+
 // import: the inverse of k_export (keys unique within one call; an existing unit is overwritten); colour as the
 // volume keeps it (CT)
 template <typename CT>
@@ -1284,7 +1411,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
     void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, d.vcol, v->mult,
-                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, d.fmask, d.bslots, d.work,
+                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, d.fmask, d.bslots, d.work,
                     v->bframes, v->bdm, v->brgba};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1544,6 +1671,57 @@ ot_status ot_tsdf_import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, con
 ot_status ot_tsdf_import_units_color64(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf,
                                        const float* weight, const double* color, void* stream) {
     return import_units<double>(vol, n, keys, tsdf, weight, color, S(stream));
+}
+
+ot_status ot_tsdf_export_border(ot_tsdf* vol, int64_t capacity, int32_t* keys, float* tsdf, float* weight, void* color,
+                                int64_t* n_exported_host, void* stream) {
+    if (!vol || !keys || !tsdf || !weight || !n_exported_host) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    *n_exported_host = 0;
+    int64_t nu = 0;
+    ot_status st = tsdf_sorted_units(vol, S(stream), &nu);
+    if (st != OT_OK) return st;
+    if (nu == 0) return OT_OK;
+    unsigned* own = (unsigned*)scratch(sizeof(unsigned) * (size_t)nu + 256, 16);
+    if (!own) return fail(OT_ERR_HIP, "scratch allocation failed");
+    int64_t no = 0;  // the own units (halo units imported earlier are not this shard's border)
+    st = compact(nu, OwnedPred{vol->dev, vol->sorted_ids}, OwnedEmit{vol->sorted_ids, own}, S(stream), &no, 13);
+    if (st != OT_OK) return st;
+    if (no > capacity) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] export: more units than the output capacity");
+    if (no > 0) {
+        if (vol->color64)
+            hipLaunchKernelGGL(k_export_border<double>, dim3((unsigned)no), dim3(256), 0, S(stream), vol->dev, own,
+                               keys, tsdf, weight, (double*)color);
+        else
+            hipLaunchKernelGGL(k_export_border<float>, dim3((unsigned)no), dim3(256), 0, S(stream), vol->dev, own,
+                               keys, tsdf, weight, (float*)color);
+        OT_LAUNCH_CHECK();
+    }
+    OT_HIP_TRY(hipStreamSynchronize(S(stream)));
+    *n_exported_host = no;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_import_border(ot_tsdf* vol, int64_t n, const int32_t* keys, const float* tsdf, const float* weight,
+                                const void* color, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!vol || n < 0 || (n > 0 && (!keys || !tsdf || !weight)))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import_border: invalid arguments");
+    ot_status st = tsdf_flush(vol, stream);
+    if (st != OT_OK) return st;
+    if (n == 0) return OT_OK;
+    const void* c = vol->color_type == OT_COLOR_RGB8 ? color : nullptr;
+    if (vol->color64)
+        hipLaunchKernelGGL(k_import_border<double>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf,
+                           weight, (const double*)c);
+    else
+        hipLaunchKernelGGL(k_import_border<float>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf,
+                           weight, (const float*)c);
+    OT_LAUNCH_CHECK();
+    vol->sorted_units = -1;
+    st = check_errors(vol, stream);
+    if (st != OT_OK) return st;
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
 }
 
 }  // extern "C"

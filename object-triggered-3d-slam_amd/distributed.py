@@ -93,6 +93,101 @@ def assemble_sharded_volume(volume, group=None):
     return merged
 
 
+BORDER_VOX = 721  # low-face voxels per unit (tsdf.h)
+
+
+def pack_border(keys, tsdf, weight, color):
+    """export_border's arrays -> one int32 row per unit (floats as raw bits: the exchange is exact)."""
+    import torch
+
+    n = keys.shape[0]
+    return torch.cat([keys.reshape(n, 3).to(torch.int32), tsdf.reshape(n, BORDER_VOX).view(torch.int32),
+                      weight.reshape(n, BORDER_VOX).view(torch.int32),
+                      color.reshape(n, -1).contiguous().view(torch.int32)], 1)
+
+
+def unpack_border(rows):
+    """Inverse of pack_border; the row width tells float32 from float64 colours."""
+    import torch
+
+    n = rows.shape[0]
+    f = rows[:, 3:3 + 2 * BORDER_VOX].contiguous().view(torch.float32)
+    c = rows[:, 3 + 2 * BORDER_VOX:].contiguous()
+    c = c.view(torch.float64) if rows.shape[1] == 3 + BORDER_VOX * 8 else c.view(torch.float32)
+    return (rows[:, :3].contiguous(), f[:, :BORDER_VOX].contiguous(), f[:, BORDER_VOX:].contiguous(),
+            c.reshape(n, BORDER_VOX, 3))
+
+
+def merge_shard_meshes(parts):
+    """Shards' marching-cubes outputs -> the unsharded volume's mesh, bit for bit.  parts: per shard
+    (V (n,3) f64, VC (n,3) f64 or None, T (m,3) int32, vertex keys (n,4) int32, triangle unit keys (m,3) int32).
+    A vertex is identified by its edge (owner unit key, edge bit): shards that both reference an edge computed it
+    from the same voxels with the same expression, so duplicates are identical and one is kept.  Vertices come out
+    in the canonical order (unit key, local voxel, axis), triangles in (unit key, voxel, table order) -- every
+    unit's triangles come from its one owner, already in that order."""
+    import torch
+
+    V = torch.cat([p[0] for p in parts])
+    VC = torch.cat([p[1] for p in parts]) if parts[0][1] is not None else None
+    vk = torch.cat([p[3] for p in parts]).to(torch.int64)
+    tk = torch.cat([p[4] for p in parts]).to(torch.int64)
+    # unit ordinals over every key that appears (lexicographic = the volume's packed-key order)
+    units, inv = torch.unique(torch.cat([vk[:, :3], tk]), dim=0, sorted=True, return_inverse=True)
+    vo, to = inv[:vk.shape[0]], inv[vk.shape[0]:]
+    ekey = vo * (4096 * 3) + vk[:, 3]  # (unit ordinal, edge bit): the canonical vertex order
+    uniq, vmap = torch.unique(ekey, sorted=True, return_inverse=True)
+    first = torch.full((uniq.shape[0],), ekey.shape[0], dtype=torch.int64, device=ekey.device)
+    first.scatter_reduce_(0, vmap, torch.arange(ekey.shape[0], device=ekey.device), reduce="amin")
+    Vm = V[first]
+    VCm = VC[first] if VC is not None else None
+    # triangles: shard-local vertex ids -> merged ids; units in key order, each unit's block kept as emitted
+    offs, tris = 0, []
+    for p in parts:
+        tris.append(vmap[offs + p[2].to(torch.int64)])
+        offs += p[0].shape[0]
+    Tm = torch.cat(tris)
+    order = torch.sort(to, stable=True).indices
+    return Vm, VCm, Tm[order].to(torch.int32)
+
+
+def extract_sharded_mesh(volume, group=None):
+    """Marching cubes of ONE object whose volume is spatially sharded over the ranks (ot_tsdf_set_shard), with a
+    border halo instead of whole units: every rank all-gathers the ranks' border rows (721 low-face
+    voxels per unit, ~1/5.7 of a unit), imports the ones its own units' cubes read (halo units), extracts the own
+    units' cubes, and the partial meshes are all-gathered and merged (merge_shard_meshes) into the unsharded
+    volume's mesh on every rank.  Returns (TriangleMesh, bytes of border rows this rank received)."""
+    import torch
+
+    from .geometry import TriangleMesh, _Arr
+
+    rows = pack_border(*volume.export_border())
+    allrows = all_gather_rows(rows, group)
+    volume.import_border(*unpack_border(allrows))
+    mesh, vk, tk = volume.extract_triangle_mesh(with_keys=True)
+    V = mesh._v.dev()
+    VC = mesh._vc.dev() if mesh._vc is not None else torch.zeros_like(V)
+    T = mesh._t.dev()
+    vrows = torch.cat([V.view(torch.int32), VC.view(torch.int32), vk], 1)  # 6 + 6 + 4 int32 per vertex
+    trows = torch.cat([T, tk], 1)
+    av = all_gather_rows(vrows, group)
+    at = all_gather_rows(trows, group)
+    nv = all_gather_rows(torch.tensor([[V.shape[0], T.shape[0]]], dtype=torch.int64, device=V.device), group)
+    parts, ov, ot = [], 0, 0
+    for r in range(nv.shape[0]):
+        a, b = int(nv[r, 0]), int(nv[r, 1])
+        vr, tr = av[ov:ov + a], at[ot:ot + b]
+        parts.append((vr[:, :6].contiguous().view(torch.float64), vr[:, 6:12].contiguous().view(torch.float64),
+                      tr[:, :3].contiguous(), vr[:, 12:].contiguous(), tr[:, 3:].contiguous()))
+        ov, ot = ov + a, ot + b
+    Vm, VCm, Tm = merge_shard_meshes(parts)
+    out = TriangleMesh()
+    out._v = _Arr(dev=Vm)
+    out._t = _Arr(dev=Tm)
+    if mesh._vc is not None:
+        out._vc = _Arr(dev=VCm)
+    return out, int(allrows.numel()) * 4
+
+
 def merge_object_clouds(local_clouds, group=None):
     """Rank-ordered concatenation of this rank's object clouds with everyone else's (points only: colours are
     repainted uniformly by the hybrid map, hybrid_map.py:88)."""

@@ -161,8 +161,40 @@ class ScalableTSDFVolume:
         """Keep only the units owned by `rank` of `world` (spatial sharding of one object)."""
         L.call("ot_tsdf_set_shard", self._h, int(rank), int(world))
 
-    def extract_triangle_mesh(self):
-        """ScalableTSDFVolume::ExtractTriangleMesh — GPU marching cubes (mc.hip)."""
+    def export_border(self):
+        """This shard's border (ot_tsdf_export_border): per own unit keys (U,3) int32, tsdf/weight (U,721) f32,
+        colour (U,721,3) in the volume's colour precision -- the low-face voxels that neighbouring units' marching
+        cubes read (halo units imported earlier are not exported)."""
+        n = self.num_units()
+        keys = D.empty((n, 3), "int32")
+        tsdf = D.empty((n, 721), "float32")
+        weight = D.empty((n, 721), "float32")
+        color = D.empty((n, 721, 3), "float64" if self.color_precision == 64 else "float32")
+        m = C.c_int64(0)
+        L.call("ot_tsdf_export_border", self._h, n, D.ptr(keys), D.ptr(tsdf), D.ptr(weight), D.ptr(color),
+               C.byref(m), D.stream_ptr())
+        m = m.value
+        return keys[:m], tsdf[:m], weight[:m], color[:m]
+
+    def import_border(self, keys, tsdf, weight, color=None):
+        """Other shards' border rows (export_border's layout): the ones this shard's marching cubes needs become
+        halo units; the rest are skipped."""
+        keys = D.to_device(keys, "int32")
+        n = int(keys.shape[0])
+        tsdf = D.to_device(tsdf, "float32")
+        weight = D.to_device(weight, "float32")
+        c64 = self.color_precision == 64
+        color = D.to_device(color, "float64" if c64 else "float32") if color is not None else None
+        if tuple(tsdf.shape[-1:]) != (721,) or tsdf.shape[0] != n or weight.shape[0] != n or (
+                color is not None and color.shape[0] != n):
+            raise RuntimeError("[ScalableTSDFVolume] import_border: shapes do not match export_border")
+        L.call("ot_tsdf_import_border", self._h, n, D.ptr(keys), D.ptr(tsdf), D.ptr(weight), D.ptr(color),
+               D.stream_ptr())
+
+    def extract_triangle_mesh(self, with_keys=False):
+        """ScalableTSDFVolume::ExtractTriangleMesh — GPU marching cubes (mc.hip).  with_keys: also return the merge
+        keys (vertex (U,4) int32 = owner unit key + edge bit, triangle (T,3) int32 = its cube's unit key) that
+        distributed.merge_shard_meshes uses."""
         nv, nt = C.c_int64(0), C.c_int64(0)
         L.call("ot_tsdf_extract_triangle_mesh", self._h, C.byref(nv), C.byref(nt), D.stream_ptr())
         self._keep.clear()
@@ -175,4 +207,9 @@ class ScalableTSDFVolume:
         mesh._t = _Arr(dev=T)
         if self.color_type == TSDFVolumeColorType.RGB8:
             mesh._vc = _Arr(dev=VC)
-        return mesh
+        if not with_keys:
+            return mesh
+        vk = D.empty((nv.value, 4), "int32")
+        tk = D.empty((nt.value, 3), "int32")
+        L.call("ot_tsdf_fetch_mesh_keys", self._h, D.ptr(vk), D.ptr(tk), D.stream_ptr())
+        return mesh, vk, tk

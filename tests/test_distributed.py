@@ -111,3 +111,44 @@ def test_sharded_unit_exchange_gloo(sizes):
         for got, e in zip(out[r], exp):
             assert got.shape == e.shape and np.array_equal(got.view(np.uint32) if got.dtype == np.float32 else got,
                                                            e.view(np.uint32) if e.dtype == np.float32 else e)
+
+
+def test_merge_shard_meshes_cpu():
+    """distributed.merge_shard_meshes on a synthetic canonical mesh split by unit ownership (CPU tensors): shared
+    vertices appear in several shards and are kept once, vertices and triangles come out in canonical order."""
+    import importlib
+
+    import torch
+
+    D = importlib.import_module("object-triggered-3d-slam_amd.distributed")
+    g = torch.Generator().manual_seed(0)
+    units = torch.tensor([[-1, 0, 2], [0, 0, 0], [0, 0, 1], [0, 1, 0], [1, -2, 0], [1, 0, 0]], dtype=torch.int64)
+    # canonical vertices: sorted (unit, bit) keys
+    vu = torch.randint(0, units.shape[0], (400,), generator=g)
+    vb = torch.randint(0, 4096 * 3, (400,), generator=g)
+    key = torch.unique(vu * 12288 + vb)
+    vu, vb = key // 12288, key % 12288
+    n = key.shape[0]
+    V = torch.randn(n, 3, dtype=torch.float64, generator=g)
+    VC = torch.rand(n, 3, dtype=torch.float64, generator=g)
+    vk = torch.cat([units[vu], vb[:, None]], 1).to(torch.int32)
+    # triangles grouped by unit (canonical), each referencing random vertices
+    tu = torch.sort(torch.randint(0, units.shape[0], (300,), generator=g)).values
+    T = torch.randint(0, n, (300, 3), generator=g).to(torch.int32)
+    used = torch.unique(T.flatten().long())
+    keep = torch.zeros(n, dtype=torch.bool)
+    keep[used] = True
+    # reference: only referenced vertices survive (MC emits exactly the referenced edges)
+    remap = torch.full((n,), -1, dtype=torch.int64)
+    remap[used] = torch.arange(used.shape[0])
+    Vr, VCr, Tr = V[used], VC[used], remap[T.long()].to(torch.int32)
+    parts = []
+    for shard in range(3):
+        mine = (tu % 3) == shard
+        Ts = T[mine].long()
+        loc = torch.unique(Ts.flatten())
+        lmap = torch.full((n,), -1, dtype=torch.int64)
+        lmap[loc] = torch.arange(loc.shape[0])
+        parts.append((V[loc], VC[loc], lmap[Ts].to(torch.int32), vk[loc], units[tu[mine]].to(torch.int32)))
+    Vm, VCm, Tm = D.merge_shard_meshes(parts)
+    assert torch.equal(Vm, Vr) and torch.equal(VCm, VCr) and torch.equal(Tm, Tr)

@@ -64,6 +64,56 @@ def test_shard_import_mesh_bitexact(pkg, seq16, gpu):
     assert_bitwise(np.asarray(m1.vertex_colors), np.asarray(m0.vertex_colors), "merged-shard mesh colours")
 
 
+@pytest.mark.parametrize("world,precision", [(3, 64), (8, 32)])
+def test_shard_border_halo_mesh_bitexact(pkg, seq16, gpu, world, precision):
+    """SURVEY §8(e) border halo: every shard imports the other shards' border rows (721 low-face voxels per unit)
+    it needs, extracts only its own units' cubes, and the partial meshes merge (distributed.merge_shard_meshes)
+    into the unsharded mesh bit for bit -- without moving whole units."""
+    integ = pkg.pipelines.integration
+    D = importlib.import_module(pkg.__name__ + ".distributed")
+
+    def make(shard=None):
+        v = _integrate_p(pkg, seq16, 0.01, shard, precision)
+        return v
+
+    full = make()
+    m0 = full.extract_triangle_mesh()
+    shards = [make((r, world)) for r in range(world)]
+    rows = [D.pack_border(*v.export_border()) for v in shards]
+    import torch
+
+    allrows = torch.cat(rows)
+    unit_bytes = full.num_units() * (3 + 4096 * (2 + (6 if precision == 64 else 3))) * 4
+    assert allrows.numel() * 4 < unit_bytes / 5  # border layers only
+    parts = []
+    for v in shards:
+        v.import_border(*D.unpack_border(allrows))
+        mesh, vk, tk = v.extract_triangle_mesh(with_keys=True)
+        parts.append((mesh._v.dev(), mesh._vc.dev(), mesh._t.dev(), vk, tk))
+    V, VC, T = D.merge_shard_meshes(parts)
+    assert_bitwise(V.cpu().numpy(), np.asarray(m0.vertices), "halo-merged mesh vertices")
+    assert_bitwise(VC.cpu().numpy(), np.asarray(m0.vertex_colors), "halo-merged mesh colours")
+    assert_bitwise(T.cpu().numpy(), np.asarray(m0.triangles), "halo-merged mesh triangles")
+    # every shard emitted only its own cubes: the triangle counts add up
+    assert sum(p[2].shape[0] for p in parts) == np.asarray(m0.triangles).shape[0]
+
+
+def _integrate_p(pkg, seq, voxel, shard, precision):
+    depth, color, ext = seq
+    integ = pkg.pipelines.integration
+    intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(importlib.import_module(pkg.__name__ + ".synth")))
+    vol = integ.ScalableTSDFVolume(voxel_length=voxel, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                   color_precision=precision)
+    if shard is not None:
+        vol.set_shard(*shard)
+    for k in range(depth.shape[0]):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+            convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+    return vol
+
+
 def test_shard_argument_errors(pkg, seq16, gpu):
     integ = pkg.pipelines.integration
     vol = _integrate(pkg, (seq16[0][:2], seq16[1][:2], seq16[2][:2]), 0.01)
