@@ -34,7 +34,7 @@ class _Arr:
             a = np.asarray(a)
         if D.is_tensor(a):
             return _Arr(dev=a.reshape(-1, cols).contiguous())
-        arr = np.ascontiguousarray(np.asarray(a, dtype=dtype))
+        arr = np.array(a, dtype=dtype, copy=True, order="C")  # assignment copies, as Open3D's does
         if arr.size == 0:
             arr = arr.reshape(0, cols)
         return _Arr(host=arr)
@@ -43,6 +43,13 @@ class _Arr:
         if self._h is None:
             self._h = D.to_host(self._d)
         return self._h
+
+    def host_view(self):
+        """The host array for a writable view handed to the caller: the device copy is dropped, so the next GPU use
+        uploads whatever the caller wrote (Open3D's vectors are views of the one copy)."""
+        h = self.host()
+        self._d = None
+        return h
 
     def dev(self):
         if self._d is None:
@@ -178,7 +185,7 @@ class PointCloud:
     # --- attribute access (host views) ---
     @property
     def points(self):
-        return Vector3dVector(self._xyz.host())
+        return Vector3dVector._view(self._xyz.host_view())
 
     @points.setter
     def points(self, v):
@@ -186,7 +193,7 @@ class PointCloud:
 
     @property
     def colors(self):
-        return Vector3dVector(self._rgb.host() if self._rgb is not None else np.zeros((0, 3)))
+        return Vector3dVector._view(self._rgb.host_view() if self._rgb is not None else np.zeros((0, 3)))
 
     @colors.setter
     def colors(self, v):
@@ -195,7 +202,7 @@ class PointCloud:
 
     @property
     def normals(self):
-        return Vector3dVector(self._nrm.host() if self._nrm is not None else np.zeros((0, 3)))
+        return Vector3dVector._view(self._nrm.host_view() if self._nrm is not None else np.zeros((0, 3)))
 
     @normals.setter
     def normals(self, v):
@@ -438,7 +445,7 @@ class TriangleMesh:
 
     @property
     def vertices(self):
-        return Vector3dVector(self._v.host())
+        return Vector3dVector._view(self._v.host_view())
 
     @vertices.setter
     def vertices(self, v):
@@ -446,7 +453,7 @@ class TriangleMesh:
 
     @property
     def triangles(self):
-        return Vector3iVector(self._t.host())
+        return Vector3iVector._view(self._t.host_view())
 
     @triangles.setter
     def triangles(self, t):
@@ -454,7 +461,7 @@ class TriangleMesh:
 
     @property
     def vertex_colors(self):
-        return Vector3dVector(self._vc.host() if self._vc is not None else np.zeros((0, 3)))
+        return Vector3dVector._view(self._vc.host_view() if self._vc is not None else np.zeros((0, 3)))
 
     @vertex_colors.setter
     def vertex_colors(self, v):
@@ -463,7 +470,7 @@ class TriangleMesh:
 
     @property
     def vertex_normals(self):
-        return Vector3dVector(self._vn.host() if self._vn is not None else np.zeros((0, 3)))
+        return Vector3dVector._view(self._vn.host_view() if self._vn is not None else np.zeros((0, 3)))
 
     @vertex_normals.setter
     def vertex_normals(self, v):

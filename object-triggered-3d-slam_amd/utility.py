@@ -2,6 +2,9 @@
 
 Open3D's vectors are views over std::vector<Eigen::Vector3d>; here they are thin wrappers over a host numpy
 array that `np.asarray(...)` returns without a copy (reconstruct_rgbd_filter.py:126-132 relies on that).
+Constructing one from caller data copies it, as Open3D does (pybind11 builds a new std::vector); the geometry
+getters wrap their own host array without a copy (_view) and drop the device copy, so in-place edits through
+np.asarray(pcd.points) reach the next GPU call.
 """
 from __future__ import annotations
 
@@ -16,12 +19,19 @@ class _VecN:
         if data is None:
             self._a = np.zeros((0, self._cols), self._dtype)
         else:
-            a = np.asarray(data, dtype=self._dtype)
+            a = np.array(data, dtype=self._dtype, copy=True)
             if a.size == 0:
                 a = a.reshape(0, self._cols)
             if a.ndim != 2 or a.shape[1] != self._cols:
                 raise RuntimeError(f"{type(self).__name__} expects an (N, {self._cols}) array, got {a.shape}")
             self._a = np.ascontiguousarray(a)
+
+    @classmethod
+    def _view(cls, arr):
+        """Wrap an existing (N, cols) array without copying (geometry getters)."""
+        v = cls.__new__(cls)
+        v._a = arr
+        return v
 
     def __array__(self, dtype=None, copy=None):
         return self._a if dtype is None else self._a.astype(dtype)
