@@ -622,7 +622,9 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
         }
     OT_HIP_TRY(hipMemcpyAsync(d_org, horg.data(), sizeof(double) * 3 * F, hipMemcpyHostToDevice, stream));
     GridBuild gb;
-    st = build_grid_frames(fl->vx, K, F, d_voff, d_org, hcell, dims, SOR_GRID_NBR, stream, gb, 25);  // synchronises
+    OT_HIP_TRY(hipStreamSynchronize(stream));  // hvoff (copied above) is needed on the host from here
+    st = build_grid_frames(fl->vx, K, F, d_voff, d_org, hcell, dims, SOR_GRID_NBR, stream, gb, 25,
+                           hvoff.data());  // synchronises
     if (st != OT_OK) return st;
     for (int f = 0; f <= F; ++f) fl->voff[f] = hvoff[f];
     double* avg = (double*)fl->b_avg.get((size_t)K * 8 + (size_t)F * 32 + 256);

@@ -63,10 +63,12 @@ struct GridBuild {
 
 // Build the grid of n points (xyz device [n][3]) grouped in nframes frames.  d_foff / d_origin: device arrays
 // ([F+1] ints, [F][3] doubles) that must outlive the grid; dims: cells per axis covering every frame; nbr: the
-// GRID_* structures to precompute.  Scratch
+// GRID_* structures to precompute; h_foff (optional host copy of the frame offsets, <= 64 frames): the cell sort
+// runs per frame (segmented, cell bits only) instead of over frame-prefixed keys.  Scratch
 // slots slot0 .. slot0 + 2.  Synchronises (cell count).
 ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int* d_foff, const double* d_origin,
-                            double h, const int dims[3], int nbr, hipStream_t stream, GridBuild& out, int slot0);
+                            double h, const int dims[3], int nbr, hipStream_t stream, GridBuild& out, int slot0,
+                            const int* h_foff = nullptr);
 
 // Statistical outlier removal over a built grid (Open3D RemoveStatisticalOutliers per frame):
 // avg[i] = mean kNN distance of point i (-1 when none); per frame the cloud mean and squared-deviation sum are

@@ -610,7 +610,8 @@ static int bits_for_host(int64_t v) {  // bits to represent 0..v
 }
 
 ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int* d_foff, const double* d_origin,
-                            double h, const int dims[3], int nbr, hipStream_t stream, GridBuild& out, int slot0) {
+                            double h, const int dims[3], int nbr, hipStream_t stream, GridBuild& out, int slot0,
+                            const int* h_foff) {
     GridDev& g = out.g;
     g.h = h;
     g.origin = d_origin;
@@ -646,7 +647,13 @@ ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int
         hipLaunchKernelGGL(k_cell_keys<unsigned>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, xyz, n, g,
                            k32, vin, err);
         OT_LAUNCH_CHECK();
-        st = sort_pairs_u32_u32(k32, k32o, vin, vout, (size_t)n, std::max(end_bit, 1), stream, 3);
+        if (h_foff && nframes > 1 && nframes <= 64) {  // frames are contiguous: sort each on its cell bits alone
+            std::vector<int64_t> seg((size_t)nframes + 1);
+            for (int f = 0; f <= nframes; ++f) seg[f] = h_foff[f];
+            st = sort_segments_u32_u32(k32, k32o, vin, vout, seg.data(), nframes, std::max(g.sf, 1), stream, 3);
+        } else {
+            st = sort_pairs_u32_u32(k32, k32o, vin, vout, (size_t)n, std::max(end_bit, 1), stream, 3);
+        }
         if (st != OT_OK) return st;
         hipLaunchKernelGGL(k_widen_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, (const unsigned*)k32o,
                            n, kout);
