@@ -605,13 +605,14 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 }
 
 // occupancy floor the integrate is compiled for: the float32-colour kernel allocates 64 VGPRs (8 waves
-// per SIMD) on its own; the float64-colour state and its IEEE f64 divides need 106 (4 waves per SIMD, no scratch —
-// forcing 5 or 6 waves spills)
+// per SIMD) on its own; the float64-colour state and its IEEE f64 divides want ~106, and capping them at 96 (5 waves
+// per SIMD, a few bytes of scratch) is 12-14 % faster than the spill-free 4 waves (measured: 4 / 5 / 6 / 7 / 8 waves
+// = 0.78-0.81 / 0.70 / 0.73 / 0.74 / 0.76 ms per 32-frame launch)
 #ifndef OT_WAVES_PER_EU
 #define OT_WAVES_PER_EU 4
 #endif
 #ifndef OT_WAVES_PER_EU_C64
-#define OT_WAVES_PER_EU_C64 4
+#define OT_WAVES_PER_EU_C64 5
 #endif
 // One workgroup of SLICES waves per unit, so a unit's frame footprint is gathered through one CU's L1; units are
 // assigned by a static grid stride that every wave derives on its own: no barriers, no LDS, no atomics.
@@ -755,7 +756,7 @@ __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_P
                             CT nr, ng, nb;
                             if (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
                                 const double wd = (double)wv, w1d = (double)w1;
-                                nr = (CT)(((double)cr[k] * wd + (double)(cv[k] & 0xFFu)) / w1d);
+nr = (CT)(((double)cr[k] * wd + (double)(cv[k] & 0xFFu)) / w1d);
                                 ng = (CT)(((double)cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu)) / w1d);
                                 nb = (CT)(((double)cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu)) / w1d);
                             } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
