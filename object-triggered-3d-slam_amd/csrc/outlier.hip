@@ -266,7 +266,7 @@ __device__ inline void sor_rings(const GridDev& g, const double q[3], const doub
                 }
             }
         const double guard = block_guard(g, q, o, (double)r);
-        if (have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard)) return;
+        if (have >= fend - fbeg || (best[KMAX - 1] < INFINITY && best[KMAX - 1] <= guard * guard)) return;
     }
     topk_reset<KMAX>(best, kk);
     scan_range<KMAX>(g.sxyz, q, (int)fbeg, (int)fend, best);
@@ -395,12 +395,17 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
             cell_fracs(g, q, o, lo, hi);
             const int2* r5 = g.nbr5 ? g.nbr5 + (int64_t)c * NBR5 : nullptr;
             const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
+            bool counted_all = true;  // have counts every point of the 5x5x5 block
             for (int u = 0; u < NBR5; ++u) {
                 const int t = c_cols5[u];
                 const int dx = t / 5 - 2, dy = t % 5 - 2;
                 const bool inner = dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1;
                 const double ex = face_gap(lo[0], hi[0], dx, g.h), ey = face_gap(lo[1], hi[1], dy, g.h);
                 const double e2 = ex * ex + ey * ey;
+                if (e2 >= best[KMAX - 1]) {  // the whole column is at least the k-th distance away: not even probed
+                    counted_all = false;
+                    continue;
+                }
                 int2 full, mid = make_int2(0, 0);
                 if (r5) {
                     full = r5[t];
@@ -422,7 +427,11 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
                 }
             }
             const double guard = block_guard(g, q, o, 2.0);
-            settled = have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard);
+            // the list is full exactly when kk points were scanned (nothing is skipped while the k-th distance is
+            // infinite); a skipped column lies beyond the k-th distance
+            settled = (counted_all && have >= fend - fbeg) ||
+                      (best[KMAX - 1] < INFINITY && best[KMAX - 1] <= guard * guard);
+            if (!counted_all) have = 0;  // only a full count may end the rings through the whole-frame test
             rnext = 3;
         }
         if (!settled) sor_rings<KMAX>(g, q, o, f, rnext, fbeg, fend, kk, have, best);
