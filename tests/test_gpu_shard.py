@@ -124,3 +124,28 @@ def test_shard_argument_errors(pkg, seq16, gpu):
     with pytest.raises(RuntimeError, match="rank < world"):
         fresh.set_shard(2, 2)
     fresh.set_shard(0, 1)  # world 1: no sharding
+
+
+def test_border_api_errors(pkg, seq16, gpu):
+    """export_border capacity and import_border shape checks; an unsharded volume exports every unit and imports
+    nothing from rows it owns."""
+    import ctypes as C
+
+    import torch
+
+    L = pkg._lib
+    vol = _integrate_p(pkg, (seq16[0][:2], seq16[1][:2], seq16[2][:2]), 0.01, None, 32)
+    n = vol.num_units()
+    keys, tsdf, weight, color = vol.export_border()
+    assert keys.shape[0] == n and tsdf.shape == (n, 721) and color.shape == (n, 721, 3)
+    small = torch.empty((1, 3), dtype=torch.int32, device="cuda")
+    t1 = torch.empty((1, 721), dtype=torch.float32, device="cuda")
+    m = C.c_int64(0)
+    with pytest.raises(RuntimeError, match="capacity"):
+        L.call("ot_tsdf_export_border", vol._h, 1, C.c_void_p(small.data_ptr()), C.c_void_p(t1.data_ptr()),
+               C.c_void_p(t1.data_ptr()), None, C.byref(m), None)
+    with pytest.raises(RuntimeError, match="import_border"):
+        vol.import_border(keys, tsdf[:, :100], weight, color)
+    before = vol.num_units()
+    vol.import_border(keys, tsdf, weight, color)  # every row is owned here (unsharded): nothing is imported
+    assert vol.num_units() == before
