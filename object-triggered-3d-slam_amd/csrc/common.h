@@ -79,6 +79,22 @@ __host__ __device__ inline unsigned long long mix64(unsigned long long z) {
     return z ^ (z >> 31);
 }
 
+// fl(x / y) without a division, from r = fl(1 / y): q0 = fl(x r) lies within an ulp of x / y and r within half an
+// ulp of 1 / y, so fl(q0 + fl(x - q0 y) r) is the correctly rounded quotient (Markstein; both fma's exact in the
+// remainder) barring over/underflow, which the callers' ranges (pixel coordinates, depths, colours, counts) exclude.
+// A zero x keeps its sign through q0.  Checked on the host against IEEE division over every u16 depth for 3000+
+// scales (float) and 5e8 unprojection / colour / average quotients (double).
+__device__ inline double div_rn(double x, double y, double r) {
+    const double q0 = x * r;
+    const double q = __builtin_fma(__builtin_fma(-q0, y, x), r, q0);
+    return q != 0.0 ? q : q0;
+}
+__device__ inline float div_rn(float x, float y, float r) {
+    const float q0 = x * r;
+    const float q = __builtin_fmaf(__builtin_fmaf(-q0, y, x), r, q0);
+    return q != 0.0f ? q : q0;
+}
+
 // ------------------------------------------------------------------------ wave / block primitives
 __device__ inline unsigned lane_id() { return __lane_id(); }
 

@@ -43,8 +43,9 @@ struct FbParams {
     const uint16_t* depth;  // [F][h][w]
     const uint8_t* color;   // [F][h][w][3]
     int w, h, tpf;          // tiles per frame
-    float scale_f;
+    float scale_f, rscale_f;  // rscale_f = fl(1 / scale_f) (div_rn)
     double trunc, fx, fy, cx, cy, vs, inv_vs;
+    double rfx, rfy;  // fl(1 / fx), fl(1 / fy)
     FbFrame* frames;
     int F;
 };
@@ -55,8 +56,8 @@ __device__ inline bool fb_point(const FbParams& p, const double* m, float d, int
     const unsigned pu = (unsigned)pix, rq = pu / (unsigned)p.w;
     const int r = (int)rq, c = (int)(pu - rq * (unsigned)p.w);
     const double z = (double)d;
-    const double x = ((double)c - p.cx) * z / p.fx;
-    const double y = ((double)r - p.cy) * z / p.fy;
+    const double x = div_rn(((double)c - p.cx) * z, p.fx, p.rfx);
+    const double y = div_rn(((double)r - p.cy) * z, p.fy, p.rfy);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const double a = m[k * 4 + 0] * x;
@@ -95,7 +96,7 @@ __device__ inline void fb_depth8(const FbParams& p, const uint16_t* __restrict__
     }
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
-        f[k] = f[k] / p.scale_f;
+        f[k] = div_rn(f[k], p.scale_f, p.rscale_f);
         if ((double)f[k] >= p.trunc) f[k] = 0.0f;
     }
 }
@@ -321,19 +322,20 @@ __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* _
         for (int k = 0; k < VB; ++k) {
             if (j0 + k >= end) break;
             double xyz[3];
-            fb_point(p, m, dd[k] / p.scale_f, pix[k], xyz);  // valid by construction (d > 0, below trunc)
+            // valid by construction (d > 0, below trunc)
+            fb_point(p, m, div_rn(dd[k], p.scale_f, p.rscale_f), pix[k], xyz);
 #pragma unroll
             for (int a = 0; a < 3; ++a) sp[a] += xyz[a];
-            sc[0] += (double)cc[k][0] / 255.0;
-            sc[1] += (double)cc[k][1] / 255.0;
-            sc[2] += (double)cc[k][2] / 255.0;
+            sc[0] += div_rn((double)cc[k][0], 255.0, 1.0 / 255.0);
+            sc[1] += div_rn((double)cc[k][1], 255.0, 1.0 / 255.0);
+            sc[2] += div_rn((double)cc[k][2], 255.0, 1.0 / 255.0);
         }
     }
-    const double cnt = (double)(end - beg);
+    const double cnt = (double)(end - beg), rc = 1.0 / cnt;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        vx[s * 3 + a] = sp[a] / cnt;
-        vc[s * 3 + a] = sc[a] / cnt;
+        vx[s * 3 + a] = div_rn(sp[a], cnt, rc);
+        vc[s * 3 + a] = div_rn(sc[a], cnt, rc);
     }
 }
 
@@ -523,9 +525,12 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     p.h = H;
     p.tpf = tpf;
     p.scale_f = (float)fl->depth_scale;
+    p.rscale_f = 1.0f / p.scale_f;
     p.trunc = fl->depth_trunc;
     p.fx = fl->intr.fx;
     p.fy = fl->intr.fy;
+    p.rfx = 1.0 / p.fx;
+    p.rfy = 1.0 / p.fy;
     p.cx = fl->intr.cx;
     p.cy = fl->intr.cy;
     p.vs = vs;

@@ -756,7 +756,7 @@ __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_P
                             CT nr, ng, nb;
                             if (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
                                 const double wd = (double)wv, w1d = (double)w1;
-nr = (CT)(((double)cr[k] * wd + (double)(cv[k] & 0xFFu)) / w1d);
+                                nr = (CT)(((double)cr[k] * wd + (double)(cv[k] & 0xFFu)) / w1d);
                                 ng = (CT)(((double)cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu)) / w1d);
                                 nb = (CT)(((double)cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu)) / w1d);
                             } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
