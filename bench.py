@@ -550,8 +550,7 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t1)
         single = round(float(np.median(ts)) * 1e3, 3)
-    merge = "RCCL all-gather over xGMI" if (world > 1 and COLL_DEV == "cuda") else \
-        ("gloo all-gather" if world > 1 else "local concatenation (N=1: no process group, no collective)")
+    merge = _merge_label(world)
     return {"workload": f"configs[3]: {args.objects} object scans x {args.object_frames} 640x480 frames, "
                         f"{args.voxel * 1000:g} mm TSDF -> mesh -> normals -> 100k samples -> z mask per object, "
                         f"contiguous object shards over {world} GPU(s) ({T} concurrent streams per GPU), merge: {merge}",
@@ -559,6 +558,13 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
             "objects_per_rank": len(ids), "merged_points": int(merged.shape[0]), "merge": merge,
             "single_object_ms": single,
             "single_object_note": "median of 5, object 0 of this rank on one stream, same pipeline, no merge"}
+
+
+def _merge_label(world):
+    """the collective a merge actually runs at this world size / backend"""
+    if world == 1:
+        return "local concatenation (N=1: no process group, no collective)"
+    return "RCCL all-gather over xGMI" if COLL_DEV == "cuda" else "gloo all-gather"
 
 
 def hybrid_fusion(args, L, synth, torch, dist, rank, world):
@@ -597,7 +603,7 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
         # change detection of every object vs its saved version: one multi-object voxel-key diff
         na, nr = C.c_int64(0), C.c_int64(0)
         if objs:
-                L.call("ot_voxel_key_diff_multi", C.c_void_p(cat_new.data_ptr()), off_new.ctypes.data_as(C.c_void_p),
+            L.call("ot_voxel_key_diff_multi", C.c_void_p(cat_new.data_ptr()), off_new.ctypes.data_as(C.c_void_p),
                    C.c_void_p(cat_old.data_ptr()), off_old.ctypes.data_as(C.c_void_p), len(objs), 0.02, origin,
                    C.c_void_p(keys_a.data_ptr()), C.byref(na), C.c_void_p(keys_r.data_ptr()), C.byref(nr), stream)
         added, removed = na.value, nr.value
@@ -623,7 +629,7 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
         dist.all_reduce(t)
     return {"workload": f"configs[4]: 1024x1024 occupancy grid @ 5 cm + {args.hybrid_objects} object clouds, "
                         "change detection vs the saved map (smart_paste grid merge + 2 cm voxel-key diff per object), "
-                        f"hybrid cloud assembled by RCCL all-gather over {world} GPU(s)",
+                        f"hybrid cloud assembled over {world} GPU(s), merge: {_merge_label(world)}",
             "ms": round(dt * 1e3, 3), "mpoints_per_s": round(int(t.item()) / dt / 1e6, 2),
             "merged_points": int(merged.shape[0]) if rank == 0 else None,
             "changed_grid_cells": stats.get("changed_cells"), "added_keys_rank0": stats.get("added"),

@@ -17,8 +17,8 @@ from conftest import assert_bitwise
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_chain(O, depth, color, ext, intr_t, trunc=5.0, vs=0.005, k=20, ratio=2.0):
-    xyz, rgb = O.unproject(O.depth_to_float(depth, 1000.0, trunc), color, intr_t, ext)
+def _oracle_chain(O, depth, color, ext, intr_t, trunc=5.0, vs=0.005, k=20, ratio=2.0, scale=1000.0):
+    xyz, rgb = O.unproject(O.depth_to_float(depth, scale, trunc), color, intr_t, ext)
     v, vc, _, _ = O.voxel_down_sample(xyz, rgb, vs)
     idx, avg = O.remove_statistical_outlier(v, k, ratio)
     return xyz.shape[0], v, vc, avg, idx
@@ -121,6 +121,26 @@ def test_batch_wide_keys_match_per_call(pkg, synth, gpu):
         bkept, bind = flt.frame(f)
         assert_bitwise(np.asarray(bdown.points), np.asarray(down.points), f"wide-key voxels (frame {f})")
         assert bind == ind, f"wide-key kept indices (frame {f})"
+
+
+@pytest.mark.parametrize("scale", [5000.0, 1234.5])
+def test_batch_odd_scale_and_intrinsics(pkg, O, synth, scale, gpu):
+    """Depth scales other than 1000 and intrinsics with non-half principal points and fx != fy: the batch's
+    reciprocal-product divisions (depth / scale in float32, (c - cx) z / fx, colour / 255, sum / count in float64)
+    must still give the IEEE quotients, frame by frame against the oracle chain."""
+    intr_t = (640, 480, 517.31, 516.07, 318.71, 243.29)
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=7), n_frames=32, frames=[4, 19])
+    flt = pkg.filters.RGBDFilterBatch(pkg.camera.PinholeCameraIntrinsic(*intr_t), max_frames=2, depth_scale=scale,
+                                      depth_trunc=3.0, voxel_size=0.004).run(depth, color, ext)
+    for f in range(2):
+        P, v, vc, avg, idx = _oracle_chain(O, depth[f], color[f], ext[f], intr_t, trunc=3.0, vs=0.004, scale=scale)
+        assert flt.point_offsets[f + 1] - flt.point_offsets[f] == P
+        down, davg = flt.voxel_cloud(f)
+        assert_bitwise(np.asarray(down.points), v, f"scale {scale} voxel averages (frame {f})")
+        assert_bitwise(np.asarray(down.colors), vc, f"scale {scale} voxel colours (frame {f})")
+        assert_bitwise(davg, avg, f"scale {scale} mean kNN distances (frame {f})")
+        _, ind = flt.frame(f)
+        assert_bitwise(np.asarray(ind, np.int64), idx, f"scale {scale} kept indices (frame {f})")
 
 
 def test_batch_errors(pkg, synth, gpu):
