@@ -3,7 +3,7 @@
 // simulates waves of 64 consecutive sorted queries scanning their candidate ranges in lockstep: per range slot the
 // wave runs max-lane-length steps, and a step executes the top-k insertion chain when ANY lane inserts.
 // Reports candidates per query, per-lane insertions, and wave-level step / insertion-step counts.
-//   g++ -O2 -std=c++17 -o /tmp/sor_sim tools/sor_sim.cpp && /tmp/sor_sim cloud.npy k h_mult [order]
+//   g++ -O2 -std=c++17 -o /tmp/sor_sim tools/sor_sim.cpp && /tmp/sor_sim cloud.npy k h_mult [R [zorder [flat]]]
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -38,6 +38,7 @@ int main(int argc, char** argv) {
     const double hm = atof(argv[3]);  // cell = hm * 5 mm
     const int R = argc > 4 ? atoi(argv[4]) : 1;  // stage-1 block radius in cells
     const int zorder = argc > 5 ? atoi(argv[5]) : 0;  // 1: own z-cell first inside a column
+    const int flat = argc > 6 ? atoi(argv[6]) : 0;  // 1: the lane's slots as one flattened lockstep stream
     const double h = hm * 0.005;
     double mn[3] = {1e30, 1e30, 1e30};
     for (size_t i = 0; i < n; ++i)
@@ -71,7 +72,7 @@ int main(int argc, char** argv) {
         return a.first * a.first + a.second * a.second < b.first * b.first + b.second * b.second;
     });
     const int nslot = (int)cols.size() * (zorder ? W : 1);
-    long long stage2_steps = 0, tot_cand = 0, tot_ins = 0, wave_steps = 0, wave_ins_steps = 0, unsettled = 0;
+    long long trans_steps = 0, stage2_steps = 0, tot_cand = 0, tot_ins = 0, wave_steps = 0, wave_ins_steps = 0, unsettled = 0;
     std::vector<std::vector<std::pair<int, int>>> plan(64, std::vector<std::pair<int, int>>(nslot));
     std::vector<std::vector<double>> best(64, std::vector<double>(K));
     std::vector<double> lo(64 * 2), hi(64 * 2), lz(64), hz(64);
@@ -108,7 +109,43 @@ int main(int argc, char** argv) {
             }
             std::fill(best[l].begin(), best[l].end(), INFINITY);
         }
-        for (int u = 0; u < nslot; ++u) {
+        if (flat) {  // one flattened candidate stream per lane: column transitions inside the lockstep loop
+            std::vector<int> uu(nl, 0), mm(nl, 0), ee(nl, 0);
+            auto advance = [&](int l) {  // next non-culled slot of lane l (culled against its current k-th)
+                while (mm[l] >= ee[l] && uu[l] < nslot) {
+                    const int u = uu[l]++;
+                    const int ci = zorder ? u / W : u;
+                    const int dx = cols[ci].first, dy = cols[ci].second;
+                    double ex = dx < 0 ? lo[l * 2] + (-dx - 1) * h : (dx > 0 ? hi[l * 2] + (dx - 1) * h : 0.0);
+                    double ey = dy < 0 ? lo[l * 2 + 1] + (-dy - 1) * h : (dy > 0 ? hi[l * 2 + 1] + (dy - 1) * h : 0.0);
+                    if (ex * ex + ey * ey < best[l][K - 1]) mm[l] = plan[l][u].first, ee[l] = plan[l][u].second;
+                }
+            };
+            for (;;) {
+                bool live = false, any = false, trans = false;
+                for (int l = 0; l < nl; ++l) {
+                    if (mm[l] >= ee[l]) { advance(l); trans = true; }
+                    if (mm[l] >= ee[l]) continue;
+                    live = true;
+                    const size_t j = w0 + l, m = mm[l]++;
+                    const double d0 = S[j * 3] - S[m * 3], d1 = S[j * 3 + 1] - S[m * 3 + 1], d2 = S[j * 3 + 2] - S[m * 3 + 2];
+                    const double d = (d0 * d0 + d1 * d1) + d2 * d2;
+                    ++tot_cand;
+                    if (d < best[l][K - 1]) {
+                        any = true;
+                        ++tot_ins;
+                        auto& bb = best[l];
+                        bb[K - 1] = d;
+                        for (int i = K - 1; i > 0 && bb[i] < bb[i - 1]; --i) std::swap(bb[i], bb[i - 1]);
+                    }
+                }
+                if (!live) break;
+                ++wave_steps;
+                wave_ins_steps += any;
+                trans_steps += trans;
+            }
+        }
+        for (int u = 0; u < nslot && !flat; ++u) {
             const int ci = zorder ? u / W : u;
             const int dx = cols[ci].first, dy = cols[ci].second;
             int maxlen = 0;
@@ -179,6 +216,7 @@ int main(int argc, char** argv) {
            n, h, R, zorder, cells.size(), nq / cells.size(), tot_cand / nq, tot_ins / nq, wave_steps / nw,
            wave_ins_steps / nw, 100.0 * wave_ins_steps / std::max<long long>(wave_steps, 1), 100.0 * unsettled / nq,
            (12.0 * wave_steps + 42.0 * wave_ins_steps) / nq);
+    printf("   flat %d: wave steps with a column transition %.1f\n", flat, trans_steps / nw);
     printf("   stage-2 wave steps per wave %.1f -> model incl. stage 2 (54/step) per query %.1f\n", stage2_steps / nw,
            (12.0 * wave_steps + 42.0 * wave_ins_steps + 54.0 * stage2_steps) / nq);
 }
