@@ -373,7 +373,8 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
 // Stage 2 for the pending queries (grid-stride over the device count): R = 1 completes the 5x5x5 block (the inner
 // columns' cells at z-2 / z+2 and the 16 outer columns, each skipped when provably too far), then Chebyshev rings.
 template <int KMAX, int R>
-__global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* avg, SorPend pd) {
+__global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* avg, SorPend pd, SorPend pd3) {
+    static_assert(R == 1 || R == 2, "stage 3 starts at ring 3");
     const int cnt = *pd.count;
     for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < cnt; s += (int64_t)gridDim.x * 256) {
         const int64_t j = pd.j[s];
@@ -431,11 +432,151 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
             // infinite); a skipped column lies beyond the k-th distance
             settled = (counted_all && have >= fend - fbeg) ||
                       (best[KMAX - 1] < INFINITY && best[KMAX - 1] <= guard * guard);
-            if (!counted_all) have = 0;  // only a full count may end the rings through the whole-frame test
+            if (!counted_all) have = -1;  // only a full count may end the rings through the whole-frame test
             rnext = 3;
         }
-        if (!settled) sor_rings<KMAX>(g, q, o, f, rnext, fbeg, fend, kk, have, best);
+        if (!settled) {
+            // stage 3 (one wave per query) unless its list is full; a query left here walks the rings serially
+            const int s3 = atomicAdd(pd3.count, 1);
+            if (s3 < pd3.cap) {
+                pd3.j[s3] = (int)j;
+                pd3.have[s3] = have;
+#pragma unroll
+                for (int i = 0; i < KMAX; ++i) pd3.best[(int64_t)i * pd3.cap + s3] = best[i];
+                continue;
+            }
+            sor_rings<KMAX>(g, q, o, f, rnext, fbeg, fend, kk, have, best);
+        }
         avg[g.sidx[j]] = sor_mean<KMAX>(best, kk);
+    }
+}
+
+// Stage 3: the few queries whose k-th distance lies beyond their 5x5x5 block (isolated points: 0.02-0.2 % of a
+// configs[2] frame) — one WAVE per query.  Run by one lane each, their Chebyshev rings cost thousands of dependent
+// hash probes in series and set the whole kernel's tail.  Here ring r's (2r+1)^2 columns are split over the lanes
+// (outer columns: cells z-r..z+r, inner columns: z-r and z+r only, each skipped when provably beyond the current
+// k-th distance); every lane keeps its own register list, and after each ring the wave merges the 64 lists into the
+// shared list (LDS, kk extraction rounds of a wave-wide minimum).  Lane 0 starts a ring from the shared list and
+// the other lanes from an empty list whose top is the shared k-th distance: a candidate enters only when it beats
+// that, and a copy of the k-th value ties the real one, so the merged multiset of the kk smallest distances (all
+// the mean needs) is exactly the serial walk's.  After SOR_RMAX3 rings the wave scans the whole frame.
+constexpr int SOR_RMAX3 = 16;
+
+__device__ inline double wave_min_d(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+    return v;
+}
+
+// gl[0..KMAX) = the kk smallest of the 64 lanes' lists (ascending, right-aligned, -inf padding); lds: 64*KMAX
+template <int KMAX>
+__device__ inline void wave_merge(double* lds, double* gl, const double (&L)[KMAX], int kk) {
+    const int l = (int)lane_id();
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) lds[i * 64 + l] = L[i];
+    __syncthreads();
+    int p = KMAX - kk;
+    for (int i = 0; i < KMAX; ++i) {
+        if (i < KMAX - kk) {
+            if (l == 0) gl[i] = -INFINITY;
+            continue;
+        }
+        const double v = p < KMAX ? lds[p * 64 + l] : INFINITY;
+        const double m = wave_min_d(v);
+        const unsigned long long b = __ballot(v == m);
+        if (l == __ffsll((long long)b) - 1) ++p;
+        if (l == 0) gl[i] = m;
+    }
+    __syncthreads();
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(64) void k_sor_knn_wave(GridDev g, int k, double* avg, SorPend pd3) {
+    __shared__ double lds[64 * KMAX];
+    __shared__ double gl[KMAX];
+    const int cnt = (int)min((int64_t)*pd3.count, pd3.cap);
+    const int l = (int)lane_id();
+    for (int64_t s = blockIdx.x; s < cnt; s += gridDim.x) {
+        const int64_t j = pd3.j[s];
+        const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, j) : 0;
+        const int64_t fbeg = g.foff[f], fend = g.foff[f + 1];
+        const double* o = g.origin + 3 * f;
+        const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
+        const int kk = (int)((int64_t)k < fend - fbeg ? k : fend - fbeg);
+        if (l < KMAX) gl[l] = pd3.best[(int64_t)l * pd3.cap + s];
+        if (KMAX > 64 && l == 0)
+            for (int i = 64; i < KMAX; ++i) gl[i] = pd3.best[(int64_t)i * pd3.cap + s];
+        __syncthreads();
+        long long have = pd3.have[s];  // < 0: not every point of the scanned cube was counted
+        const int cx = cell_coord(q[0], o[0], g.h), cy = cell_coord(q[1], o[1], g.h), cz = cell_coord(q[2], o[2], g.h);
+        double lo[3], hi[3];
+        cell_fracs(g, q, o, lo, hi);
+        double L[KMAX];
+        bool settled = false;
+        for (int r = 3; r <= SOR_RMAX3 && !settled; ++r) {
+            const double gk = gl[KMAX - 1];
+            if (l == 0) {
+#pragma unroll
+                for (int i = 0; i < KMAX; ++i) L[i] = gl[i];
+            } else {
+                topk_reset<KMAX>(L, kk);
+                L[KMAX - 1] = gk;
+            }
+            long long hl = 0;
+            bool cull = false;
+            const int W = 2 * r + 1;
+            for (int t = l; t < W * W; t += 64) {
+                const int dx = t / W - r, dy = t % W - r;
+                const double ex = face_gap(lo[0], hi[0], dx, g.h), ey = face_gap(lo[1], hi[1], dy, g.h);
+                const double e2 = ex * ex + ey * ey;
+                if (dx == -r || dx == r || dy == -r || dy == r) {
+                    if (!(e2 < gk)) {
+                        cull = true;
+                        continue;
+                    }
+                    const int2 se = column_range(g, grid_column(g, f, cx + dx, cy + dy), cz - r, cz + r);
+                    scan_range<KMAX>(g.sxyz, q, se.x, se.y, L);
+                    hl += se.y - se.x;
+                } else {
+                    const double ezl = face_gap(lo[2], hi[2], -r, g.h), ezh = face_gap(lo[2], hi[2], r, g.h);
+                    const bool a = e2 + ezl * ezl < gk, b = e2 + ezh * ezh < gk;
+                    if (!a || !b) cull = true;
+                    if (!a && !b) continue;
+                    const int2 col = grid_column(g, f, cx + dx, cy + dy);
+                    if (a) {
+                        const int2 se = column_range(g, col, cz - r, cz - r);
+                        scan_range<KMAX>(g.sxyz, q, se.x, se.y, L);
+                        hl += se.y - se.x;
+                    }
+                    if (b) {
+                        const int2 se = column_range(g, col, cz + r, cz + r);
+                        scan_range<KMAX>(g.sxyz, q, se.x, se.y, L);
+                        hl += se.y - se.x;
+                    }
+                }
+            }
+            wave_merge<KMAX>(lds, gl, L, kk);
+            if (__any(cull)) have = -1;
+            if (have >= 0) have += wave_sum(hl);
+            const double guard = block_guard(g, q, o, (double)r);
+            const double kth = gl[KMAX - 1];
+            settled = have >= fend - fbeg || (kth < INFINITY && kth <= guard * guard);
+        }
+        if (!settled) {  // the whole frame from scratch, the points split over the lanes
+            topk_reset<KMAX>(L, kk);
+            for (int64_t m = fbeg + l; m < fend; m += 64) {
+                const double d = d2_l2(q, g.sxyz + m * 3);
+                if (d < L[KMAX - 1]) topk_insert<KMAX>(L, d);
+            }
+            wave_merge<KMAX>(lds, gl, L, kk);
+        }
+        if (l == 0) {
+            double best[KMAX];
+#pragma unroll
+            for (int i = 0; i < KMAX; ++i) best[i] = gl[i];
+            avg[g.sidx[j]] = sor_mean<KMAX>(best, kk);
+        }
+        __syncthreads();  // gl is reloaded for the next query
     }
 }
 
@@ -726,22 +867,31 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
     // pending list of stage-1 misses (device count; capacity n)
     const int km = kk <= 4 ? 4 : kk <= 8 ? 8 : kk <= 12 ? 12 : kk <= 16 ? 16 : kk <= 20 ? 20 : kk <= 24 ? 24
                  : kk <= 32 ? 32 : kk <= 48 ? 48 : 64;
-    char* pw = (char*)scratch((size_t)n * (4 + 8 + 8 * (size_t)km) + 512, slot0 + 1);
+    // and of stage-2 misses (stage 3, one wave each; capacity n / 32 + 4096, overflow walks its rings serially)
+    const int64_t cap3 = std::min<int64_t>(n, n / 32 + 4096);
+    const size_t per = 4 + 8 + 8 * (size_t)km;
+    char* pw = (char*)scratch((size_t)(n + cap3) * per + 1024, slot0 + 1);
     if (!pw) return fail(OT_ERR_HIP, "scratch allocation failed");
-    SorPend pd;
+    SorPend pd, pd3;
     pd.count = (int*)pw;
+    pd3.count = pd.count + 1;
     pd.j = (int*)(pw + 256);
     pd.have = (long long*)(((uintptr_t)(pd.j + n) + 15) & ~(uintptr_t)15);
     pd.best = (double*)(pd.have + n);
     pd.cap = n;
-    OT_HIP_TRY(hipMemsetAsync(pd.count, 0, sizeof(int), stream));
+    pd3.j = (int*)(((uintptr_t)(pd.best + (size_t)km * n) + 255) & ~(uintptr_t)255);
+    pd3.have = (long long*)(((uintptr_t)(pd3.j + cap3) + 15) & ~(uintptr_t)15);
+    pd3.best = (double*)(pd3.have + cap3);
+    pd3.cap = cap3;
+    OT_HIP_TRY(hipMemsetAsync(pd.count, 0, 2 * sizeof(int), stream));
     const unsigned rgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid / 4, 1), 2048);
 #define OT_SOR_LAUNCH(KM)                                                                                           \
     do {                                                                                                            \
         hipLaunchKernelGGL((k_sor_knn<KM, SOR_BLOCK_R>), dim3(grid), dim3(256), 0, stream, gb.g, n,                 \
                            (int)nb_neighbors, avg, pd);                                                             \
         hipLaunchKernelGGL((k_sor_knn_rest<KM, SOR_BLOCK_R>), dim3(rgrid), dim3(256), 0, stream, gb.g,              \
-                           (int)nb_neighbors, avg, pd);                                                             \
+                           (int)nb_neighbors, avg, pd, pd3);                                                        \
+        hipLaunchKernelGGL((k_sor_knn_wave<KM>), dim3(1024), dim3(64), 0, stream, gb.g, (int)nb_neighbors, avg, pd3); \
     } while (0)
     if (kk <= 4) OT_SOR_LAUNCH(4);
     else if (kk <= 8) OT_SOR_LAUNCH(8);

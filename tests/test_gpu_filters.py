@@ -95,6 +95,27 @@ def test_sor_bitexact(pkg, O, frame_cloud, k, ratio):
     assert not set(range(ds.shape[0] - 50, ds.shape[0])) <= set(ridx.tolist())
 
 
+@pytest.mark.parametrize("k", [20, 64])
+def test_sor_sparse_tail(pkg, O, frame_cloud, k):
+    """Stage 3 of the SOR kNN (one wave per query, rings split over the lanes, lists merged per ring): points whose
+    k-th neighbour lies beyond their 5x5x5 cell block -- isolated points at geometric distances (5 cm .. 20 m) from
+    the surface, clusters of fewer than k points, a far sparse line; k = 64 also merges 64-entry lists."""
+    xyz, rgb = frame_cloud
+    ds = O.voxel_down_sample(xyz, rgb, 0.01)[0]
+    rng = np.random.default_rng(7)
+    c = ds.mean(0)
+    dirs = rng.normal(size=(300, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    iso = c + dirs * np.geomspace(0.05, 20.0, 300)[:, None]
+    clusters = [c + rng.uniform(-3, 3, 3) + rng.normal(scale=0.01, size=(m, 3)) for m in rng.integers(2, 16, 30)]
+    line = c + np.array([5.0, 0.0, 0.0]) + np.linspace(0.0, 1.0, 40)[:, None] * np.array([0.0, 0.0, 1.0])
+    pts = np.ascontiguousarray(np.concatenate([ds, iso] + clusters + [line]))
+    idx, avg = _sor_gpu(pkg, pts, k, 1.0)
+    ridx, ravg = O.remove_statistical_outlier(pts, k, 1.0)
+    assert_bitwise(avg, ravg, f"SOR({k}) mean kNN distance, sparse tail")
+    assert_bitwise(idx, ridx, f"SOR({k}) kept indices, sparse tail")
+
+
 def _sor_gpu(pkg, pts, k, ratio):
     L = pkg._lib
     d = torch.from_numpy(np.ascontiguousarray(pts)).cuda()
