@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--objects", type=int, default=8,
                     help="configs[3]: object scans shared by all ranks (full per-object pipeline + RCCL merge); 0 = skip")
     ap.add_argument("--object-frames", type=int, default=64, help="configs[3]: frames per object scan")
-    ap.add_argument("--filter-streams", type=int, default=2,
+    ap.add_argument("--filter-streams", type=int, default=3,
                     help="configs[2]: batches filtered concurrently (host threads x HIP streams)")
     ap.add_argument("--object-streams", type=int, default=2,
                     help="configs[3]: objects reconstructed concurrently per GPU (host threads x HIP streams)")
