@@ -608,6 +608,9 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 // per SIMD) on its own; the float64-colour state and its IEEE f64 divides want ~106, and capping them at 96 (5 waves
 // per SIMD, a few bytes of scratch) is 12-14 % faster than the spill-free 4 waves (measured: 4 / 5 / 6 / 7 / 8 waves
 // = 0.78-0.81 / 0.70 / 0.73 / 0.74 / 0.76 ms per 32-frame launch)
+#ifndef OT_SKIP_IDLE_STORE
+#define OT_SKIP_IDLE_STORE 1  // slices with no update in the batch are not written back (-1.5 % integrate)
+#endif
 #ifndef OT_WAVES_PER_EU
 #define OT_WAVES_PER_EU 4
 #endif
@@ -672,6 +675,7 @@ __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_P
                 const float px = (p.half + p.vl * (float)x) + ox;
                 const float py = (p.half + p.vl * (float)y) + oy;
                 const float pz = p.half + oz;
+                const unsigned upd0 = upd;
                 for (unsigned long long m = mask; m; m &= m - 1) {
                     const int f = __ffsll((long long)m) - 1;
                     const BatchFrame& fr = frames[f];
@@ -773,6 +777,10 @@ __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_P
                         upd += doit ? 1u : 0u;
                     }
                 }
+#if OT_SKIP_IDLE_STORE
+                // a slice none of whose voxels updated in this batch still holds its HBM values (fresh ones: zeros)
+                if (!fresh && !__any(upd != upd0)) continue;
+#endif
 #pragma unroll
                 for (int k = 0; k < BZ; ++k) {
                     const int vi = (z0 + k) * 256 + col;
