@@ -206,6 +206,9 @@ def main():
     if traffic and kernel_ms_avg > 0:  # measured HBM bytes per launch over the same launch time
         roofline["hbm_achieved"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9, 1)
         roofline["hbm_frac"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    ient, _ = _pmc_entry(args, L, "k_batch_integrate", {"voxel": args.voxel, "frames": args.frames, "batch": args.batch})
+    if ient and ient.get("valu_busy_frac") is not None:  # the other ceiling: vector-ALU issue (PMC, same build)
+        roofline["valu_busy_frac"] = round(ient["valu_busy_frac"], 4)
 
     if args.calib:  # a kernel with a known read byte count and the integrate kernel's pool access pattern
         nu = n_units.value
@@ -758,13 +761,28 @@ def filter_stream(fs):
                          "algorithmic_bytes_per_frame": round(bytes_frame),
                          "achieved": round(bytes_frame * nf / dt / 1e9, 2),
                          "frac": round(bytes_frame * nf / dt / 1e9 / HBM_PEAK_GBS, 5)},
+            "kernel_roofline": _sor_roofline(args, fs.L),
             "cpu_baseline": {"mpoints_per_s": round(cpu_pts / cdt / 1e6, 3), "cores": cores, "kind": "port",
                              "sample": f"frames {sample} of the same stream, CPU oracle chain, 1 warm-up + median of 5"}}
 
 
-def _traffic(args, L, kernel, config):
-    """Measured HBM bytes per launch of `kernel` from profiles/pmc_traffic.json -- only when the file was taken on
-    this build (source hash) and the same workload; else (None, reason)."""
+def _sor_roofline(args, L):
+    """The chain's dominant kernel, k_sor_knn (SOR stage 1), against the ceiling that binds it: vector-ALU issue
+    (PMC SQ_ACTIVE_INST_VALU x 4 per SIMD-cycle of the dispatch, same build; tools/pmc.sh runs it on 32-frame
+    batches of the same stream).  Its HBM traffic is reported beside it."""
+    ent, note = _pmc_entry(args, L, "k_sor_knn", {})
+    if not ent or ent.get("valu_busy_frac") is None:
+        return {"kernel": "k_sor_knn", "bound": "valu", "frac": None, "source": note}
+    cyc = ent.get("dispatch_cycles")
+    return {"kernel": "k_sor_knn", "bound": "valu", "frac": round(ent["valu_busy_frac"], 4),
+            "valu_insts_per_launch": ent.get("valu_insts_per_launch"), "frames_per_launch": 32,
+            "dispatch_cycles": round(cyc) if cyc else None,
+            "hbm_bytes_per_launch": ent.get("bytes_per_launch"), "source": note}
+
+
+def _pmc_entry(args, L, kernel, config):
+    """The PMC summary of `kernel` from profiles/pmc_traffic.json -- only when the file was taken on this build
+    (source hash) and the same workload; else (None, reason)."""
     try:
         with open(args.traffic) as f:
             tr = json.load(f)
@@ -777,7 +795,13 @@ def _traffic(args, L, kernel, config):
         return None, f"stale PMC file (source hash {tr.get('source_hash')} != {L.source_hash()})"
     if any(tr.get("config", {}).get(k) != v for k, v in config.items()):
         return None, f"PMC file workload {tr.get('config')} != {config}"
-    return ent["bytes_per_launch"], f"{os.path.relpath(args.traffic, ROOT)} (source hash {tr['source_hash']})"
+    return ent, f"{os.path.relpath(args.traffic, ROOT)} (source hash {tr['source_hash']})"
+
+
+def _traffic(args, L, kernel, config):
+    """Measured HBM bytes per launch of `kernel` (same build and workload), else (None, reason)."""
+    ent, note = _pmc_entry(args, L, kernel, config)
+    return (ent["bytes_per_launch"] if ent else None), note
 
 
 def cpu_baseline(depth, color, ext, intr_t, args):

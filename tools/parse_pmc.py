@@ -59,6 +59,14 @@ def main():
             ent["stall_shares"] = {"wait_any": k.get("SQ_WAIT_ANY", 0) / wc, "wait_inst_any": k.get("SQ_WAIT_INST_ANY", 0) / wc,
                                    "active_inst_any": k.get("SQ_ACTIVE_INST_ANY", 0) / wc,
                                    "active_valu": k.get("SQ_ACTIVE_INST_VALU", 0) / wc}
+        if k.get("SQ_ACTIVE_INST_VALU") and k.get("GRBM_GUI_ACTIVE"):
+            # VALU issue: wave-cycles with a VALU instruction in flight (quad-cycle counter x 4) per SIMD-cycle of
+            # the dispatch (GRBM_GUI_ACTIVE sums the 8 XCDs' cycles; MI355X_MICROARCH.md): the roofline of a kernel
+            # bound by vector-ALU issue rather than by bytes
+            cyc = k["GRBM_GUI_ACTIVE"] / 8.0
+            ent["valu_busy_frac"] = k["SQ_ACTIVE_INST_VALU"] * 4.0 / 1024.0 / cyc
+            ent["valu_insts_per_launch"] = k.get("SQ_INSTS_VALU")
+            ent["dispatch_cycles"] = cyc
         out["kernels_traffic"][kern] = ent
     print(json.dumps(out, indent=1))
 
