@@ -123,6 +123,31 @@ def test_batch_wide_keys_match_per_call(pkg, synth, gpu):
         assert bind == ind, f"wide-key kept indices (frame {f})"
 
 
+def test_batch_sparse_tail(pkg, O, synth, gpu):
+    """SOR stages 2-3 inside the batched chain (frame in the grid key): speckle pixels at far depths become isolated
+    voxels whose k-th neighbour lies many cells away (one wave per query, rings and the whole-frame scan bounded by
+    their own frame), and a frame of 12 valid pixels has fewer points than k."""
+    intr_t = synth.REF_INTRINSICS_640
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=11), n_frames=32, frames=[3, 14, 27])
+    depth = depth.copy()
+    rng = np.random.default_rng(4)
+    for f in (0, 1):
+        iy, ix = rng.integers(0, 480, 300), rng.integers(0, 640, 300)
+        depth[f][iy, ix] = rng.integers(300, 2999, 300).astype(np.uint16)   # speckles at any depth
+    keep = np.zeros_like(depth[2])
+    iy, ix = rng.integers(0, 480, 12), rng.integers(0, 640, 12)
+    keep[iy, ix] = depth[2][iy, ix]
+    depth[2] = keep                                                          # 12 valid pixels (< k = 20)
+    flt = _run_batch(pkg, intr_t, depth, color, ext, max_frames=3, trunc=3.0)
+    for f in range(3):
+        P, v, vc, avg, idx = _oracle_chain(O, depth[f], color[f], ext[f], intr_t, trunc=3.0)
+        down, davg = flt.voxel_cloud(f)
+        assert_bitwise(np.asarray(down.points), v, f"sparse-tail voxels (frame {f})")
+        assert_bitwise(davg, avg, f"sparse-tail mean kNN distances (frame {f})")
+        _, ind = flt.frame(f)
+        assert_bitwise(np.asarray(ind, np.int64), idx, f"sparse-tail kept indices (frame {f})")
+
+
 @pytest.mark.parametrize("scale", [5000.0, 1234.5])
 def test_batch_odd_scale_and_intrinsics(pkg, O, synth, scale, gpu):
     """Depth scales other than 1000 and intrinsics with non-half principal points and fx != fy: the batch's
