@@ -523,7 +523,7 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
         sizes["local"] = sum(int(c.shape[0]) for c in clouds)
         return merged
 
-    dt, merged = _timed(torch, dist, world, run, 3)
+    dt, merged = _timed(torch, dist, world, run, 10)  # ~20 ms per call: 10 calls keep run-to-run noise near 2 %
     pool.shutdown()
 
     # one object end to end on one stream (integrate -> mesh -> normals -> 100k samples -> z mask): the latency that
