@@ -608,11 +608,14 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 // per SIMD) on its own; the float64-colour state and its IEEE f64 divides want ~106, and capping them at 96 (5 waves
 // per SIMD, a few bytes of scratch) is 12-14 % faster than the spill-free 4 waves (measured: 4 / 5 / 6 / 7 / 8 waves
 // = 0.78-0.81 / 0.70 / 0.73 / 0.74 / 0.76 ms per 32-frame launch)
+#ifndef OT_MASK_INVALID_LOADS
+#define OT_MASK_INVALID_LOADS 1  // lanes whose voxel projects outside the image issue no depth gather (with the
+#endif                           // 64-VGPR cap below: integrate 0.415-0.421 -> 0.409-0.412 ms; at 66 VGPRs 0.59)
 #ifndef OT_SKIP_IDLE_STORE
 #define OT_SKIP_IDLE_STORE 1  // slices with no update in the batch are not written back (-1.5 % integrate)
 #endif
 #ifndef OT_WAVES_PER_EU
-#define OT_WAVES_PER_EU 4
+#define OT_WAVES_PER_EU 8  // float32 colour: 64 VGPRs, 8 waves per SIMD (the kernel lives on its occupancy)
 #endif
 #ifndef OT_WAVES_PER_EU_C64
 #define OT_WAVES_PER_EU_C64 5
@@ -730,10 +733,19 @@ __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_P
                     float dv[BZ], mv[BZ];
 #pragma unroll
                     for (int k = 0; k < BZ; ++k) {
+#if OT_MASK_INVALID_LOADS
+                        dv[k] = mv[k] = 0.0f;
+                        if (pixv[k] >= 0) {
+                            const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
+                            dv[k] = __uint_as_float(raw.x);
+                            mv[k] = __uint_as_float(raw.y);
+                        }
+#else
                         const int qx = pixv[k] < 0 ? 0 : pixv[k];
                         const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, qx * 8, 0, 0);
                         dv[k] = __uint_as_float(raw.x);
                         mv[k] = __uint_as_float(raw.y);
+#endif
                     }
                     // phase C: the depth test; colour gathered only by the lanes whose voxel updates
                     bool doitv[BZ];
