@@ -17,7 +17,7 @@ rows = list(csv.DictReader(open("gpurun_out/sv_${v}_prof/kernel_stats.csv")))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print("  total ms", round(tot / 1e6, 2))
 for r in rows:
-    if "sor" in r["Name"] or "cell_nbr" in r["Name"]:
+    if "sor" in r["Name"] or "cell_nbr" in r["Name"] or "fb_reduce" in r["Name"]:
         print("  ", r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us avg", r["Name"][:50])
 PY
 done
