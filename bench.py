@@ -8,7 +8,7 @@ reconstruct_rgbd_filter.py:154-155) => weak scaling, no data-path collective; ba
 timing.  Prints ONE JSON line on rank 0.
 
 Also reported:
-  roofline     — dominant kernel (k_batch_integrate): algorithmic bytes per launch (5*W*H + 40*U_f)
+  roofline     — dominant kernel (k_batch_integrate<true>, float64 colour): algorithmic bytes per launch (5*W*H + 40*U_f)
                  over its mean device time measured with HIP events on the launch stream (`frac` = `frac_effective`:
                  temporal blocking keeps voxel state on chip across a batch, so it may exceed 1), and the measured HBM
                  bytes per launch from rocprofv3 PMC counters (profiles/pmc_traffic.json, used only when its source
@@ -52,9 +52,12 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
     ap.add_argument("--cpu-frames", type=int, default=32, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--sustain", type=float, default=1.5, help="seconds of sustained headline steps (0 = skip)")
-    ap.add_argument("--color64", type=int, default=1, help="also time the headline at float64 colour precision")
+    ap.add_argument("--color-bits", type=int, default=64, choices=(32, 64),
+                    help="headline colour precision: 64 = Open3D's float64 TSDFVoxel::color_ (the C ABI and facade "
+                         "default, bit-exact colours); 32 = float32 colour state")
+    ap.add_argument("--color32", type=int, default=1,
+                    help="also time the headline workload with float32 colour state (a labelled secondary leg)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--calib", action="store_true", help="after timing, run export_units once (PMC calibration)")
     ap.add_argument("--filter-frames", type=int, default=512,
                     help="configs[2] stream length, distinct frames (1280x720 unproject + 5 mm voxel + SOR); 0 = skip")
     ap.add_argument("--filter-batch", type=int, default=32, help="configs[2]: frames per batched chain call")
@@ -124,6 +127,7 @@ def main():
 
     vol = C.c_void_p()
     L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
+    L.call("ot_tsdf_set_color_precision", vol, args.color_bits)  # 64 is already the default; explicit for the record
     if args.batch > 0:
         L.call("ot_tsdf_set_batch", vol, args.batch)
     frame_bytes = W * H
@@ -189,37 +193,40 @@ def main():
     frames_total = world * args.frames * args.steps
     value = frames_total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
+    # 40 B per voxel update = read + write of a 20-B record (f32 tsdf, weight, 3 x f32 colour) whatever
+    # the layout -- also at colour precision 64, whose record is 32 B (the figure stays the survey's, so the two
+    # precisions' fractions compare the same work)
     algo_bytes_step = 5.0 * W * H * args.frames + 40.0 * upd.value
     per_launch_bytes = algo_bytes_step / max(klaunch.value, 1)
     kernel_ms_avg = kms.value / max(klaunch.value, 1)
     achieved = per_launch_bytes / (kernel_ms_avg * 1e-3) / 1e9 if kernel_ms_avg > 0 else 0.0
-    traffic, traffic_note = _traffic(args, L, "k_batch_integrate", {"voxel": args.voxel, "frames": args.frames,
-                                                                    "batch": args.batch})
+    kname = "k_batch_integrate<true>" if args.color_bits == 64 else "k_batch_integrate<false>"
+    pmc_cfg = {"voxel": args.voxel, "frames": args.frames, "batch": args.batch, "color_bits": args.color_bits}
+    traffic, traffic_note = _traffic(args, L, kname, pmc_cfg)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "frac_effective": round(achieved / HBM_PEAK_GBS, 4),
                 "effective": args.batch != 1,  # voxel state reused on chip across a batch
                 "traffic": traffic, "traffic_source": traffic_note,
-                "kernel": "k_integrate" if args.batch == 1 else "k_batch_integrate",
+                "kernel": ("k_integrate" if args.batch == 1 else "k_batch_integrate") +
+                          ("<true>" if args.color_bits == 64 else "<false>"),
+                "color_bits": args.color_bits,
                 "kernel_ms_avg": round(kernel_ms_avg, 5), "launches_per_step": klaunch.value,
                 "algorithmic_bytes_per_launch": round(per_launch_bytes),
                 "voxel_updates_per_frame": round(upd.value / args.frames)}
     if traffic and kernel_ms_avg > 0:  # measured HBM bytes per launch over the same launch time
         roofline["hbm_achieved"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9, 1)
         roofline["hbm_frac"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-    ient, _ = _pmc_entry(args, L, "k_batch_integrate", {"voxel": args.voxel, "frames": args.frames, "batch": args.batch})
+    ient, _ = _pmc_entry(args, L, kname, pmc_cfg)
     if ient and ient.get("valu_busy_frac") is not None:  # the other ceiling: vector-ALU issue (PMC, same build)
         roofline["valu_busy_frac"] = round(ient["valu_busy_frac"], 4)
-
-    if args.calib:  # a kernel with a known read byte count and the integrate kernel's pool access pattern
-        nu = n_units.value
-        bufs = [torch.empty((nu, 4096, k), dtype=torch.float32, device="cuda") for k in (1, 1, 3)]
-        L.call("ot_tsdf_export_units", vol, nu, None, *[C.c_void_p(b.data_ptr()) for b in bufs], stream)
-        torch.cuda.synchronize()
+    if ient:  # raw counters and the correction applied to them (calibrated on 8-B gathers, tools/fetch_calib.hip)
+        roofline["traffic_raw"] = {k: ient.get(k) for k in ("raw_fetch_kib", "raw_write_kib", "fetch_correction",
+                                                            "fetch_correction_source", "write_correction")}
 
     # configs[2] stream set up (uploaded, handles + worker threads warmed) before the other legs allocate
     fstream = FilterStream(args, L, synth, torch, filt_frames) if (args.filter_frames > 0 and rank == 0) else None
-    color64 = headline_color64(args, L, lib, torch, dist, world, d_depth, d_color, ext, intr, stream, upd.value) \
-        if args.color64 else None
+    color32 = headline_color32(args, L, lib, torch, dist, world, d_depth, d_color, ext, intr, stream, upd.value) \
+        if (args.color32 and args.color_bits == 64) else None
 
     # leg order: OT_BENCH_ORDER may repeat legs and insert "sleep" (5 s idle) for diagnosis; the
     # reported filtered / objects objects are the first run of each, later filtered runs go to filtered_repeat_ms
@@ -255,13 +262,19 @@ def main():
 
     out = {"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32 tsdf/weight + f64 colour" if args.color_bits == 64 else "f32 (colour state f32)",
+           "data": "synthetic",
            "config": {"workload": "configs[1]: 256-frame 640x480 RGB-D TSDF integration, 5 mm voxel, "
-                                  "sdf_trunc 0.04, one object scan per GPU (synthetic box-on-floor ring scan)",
+                                  "sdf_trunc 0.04, one object scan per GPU (synthetic box-on-floor ring scan), "
+                                  f"colour precision {args.color_bits}" +
+                                  (" (Open3D's float64 TSDFVoxel::color_, exact division: bit-exact colours)"
+                                   if args.color_bits == 64 else " (float32 colour state, |rel| <= 1e-4)"),
+                      "color_precision": args.color_bits,
                       "frames_per_step": args.frames, "width": W, "height": H, "voxel_length": args.voxel,
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
-           "roofline": roofline, "cpu_baseline": cpu, "sustained": sustained, "color64": color64,
+           "roofline": roofline, "cpu_baseline": cpu, "sustained": sustained, "color32": color32,
            "filtered": filt, "objects": objects,
            "hybrid_map": hybrid, "single_frame": single, "spatial": spatial, "source_hash": L.source_hash()}
     if rank == 0:
@@ -272,13 +285,13 @@ def main():
         dist.destroy_process_group()
 
 
-def headline_color64(args, L, lib, torch, dist, world, d_depth, d_color, ext, intr, stream, updates_f32):
-    """The configs[1] workload with the voxel colour state at Open3D's precision (float64, exact division:
-    ot_tsdf_set_color_precision(64), bit-exact colours) -- what reference precision costs next to the float32
-    headline.  Same frames, same timing method (K steps between barrier + synchronize, max over ranks)."""
+def headline_color32(args, L, lib, torch, dist, world, d_depth, d_color, ext, intr, stream, updates_c64):
+    """Secondary leg, labelled: the configs[1] workload with the voxel colour state in float32 (one reciprocal per
+    update, |rel| <= 1e-4 against Open3D's float64 colour; tsdf, weight and the update set are bit-identical).  Same
+    frames, same timing method (K steps between barrier + synchronize, max over ranks)."""
     vol = C.c_void_p()
     L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
-    L.call("ot_tsdf_set_color_precision", vol, 64)
+    L.call("ot_tsdf_set_color_precision", vol, 32)
     if args.batch > 0:
         L.call("ot_tsdf_set_batch", vol, args.batch)
     W, H = intr.width, intr.height
@@ -306,10 +319,21 @@ def headline_color64(args, L, lib, torch, dist, world, d_depth, d_color, ext, in
     kms, kl = C.c_double(0.0), C.c_int64(0)
     L.call("ot_tsdf_kernel_time", vol, C.byref(kms), C.byref(kl))
     L.call("ot_tsdf_destroy", vol)
-    return {"workload": "configs[1] with colour precision 64 (float64 running colour mean, exact division: Open3D's "
-                        "TSDFVoxel::color_)", "steps": steps, "frames_per_s": round(world * args.frames / dt, 1),
-            "ms_per_step": round(dt * 1e3, 3), "kernel_ms_avg": round(kms.value / max(kl.value, 1), 5),
-            "voxel_updates_match_f32": upd.value == updates_f32}
+    kavg = kms.value / max(kl.value, 1)
+    per_launch = (5.0 * W * H * args.frames + 40.0 * upd.value) / max(kl.value, 1)
+    ent, note = _pmc_entry(args, L, "k_batch_integrate<false>", {"voxel": args.voxel, "frames": args.frames,
+                                                                 "batch": args.batch, "color_bits": 32})
+    roof = {"kernel": "k_batch_integrate<false>", "kernel_ms_avg": round(kavg, 5),
+            "frac_effective": round(per_launch / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kavg > 0 else None}
+    if ent and kavg > 0:
+        roof["hbm_frac"] = round(ent["bytes_per_launch"] / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        roof["traffic"] = ent["bytes_per_launch"]
+    else:
+        roof["traffic_source"] = note
+    return {"workload": "configs[1] with colour precision 32 (float32 colour state, one reciprocal per update, "
+                        "|rel| <= 1e-4 vs Open3D's float64 colour) -- a faster, narrower variant, not the headline",
+            "steps": steps, "frames_per_s": round(world * args.frames / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+            "roofline": roof, "voxel_updates_match_headline": upd.value == updates_c64}
 
 
 def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
@@ -793,8 +817,9 @@ def _pmc_entry(args, L, kernel, config):
         return None, f"no PMC entry for {kernel}"
     if tr.get("source_hash") != L.source_hash():
         return None, f"stale PMC file (source hash {tr.get('source_hash')} != {L.source_hash()})"
-    if any(tr.get("config", {}).get(k) != v for k, v in config.items()):
-        return None, f"PMC file workload {tr.get('config')} != {config}"
+    cfg = ent.get("config", tr.get("config", {}))
+    if any(cfg.get(k) != v for k, v in config.items()):
+        return None, f"PMC entry workload {cfg} != {config}"
     return ent, f"{os.path.relpath(args.traffic, ROOT)} (source hash {tr['source_hash']})"
 
 
@@ -826,9 +851,9 @@ def cpu_baseline(depth, color, ext, intr_t, args):
     dt = float(np.median(times))
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     return {"value": round(n / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} of the {args.frames} frames, same synthetic scan, one fresh volume per pass, "
-                      f"1 warm-up + median of 5 passes, depth->float excluded (done before timing), "
-                      f"OMP_NUM_THREADS={cores}",
+            "sample": f"first {n} of the {args.frames} frames, same synthetic scan, one fresh volume per pass "
+                      f"(float64 colour state, as Open3D and the headline), 1 warm-up + median of 5 passes, "
+                      f"depth->float excluded (done before timing), OMP_NUM_THREADS={cores}",
             "pass_seconds": [round(t, 3) for t in times]}
 
 

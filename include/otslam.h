@@ -175,6 +175,9 @@ ot_status ot_tsdf_integrate_u16(ot_tsdf* vol, const uint16_t* depth, const uint8
                                 const ot_intrinsics* intrinsic, const double extrinsic[16],
                                 double depth_scale, double depth_trunc, void* stream);
 ot_status ot_tsdf_flush(ot_tsdf* vol, void* stream);
+/* Frames queued on the host for the next batch (their input buffers are still referenced; every frame queued before
+ * them has been enqueued on its stream).  Host-only, no synchronisation. */
+ot_status ot_tsdf_pending_frames(const ot_tsdf* vol, int32_t* n_host);
 /* Batch size used by ot_tsdf_integrate_u16 (1 = integrate immediately, default 32). */
 ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames);
 
@@ -183,11 +186,13 @@ ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n_units_host, void* stream);
 /* Cumulative voxel updates and volume-unit integrations since create/reset (flushes on `stream`, synchronises it). */
 ot_status ot_tsdf_counters(ot_tsdf* vol, int64_t* voxel_updates_host, int64_t* unit_integrations_host,
                            void* stream);
-/* Colour state precision: 64 keeps each voxel's running colour mean in float64 with exact IEEE division, as Open3D's
- * TSDFVoxel::color_ (Eigen::Vector3d; reconstruct_rgbd_filter.py:81-85 -> SURVEY A.3(iv)) -- bit-exact colours;
- * 32 (default of the C ABI) keeps float32 with one hardware reciprocal per update (|rel| <= 1e-4, faster).  Call
- * before the first integrate. */
+/* Colour state precision: 64 (the default, as in the Python facade) keeps each voxel's running colour mean in float64
+ * with exact IEEE division, as Open3D's TSDFVoxel::color_ (Eigen::Vector3d; reconstruct_rgbd_filter.py:81-85 ->
+ * SURVEY A.3(iv)) -- bit-exact colours, 128-KiB unit records; 32 keeps float32 with one hardware reciprocal per update
+ * (|rel| <= 1e-4, 80-KiB records, faster).  NoColor volumes keep no colour state whatever the setting (get reports
+ * 32).  Call before the first integrate (the unit pool is reallocated when the record size changes). */
 ot_status ot_tsdf_set_color_precision(ot_tsdf* vol, int32_t bits);
+ot_status ot_tsdf_get_color_precision(const ot_tsdf* vol, int32_t* bits_host);
 
 /* Kernel timing for roofline reporting: when enabled, HIP events bracket every launch of the dominant
  * integration kernel on the caller's stream; ot_tsdf_kernel_time returns the summed device time (ms) and the
@@ -200,8 +205,10 @@ ot_status ot_tsdf_kernel_time(ot_tsdf* vol, double* total_ms_host, int64_t* laun
  * NULL.  Device pointers; every output holds `capacity` units. */
 ot_status ot_tsdf_export_units(ot_tsdf* vol, int64_t capacity, int32_t* keys, float* tsdf, float* weight,
                                float* color, void* stream);
-/* The float64 colours of a colour-precision-64 volume, [U][4096][3] in export_units' order.  Both exports fail with
- * OT_ERR_CAPACITY when the volume holds more than `capacity` units (outputs sized from an older unit count). */
+/* The colours as float64, [U][4096][3] in export_units' order: exact for a colour-precision-64 volume, the float32
+ * state widened otherwise.  Both exports fail with OT_ERR_CAPACITY when the volume holds more than `capacity` units
+ * (outputs sized from an older unit count).  A spatially sharded volume exports (and ot_tsdf_num_units counts) only
+ * its own units, not the halo units ot_tsdf_import_border added. */
 ot_status ot_tsdf_export_color64(ot_tsdf* vol, int64_t capacity, double* color, void* stream);
 
 /* The inverse of ot_tsdf_export_units (same layouts): insert n units, overwriting any unit with the same key;

@@ -65,9 +65,11 @@ SIGNATURES = {
     "ot_tsdf_integrate_u16": [_p, _p, _p, _pint, _p, _d, _d, _p],
     "ot_tsdf_flush": [_p, _p],
     "ot_tsdf_set_batch": [_p, _i32],
+    "ot_tsdf_pending_frames": [_p, _p],
     "ot_tsdf_num_units": [_p, _pi64, _p],
     "ot_tsdf_counters": [_p, _pi64, _pi64, _p],
     "ot_tsdf_set_color_precision": [_p, _i32],
+    "ot_tsdf_get_color_precision": [_p, _p],
     "ot_tsdf_export_color64": [_p, _i64, _p, _p],
     "ot_tsdf_set_profiling": [_p, _i32],
     "ot_tsdf_kernel_time": [_p, C.POINTER(C.c_double), _pi64],

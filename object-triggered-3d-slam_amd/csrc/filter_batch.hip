@@ -508,7 +508,11 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     // the pinned table is rewritten only after the previous run's copy has completed (every run synchronises)
     for (int f = 0; f < F; ++f) inverse4(extrinsics_host + 16 * f, fl->h_frames[f].pose);
     FbFrame* d_frames = (FbFrame*)fl->b_frames.get(sizeof(FbFrame) * F);
-    int* d_tc = (int*)fl->b_tiles.get((size_t)F * tpf * (4 + 48) + 1024 + (size_t)(F + 1) * 24);
+    // layout: tile counts i32 [F*tpf] | align 64 | tile bounds u64 [F*tpf][6] | frame bounds u64 [F][6] | kbits i32 [4]
+    // | totals i64 [2] | voff i32 [F+1] | poff i32 [F]
+    const size_t tiles_bytes = (size_t)F * tpf * 4 + 63 + (size_t)F * tpf * 48 + (size_t)F * 48 + 16 + 16 +
+                               (size_t)(F + 1) * 4 + (size_t)F * 4;
+    int* d_tc = (int*)fl->b_tiles.get(tiles_bytes);
     if (!d_frames || !d_tc) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
     unsigned long long* d_tb = (unsigned long long*)(((uintptr_t)(d_tc + (size_t)F * tpf) + 63) & ~(uintptr_t)63);
     unsigned long long* d_fb = d_tb + (size_t)F * tpf * 6;

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
             const int lz = c / (T17 * T17), lx = (c / T17) % T17, ly = c % T17;
             const int nid = snbr[((lx >> 4) << 2) | ((ly >> 4) << 1) | (lz >> 4)];
             if (nid >= 0) {
-                const float* base = d.vox + (size_t)nid * UNIT_FLOATS;
+                const float* base = unit_base(d, nid);
                 const int vi = (lz & 15) * 256 + (lx & 15) * 16 + (ly & 15);
                 fv[i] = base[vi];
                 wv[i] = base[UNIT_VOX + vi];
@@ -196,10 +196,10 @@ __global__ __launch_bounds__(EWORDS) void k_mc_count(McDev m) {
 // tsdf and colour of one voxel; colour from the float64 pool when the volume keeps it (exact: a float colour widens
 // to double exactly, as Open3D's float-to-double promotion)
 __device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z, float& f, double c[3]) {
-    const float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    const float* base = unit_base(d, id);
     const int vi = z * 256 + x * 16 + y;
     f = base[vi];
-    if (d.vcol) {
+    if (d.color64) {
         const double* cb = color_base<double>(d, id);
         c[0] = cb[vi];
         c[1] = cb[UNIT_VOX + vi];

@@ -21,7 +21,8 @@ namespace ot {
 constexpr int UNIT_RES = 16;
 constexpr int UNIT_VOX = UNIT_RES * UNIT_RES * UNIT_RES;  // 4096
 constexpr int UNIT_FIELDS = 5;
-constexpr int UNIT_FLOATS = UNIT_FIELDS * UNIT_VOX;  // 20480 floats = 80 KiB
+constexpr int UNIT_FLOATS = UNIT_FIELDS * UNIT_VOX;  // float32 colour record: 20480 floats = 80 KiB
+constexpr int UNIT_FLOATS_C64 = 8 * UNIT_VOX;        // float64 colour record: tsdf, weight (f32) + r, g, b (f64) = 128 KiB
 
 // counters[] slots
 constexpr int C_TOUCHED = 0;   // units touched by the current frame
@@ -43,8 +44,9 @@ struct TsdfDev {
     int* counters;
     unsigned long long* stats;
     int* unit_keys;
-    float* vox;
-    double* vcol;               // float64 colour pool [id][3][4096] (colour precision 64), else nullptr
+    float* vox;                 // unit pool: max_units records of unit_floats floats
+    int unit_floats;            // record stride: UNIT_FLOATS (float32 colour / NoColor) or UNIT_FLOATS_C64
+    int color64;                // 1: the record's colour planes are float64 (colour precision 64, RGB8 volumes)
     unsigned long long* fmask;  // per hash slot: frames of the current batch that touch the unit (bit f)
     int* bslots;                // hash slots touched by the current batch (first-touch order)
     void* work;                 // per touched slot of the batch: unit header (UnitWork, 32 B) for the integrate
@@ -61,17 +63,12 @@ __host__ __device__ inline bool unit_owned(const TsdfDev& d, unsigned long long 
     return (int)((unsigned)(mix64(key + 0x9E3779B97F4A7C15ull) >> 32) % (unsigned)d.shard_world) == d.shard_rank;
 }
 
-// a unit's colour planes r, g, b (4096 each, voxel vi = z*256 + x*16 + y): the float planes inside the voxel
-// record, or the float64 pool when the volume keeps colour at Open3D's precision
+// a unit's record: tsdf plane, weight plane, then the colour planes r, g, b (4096 each, voxel vi = z*256 + x*16 + y)
+// in float32 or, when the volume keeps colour at Open3D's precision, float64 (the record is then 128 KiB)
+__host__ __device__ inline float* unit_base(const TsdfDev& d, int id) { return d.vox + (size_t)id * d.unit_floats; }
 template <typename CT>
-__device__ inline CT* color_base(const TsdfDev& d, int id);
-template <>
-__device__ inline float* color_base<float>(const TsdfDev& d, int id) {
-    return d.vox + (size_t)id * UNIT_FLOATS + 2 * UNIT_VOX;
-}
-template <>
-__device__ inline double* color_base<double>(const TsdfDev& d, int id) {
-    return d.vcol + (size_t)id * 3 * UNIT_VOX;
+__device__ inline CT* color_base(const TsdfDev& d, int id) {
+    return reinterpret_cast<CT*>(unit_base(d, id) + 2 * UNIT_VOX);
 }
 
 // Border voxels of a unit: every voxel with x == 0, y == 0 or z == 0 (3 * 256 - 3 * 16 + 1 = 721), the only

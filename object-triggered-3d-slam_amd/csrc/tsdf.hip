@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
         const int id = ent & 0x7FFFFFFF;
         const bool fresh = ent < 0;
         const int kx = d.unit_keys[id * 3 + 0], ky = d.unit_keys[id * 3 + 1], kz = d.unit_keys[id * 3 + 2];
-        float* base = d.vox + (size_t)id * UNIT_FLOATS;
+        float* base = unit_base(d, id);
         CT* cbase = color_base<CT>(d, id);
         float pc[3];
         column_origin(p, kx, ky, kz, x, y, pc);
@@ -622,7 +622,7 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 #endif
 // One workgroup of SLICES waves per unit, so a unit's frame footprint is gathered through one CU's L1; units are
 // assigned by a static grid stride that every wave derives on its own: no barriers, no LDS, no atomics.
-// C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the separate pool d.vcol
+// C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes
 template <bool C64>
 __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
@@ -645,11 +645,11 @@ __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_P
                 const int x = (s & 2) * 4 + (lane >> 3), y = (s & 1) * 8 + (lane & 7);
                 const int col = x * 16 + y;
                 const int z0 = (s >> 2) * BZ;
-                float* base = d.vox + (size_t)id * UNIT_FLOATS;
+                float* base = d.vox + (size_t)id * (C64 ? UNIT_FLOATS_C64 : UNIT_FLOATS);
                 // colour plane c of voxel vi: float32 planes addressed from base (one address register for the
-                // whole record: a separate colour pointer costs ~34 VGPRs in this kernel), float64 from the pool
-                const __amdgpu_buffer_rsrc_t col64 =
-                    make_rsrc(C64 ? (const void*)color_base<double>(d, id) : (const void*)base, 3 * UNIT_VOX * 8);
+                // whole record: a separate colour pointer costs ~34 VGPRs in this kernel), float64 through a buffer
+                // resource over the record's float64 planes
+                const __amdgpu_buffer_rsrc_t col64 = make_rsrc(base + 2 * UNIT_VOX, 3 * UNIT_VOX * 8);
                 float ts[BZ], wt[BZ];
                 CT cr[BZ], cg[BZ], cb[BZ];
 #pragma unroll
@@ -823,7 +823,7 @@ __global__ __launch_bounds__(256) void k_export(TsdfDev d, const unsigned* sorte
     const int r = blockIdx.x;
     const int id = (int)sorted_ids[r];
     const int tid = threadIdx.x;
-    const float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    const float* base = unit_base(d, id);
     const CT* cbase = color_base<CT>(d, id);
     if (keys && tid < 3) keys[(int64_t)r * 3 + tid] = d.unit_keys[id * 3 + tid];
     for (int z = 0; z < UNIT_RES; ++z) {
@@ -845,7 +845,7 @@ __global__ __launch_bounds__(256) void k_export_border(TsdfDev d, const unsigned
                                                        float* tsdf, float* weight, CT* color) {
     const int r = blockIdx.x;
     const int id = (int)sorted_ids[r];
-    const float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    const float* base = unit_base(d, id);
     const CT* cbase = color_base<CT>(d, id);
     if (threadIdx.x < 3) keys[(int64_t)r * 3 + threadIdx.x] = d.unit_keys[id * 3 + threadIdx.x];
     for (int b = threadIdx.x; b < BORDER_VOX; b += 256) {
@@ -926,7 +926,7 @@ __global__ __launch_bounds__(256) void k_import_border(TsdfDev d, const int32_t*
     __syncthreads();
     const int id = s_id;
     if (id < 0) return;
-    float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    float* base = unit_base(d, id);
     CT* cbase = color_base<CT>(d, id);
     if (s_fresh) {
         for (int vi = threadIdx.x; vi < UNIT_VOX; vi += 256) {
@@ -964,6 +964,26 @@ struct OwnedEmit {
     unsigned* out;
     __device__ void operator()(int64_t r, int64_t pos) const { out[pos] = sorted_ids[r]; }
 };
+
+// Units an export lists: every unit in sorted key order or, for a spatially sharded volume, only its own units -- the
+// halo units imported for marching cubes (k_import_border) are copies of other shards' border rows, and exporting
+// them would hand their keys to an assembly twice (the second time with zeros inside the unit).
+static ot_status export_list(ot_tsdf* vol, hipStream_t stream, const unsigned** ids, int64_t* n) {
+    int64_t nu = 0;
+    ot_status st = tsdf_sorted_units(vol, stream, &nu);
+    if (st != OT_OK) return st;
+    *ids = vol->sorted_ids;
+    *n = nu;
+    if (vol->dev.shard_world <= 1 || nu == 0) return OT_OK;
+    unsigned* own = (unsigned*)scratch(sizeof(unsigned) * (size_t)nu + 256, 16);
+    if (!own) return fail(OT_ERR_HIP, "scratch allocation failed");
+    int64_t no = 0;
+    st = compact(nu, OwnedPred{vol->dev, vol->sorted_ids}, OwnedEmit{vol->sorted_ids, own}, stream, &no, 13);
+    if (st != OT_OK) return st;
+    *ids = own;
+    *n = no;
+    return OT_OK;
+}
 
 // import: the inverse of k_export (keys unique within one call; an existing unit is overwritten); colour as the
 // volume keeps it (CT)
@@ -1004,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_import(TsdfDev d, const int32_t* __rest
     __syncthreads();
     const int id = s_id;
     if (id < 0) return;
-    float* base = d.vox + (size_t)id * UNIT_FLOATS;
+    float* base = unit_base(d, id);
     CT* cbase = color_base<CT>(d, id);
     for (int z = 0; z < UNIT_RES; ++z) {
         const int vi = z * 256 + tid;
@@ -1409,7 +1429,11 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
     if ((e = hipMalloc(&d.counters, sizeof(int) * N_COUNTERS)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.stats, sizeof(unsigned long long) * 4)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.unit_keys, sizeof(int) * 3 * max_units)) != hipSuccess) return cleanup(e);
-    if ((e = hipMalloc(&d.vox, sizeof(float) * (size_t)UNIT_FLOATS * max_units)) != hipSuccess) return cleanup(e);
+    // RGB8 volumes keep colour at Open3D's precision (float64, 128-KiB records) unless set_color_precision(32)
+    v->color64 = color_type == OT_COLOR_RGB8;
+    d.color64 = v->color64 ? 1 : 0;
+    d.unit_floats = v->color64 ? UNIT_FLOATS_C64 : UNIT_FLOATS;
+    if ((e = hipMalloc(&d.vox, sizeof(float) * (size_t)d.unit_floats * max_units)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&v->sorted_ids, sizeof(unsigned) * max_units)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.fmask, sizeof(unsigned long long) * cap)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.bslots, sizeof(int) * cap)) != hipSuccess) return cleanup(e);
@@ -1431,7 +1455,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     (void)hipDeviceSynchronize();
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
-    void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, d.vcol, v->mult,
+    void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, v->mult,
                     v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, d.fmask, d.bslots, d.work,
                     v->bframes, v->bdm, v->brgba};
     for (void* p : ptrs)
@@ -1521,6 +1545,12 @@ ot_status ot_tsdf_flush(ot_tsdf* vol, void* stream) {
     return tsdf_flush(vol, S(stream));
 }
 
+ot_status ot_tsdf_pending_frames(const ot_tsdf* vol, int32_t* n_host) {
+    if (!vol || !n_host) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    *n_host = (int32_t)vol->pending.size();
+    return OT_OK;
+}
+
 ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames) {
     if (!vol || max_frames < 1) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] batch must be >= 1");
     vol->batch_max = max_frames;
@@ -1532,6 +1562,10 @@ ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n, void* stream_) {
     hipStream_t stream = S(stream_);
     ot_status st = tsdf_flush(vol, stream);  // queued frames, on the caller's stream
     if (st != OT_OK) return st;
+    if (vol->dev.shard_world > 1) {  // a shard counts its own units (halo units are not exported)
+        const unsigned* ids = nullptr;
+        return export_list(vol, stream, &ids, n);
+    }
     int nu = 0;
     OT_HIP_TRY(hipMemcpyAsync(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost, stream));
     OT_HIP_TRY(hipStreamSynchronize(stream));
@@ -1559,14 +1593,24 @@ ot_status ot_tsdf_set_color_precision(ot_tsdf* vol, int32_t bits) {
     OT_HIP_TRY(hipMemcpy(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost));
     if (nu != 0 || !vol->pending.empty())
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] set the colour precision before the first integrate");
-    if (bits == 64 && !vol->dev.vcol)
-        OT_HIP_TRY(hipMalloc(&vol->dev.vcol, sizeof(double) * 3 * (size_t)UNIT_VOX * vol->max_units));
-    if (bits == 32 && vol->dev.vcol) {  // kernels take the float64 pool whenever it exists
+    // NoColor volumes keep no colour state: the float32 record (zero colour planes) whatever the precision
+    const bool c64 = bits == 64 && vol->color_type == OT_COLOR_RGB8;
+    if (c64 != vol->color64) {  // the record stride changes: reallocate the (still empty) pool
+        const int uf = c64 ? UNIT_FLOATS_C64 : UNIT_FLOATS;
         OT_HIP_TRY(hipDeviceSynchronize());
-        OT_HIP_TRY(hipFree(vol->dev.vcol));
-        vol->dev.vcol = nullptr;
+        OT_HIP_TRY(hipFree(vol->dev.vox));
+        vol->dev.vox = nullptr;
+        OT_HIP_TRY(hipMalloc(&vol->dev.vox, sizeof(float) * (size_t)uf * vol->max_units));
+        vol->dev.unit_floats = uf;
+        vol->dev.color64 = c64 ? 1 : 0;
+        vol->color64 = c64;
     }
-    vol->color64 = bits == 64;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_get_color_precision(const ot_tsdf* vol, int32_t* bits) {
+    if (!vol || !bits) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    *bits = vol->color64 ? 64 : 32;
     return OT_OK;
 }
 
@@ -1606,16 +1650,17 @@ ot_status ot_tsdf_export_units(ot_tsdf* vol, int64_t capacity, int32_t* keys, fl
                                void* stream) {
     if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     int64_t nu = 0;
-    ot_status st = tsdf_sorted_units(vol, S(stream), &nu);
+    const unsigned* ids = nullptr;
+    ot_status st = export_list(vol, S(stream), &ids, &nu);
     if (st != OT_OK) return st;
     if (nu > capacity) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] export: more units than the output capacity");
     if (nu == 0) return OT_OK;
     if (vol->color64)
-        hipLaunchKernelGGL((k_export<double, float>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev,
-                           vol->sorted_ids, keys, tsdf, weight, color);
+        hipLaunchKernelGGL((k_export<double, float>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev, ids, keys,
+                           tsdf, weight, color);
     else
-        hipLaunchKernelGGL((k_export<float, float>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev,
-                           vol->sorted_ids, keys, tsdf, weight, color);
+        hipLaunchKernelGGL((k_export<float, float>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev, ids, keys,
+                           tsdf, weight, color);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(S(stream)));
     return OT_OK;
@@ -1623,14 +1668,18 @@ ot_status ot_tsdf_export_units(ot_tsdf* vol, int64_t capacity, int32_t* keys, fl
 
 ot_status ot_tsdf_export_color64(ot_tsdf* vol, int64_t capacity, double* color, void* stream) {
     if (!vol || !color) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
-    if (!vol->color64) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] export_color64 needs colour precision 64");
     int64_t nu = 0;
-    ot_status st = tsdf_sorted_units(vol, S(stream), &nu);
+    const unsigned* ids = nullptr;
+    ot_status st = export_list(vol, S(stream), &ids, &nu);
     if (st != OT_OK) return st;
     if (nu > capacity) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] export: more units than the output capacity");
     if (nu == 0) return OT_OK;
-    hipLaunchKernelGGL((k_export<double, double>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev,
-                       vol->sorted_ids, nullptr, nullptr, nullptr, color);
+    if (vol->color64)
+        hipLaunchKernelGGL((k_export<double, double>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev, ids,
+                           nullptr, nullptr, nullptr, color);
+    else  // float32 colour state (or NoColor's zero planes) widens exactly
+        hipLaunchKernelGGL((k_export<float, double>), dim3((unsigned)nu), dim3(256), 0, S(stream), vol->dev, ids,
+                           nullptr, nullptr, nullptr, color);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(S(stream)));
     return OT_OK;
@@ -1666,14 +1715,18 @@ static ot_status import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, cons
     if (!vol || n < 0 || (n > 0 && (!keys || !tsdf || !weight)))
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: invalid arguments");
     if (n > vol->max_units) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: more units than max_units");
-    if (vol->color64 != (sizeof(CT) == 8))
+    const bool rgb8 = vol->color_type == OT_COLOR_RGB8;
+    if (rgb8 && vol->color64 != (sizeof(CT) == 8))
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: colour dtype does not match the volume's "
                                              "colour precision");
     ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
     if (n == 0) return OT_OK;
-    hipLaunchKernelGGL(k_import<CT>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf, weight,
-                       vol->color_type == OT_COLOR_RGB8 ? color : nullptr);
+    if (rgb8)
+        hipLaunchKernelGGL(k_import<CT>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf, weight, color);
+    else  // NoColor: float32 record, zero colour planes
+        hipLaunchKernelGGL(k_import<float>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf, weight,
+                           (const float*)nullptr);
     OT_LAUNCH_CHECK();
     vol->sorted_units = -1;  // the sorted-unit cache no longer matches
     st = check_errors(vol, stream);
@@ -1698,18 +1751,17 @@ ot_status ot_tsdf_export_border(ot_tsdf* vol, int64_t capacity, int32_t* keys, f
                                 int64_t* n_exported_host, void* stream) {
     if (!vol || !keys || !tsdf || !weight || !n_exported_host) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     *n_exported_host = 0;
-    int64_t nu = 0;
-    ot_status st = tsdf_sorted_units(vol, S(stream), &nu);
-    if (st != OT_OK) return st;
-    if (nu == 0) return OT_OK;
-    unsigned* own = (unsigned*)scratch(sizeof(unsigned) * (size_t)nu + 256, 16);
-    if (!own) return fail(OT_ERR_HIP, "scratch allocation failed");
     int64_t no = 0;  // the own units (halo units imported earlier are not this shard's border)
-    st = compact(nu, OwnedPred{vol->dev, vol->sorted_ids}, OwnedEmit{vol->sorted_ids, own}, S(stream), &no, 13);
+    const unsigned* own = nullptr;
+    ot_status st = export_list(vol, S(stream), &own, &no);
     if (st != OT_OK) return st;
+    if (no == 0) return OT_OK;
     if (no > capacity) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] export: more units than the output capacity");
     if (no > 0) {
-        if (vol->color64)
+        if (vol->color_type != OT_COLOR_RGB8)  // NoColor: no colour rows (the caller's buffer is left as it is)
+            hipLaunchKernelGGL(k_export_border<float>, dim3((unsigned)no), dim3(256), 0, S(stream), vol->dev, own,
+                               keys, tsdf, weight, (float*)nullptr);
+        else if (vol->color64)
             hipLaunchKernelGGL(k_export_border<double>, dim3((unsigned)no), dim3(256), 0, S(stream), vol->dev, own,
                                keys, tsdf, weight, (double*)color);
         else
@@ -1731,7 +1783,7 @@ ot_status ot_tsdf_import_border(ot_tsdf* vol, int64_t n, const int32_t* keys, co
     if (st != OT_OK) return st;
     if (n == 0) return OT_OK;
     const void* c = vol->color_type == OT_COLOR_RGB8 ? color : nullptr;
-    if (vol->color64)
+    if (vol->color64)  // (only RGB8 volumes store float64 colour)
         hipLaunchKernelGGL(k_import_border<double>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf,
                            weight, (const double*)c);
     else

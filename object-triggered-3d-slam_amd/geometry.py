@@ -19,10 +19,11 @@ from .utility import DoubleVector, Vector3dVector, Vector3iVector
 class _Arr:
     """An (N, k) array living on the host (numpy) and/or the device (torch)."""
 
-    __slots__ = ("_h", "_d")
+    __slots__ = ("_h", "_d", "_viewed")
 
     def __init__(self, host=None, dev=None):
         self._h, self._d = host, dev
+        self._viewed = False  # a writable host view was handed out: the host copy is authoritative
 
     @staticmethod
     def wrap(a, dtype, cols):
@@ -45,16 +46,22 @@ class _Arr:
         return self._h
 
     def host_view(self):
-        """The host array for a writable view handed to the caller: the device copy is dropped, so the next GPU use
-        uploads whatever the caller wrote (Open3D's vectors are views of the one copy)."""
+        """The host array for a writable view handed to the caller (Open3D's vectors are views of the one copy).
+        From now on the host copy is authoritative: every later GPU use uploads it again, so edits made through
+        any view taken earlier are seen; reads alone (len(mesh.vertices)) cost one download."""
         h = self.host()
-        self._d = None
+        self._viewed = True
         return h
 
     def dev(self):
-        if self._d is None:
+        if self._d is None or self._viewed:
             self._d = D.to_device(self._h)
         return self._d
+
+    def copy(self):
+        if self._viewed or self._d is None:
+            return _Arr(host=self.host().copy())
+        return _Arr(dev=self._d.clone())
 
     def __len__(self):
         return (self._h if self._h is not None else self._d).shape[0]
@@ -257,7 +264,8 @@ class PointCloud:
 
     def __add__(self, other):
         out = PointCloud()
-        out._xyz, out._rgb, out._nrm = self._xyz, self._rgb, self._nrm
+        cp = lambda a: a.copy() if a is not None else None  # a new cloud never shares arrays with an operand
+        out._xyz, out._rgb, out._nrm = cp(self._xyz), cp(self._rgb), cp(self._nrm)
         out += other
         return out
 
@@ -405,7 +413,7 @@ def _cat_dev(a, b):
     import torch
 
     if a is None:
-        return _Arr(dev=b.dev().clone())
+        return b.copy()
     return _Arr(dev=torch.cat([a.dev(), b.dev()], dim=0))
 
 

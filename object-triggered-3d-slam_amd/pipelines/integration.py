@@ -50,8 +50,10 @@ class ScalableTSDFVolume:
         self._batch = 32
         if batch_frames is not None:
             self.set_batch(batch_frames)
-        self.color_precision = int(color_precision)
-        L.call("ot_tsdf_set_color_precision", self._h, self.color_precision)
+        L.call("ot_tsdf_set_color_precision", self._h, int(color_precision))
+        bits = C.c_int32(0)
+        L.call("ot_tsdf_get_color_precision", self._h, C.byref(bits))
+        self.color_precision = bits.value  # NoColor volumes keep no colour state (32: zero float planes)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -67,11 +69,23 @@ class ScalableTSDFVolume:
         self._batch = int(frames)
 
     def _queued(self, item):
-        """Keep a queued frame's device images alive while the C side holds it; the C side integrates its queue
-        (asynchronously, on the caller's stream, which orders any reuse of the freed memory) when it is full."""
+        """Keep a queued frame's device images alive while the C side holds it.  Each tensor is recorded on the
+        current (launch) stream, so the caching allocator cannot hand its memory to another stream before the
+        kernels that read it have run, whichever stream allocated it."""
+        s = D.torch.cuda.current_stream()
+        for t in item:
+            if t is not None:
+                t.record_stream(s)
         self._keep.append(item)
-        if len(self._keep) >= min(self._batch, 64):
-            self._keep.clear()
+
+    def _release(self):
+        """Drop the references of the frames the C side has consumed (enqueued on their stream): all but the
+        ot_tsdf_pending_frames() newest."""
+        n = C.c_int32(0)
+        L.call("ot_tsdf_pending_frames", self._h, C.byref(n))
+        done = len(self._keep) - n.value
+        if done > 0:
+            del self._keep[:done]
 
     def reset(self):
         """ScalableTSDFVolume::Reset, ordered on the current stream (no device-wide synchronisation)."""
@@ -98,11 +112,13 @@ class ScalableTSDFVolume:
             self._queued((d16, cdev))
             L.call("ot_tsdf_integrate_u16", self._h, D.ptr(d16), D.ptr(cdev), C.byref(intr),
                    ext.ctypes.data_as(C.c_void_p), scale, trunc, D.stream_ptr())
+            self._release()
         else:
             ddev = depth.dev()
             self._queued((ddev, cdev))
             L.call("ot_tsdf_integrate", self._h, D.ptr(ddev), D.ptr(cdev), C.byref(intr),
                    ext.ctypes.data_as(C.c_void_p), D.stream_ptr())
+            self._release()
 
     def flush(self):
         L.call("ot_tsdf_flush", self._h, D.stream_ptr())
@@ -170,6 +186,8 @@ class ScalableTSDFVolume:
         tsdf = D.empty((n, 721), "float32")
         weight = D.empty((n, 721), "float32")
         color = D.empty((n, 721, 3), "float64" if self.color_precision == 64 else "float32")
+        if self.color_type != TSDFVolumeColorType.RGB8:
+            color.zero_()  # NoColor: the C side writes no colour rows
         m = C.c_int64(0)
         L.call("ot_tsdf_export_border", self._h, n, D.ptr(keys), D.ptr(tsdf), D.ptr(weight), D.ptr(color),
                C.byref(m), D.stream_ptr())

@@ -23,4 +23,18 @@ def test_point_cloud_assignment_copies_and_getter_is_view():
     view = np.asarray(pcd.points)
     view[2, 2] = 42.0  # an in-place edit through the view, as reconstruct_rgbd_filter.py-style code does
     assert np.asarray(pcd.points)[2, 2] == 42.0
-    assert pcd._xyz._d is None  # no stale device copy survives a handed-out view
+    assert pcd._xyz._viewed  # the host copy is authoritative: every later GPU use uploads it again
+
+
+def test_add_never_aliases_operands():
+    """pcd + <empty cloud> is a new cloud, not the same arrays (in-place edits must not leak)."""
+    pcd = pkg.geometry.PointCloud()
+    pcd.points = pkg.utility.Vector3dVector(np.arange(12, dtype=np.float64).reshape(4, 3))
+    pcd.colors = pkg.utility.Vector3dVector(np.full((4, 3), 0.5))
+    out = pcd + pkg.geometry.PointCloud()
+    np.asarray(out.points)[0, 0] = -1.0
+    np.asarray(out.colors)[0, 0] = 0.0
+    assert np.asarray(pcd.points)[0, 0] == 0.0 and np.asarray(pcd.colors)[0, 0] == 0.5
+    both = pkg.geometry.PointCloud() + pcd
+    np.asarray(both.points)[1, 1] = 99.0
+    assert np.asarray(pcd.points)[1, 1] == 4.0

@@ -29,8 +29,9 @@ def oracle_volume(O, synth, scan):
     return ref.export(), ref.total_updates(), ref.unit_integrations()
 
 
-@pytest.mark.parametrize("bits", [32, 64])
+@pytest.mark.parametrize("bits", [32, 64, None])
 def test_bench_workload_bitexact(pkg, synth, scan, oracle_volume, gpu, bits):
+    """bits None: the C ABI default (no set_color_precision call) -- colour precision 64, as the facade."""
     L = pkg._lib
     lib = L.load()
     intr_t = synth.REF_INTRINSICS_640
@@ -44,7 +45,12 @@ def test_bench_workload_bitexact(pkg, synth, scan, oracle_volume, gpu, bits):
     vol = C.c_void_p()
     L.call("ot_tsdf_create", 0.005, 0.04, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
     try:
-        L.call("ot_tsdf_set_color_precision", vol, bits)
+        if bits is not None:
+            L.call("ot_tsdf_set_color_precision", vol, bits)
+        got = C.c_int32(0)
+        L.call("ot_tsdf_get_color_precision", vol, C.byref(got))
+        assert got.value == (bits or 64)
+        bits = got.value
         npx = W * H
         for k in range(256):
             st = lib.ot_tsdf_integrate_u16(vol, C.c_void_p(d16.data_ptr() + k * npx * 2),

@@ -181,3 +181,20 @@ def test_batch_errors(pkg, synth, gpu):
         flt.run(d, c, np.stack([np.eye(4)] * 3))           # more frames than max_frames
     with pytest.raises(RuntimeError, match="Unsupported image format"):
         flt.run(d[:1, :100], c[:1, :100], np.eye(4)[None])  # wrong image size
+
+
+def test_batch_tiny_images_many_frames(pkg, O, synth, gpu):
+    """a 32x32 intrinsic (one pixel tile per frame) with 256 frames per run: the per-run tile / frame
+    tables (frame bounds, key widths, point and voxel offsets) grow with the frame count, not with the image, and
+    must fit their allocation.  Every frame vs the oracle chain."""
+    intr_t = (32, 32, 28.3, 28.3, 15.5, 15.5)  # the reference's hfov at 32 px
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=2), n_frames=256, intr=intr_t)
+    flt = _run_batch(pkg, intr_t, depth, color, ext, max_frames=256, trunc=5.0)
+    for f in range(0, 256, 5):
+        P, v, vc, avg, idx = _oracle_chain(O, depth[f], color[f], ext[f], intr_t)
+        assert flt.point_offsets[f + 1] - flt.point_offsets[f] == P
+        down, davg = flt.voxel_cloud(f)
+        assert_bitwise(np.asarray(down.points).reshape(-1, 3), v.reshape(-1, 3), f"tiny-image voxels (frame {f})")
+        assert_bitwise(davg, avg, f"tiny-image mean kNN distances (frame {f})")
+        _, ind = flt.frame(f)
+        assert_bitwise(np.asarray(ind, np.int64), idx, f"tiny-image kept indices (frame {f})")

@@ -149,3 +149,38 @@ def test_border_api_errors(pkg, seq16, gpu):
     before = vol.num_units()
     vol.import_border(keys, tsdf, weight, color)  # every row is owned here (unsharded): nothing is imported
     assert vol.num_units() == before
+
+
+def test_assemble_after_halo_extraction_bitexact(pkg, seq16, gpu):
+    """after a shard imported halo units (import_border) and extracted its mesh, export_units and
+    num_units still cover only its own units, so assembling the shards' exports in one volume (what
+    distributed.assemble_sharded_volume does over ranks) gives the unsharded volume and mesh bit for bit -- no
+    duplicate keys, no zero halo copy overwriting the owner's data."""
+    integ = pkg.pipelines.integration
+    D = importlib.import_module(pkg.__name__ + ".distributed")
+    world = 3
+    full = _integrate_p(pkg, seq16, 0.01, None, 64)
+    fk, ft, fw, fc = (_host(a) for a in full.export_units())
+    m0 = full.extract_triangle_mesh()
+    shards = [_integrate_p(pkg, seq16, 0.01, (r, world), 64) for r in range(world)]
+    own = [v.num_units() for v in shards]
+    import torch
+
+    allrows = torch.cat([D.pack_border(*v.export_border()) for v in shards])
+    for v in shards:
+        v.import_border(*D.unpack_border(allrows))
+        v.extract_triangle_mesh()
+    assert [v.num_units() for v in shards] == own  # halo units are not counted
+    merged = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
+    exports = [v.export_units() for v in shards]
+    assert sum(int(e[0].shape[0]) for e in exports) == fk.shape[0]
+    for e in exports:
+        merged.import_units(*e)
+    mk, mt, mw, mc = (_host(a) for a in merged.export_units())
+    assert_bitwise(mk, fk, "assembled keys")
+    assert_bitwise(mt, ft, "assembled tsdf")
+    assert_bitwise(mw, fw, "assembled weight")
+    assert_bitwise(mc, fc, "assembled colour")
+    m1 = merged.extract_triangle_mesh()
+    assert_bitwise(np.asarray(m1.vertices), np.asarray(m0.vertices), "assembled mesh vertices")
+    assert_bitwise(np.asarray(m1.vertex_colors), np.asarray(m0.vertex_colors), "assembled mesh colours")

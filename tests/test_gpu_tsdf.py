@@ -218,10 +218,74 @@ def test_tsdf_capacity_error(pkg, gpu, synth, seq16):
 
 @pytest.mark.parametrize("batch", [1, 32])
 def test_float32_colour_mode(pkg, O, synth, seq16, gpu, batch):
-    """colour precision 32 (the C ABI default, the headline's setting): tsdf / weight still bit-exact, colour within
+    """colour precision 32 (the labelled secondary bench leg): tsdf / weight still bit-exact, colour within
     1e-4; both the per-frame (batch 1) and the fused kernel."""
     depth, color, ext = seq16
     vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, batch=batch, color_precision=32)
     _compare_volumes(vol, ref)
     with pytest.raises(RuntimeError, match="colour precision"):  # float64 colours into a float32 volume
         pkg._lib.call("ot_tsdf_import_units_color64", vol._h, 0, None, None, None, None, None)
+
+
+def test_nocolor_volume_default_precision(pkg, O, gpu, synth, seq16):
+    """NoColor volumes keep no colour state whatever the requested precision (the facade asks for 64): float32
+    records with zero colour planes, exports / imports at either dtype, tsdf and weight bit-exact vs the oracle."""
+    depth, color, ext = seq16
+    integ = _integration(pkg)
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    vol = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04)
+    assert vol.color_precision == 32
+    ref = O.TSDF(0.01, 0.04, 0, 4)
+    for k in range(depth.shape[0]):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), None, intr_t, ext[k])
+    keys, tsdf, weight, col = (t.cpu().numpy() for t in vol.export_units(color_dtype="float64"))
+    rk, rt, rw, _ = ref.export()
+    assert_bitwise(keys, rk, "NoColor unit keys")
+    assert_bitwise(tsdf, rt, "NoColor tsdf")
+    assert_bitwise(weight, rw, "NoColor weight")
+    assert not col.any()
+    kb, tb, wb, cb = vol.export_border()
+    assert not cb.cpu().numpy().any()
+    twin = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04)
+    twin.import_units(*vol.export_units())
+    assert_bitwise(twin.export_units()[1].cpu().numpy(), rt, "NoColor import / export round trip")
+
+
+def test_frame_lifetime_across_streams(pkg, O, gpu, synth):
+    """frames allocated on one stream and integrated on another, their Python references dropped
+    right after the call.  The facade records the launch stream on every queued tensor and releases a frame only
+    once the C side has consumed it (ot_tsdf_pending_frames), so the caching allocator cannot recycle a frame's
+    memory (here: overwritten by garbage allocated on the producer stream) before its batch runs: bit-exact."""
+    import torch
+
+    depth, color, ext = synth.make_sequence(n_frames=24)
+    integ = _integration(pkg)
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    vol = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                   batch_frames=8)
+    ref = O.TSDF(0.01, 0.04, 1, 4)
+    producer, consumer = torch.cuda.Stream(), torch.cuda.Stream()
+    for k in range(depth.shape[0]):
+        with torch.cuda.stream(producer):
+            d16 = torch.from_numpy(depth[k].view(np.int16)).cuda().view(torch.uint16)
+            col = torch.from_numpy(color[k]).cuda()
+        producer.synchronize()
+        with torch.cuda.stream(consumer):
+            rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+                pkg.geometry.Image(col), pkg.geometry.Image(d16), convert_rgb_to_intensity=False)
+            vol.integrate(rgbd, intr, ext[k])
+        del rgbd, d16, col
+        with torch.cuda.stream(producer):  # garbage into whatever memory the allocator hands out now
+            junk = torch.full((480 * 640 * 3,), 255, dtype=torch.uint8, device="cuda")
+            junk2 = torch.full((480 * 640,), 7, dtype=torch.int16, device="cuda")
+            del junk, junk2
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
+        if k % 8 != 7:
+            assert len(vol._keep) >= 1  # queued frames stay referenced until their batch is enqueued
+    with torch.cuda.stream(consumer):
+        _compare_volumes(vol, ref)

@@ -1,10 +1,17 @@
 """Summarise rocprofv3 --pmc CSVs per kernel (mean per dispatch) and derive HBM bytes per launch of the roofline
-kernels.  FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE
-under-reports wide coalesced reads by 2x; k_batch_integrate's access widths are not the calibrated 16-B streaming
-pattern, so its read side is calibrated on k_export (bench.py --calib), whose reads have the integrate kernel's
-exact 4-B-per-lane row pattern over the voxel pool and a known byte count (80 KiB per unit).  Other kernels use the
-guide's 2x.  The output is tagged with the build's source hash and the workload, and bench.py uses it only when both
-match."""
+kernels.  FETCH_SIZE / WRITE_SIZE are KiB per dispatch.
+
+gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE under-reports wide coalesced streaming reads by 2x, and other
+access widths are uncalibrated.  The correction applied here is MEASURED on the access pattern it is applied to:
+tools/fetch_calib.hip reads / writes a 1-GiB buffer exactly once per pattern (16-B streaming, 8-B and 4-B buffer
+gathers consuming whole lines, an 8-B half-line granularity probe, 8-B buffer stores), so each pattern's factor =
+known bytes / counter bytes.  k_batch_integrate's reads are 8-B buffer gathers (staged depth + multiplier; float64
+colour state) and 4-B gathers (colour, float32 planes): it takes the 8-B gather factor; k_sor_knn (8-B point gathers)
+too; the write side takes the 8-B store factor.  Raw counters and the factor are reported side by side.
+
+Usage: parse_pmc.py --calib <dir>... -- <dir>...   (kernels named k_batch_integrate keep their template argument:
+<true> = float64 colour, <false> = float32 colour).  The output is tagged with the build's source hash and each
+entry with its workload; bench.py uses an entry only when both match."""
 import csv
 import glob
 import importlib
@@ -15,7 +22,15 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-ROOF = ("k_batch_integrate", "k_sor_knn")
+ROOF = ("k_batch_integrate<true>", "k_batch_integrate<false>", "k_sor_knn")
+BASE_CFG = {"voxel": 0.005, "frames": 256, "batch": 0}
+
+
+def short_name(full):
+    base = full.split("(")[0].split("::")[-1]
+    if base.startswith("k_batch_integrate<"):
+        return base
+    return base.split("<")[0]
 
 
 def load(dirs):
@@ -24,36 +39,70 @@ def load(dirs):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    short = row.get("Kernel_Name", "").split("(")[0].split("::")[-1].split("<")[0]
-                    per[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                    per[short_name(row.get("Kernel_Name", ""))][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return per
 
 
-def main():
-    dirs = sys.argv[1:]
+def calibration(dirs):
+    """Factors known bytes / counter bytes per fetch_calib pattern (None when the calibration run is missing)."""
     per = load(dirs)
-    summary = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
-    L = importlib.import_module("object-triggered-3d-slam_amd._lib")
-    units = None
+    summ = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
+    known = None
     for d in dirs:
         for f in glob.glob(os.path.join(d, "*.log")) + [d + ".log"]:
             if os.path.exists(f):
                 for line in open(f):
-                    if line.startswith("{") and '"volume_units"' in line:
-                        units = json.loads(line)["config"]["volume_units"]
-    exp = summary.get("k_export", {})
-    calib = (units * 81920.0) / (exp["FETCH_SIZE"] * 1024.0) if (exp.get("FETCH_SIZE") and units) else None
-    out = {"source_hash": L.source_hash(), "config": {"voxel": 0.005, "frames": 256, "batch": 0},
-           "kernels_traffic": {}, "kernels": summary}
+                    if line.startswith("{") and "known_read_bytes" in line:
+                        known = json.loads(line)
+    if not known:
+        return None
+    out = {"buffer_bytes": known["buffer_bytes"], "patterns": {}}
+    for k, b in known["known_read_bytes"].items():
+        kern = k.replace("_used", "").replace("_lines", "")
+        fs = summ.get(kern, {}).get("FETCH_SIZE")
+        if fs:
+            out["patterns"][k] = {"raw_fetch_kib": fs, "known_bytes": b, "factor": b / (fs * 1024.0)}
+    for k, b in known["known_write_bytes"].items():
+        ws = summ.get(k, {}).get("WRITE_SIZE")
+        if ws:
+            out["patterns"][k] = {"raw_write_kib": ws, "known_bytes": b, "factor": b / (ws * 1024.0)}
+    return out
+
+
+def main():
+    argv = sys.argv[1:]
+    calib_dirs, dirs = [], argv
+    if argv and argv[0] == "--calib":
+        sep = argv.index("--")
+        calib_dirs, dirs = argv[1:sep], argv[sep + 1:]
+    per = load(dirs)
+    summary = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
+    L = importlib.import_module("object-triggered-3d-slam_amd._lib")
+    cal = calibration(calib_dirs) if calib_dirs else None
+    pat = (cal or {}).get("patterns", {})
+    f8 = pat.get("k_cal_gather8", {}).get("factor")
+    w8 = pat.get("k_cal_store8", {}).get("factor")
+    out = {"source_hash": L.source_hash(), "config": BASE_CFG, "calibration": cal, "kernels_traffic": {},
+           "kernels": summary}
     for kern in ROOF:
         k = summary.get(kern, {})
         if k.get("FETCH_SIZE") is None or k.get("WRITE_SIZE") is None:
             continue
-        corr = calib if (kern == "k_batch_integrate" and calib) else 2.0
-        fetch = k["FETCH_SIZE"] * 1024.0 * corr
-        write = k["WRITE_SIZE"] * 1024.0
-        ent = {"bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch), "write_bytes": round(write),
-               "fetch_correction": corr, "raw_fetch_kib": k["FETCH_SIZE"], "raw_write_kib": k["WRITE_SIZE"]}
+        fcorr = f8 if f8 else 2.0
+        wcorr = w8 if w8 else 1.0
+        fetch = k["FETCH_SIZE"] * 1024.0 * fcorr
+        write = k["WRITE_SIZE"] * 1024.0 * wcorr
+        cfg = dict(BASE_CFG)
+        if kern.startswith("k_batch_integrate"):
+            cfg["color_bits"] = 64 if kern.endswith("<true>") else 32
+        else:
+            cfg = {}
+        ent = {"config": cfg, "bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch),
+               "write_bytes": round(write), "fetch_correction": fcorr, "write_correction": wcorr,
+               "fetch_correction_source": "tools/fetch_calib.hip k_cal_gather8 (8-B buffer gathers, measured)" if f8
+               else "MI355X_MICROARCH.md 2x (16-B streaming reads; no calibration run)",
+               "raw_fetch_kib": k["FETCH_SIZE"], "raw_write_kib": k["WRITE_SIZE"],
+               "raw_bytes_per_launch": round((k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0)}
         if k.get("SQ_WAVE_CYCLES"):
             wc = k["SQ_WAVE_CYCLES"]
             ent["stall_shares"] = {"wait_any": k.get("SQ_WAIT_ANY", 0) / wc, "wait_inst_any": k.get("SQ_WAIT_INST_ANY", 0) / wc,
@@ -67,6 +116,9 @@ def main():
             ent["valu_busy_frac"] = k["SQ_ACTIVE_INST_VALU"] * 4.0 / 1024.0 / cyc
             ent["valu_insts_per_launch"] = k.get("SQ_INSTS_VALU")
             ent["dispatch_cycles"] = cyc
+        if k.get("TA_TA_BUSY_sum") and k.get("GRBM_GUI_ACTIVE"):
+            ent["ta_busy_frac"] = k["TA_TA_BUSY_sum"] / 256.0 / (k["GRBM_GUI_ACTIVE"] / 8.0)
+            ent["td_busy_frac"] = k.get("TD_TD_BUSY_sum", 0) / 256.0 / (k["GRBM_GUI_ACTIVE"] / 8.0)
         out["kernels_traffic"][kern] = ent
     print(json.dumps(out, indent=1))
 
