@@ -249,6 +249,17 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices_host, 
  * triangles int32 [T][3].  Device pointers. */
 ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors,
                                       int32_t* triangles, void* stream);
+/* Serial of the last extraction (ot_tsdf_extract_triangle_mesh), or -1 once the volume has changed since (frames
+ * integrated, reset, units imported). */
+ot_status ot_tsdf_mesh_serial(const ot_tsdf* vol, int64_t* serial_host);
+/* mesh.compute_vertex_normals() (reconstruct_rgbd_filter.py:113) of the mesh of extraction `serial`, whose
+ * arrays (device pointers, unmodified) are passed: the same bits as ot_mesh_compute_vertex_normals, from the
+ * marching-cubes structure kept with the volume (each vertex is a cut edge; its triangles are those of the <= 4 cubes
+ * sharing it, walked in triangle order) instead of a sort of the 3T corners.  OT_ERR_INVALID_ARGUMENT when the volume
+ * changed since that extraction or the sizes differ (take ot_mesh_compute_vertex_normals then).  Ordered on `stream`,
+ * no synchronisation. */
+ot_status ot_tsdf_mesh_vertex_normals(ot_tsdf* vol, int64_t serial, const double* vertices, int64_t n_vertices,
+                                      const int32_t* triangles, int64_t n_triangles, double* out, void* stream);
 /* Merge keys of the extracted mesh (device pointers, NULL to skip): per vertex int32 [V][4] = owner unit key
  * (x, y, z) and edge bit (local voxel x*256+y*16+z times 3 plus axis) -- the canonical vertex order; per triangle
  * int32 [T][3] = the unit key of its cube. */

@@ -106,6 +106,35 @@ __device__ inline int wave_excl_count(bool pred, int& total) {
     return __popcll(m & lt);
 }
 
+// TriangleMesh::ComputeVertexNormals' last step on the accumulated (unnormalised) sum: normalise, NaN -> (0, 0, 1)
+__device__ inline void finish_vertex_normal(double n[3]) {
+    const double sq = (n[0] * n[0] + n[1] * n[1]) + n[2] * n[2];
+    if (sq > 0.0) {
+        const double s = sqrt(sq);
+        n[0] /= s;
+        n[1] /= s;
+        n[2] /= s;
+    }
+    if (isnan(n[0])) {
+        n[0] = 0.0;
+        n[1] = 0.0;
+        n[2] = 1.0;
+    }
+}
+
+// triangle normal (v1 - v0) x (v2 - v0), unnormalised (Open3D ComputeTriangleNormals(false))
+__device__ inline void triangle_normal(const double* __restrict__ V, int32_t a, int32_t b, int32_t c, double out[3]) {
+    double e1[3], e2[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        e1[d] = V[(int64_t)b * 3 + d] - V[(int64_t)a * 3 + d];
+        e2[d] = V[(int64_t)c * 3 + d] - V[(int64_t)a * 3 + d];
+    }
+    out[0] = e1[1] * e2[2] - e1[2] * e2[1];
+    out[1] = e1[2] * e2[0] - e1[0] * e2[2];
+    out[2] = e1[0] * e2[1] - e1[1] * e2[0];
+}
+
 template <typename T>
 __device__ inline T wave_sum(T v) {
 #pragma unroll

@@ -42,9 +42,33 @@ struct McDev {
     long long* vert_cnt;         // [rank]
     long long* tri_base;         // [rank]
     long long* vert_base;        // [rank]
+    unsigned short* ctri;        // [id][4096] (cube byte order): first triangle of the cube inside its unit
     int4* vk;                    // per vertex: owner unit key + edge bit (the merge key of a sharded extraction)
     int32_t* tk;                 // per triangle: its cube's unit key
 };
+
+// the marching-cubes workspace of U units, carved from one allocation (kept with the volume: MeshBuffers::ws)
+static size_t mc_ws_bytes(int64_t U) {
+    return (size_t)U * (4 * 8 + 4 + 8 * 4 + EWORDS * 4 * 2 + UNIT_VOX + UNIT_VOX * 2) + 16 * 256;
+}
+static void mc_layout(char* ws, int64_t U, McDev& m) {
+    char* p = ws;
+    auto take = [&](size_t n) {
+        char* q = p;
+        p += (n + 255) & ~(size_t)255;
+        return q;
+    };
+    m.tri_cnt = (long long*)take(sizeof(long long) * U);
+    m.vert_cnt = (long long*)take(sizeof(long long) * U);
+    m.tri_base = (long long*)take(sizeof(long long) * U);
+    m.vert_base = (long long*)take(sizeof(long long) * U);
+    m.rank_of = (int*)take(sizeof(int) * U);
+    m.nbr = (int*)take(sizeof(int) * 8 * U);
+    m.eflags = (unsigned*)take(sizeof(unsigned) * EWORDS * U);
+    m.wprefix = (int*)take(sizeof(int) * EWORDS * U);
+    m.cubes = (unsigned char*)take((size_t)UNIT_VOX * U);
+    m.ctri = (unsigned short*)take(sizeof(unsigned short) * UNIT_VOX * U);
+}
 
 __device__ inline int find_unit(const TsdfDev& d, int x, int y, int z) {
     if (!key_in_range(x, y, z)) return -1;
@@ -285,6 +309,20 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
     int total;
     const int pre = block_excl_scan_256(cnt, total);  // contains __syncthreads (snbr visible after)
     long long out = m.tri_base[r] + pre;
+    {  // per cube its first triangle inside the unit (<= 5 * 4096 < 2^16): the vertex-normal walk's index
+        unsigned off[8];
+        int o = pre;
+#pragma unroll
+        for (int z = 0; z < UNIT_RES; z += 2) {
+            const int n0 = c_ntri[(cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu];
+            const int n1 = c_ntri[(cw[(z + 1) >> 2] >> (((z + 1) & 3) * 8)) & 0xFFu];
+            off[z >> 1] = (unsigned)o | ((unsigned)(o + n0) << 16);
+            o += n0 + n1;
+        }
+        uint4* dst = reinterpret_cast<uint4*>(m.ctri + (size_t)id * UNIT_VOX + t * 16);
+        dst[0] = make_uint4(off[0], off[1], off[2], off[3]);
+        dst[1] = make_uint4(off[4], off[5], off[6], off[7]);
+    }
     const int x = t >> 4, y = t & 15;
     for (int z = 0; z < UNIT_RES; ++z) {
         const int cube = (int)((cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu);
@@ -304,6 +342,65 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
             ++out;
         }
     }
+}
+
+// TriangleMesh::ComputeVertexNormals of an extracted mesh from its marching-cubes structure: a vertex is
+// a cut edge (global voxel g, axis a), and exactly the 4 cubes g - eshift(e) over the 4 edges e along a contain it.
+// Their triangles are the vertex's triangles; walking the cubes in ascending triangle index (unit rank, then the cube's
+// offset inside the unit) and each cube's triangles in table order adds the triangle normals in triangle order --
+// Open3D's loop over the triangles -- with no sort of the 3T corners.  One lane per vertex.
+__global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t units, const double* __restrict__ V,
+                                                     const int32_t* __restrict__ T, int64_t nv, double* __restrict__ N) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v >= nv) return;
+    const int4 key = m.vk[v];
+    const int local = key.w / 3, axis = key.w % 3;
+    const int g[3] = {key.x * UNIT_RES + (local >> 8), key.y * UNIT_RES + ((local >> 4) & 15),
+                      key.z * UNIT_RES + (local & 15)};
+    long long start[4];
+    int cubev[4], edge[4];
+    int nc = 0;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+        if (c_eshift[e][3] != axis) continue;
+        const int c[3] = {g[0] - c_eshift[e][0], g[1] - c_eshift[e][1], g[2] - c_eshift[e][2]};
+        const int id = find_unit(d, c[0] >> 4, c[1] >> 4, c[2] >> 4);  // arithmetic shift: floor for negatives
+        if (id < 0 || id >= units) continue;
+        const int ci = ((c[0] & 15) * 16 + (c[1] & 15)) * 16 + (c[2] & 15);
+        const int cube = m.cubes[(size_t)id * UNIT_VOX + ci];
+        if (cube == 0) continue;
+        start[nc] = m.tri_base[m.rank_of[id]] + m.ctri[(size_t)id * UNIT_VOX + ci];
+        cubev[nc] = cube;
+        edge[nc] = e;
+        ++nc;
+    }
+    // ascending triangle index (<= 4 cubes: insertion sort)
+    for (int i = 1; i < nc; ++i)
+        for (int j = i; j > 0 && start[j] < start[j - 1]; --j) {
+            const long long ts = start[j];
+            start[j] = start[j - 1], start[j - 1] = ts;
+            const int tc = cubev[j];
+            cubev[j] = cubev[j - 1], cubev[j - 1] = tc;
+            const int te = edge[j];
+            edge[j] = edge[j - 1], edge[j - 1] = te;
+        }
+    double n[3] = {0.0, 0.0, 0.0};
+    for (int i = 0; i < nc; ++i) {
+        long long tri = start[i];
+        for (int k = 0; k < 15 && c_tri[cubev[i]][k] != -1; k += 3, ++tri) {
+            const int e = edge[i];
+            if (c_tri[cubev[i]][k] != e && c_tri[cubev[i]][k + 1] != e && c_tri[cubev[i]][k + 2] != e) continue;
+            double tn[3];
+            triangle_normal(V, T[tri * 3], T[tri * 3 + 1], T[tri * 3 + 2], tn);
+            n[0] += tn[0];
+            n[1] += tn[1];
+            n[2] += tn[2];
+        }
+    }
+    finish_vertex_normal(n);
+    N[v * 3 + 0] = n[0];
+    N[v * 3 + 1] = n[1];
+    N[v * 3 + 2] = n[2];
 }
 
 static std::atomic<bool> g_tables_uploaded{false};
@@ -356,30 +453,27 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     vol->mesh.nv = vol->mesh.nt = 0;
     *n_vertices = *n_triangles = 0;
     if (U == 0) return OT_OK;
-    // workspace: ids are dense in [0, U)
-    const size_t bytes = (size_t)U * (4 * 8 + 4 + 8 * 4 + EWORDS * 4 * 2 + UNIT_VOX) + 16 * 256;
-    char* ws = (char*)scratch(bytes, 14);
-    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    // workspace (ids are dense in [0, U)), kept with the volume after the extraction (MeshBuffers::ws)
+    MeshBuffers& mb = vol->mesh;
+    mb.valid = false;
+    const size_t bytes = mc_ws_bytes(U);
+    if (mb.ws_bytes < bytes) {
+        if (mb.ws) {
+            OT_HIP_TRY(hipStreamSynchronize(stream));
+            OT_HIP_TRY(hipFree(mb.ws));
+            mb.ws = nullptr;
+            mb.ws_bytes = 0;
+        }
+        const size_t nb = bytes + bytes / 4;
+        OT_HIP_TRY(hipMalloc(&mb.ws, nb));
+        mb.ws_bytes = nb;
+        note_alloc();
+    }
     McDev m;
     m.sorted_ids = vol->sorted_ids;
     m.vk = nullptr;
     m.tk = nullptr;
-    char* p = ws;
-    auto take = [&](size_t n) {
-        char* q = p;
-        p += (n + 255) & ~(size_t)255;
-        return q;
-    };
-    m.tri_cnt = (long long*)take(sizeof(long long) * U);
-    m.vert_cnt = (long long*)take(sizeof(long long) * U);
-    m.tri_base = (long long*)take(sizeof(long long) * U);
-    m.vert_base = (long long*)take(sizeof(long long) * U);
-    m.rank_of = (int*)take(sizeof(int) * U);
-    m.nbr = (int*)take(sizeof(int) * 8 * U);
-    m.eflags = (unsigned*)take(sizeof(unsigned) * EWORDS * U);
-    m.wprefix = (int*)take(sizeof(int) * EWORDS * U);
-    m.cubes = (unsigned char*)take((size_t)UNIT_VOX * U);
-    if ((size_t)(p - ws) > bytes) return fail(OT_ERR_HIP, "mc workspace overflow");
+    mc_layout((char*)mb.ws, U, m);
     const unsigned g = (unsigned)U;
     hipLaunchKernelGGL(k_mc_prepare, dim3(g), dim3(256), 0, stream, vol->dev, m);
     hipLaunchKernelGGL(k_mc_classify, dim3(g), dim3(256), 0, stream, vol->dev, m);
@@ -397,7 +491,6 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     OT_HIP_TRY(hipStreamSynchronize(stream));
     const int64_t nt = tails[0] + tails[1], nv = tails[2] + tails[3];
     if (nv > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] more than 2^31 vertices");
-    MeshBuffers& mb = vol->mesh;
     int64_t capc = mb.cap_v;
     st = grow(mb.v, mb.cap_v, nv * 3);
     if (st != OT_OK) return st;
@@ -418,8 +511,37 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     OT_HIP_TRY(hipStreamSynchronize(stream));
     mb.nv = nv;
     mb.nt = nt;
+    mb.ws_units = U;
+    mb.serial += 1;
+    mb.valid = true;
     *n_vertices = nv;
     *n_triangles = nt;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_mesh_serial(const ot_tsdf* vol, int64_t* serial_host) {
+    if (!vol || !serial_host) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    *serial_host = vol->mesh.valid ? vol->mesh.serial : -1;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_mesh_vertex_normals(ot_tsdf* vol, int64_t serial, const double* vertices, int64_t n_vertices,
+                                      const int32_t* triangles, int64_t n_triangles, double* out, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!vol || (n_vertices > 0 && (!vertices || !out)) || (n_triangles > 0 && !triangles))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ComputeVertexNormals] invalid arguments");
+    const MeshBuffers& mb = vol->mesh;
+    if (!mb.valid || serial != mb.serial || n_vertices != mb.nv || n_triangles != mb.nt)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ComputeVertexNormals] the volume changed since this mesh was extracted");
+    if (n_vertices == 0) return OT_OK;
+    McDev m;
+    m.sorted_ids = vol->sorted_ids;
+    mc_layout((char*)mb.ws, mb.ws_units, m);
+    m.vk = mb.vk;
+    m.tk = mb.tk;
+    hipLaunchKernelGGL(k_mc_vnormals, dim3((unsigned)((n_vertices + 255) / 256)), dim3(256), 0, stream, vol->dev, m,
+                       mb.ws_units, vertices, triangles, n_vertices, out);
+    OT_LAUNCH_CHECK();
     return OT_OK;
 }
 

@@ -24,15 +24,11 @@ __global__ __launch_bounds__(256) void k_tri_normals(const double* __restrict__ 
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= nt) return;
     const int32_t a = T[t * 3], b = T[t * 3 + 1], c = T[t * 3 + 2];
-    double e1[3], e2[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        e1[d] = V[(int64_t)b * 3 + d] - V[(int64_t)a * 3 + d];
-        e2[d] = V[(int64_t)c * 3 + d] - V[(int64_t)a * 3 + d];
-    }
-    TN[t * 3 + 0] = e1[1] * e2[2] - e1[2] * e2[1];
-    TN[t * 3 + 1] = e1[2] * e2[0] - e1[0] * e2[2];
-    TN[t * 3 + 2] = e1[0] * e2[1] - e1[1] * e2[0];
+    double tn[3];
+    triangle_normal(V, a, b, c, tn);
+    TN[t * 3 + 0] = tn[0];
+    TN[t * 3 + 1] = tn[1];
+    TN[t * 3 + 2] = tn[2];
     keys[t * 3 + 0] = (unsigned long long)(unsigned)a;
     keys[t * 3 + 1] = (unsigned long long)(unsigned)b;
     keys[t * 3 + 2] = (unsigned long long)(unsigned)c;
@@ -65,18 +61,7 @@ __global__ __launch_bounds__(256) void k_vertex_normals(const unsigned long long
             n[2] += TN[t * 3 + 2];
         }
     }
-    const double sq = (n[0] * n[0] + n[1] * n[1]) + n[2] * n[2];
-    if (sq > 0.0) {
-        const double s = sqrt(sq);
-        n[0] /= s;
-        n[1] /= s;
-        n[2] /= s;
-    }
-    if (isnan(n[0])) {
-        n[0] = 0.0;
-        n[1] = 0.0;
-        n[2] = 1.0;
-    }
+    finish_vertex_normal(n);
     N[v * 3 + 0] = n[0];
     N[v * 3 + 1] = n[1];
     N[v * 3 + 2] = n[2];

@@ -112,6 +112,13 @@ struct PendingFrame {
 };
 
 struct MeshBuffers {
+    // the marching-cubes structure of the last extraction (per-unit cube bytes, triangle offsets, ...; mc.hip
+    // mc_layout), kept with the volume so ComputeVertexNormals can walk each vertex's cubes instead of sorting corners
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    int64_t ws_units = 0;
+    int64_t serial = 0;   // extraction count; the structure is valid for `serial` while `valid`
+    bool valid = false;   // cleared by anything that changes the volume (integrate, reset, import)
     double* v = nullptr;
     double* c = nullptr;
     int32_t* t = nullptr;
@@ -132,6 +139,7 @@ struct ot_tsdf {
     int64_t hash_cap = 0;
     ot::TsdfDev dev{};
     int frame_id = 0;
+    bool imported = false;  // units imported since reset (arbitrary state: no reciprocal-table integrate)
     // multiplier image cache
     float* mult = nullptr;
     ot_intrinsics mult_intr{};

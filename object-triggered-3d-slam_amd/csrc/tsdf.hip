@@ -605,9 +605,7 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 }
 
 // occupancy floor the integrate is compiled for: the float32-colour kernel allocates 64 VGPRs (8 waves
-// per SIMD) on its own; the float64-colour state and its IEEE f64 divides want ~106, and capping them at 96 (5 waves
-// per SIMD, a few bytes of scratch) is 12-14 % faster than the spill-free 4 waves (measured: 4 / 5 / 6 / 7 / 8 waves
-// = 0.78-0.81 / 0.70 / 0.73 / 0.74 / 0.76 ms per 32-frame launch)
+// per SIMD) on its own; the float64-colour state wants more (C64 cap below)
 #ifndef OT_MASK_INVALID_LOADS
 #define OT_MASK_INVALID_LOADS 1  // lanes whose voxel projects outside the image issue no depth gather (with the
 #endif                           // 64-VGPR cap below: integrate 0.415-0.421 -> 0.409-0.412 ms; at 66 VGPRs 0.59)
@@ -620,13 +618,38 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 #ifndef OT_WAVES_PER_EU_C64
 #define OT_WAVES_PER_EU_C64 5
 #endif
+#ifndef OT_RCP_TABLE
+#define OT_RCP_TABLE 1  // 0: never take the FAST (reciprocal table) kernel
+#endif
+#ifndef OT_C64_SKIP
+#define OT_C64_SKIP 1  // float64 colour update only for the voxels k with an updating lane in the wave
+#endif
+// Reciprocal table: y[n] = RN(1/n) for n in [1, RCP_N].  For b = w + 1 an integer in that range, q0 = RN(a*y),
+// r = fma(-b, q0, a) (exact), q = RN(q0 + r*y) is RN(a/b) -- Markstein's theorem (y correctly rounded, q0 within one
+// ulp, no underflow in r; binary32 and binary64 alike): the IEEE quotient bit for bit with 3 operations and an LDS
+// load instead of the ~10-instruction division sequence.  The host takes this kernel (FAST) only while every weight
+// is an integer count of updates below RCP_N (frames since reset + the batch < RCP_N) and the state comes from
+// integration alone (no imported units): then |a| is 0 or far above the underflow range (tsdf: a sum of a running
+// mean and a term quantised by the depth / camera-distance floats; colour: c*w + rgb >= 0 with c a mean of bytes).
+// Otherwise the IEEE divisions (FAST = false).
+constexpr int RCP_N = 4096;
+
 // One workgroup of SLICES waves per unit, so a unit's frame footprint is gathered through one CU's L1; units are
-// assigned by a static grid stride that every wave derives on its own: no barriers, no LDS, no atomics.
+// assigned by a static grid stride that every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes
-template <bool C64>
+template <bool C64, bool FAST>
 __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
     using CT = typename std::conditional<C64, double, float>::type;
+    __shared__ float s_r32[FAST ? RCP_N + 1 : 1];
+    __shared__ double s_r64[(FAST && C64) ? RCP_N + 1 : 1];
+    if constexpr (FAST) {
+        for (int n = threadIdx.x; n <= RCP_N; n += 64 * SLICES) {
+            s_r32[n] = 1.0f / (float)n;  // IEEE (correctly rounded) quotients
+            if constexpr (C64) s_r64[n] = 1.0 / (double)n;
+        }
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63;
     const int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // slice of this wave
     const int n = d.counters[pc];
@@ -766,24 +789,52 @@ __global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_P
                         const float tn = (sv < 1.0f) ? sv : 1.0f;
                         const float wv = wt[k];
                         const float w1 = wv + 1.0f;
-                        const float tsn = (ts[k] * wv + tn) / w1;  // exact IEEE quotient: tsdf bit-exact
+                        const float ta = ts[k] * wv + tn;
+                        float tsn;  // (tsdf * w + t) / (w + 1): the IEEE quotient, tsdf bit-exact
+                        if constexpr (FAST) {
+                            const float y = s_r32[(int)w1];
+                            const float q0 = ta * y;
+                            tsn = __builtin_fmaf(__builtin_fmaf(-w1, q0, ta), y, q0);
+                        } else {
+                            tsn = ta / w1;
+                        }
                         ts[k] = doit ? tsn : ts[k];
                         if (use_color) {
-                            CT nr, ng, nb;
-                            if (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
-                                const double wd = (double)wv, w1d = (double)w1;
-                                nr = (CT)(((double)cr[k] * wd + (double)(cv[k] & 0xFFu)) / w1d);
-                                ng = (CT)(((double)cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu)) / w1d);
-                                nb = (CT)(((double)cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu)) / w1d);
+                            if constexpr (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
+#if OT_C64_SKIP
+                                if (__any(doit)) {
+#else
+                                {
+#endif
+                                    const double wd = (double)wv, w1d = (double)w1;
+                                    const double ar = cr[k] * wd + (double)(cv[k] & 0xFFu);
+                                    const double ag = cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu);
+                                    const double ab = cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu);
+                                    double nr, ng, nb;
+                                    if constexpr (FAST) {
+                                        const double y = s_r64[(int)w1];
+                                        const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
+                                        nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
+                                        ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
+                                        nb = __builtin_fma(__builtin_fma(-w1d, q0b, ab), y, q0b);
+                                    } else {
+                                        nr = ar / w1d;
+                                        ng = ag / w1d;
+                                        nb = ab / w1d;
+                                    }
+                                    cr[k] = doit ? nr : cr[k];
+                                    cg[k] = doit ? ng : cg[k];
+                                    cb[k] = doit ? nb : cb[k];
+                                }
                             } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
                                 const float rw = __builtin_amdgcn_rcpf(w1);
-                                nr = (CT)(((float)cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw);
-                                ng = (CT)(((float)cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw);
-                                nb = (CT)(((float)cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw);
+                                const float nr = ((float)cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
+                                const float ng = ((float)cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
+                                const float nb = ((float)cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                                cr[k] = doit ? nr : cr[k];
+                                cg[k] = doit ? ng : cg[k];
+                                cb[k] = doit ? nb : cb[k];
                             }
-                            cr[k] = doit ? nr : cr[k];
-                            cg[k] = doit ? ng : cg[k];
-                            cb[k] = doit ? nb : cb[k];
                         }
                         wt[k] = doit ? w1 : wv;
                         upd += doit ? 1u : 0u;
@@ -1184,14 +1235,20 @@ static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t
 #endif
 // Grid of k_batch_integrate: OT_GRID_MULT x the co-resident workgroups (cached per device; a benign race at worst
 // computes the same value twice).
-static int integrate_grid(bool c64) {
-    static int cache[2][64] = {{0}};
+template <bool C64, bool FAST>
+static const void* integrate_kernel() {
+    return (const void*)k_batch_integrate<C64, FAST>;
+}
+
+static int integrate_grid(bool c64, bool fast) {
+    static int cache[4][64] = {{0}};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 4096;
-    int* cache_c = cache[c64 ? 1 : 0];
+    int* cache_c = cache[(c64 ? 2 : 0) + (fast ? 1 : 0)];
     if (!cache_c[dev]) {
         int per_cu = 0, cus = 0;
-        const void* kern = c64 ? (const void*)k_batch_integrate<true> : (const void*)k_batch_integrate<false>;
+        const void* kern = c64 ? (fast ? integrate_kernel<true, true>() : integrate_kernel<true, false>())
+                               : (fast ? integrate_kernel<false, true>() : integrate_kernel<false, false>());
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * SLICES, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 ||
             cus <= 0)
@@ -1274,19 +1331,26 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, tp, vol->dev, n);
     hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc);
-    const int grid = integrate_grid(vol->color64);
+    // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
+    // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
+    const bool fast = OT_RCP_TABLE && !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
+    const int grid = integrate_grid(vol->color64, fast);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
         OT_HIP_TRY(hipEventCreate(&e0));
         OT_HIP_TRY(hipEventCreate(&e1));
         OT_HIP_TRY(hipEventRecord(e0, stream));
     }
-    if (vol->color64)
-        hipLaunchKernelGGL(k_batch_integrate<true>, dim3(grid), dim3(64 * SLICES), 0, stream,
-                           (const BatchFrame*)vol->bframes, ip0, vol->dev, (const UnitWork*)vol->dev.work, pc);
+    const BatchFrame* bf = vol->bframes;
+    const UnitWork* uw = (const UnitWork*)vol->dev.work;
+    if (vol->color64 && fast)
+        hipLaunchKernelGGL((k_batch_integrate<true, true>), dim3(grid), dim3(64 * SLICES), 0, stream, bf, ip0, vol->dev, uw, pc);
+    else if (vol->color64)
+        hipLaunchKernelGGL((k_batch_integrate<true, false>), dim3(grid), dim3(64 * SLICES), 0, stream, bf, ip0, vol->dev, uw, pc);
+    else if (fast)
+        hipLaunchKernelGGL((k_batch_integrate<false, true>), dim3(grid), dim3(64 * SLICES), 0, stream, bf, ip0, vol->dev, uw, pc);
     else
-        hipLaunchKernelGGL(k_batch_integrate<false>, dim3(grid), dim3(64 * SLICES), 0, stream,
-                           (const BatchFrame*)vol->bframes, ip0, vol->dev, (const UnitWork*)vol->dev.work, pc);
+        hipLaunchKernelGGL((k_batch_integrate<false, false>), dim3(grid), dim3(64 * SLICES), 0, stream, bf, ip0, vol->dev, uw, pc);
     vol->batch_pc ^= 1;  // only once this batch's kernels are queued (its units kernel zeroes the other counter)
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
@@ -1318,6 +1382,7 @@ ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream) {
     size_t i = 0;
     std::vector<PendingFrame> frames;
     frames.swap(vol->pending);
+    if (!frames.empty()) vol->mesh.valid = false;  // the volume changes: the last extraction's structure is stale
     while (i < frames.size()) {
         // a batch: consecutive frames with identical intrinsics, at most batch_max (<= 64)
         size_t n = 1;
@@ -1456,7 +1521,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
     void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, v->mult,
-                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, d.fmask, d.bslots, d.work,
+                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, d.fmask, d.bslots, d.work,
                     v->bframes, v->bdm, v->brgba};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1479,10 +1544,12 @@ ot_status ot_tsdf_reset(ot_tsdf* v) {
     OT_HIP_TRY(hipDeviceSynchronize());
     v->batch_pc = C_BATCH_PAIRS;
     v->frame_id = 0;
+    v->imported = false;
     v->pending.clear();
     v->sorted_frame = -1;
     v->sorted_units = -1;
     v->mesh.nv = v->mesh.nt = 0;
+    v->mesh.valid = false;
     return OT_OK;
 }
 
@@ -1500,9 +1567,11 @@ ot_status ot_tsdf_reset_async(ot_tsdf* v, void* stream_) {
     OT_HIP_TRY(hipMemsetAsync(d.stats, 0, sizeof(unsigned long long) * 4, stream));
     v->batch_pc = C_BATCH_PAIRS;
     v->frame_id = 0;
+    v->imported = false;
     v->sorted_frame = -1;
     v->sorted_units = -1;
     v->mesh.nv = v->mesh.nt = 0;
+    v->mesh.valid = false;
     return OT_OK;
 }
 
@@ -1729,6 +1798,8 @@ static ot_status import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, cons
                            (const float*)nullptr);
     OT_LAUNCH_CHECK();
     vol->sorted_units = -1;  // the sorted-unit cache no longer matches
+    vol->imported = true;    // arbitrary state: the IEEE-division integrate from now on
+    vol->mesh.valid = false;
     st = check_errors(vol, stream);
     if (st != OT_OK) return st;
     OT_HIP_TRY(hipStreamSynchronize(stream));
@@ -1791,6 +1862,8 @@ ot_status ot_tsdf_import_border(ot_tsdf* vol, int64_t n, const int32_t* keys, co
                            weight, (const float*)c);
     OT_LAUNCH_CHECK();
     vol->sorted_units = -1;
+    vol->imported = true;  // halo units hold other shards' state (read by marching cubes; kept exact anyway)
+    vol->mesh.valid = false;
     st = check_errors(vol, stream);
     if (st != OT_OK) return st;
     OT_HIP_TRY(hipStreamSynchronize(stream));

@@ -451,6 +451,7 @@ class TriangleMesh:
         self._vc = None
         self._vn = None
 
+        self._mc = None  # (volume handle, extraction serial) of a mesh fresh out of extract_triangle_mesh
     @property
     def vertices(self):
         return Vector3dVector._view(self._v.host_view())
@@ -458,6 +459,7 @@ class TriangleMesh:
     @vertices.setter
     def vertices(self, v):
         self._v = _Arr.wrap(v, np.float64, 3)
+        self._mc = None
 
     @property
     def triangles(self):
@@ -466,6 +468,7 @@ class TriangleMesh:
     @triangles.setter
     def triangles(self, t):
         self._t = _Arr.wrap(t, np.int32, 3)
+        self._mc = None
 
     @property
     def vertex_colors(self):
@@ -504,11 +507,22 @@ class TriangleMesh:
         return f"TriangleMesh with {len(self._v)} points and {len(self._t)} triangles."
 
     def compute_vertex_normals(self, normalized=True):
-        """TriangleMesh::ComputeVertexNormals (reconstruct_rgbd_filter.py:113) — ot_mesh_compute_vertex_normals."""
+        """TriangleMesh::ComputeVertexNormals (reconstruct_rgbd_filter.py:113).  A mesh fresh out of
+        extract_triangle_mesh (arrays not reassigned or viewed for writing since) takes the marching-cubes walk of its
+        volume (ot_tsdf_mesh_vertex_normals: each vertex's <= 4 cubes in triangle order); any other mesh, or a volume
+        changed since, the generic corner sort (ot_mesh_compute_vertex_normals).  Both give the same bits."""
         nv, nt = len(self._v), len(self._t)
         if nv == 0:
             return self
         out = D.empty((nv, 3), "float64")
+        mc = getattr(self, "_mc", None)
+        vol = mc[0]() if mc is not None else None
+        if vol is not None and getattr(vol, "_h", None) is not None and not self._v._viewed and not self._t._viewed:
+            st = L.load().ot_tsdf_mesh_vertex_normals(vol._h, mc[1], D.ptr(self._v.dev()), nv, D.ptr(self._t.dev()),
+                                                       nt, D.ptr(out), D.stream_ptr())
+            if st == L.OT_OK:
+                self._vn = _Arr(dev=out)
+                return self
         L.call("ot_mesh_compute_vertex_normals", D.ptr(self._v.dev()), nv, D.ptr(self._t.dev()), nt, D.ptr(out),
                D.stream_ptr())
         self._vn = _Arr(dev=out)

@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import ctypes as C
 import enum
+import weakref
 
 import numpy as np
 
@@ -223,6 +224,10 @@ class ScalableTSDFVolume:
         mesh = TriangleMesh()
         mesh._v = _Arr(dev=V)
         mesh._t = _Arr(dev=T)
+        serial = C.c_int64(-1)
+        L.call("ot_tsdf_mesh_serial", self._h, C.byref(serial))
+        # normals via the marching-cubes structure kept with this volume (weakly referenced: the mesh outlives it)
+        mesh._mc = (weakref.ref(self), serial.value) if serial.value >= 0 else None
         if self.color_type == TSDFVolumeColorType.RGB8:
             mesh._vc = _Arr(dev=VC)
         if not with_keys:

@@ -136,7 +136,7 @@ def test_configs4_hybrid_full_size_bitexact(pkg, O, synth, gpu):
     assert_bitwise(d_base.cpu().numpy(), ref_grid, "smart_paste 1024x1024 grid")
     assert ch.value == int((ref_grid != old_map).sum()) > 10000
     ref_occ = O.occupancy_to_points(ref_grid, 100, 0.05, -25.6, -25.6)
-    assert nq.value == len(ref_occ) > 10000
+    assert nq.value == len(ref_occ) > 1000
     assert_bitwise(occ[:nq.value].cpu().numpy(), ref_occ, "occupied-cell cloud")
     ra, rr = [], []
     for j in range(n_obj):

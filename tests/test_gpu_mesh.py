@@ -107,3 +107,82 @@ def test_sampling_batch_matches_single(pkg, O, synth, seq16, meshes):
             assert_bitwise(np.asarray(c.normals), np.asarray(one.normals), "batched normals")
     P, _, _ = O.sample_points_uniformly(V, T, 20000, 5, VN=O.vertex_normals(V, T), VC=VC)
     assert_bitwise(np.asarray(clouds[0].points), P, "batched vs oracle")
+
+
+@pytest.mark.parametrize("voxel", [0.01, 0.005])
+def test_vertex_normals_mc_walk_bitexact(pkg, O, synth, seq16, gpu, voxel):
+    """compute_vertex_normals on a mesh fresh out of extract_triangle_mesh takes the marching-cubes walk
+    (ot_tsdf_mesh_vertex_normals: each vertex's <= 4 cubes in triangle order, no corner sort); bit-exact vs the oracle
+    and vs the generic corner-sort kernel on the same arrays.  Once the volume changes, the walk refuses and the
+    facade falls back to the generic kernel (same bits)."""
+    import ctypes as C
+
+    import torch
+
+    L = pkg._lib
+    depth, color, ext = seq16
+    vol, ref = _volumes(pkg, O, synth, depth, color, ext, voxel)
+    mesh = vol.extract_triangle_mesh()
+    assert mesh._mc is not None
+    nv, nt = len(mesh._v), len(mesh._t)
+    V, T = mesh._v.dev(), mesh._t.dev()
+    walk = torch.empty((nv, 3), dtype=torch.float64, device="cuda")
+    st = L.load().ot_tsdf_mesh_vertex_normals(vol._h, mesh._mc[1], C.c_void_p(V.data_ptr()), nv,
+                                              C.c_void_p(T.data_ptr()), nt, C.c_void_p(walk.data_ptr()), None)
+    assert st == 0, L.load().ot_last_error()
+    generic = torch.empty_like(walk)
+    L.call("ot_mesh_compute_vertex_normals", C.c_void_p(V.data_ptr()), nv, C.c_void_p(T.data_ptr()), nt,
+           C.c_void_p(generic.data_ptr()), None)
+    rV, _, rT = ref.extract_triangle_mesh()
+    rN = O.vertex_normals(rV, rT)
+    assert_bitwise(walk.cpu().numpy(), rN, "vertex normals (marching-cubes walk)")
+    assert_bitwise(generic.cpu().numpy(), rN, "vertex normals (corner sort)")
+    mesh.compute_vertex_normals()  # the facade's choice: the walk
+    assert_bitwise(np.asarray(mesh.vertex_normals), rN, "facade vertex normals")
+    # the volume changes: the walk refuses, the facade falls back
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), convert_rgb_to_intensity=False)
+    vol.integrate(rgbd, pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth)), ext[0])
+    vol.flush()
+    st = L.load().ot_tsdf_mesh_vertex_normals(vol._h, mesh._mc[1], C.c_void_p(V.data_ptr()), nv,
+                                              C.c_void_p(T.data_ptr()), nt, C.c_void_p(walk.data_ptr()), None)
+    assert st != 0
+    stale = pkg.geometry.TriangleMesh()
+    stale._v, stale._t, stale._mc = mesh._v, mesh._t, mesh._mc
+    stale.compute_vertex_normals()
+    assert_bitwise(np.asarray(stale.vertex_normals), rN, "fallback vertex normals")
+
+
+def test_vertex_normals_mc_walk_sharded(pkg, O, synth, seq16, gpu):
+    """A spatially sharded volume's partial mesh (own cubes only; halo units supply neighbours): the walk equals the
+    corner sort on the same partial mesh."""
+    import ctypes as C
+    import importlib
+
+    import torch
+
+    L = pkg._lib
+    D = importlib.import_module(pkg.__name__ + ".distributed")
+    integ = pkg.pipelines.integration
+    depth, color, ext = seq16
+    intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth))
+    shards = []
+    for r in range(3):
+        v = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
+        v.set_shard(r, 3)
+        for k in range(depth.shape[0]):
+            v.integrate(pkg.geometry.RGBDImage.create_from_color_and_depth(
+                pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), convert_rgb_to_intensity=False), intr, ext[k])
+        shards.append(v)
+    rows = torch.cat([D.pack_border(*v.export_border()) for v in shards])
+    for v in shards:
+        v.import_border(*D.unpack_border(rows))
+        mesh = v.extract_triangle_mesh()
+        nv, nt = len(mesh._v), len(mesh._t)
+        assert nv > 1000
+        walk = torch.empty((nv, 3), dtype=torch.float64, device="cuda")
+        generic = torch.empty_like(walk)
+        Vp, Tp = C.c_void_p(mesh._v.dev().data_ptr()), C.c_void_p(mesh._t.dev().data_ptr())
+        L.call("ot_tsdf_mesh_vertex_normals", v._h, mesh._mc[1], Vp, nv, Tp, nt, C.c_void_p(walk.data_ptr()), None)
+        L.call("ot_mesh_compute_vertex_normals", Vp, nv, Tp, nt, C.c_void_p(generic.data_ptr()), None)
+        assert_bitwise(walk.cpu().numpy(), generic.cpu().numpy(), "sharded partial mesh normals")
