@@ -54,8 +54,14 @@ class _Arr:
         return h
 
     def dev(self):
-        if self._d is None or self._viewed:
+        if self._d is None:
             self._d = D.to_device(self._h)
+        elif self._viewed:  # refresh IN PLACE: pointers handed out earlier (queued kernels, job tables) stay valid
+            h = np.ascontiguousarray(self._h)
+            if tuple(h.shape) != tuple(self._d.shape):
+                self._d = D.to_device(h)
+            else:
+                self._d.copy_(D.to_device(h))
         return self._d
 
     def copy(self):
