@@ -550,6 +550,11 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
 #endif
 constexpr int BZ = OT_BZ;                     // voxels per lane along z
 constexpr int SLICES = 4 * (UNIT_RES / BZ);   // waves per unit
+#ifndef OT_INT_WG
+#define OT_INT_WG SLICES  // waves per integrate workgroup: a whole unit (SLICES), or a part of one (a divisor of SLICES)
+#endif
+constexpr int INT_WG = OT_INT_WG;
+constexpr int INT_PARTS = SLICES / INT_WG;  // workgroups per unit
 
 struct UnitWork {
     int id;                   // pool id, | 0x80000000 when fresh (state starts at zero), -1 when dropped
@@ -632,32 +637,41 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 // integration alone (no imported units): then |a| is 0 or far above the underflow range (tsdf: a sum of a running
 // mean and a term quantised by the depth / camera-distance floats; colour: c*w + rgb >= 0 with c a mean of bytes).
 // Otherwise the IEEE divisions (FAST = false).
-constexpr int RCP_N = 4096;
+#ifndef OT_RCP_N
+#define OT_RCP_N 4096
+#endif
+constexpr int RCP_N = OT_RCP_N;
 
 // One workgroup of SLICES waves per unit, so a unit's frame footprint is gathered through one CU's L1; units are
 // assigned by a static grid stride that every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes
 template <bool C64, bool FAST>
-__global__ __launch_bounds__(64 * SLICES, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_PER_EU) void k_batch_integrate(
+__global__ __launch_bounds__(64 * INT_WG, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
     using CT = typename std::conditional<C64, double, float>::type;
     __shared__ float s_r32[FAST ? RCP_N + 1 : 1];
     __shared__ double s_r64[(FAST && C64) ? RCP_N + 1 : 1];
     if constexpr (FAST) {
-        for (int n = threadIdx.x; n <= RCP_N; n += 64 * SLICES) {
+        for (int n = threadIdx.x; n <= RCP_N; n += 64 * INT_WG) {
             s_r32[n] = 1.0f / (float)n;  // IEEE (correctly rounded) quotients
             if constexpr (C64) s_r64[n] = 1.0 / (double)n;
         }
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
-    const int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // slice of this wave
     const int n = d.counters[pc];
     const int npx = p.W * p.H;
     unsigned upd = 0;  // per lane: <= BZ voxels x 64 frames x units per workgroup, far below 2^32
     {
         const int b = blockIdx.x;
-        for (int u = b; u < n; u += gridDim.x) {
+        // work item = (unit, part): the INT_PARTS parts of a unit are items 8 apart, so they run on one XCD (blocks
+        // are dealt round-robin over the 8 XCDs) at about the same time and share its L2's copy of the footprint
+        const int items = INT_PARTS == 1 ? n : ((n + 7) / 8) * 8 * INT_PARTS;
+        for (int it = b; it < items; it += gridDim.x) {
+            const int u = INT_PARTS == 1 ? it : (it / (8 * INT_PARTS)) * 8 + (it & 7);
+            if (INT_PARTS > 1 && u >= n) continue;
+            const int part = INT_PARTS == 1 ? 0 : (it >> 3) % INT_PARTS;
+            const int s = __builtin_amdgcn_readfirstlane(part * INT_WG + (int)(threadIdx.x >> 6));  // slice of this wave
             const UnitWork& w = work[u];
             const int ent = w.id;
             const unsigned long long mask = w.mask;
@@ -1249,7 +1263,7 @@ static int integrate_grid(bool c64, bool fast) {
         int per_cu = 0, cus = 0;
         const void* kern = c64 ? (fast ? integrate_kernel<true, true>() : integrate_kernel<true, false>())
                                : (fast ? integrate_kernel<false, true>() : integrate_kernel<false, false>());
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * SLICES, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * INT_WG, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 ||
             cus <= 0)
             return 4096;
@@ -1344,13 +1358,13 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     const BatchFrame* bf = vol->bframes;
     const UnitWork* uw = (const UnitWork*)vol->dev.work;
     if (vol->color64 && fast)
-        hipLaunchKernelGGL((k_batch_integrate<true, true>), dim3(grid), dim3(64 * SLICES), 0, stream, bf, ip0, vol->dev, uw, pc);
+        hipLaunchKernelGGL((k_batch_integrate<true, true>), dim3(grid), dim3(64 * INT_WG), 0, stream, bf, ip0, vol->dev, uw, pc);
     else if (vol->color64)
-        hipLaunchKernelGGL((k_batch_integrate<true, false>), dim3(grid), dim3(64 * SLICES), 0, stream, bf, ip0, vol->dev, uw, pc);
+        hipLaunchKernelGGL((k_batch_integrate<true, false>), dim3(grid), dim3(64 * INT_WG), 0, stream, bf, ip0, vol->dev, uw, pc);
     else if (fast)
-        hipLaunchKernelGGL((k_batch_integrate<false, true>), dim3(grid), dim3(64 * SLICES), 0, stream, bf, ip0, vol->dev, uw, pc);
+        hipLaunchKernelGGL((k_batch_integrate<false, true>), dim3(grid), dim3(64 * INT_WG), 0, stream, bf, ip0, vol->dev, uw, pc);
     else
-        hipLaunchKernelGGL((k_batch_integrate<false, false>), dim3(grid), dim3(64 * SLICES), 0, stream, bf, ip0, vol->dev, uw, pc);
+        hipLaunchKernelGGL((k_batch_integrate<false, false>), dim3(grid), dim3(64 * INT_WG), 0, stream, bf, ip0, vol->dev, uw, pc);
     vol->batch_pc ^= 1;  // only once this batch's kernels are queued (its units kernel zeroes the other counter)
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
