@@ -246,7 +246,8 @@ ot_status ot_tsdf_import_border(ot_tsdf* vol, int64_t n, const int32_t* keys, co
 ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices_host, int64_t* n_triangles_host,
                                         void* stream);
 /* Copy the extracted mesh out: vertices f64 [V][3], colors f64 [V][3] (0..1, NULL to skip),
- * triangles int32 [T][3].  Device pointers. */
+ * triangles int32 [T][3].  Device pointers; ordered on `stream` (no synchronisation: the extraction and these copies
+ * complete in stream order, before any later work on that stream). */
 ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors,
                                       int32_t* triangles, void* stream);
 /* Serial of the last extraction (ot_tsdf_extract_triangle_mesh), or -1 once the volume has changed since (frames

@@ -34,7 +34,8 @@ constexpr int T17 = 17;
 struct McDev {
     const unsigned* sorted_ids;  // rank -> id
     int* rank_of;                // id -> rank
-    int* nbr;                    // [id][8] neighbour ids, index dx*4 + dy*2 + dz
+    int* nbr;                    // [id][16] neighbour ids: [0, 8) offsets +(dx, dy, dz), [8, 16) offsets -(dx, dy, dz),
+                                 // index dx*4 + dy*2 + dz, dx, dy, dz in {0, 1}
     unsigned char* cubes;        // [id][4096]
     unsigned* eflags;            // [id][384]
     int* wprefix;                // [id][384]
@@ -49,7 +50,7 @@ struct McDev {
 
 // the marching-cubes workspace of U units, carved from one allocation (kept with the volume: MeshBuffers::ws)
 static size_t mc_ws_bytes(int64_t U) {
-    return (size_t)U * (4 * 8 + 4 + 8 * 4 + EWORDS * 4 * 2 + UNIT_VOX + UNIT_VOX * 2) + 16 * 256;
+    return (size_t)U * (4 * 8 + 4 + 16 * 4 + EWORDS * 4 * 2 + UNIT_VOX + UNIT_VOX * 2) + 16 * 256;
 }
 static void mc_layout(char* ws, int64_t U, McDev& m) {
     char* p = ws;
@@ -63,7 +64,7 @@ static void mc_layout(char* ws, int64_t U, McDev& m) {
     m.tri_base = (long long*)take(sizeof(long long) * U);
     m.vert_base = (long long*)take(sizeof(long long) * U);
     m.rank_of = (int*)take(sizeof(int) * U);
-    m.nbr = (int*)take(sizeof(int) * 8 * U);
+    m.nbr = (int*)take(sizeof(int) * 16 * U);
     m.eflags = (unsigned*)take(sizeof(unsigned) * EWORDS * U);
     m.wprefix = (int*)take(sizeof(int) * EWORDS * U);
     m.cubes = (unsigned char*)take((size_t)UNIT_VOX * U);
@@ -90,11 +91,12 @@ __global__ __launch_bounds__(256) void k_mc_prepare(TsdfDev d, McDev m) {
     const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
-    if (t < 8) {
-        const int dx = (t >> 2) & 1, dy = (t >> 1) & 1, dz = t & 1;
-        m.nbr[id * 8 + t] = t == 0 ? id
-                                   : find_unit(d, d.unit_keys[id * 3] + dx, d.unit_keys[id * 3 + 1] + dy,
-                                               d.unit_keys[id * 3 + 2] + dz);
+    if (t < 16) {
+        const int sg = t < 8 ? 1 : -1, q = t & 7;
+        const int dx = sg * ((q >> 2) & 1), dy = sg * ((q >> 1) & 1), dz = sg * (q & 1);
+        m.nbr[id * 16 + t] = q == 0 ? id
+                                    : find_unit(d, d.unit_keys[id * 3] + dx, d.unit_keys[id * 3 + 1] + dy,
+                                                d.unit_keys[id * 3 + 2] + dz);
     }
     if (t == 0) m.rank_of[id] = r;
     for (int w = t; w < EWORDS; w += 256) m.eflags[(size_t)id * EWORDS + w] = 0u;
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
         if (t == 0) m.tri_cnt[r] = 0;
         return;
     }
-    if (t < 8) snbr[t] = m.nbr[id * 8 + t];
+    if (t < 8) snbr[t] = m.nbr[id * 16 + t];
     for (int w = t; w < EWORDS; w += 256) sflags[w] = 0u;
     __syncthreads();
     // tile staging in the pool's memory order (z, x, y with y fastest), so a wave's loads are contiguous runs;
@@ -255,7 +257,7 @@ __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, doub
         double c0[3], c1[3];
         voxel_value(d, id, x, y, z, f0f, c0);
         int x1 = x + (axis == 0), y1 = y + (axis == 1), z1 = z + (axis == 2);
-        const int nid = m.nbr[id * 8 + (((x1 >> 4) << 2) | ((y1 >> 4) << 1) | (z1 >> 4))];
+        const int nid = m.nbr[id * 16 + (((x1 >> 4) << 2) | ((y1 >> 4) << 1) | (z1 >> 4))];
         if (nid < 0) {  // cannot happen for a valid cube (its corners have weight > 0); never read out of bounds
             f1f = f0f;
             c1[0] = c0[0], c1[1] = c0[1], c1[2] = c0[2];
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
     const int ukey[3] = {d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]};
-    if (t < 8) snbr[t] = m.nbr[id * 8 + t];
+    if (t < 8) snbr[t] = m.nbr[id * 16 + t];
     const uint4 q = *reinterpret_cast<const uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16);
     const unsigned cw[4] = {q.x, q.y, q.z, q.w};
     int cnt = 0;
@@ -360,11 +362,15 @@ __global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t
     long long start[4];
     int cubev[4], edge[4];
     int nc = 0;
+    const int owner = find_unit(d, key.x, key.y, key.z);
+    if (owner < 0 || owner >= units) return;  // cannot happen for a vertex of this extraction
 #pragma unroll
     for (int e = 0; e < 12; ++e) {
         if (c_eshift[e][3] != axis) continue;
         const int c[3] = {g[0] - c_eshift[e][0], g[1] - c_eshift[e][1], g[2] - c_eshift[e][2]};
-        const int id = find_unit(d, c[0] >> 4, c[1] >> 4, c[2] >> 4);  // arithmetic shift: floor for negatives
+        // the cube's unit is the owner or one of its -x/-y/-z neighbours (arithmetic shift: floor for negatives)
+        const int ox = key.x - (c[0] >> 4), oy = key.y - (c[1] >> 4), oz = key.z - (c[2] >> 4);
+        const int id = m.nbr[owner * 16 + 8 + (ox << 2 | oy << 1 | oz)];
         if (id < 0 || id >= units) continue;
         const int ci = ((c[0] & 15) * 16 + (c[1] & 15)) * 16 + (c[2] & 15);
         const int cube = m.cubes[(size_t)id * UNIT_VOX + ci];
@@ -507,8 +513,7 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, stream, vol->dev, m, vol->voxel_length, mb.v,
                        vol->color_type == OT_COLOR_RGB8 ? mb.c : nullptr);
     hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, mb.t);
-    OT_LAUNCH_CHECK();
-    OT_HIP_TRY(hipStreamSynchronize(stream));
+    OT_LAUNCH_CHECK();  // the mesh is complete in stream order (fetch / normals / keys are ordered after it)
     mb.nv = nv;
     mb.nt = nt;
     mb.ws_units = U;
@@ -560,7 +565,6 @@ ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* ve
     }
     if (mb.nt > 0 && triangles)
         OT_HIP_TRY(hipMemcpyAsync(triangles, mb.t, sizeof(int32_t) * 3 * mb.nt, hipMemcpyDefault, stream));
-    OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
 }
 

@@ -1412,6 +1412,13 @@ ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream) {
     return OT_OK;
 }
 
+static ot_status counter_errors(const int* c) {
+    if (c[C_OVERFLOW]) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] volume unit pool exhausted (max_units)");
+    if (c[C_HASHERR] & 1) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] unit hash table full");
+    if (c[C_HASHERR] & 2) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] unit index out of range");
+    return OT_OK;
+}
+
 static ot_status check_errors(ot_tsdf* vol, hipStream_t stream) {
     int c[N_COUNTERS];
     OT_HIP_TRY(hipMemcpyAsync(c, vol->dev.counters, sizeof(c), hipMemcpyDeviceToHost, stream));
@@ -1425,12 +1432,12 @@ static ot_status check_errors(ot_tsdf* vol, hipStream_t stream) {
 ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) {
     ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
-    st = check_errors(vol, stream);
-    if (st != OT_OK) return st;
-    int nu = 0;
-    OT_HIP_TRY(hipMemcpyAsync(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost, stream));
+    int c[N_COUNTERS];  // error flags and the unit count in one read-back
+    OT_HIP_TRY(hipMemcpyAsync(c, vol->dev.counters, sizeof(c), hipMemcpyDeviceToHost, stream));
     OT_HIP_TRY(hipStreamSynchronize(stream));
-    nu = (int)std::min<int64_t>(nu, vol->max_units);
+    st = counter_errors(c);
+    if (st != OT_OK) return st;
+    int nu = (int)std::min<int64_t>(c[C_UNITS], vol->max_units);
     *n_units = nu;
     if (vol->sorted_frame == vol->frame_id && vol->sorted_units == nu) return OT_OK;
     if (nu > 0) {
