@@ -551,8 +551,8 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
 constexpr int BZ = OT_BZ;                     // voxels per lane along z
 constexpr int SLICES = 4 * (UNIT_RES / BZ);   // waves per unit
 #ifndef OT_INT_WG
-#define OT_INT_WG SLICES  // waves per integrate workgroup: a whole unit (SLICES), or a part of one (a divisor of SLICES)
-#endif
+#define OT_INT_WG 4  // waves per integrate workgroup: a quarter unit (measured per 32-frame launch, float64 colour:
+#endif               // 16 waves 0.511 ms, 8 waves 0.452 ms, 4 waves 0.426 ms; float32 colour 0.402 / 0.383 / 0.378)
 constexpr int INT_WG = OT_INT_WG;
 constexpr int INT_PARTS = SLICES / INT_WG;  // workgroups per unit
 
@@ -638,12 +638,14 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 // mean and a term quantised by the depth / camera-distance floats; colour: c*w + rgb >= 0 with c a mean of bytes).
 // Otherwise the IEEE divisions (FAST = false).
 #ifndef OT_RCP_N
-#define OT_RCP_N 4096
+#define OT_RCP_N 2048  // 24 KiB of LDS per workgroup (float64 + float32 tables): 6 quarter-unit workgroups per CU
 #endif
 constexpr int RCP_N = OT_RCP_N;
 
-// One workgroup of SLICES waves per unit, so a unit's frame footprint is gathered through one CU's L1; units are
-// assigned by a static grid stride that every wave derives on its own: no atomics, one barrier (the reciprocal table).
+// One workgroup of INT_WG waves per unit part (a quarter unit by default: small workgroups let the CU keep 6-8 of them
+// resident instead of one 16-wave unit -- a unit-sized workgroup left the float64-colour kernel at 4 waves per SIMD
+// whatever its registers); the parts of a unit run on one XCD.  Work items are assigned by a static grid stride that
+// every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes
 template <bool C64, bool FAST>
 __global__ __launch_bounds__(64 * INT_WG, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_PER_EU) void k_batch_integrate(
