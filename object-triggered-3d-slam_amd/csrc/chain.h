@@ -20,20 +20,30 @@ struct ChainJob {
     int32_t* ex;
     long long* msum;
     int32_t* kind;    // 0 fast, 1 flagged by k_chain_chunk, 2 walked serially
-    double* start;    // exact s entering each fast chunk
+    long long* pre;   // inclusive prefix of msum inside each run of chunks (k_chain_runs), saturated at 2^53
+    int32_t* rend;    // last chunk of the run holding each chunk
+    int32_t* seg_b;   // accepted segments (first chunk, exact N, prefix base) in walk order; count in *nseg
+    long long* seg_n;
+    long long* seg_base;
+    int32_t* nseg;
 };
 
-// per-chain auxiliary arrays (bsum, start, msum, ex, kind)
-inline size_t chain_aux_bytes(int64_t n) { return (size_t)((n + CHAIN_CH - 1) / CHAIN_CH + 1) * 40 + 256; }
+// per-chain auxiliary arrays
+inline size_t chain_aux_bytes(int64_t n) { return (size_t)((n + CHAIN_CH - 1) / CHAIN_CH + 1) * 64 + 512; }
 
 inline char* chain_aux(char* cur, int64_t n, ChainJob& jb) {
     const int64_t nb = (n + CHAIN_CH - 1) / CHAIN_CH + 1;
     jb.bsum = (double*)cur;
-    jb.start = jb.bsum + nb;
-    jb.msum = (long long*)(jb.start + nb);
-    jb.ex = (int32_t*)(jb.msum + nb);
+    jb.msum = (long long*)(jb.bsum + nb);
+    jb.pre = jb.msum + nb;
+    jb.seg_n = jb.pre + nb;
+    jb.seg_base = jb.seg_n + nb;
+    jb.ex = (int32_t*)(jb.seg_base + nb);
     jb.kind = jb.ex + nb;
-    cur = (char*)(jb.kind + nb);
+    jb.rend = jb.kind + nb;
+    jb.seg_b = jb.rend + nb;
+    jb.nseg = jb.seg_b + nb;
+    cur = (char*)(jb.nseg + 2);
     return (char*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
 }
 

@@ -96,11 +96,14 @@ __global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V,
 //   k_chain_bsum   approximate chunk sums (any order)            -> bsum
 //   k_chain_guess  approximate exclusive prefix -> guessed binade e_b of s at each chunk start
 //   k_chain_chunk  M_b = sum r_t at u_b = 2^(e_b-52), flag ties / negative / non-finite / r >= 2^53
-//   k_chain_walk   one wave per chain: from the exact s at a chunk start it accepts a run of chunks at once
-//                  (wave prefix of M_b) while e(s) == e_b, no flag and N + prefix <= 2^53 - 1 (N = s / u, so
-//                  every intermediate sum stays inside the binade); any other chunk (s == 0 at the start,
-//                  binade crossing, tie, wrong guess) is walked serially in Open3D's order by one lane
-//   k_chain_emit   (CDF) every accepted chunk's values (N_b + prefix_t) * u_b, exact integers times 2^k
+//   k_chain_runs   runs = maximal stretches of unflagged chunks with one guessed binade (a flagged chunk is a run
+//                  of its own): the inclusive prefix of M_b inside each run and every chunk's run end, in parallel
+//   k_chain_walk   one wave per chain, one step per RUN instead of per 64 chunks: from the exact s (N = s / u) it
+//                  accepts the longest stretch [b, k] of the run with e(s) == e_b and N + prefix <= 2^53 - 1
+//                  (every intermediate sum stays inside the binade: the prefix is monotone, so the run end decides
+//                  at once, else a 64-way search), records the segment (b, N, prefix base) and jumps to k + 1; any
+//                  other chunk (s == 0, binade crossing, tie, wrong guess) is walked serially in Open3D's order
+//   k_chain_emit   (CDF) every accepted chunk's values (N + prefix_t) * u, exact integers times 2^k, from its segment
 // The guesses only decide which chunks take the fast path; every accepted value is proven exact by the walk's
 // check, so any input (zeros, ties, NaN, huge ranges) gives the serial chain's bits.
 constexpr int CH = CHAIN_CH;
@@ -231,7 +234,65 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
     return out;
 }
 
-constexpr int WALK_DEPTH = 4;  // groups of 64 chunk summaries the walk keeps in flight
+// one block per chain: run heads (b == 0, guessed binade changes, a flagged chunk or the chunk after one), the
+// inclusive prefix of M inside each run (saturated at 2^53: the walk only compares it against < 2^53) and each
+// chunk's run end -- a segmented scan, then a reverse pass for the ends
+__device__ inline bool run_head(const ChainJob& j, int64_t b) {
+    return b == 0 || j.kind[b] != 0 || j.kind[b - 1] != 0 || j.ex[b] != j.ex[b - 1];
+}
+
+__global__ __launch_bounds__(256) void k_chain_runs(const ChainJob* __restrict__ jobs) {
+    __shared__ long long s_val[256];
+    __shared__ int s_head[256];
+    __shared__ int s_first[256];
+    const ChainJob j = jobs[blockIdx.x];
+    const int t = threadIdx.x;
+    const int64_t nb = (j.n + CH - 1) / CH, per = (nb + 255) / 256;
+    const int64_t lo = t * per, hi = lo + per < nb ? lo + per : nb;
+    long long acc = 0;
+    int has_head = 0, first = 0x7FFFFFFF;
+    for (int64_t b = lo; b < hi; ++b) {
+        if (run_head(j, b)) {
+            acc = 0;
+            has_head = 1;
+            first = first < (int)b ? first : (int)b;
+        }
+        acc = acc + j.msum[b];
+        acc = acc < R_MAX ? acc : R_MAX;
+    }
+    s_val[t] = acc;
+    s_head[t] = has_head;
+    s_first[t] = first;
+    __syncthreads();
+    if (t == 0) {  // carries: 256 serial steps over the threads' summaries (one block, a few microseconds)
+        long long c = 0;
+        for (int i = 0; i < 256; ++i) {
+            const long long v = s_val[i];
+            const int h = s_head[i];
+            s_val[i] = c;  // carry into thread i
+            c = h ? v : (c + v < R_MAX ? c + v : R_MAX);
+        }
+        int nxt = (int)nb;  // first head after thread i's range
+        for (int i = 255; i >= 0; --i) {
+            const int f = s_first[i];
+            s_first[i] = nxt;
+            nxt = f < nxt ? f : nxt;
+        }
+    }
+    __syncthreads();
+    acc = s_val[t];
+    for (int64_t b = lo; b < hi; ++b) {
+        if (run_head(j, b)) acc = 0;
+        acc = acc + j.msum[b];
+        acc = acc < R_MAX ? acc : R_MAX;
+        j.pre[b] = acc;
+    }
+    int nxt = s_first[t];
+    for (int64_t b = hi - 1; b >= lo; --b) {
+        j.rend[b] = nxt - 1;
+        if (run_head(j, b)) nxt = (int)b;
+    }
+}
 
 template <bool CDF>
 __global__ __launch_bounds__(64) void k_chain_walk(const ChainJob* __restrict__ jobs) {
@@ -240,76 +301,71 @@ __global__ __launch_bounds__(64) void k_chain_walk(const ChainJob* __restrict__ 
     const int lane = threadIdx.x;
     const int64_t nb = (j.n + CH - 1) / CH;
     double s = 0.0;  // sum: 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0
-    // chunk summaries of the next WALK_DEPTH groups stay in flight (a register ring; static indices only)
-    int e_r[WALK_DEPTH], k_r[WALK_DEPTH];
-    long long m_r[WALK_DEPTH];
-#pragma unroll
-    for (int q = 0; q < WALK_DEPTH; ++q) {
-        const int64_t b = (int64_t)q * 64 + lane;
-        const bool in = b < nb;
-        e_r[q] = in ? j.ex[b] : EX_NONE;
-        m_r[q] = in ? j.msum[b] : 0;
-        k_r[q] = in ? j.kind[b] : 1;
-    }
-    for (int64_t g0 = 0; g0 < nb; g0 += 64 * WALK_DEPTH)
-#pragma unroll
-    for (int q = 0; q < WALK_DEPTH; ++q) {
-        const int64_t g = g0 + (int64_t)q * 64;
-        if (g >= nb) break;
-        const int64_t b = g + lane;
-        const int e_b = e_r[q], k_b = k_r[q];
-        const long long m_b = m_r[q];
-        {  // refill this ring slot with the group WALK_DEPTH ahead
-            const int64_t bn = b + 64 * WALK_DEPTH;
-            const bool in = bn < nb;
-            e_r[q] = in ? j.ex[bn] : EX_NONE;
-            m_r[q] = in ? j.msum[bn] : 0;
-            k_r[q] = in ? j.kind[bn] : 1;
-        }
-        const int lim = nb - g < 64 ? (int)(nb - g) : 64;
-        int local = 0;
-        while (local < lim) {
-            const int e = binade(s);
-            if (e != EX_NONE) {
-                const double u = pow2(e - 52);
-                const long long N = (long long)(s * pow2(52 - e));  // exact integer in [2^52, 2^53)
-                const bool act = lane >= local;
-                const long long v = act ? m_b : 0;
-                long long incl = v;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const long long t = __shfl_up(incl, d);
-                    if (lane >= d) incl += t;
+    int nseg = 0;
+    int64_t b = 0;
+    while (b < nb) {  // wave-uniform control flow: every lane holds the same s and b
+        const int k_b = j.kind[b], e_b = j.ex[b], re = j.rend[b];
+        const bool head = b == 0 || j.rend[b - 1] < b;
+        const long long base = head ? 0 : j.pre[b - 1];
+        const long long p_re = j.pre[re];
+        const int e = binade(s);
+        if (e != EX_NONE && k_b == 0 && e_b == e && base < R_MAX) {  // (a saturated base proves nothing)
+            const long long N = (long long)(s * pow2(52 - e));  // exact integer in [2^52, 2^53)
+            const long long lim = R_MAX - 1 - N + base;        // chunk c is accepted while pre[c] <= lim
+            int64_t k = re;
+            if (p_re > lim) {  // the binade ends inside the run: 64-way search for the last accepted chunk
+                int64_t lo = b - 1, hi = re;  // pre[lo] <= lim (lo = b - 1: none yet), pre[hi] > lim
+                while (hi - lo > 1) {
+                    const int64_t step = (hi - lo - 1 + 63) / 64;
+                    const int64_t c = lo + 1 + (int64_t)lane * step;
+                    const bool ok = c < hi && j.pre[c] <= lim;
+                    const unsigned long long m = __ballot(ok);
+                    const int L = __popcll(m);  // the accepted probes are a prefix (pre is monotone)
+                    const int64_t nlo = L ? lo + 1 + (int64_t)(L - 1) * step : lo;
+                    const int64_t cL = lo + 1 + (int64_t)L * step;
+                    hi = L == 0 ? lo + 1 : (cL < hi ? cL : hi);
+                    lo = nlo;
                 }
-                const bool ok = lane < lim && e_b == e && k_b == 0 && N + incl <= R_MAX - 1;
-                const unsigned long long badm = __ballot(act && !ok);
-                int fb = badm ? __ffsll((long long)badm) - 1 : 64;
-                fb = fb < lim ? fb : lim;
-                if (fb > local) {
-                    if (act && lane < fb) j.start[b] = (double)(N + incl - v) * u;
-                    const long long tot = __shfl(incl, fb - 1);
-                    s = (double)(N + tot) * u;
-                    local = fb;
-                }
+                k = lo;
             }
-            if (local < lim) {  // not provable from s: walk this chunk serially
-                s = chain_serial_chunk<CDF>(j, g + local, s, lds, lane);
-                if (lane == 0) j.kind[g + local] = 2;
-                ++local;
+            if (k >= b) {
+                if (CDF && lane == 0) {
+                    j.seg_b[nseg] = (int)b;
+                    j.seg_n[nseg] = N;
+                    j.seg_base[nseg] = base;
+                }
+                ++nseg;
+                s = (double)(N + j.pre[k] - base) * pow2(e - 52);
+                b = k + 1;
+                continue;
             }
         }
+        // not provable from s: walk this chunk serially
+        s = chain_serial_chunk<CDF>(j, b, s, lds, lane);
+        if (lane == 0) j.kind[b] = 2;
+        ++b;
     }
-    if (!CDF && lane == 0) j.out[0] = s;
+    if (lane == 0) {
+        if (!CDF) j.out[0] = s;
+        j.nseg[0] = nseg;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_chain_emit(const ChainJob* __restrict__ jobs) {
     const ChainJob j = jobs[blockIdx.y];
     const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nb = (j.n + CH - 1) / CH;
-    if (b >= nb || j.kind[b] != 0) return;
+    if (b >= nb || j.kind[b] == 2) return;  // serial chunks were written by the walk
     const int lane = threadIdx.x & 63;
+    // this chunk's segment: the last one starting at or before it
+    int lo = 0, hi = j.nseg[0];
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (j.seg_b[mid] <= b) lo = mid;
+        else hi = mid;
+    }
     const int e = j.ex[b];
     const double u = pow2(e - 52), scale = pow2(52 - e);
-    const long long N = (long long)(j.start[b] * scale);
+    const long long N = j.seg_n[lo] + (j.seg_b[lo] < b ? j.pre[b - 1] - j.seg_base[lo] : 0);
     double v[4];
     chunk_load4(j.x, j.n, b * CH, lane, v);
     long long r[4], loc = 0;
@@ -347,6 +403,7 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
     hipLaunchKernelGGL(k_chain_bsum, grid, dim3(256), 0, stream, djobs);
     hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(256), 0, stream, djobs);
     hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
+    hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(256), 0, stream, djobs);
     hipLaunchKernelGGL(k_chain_walk<CDF>, dim3(n_jobs), dim3(64), 0, stream, djobs);
     if (CDF) hipLaunchKernelGGL(k_chain_emit, grid, dim3(256), 0, stream, djobs);
 }

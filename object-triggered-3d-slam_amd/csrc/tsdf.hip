@@ -621,7 +621,7 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 #define OT_WAVES_PER_EU 8  // float32 colour: 64 VGPRs, 8 waves per SIMD (the kernel lives on its occupancy)
 #endif
 #ifndef OT_WAVES_PER_EU_C64
-#define OT_WAVES_PER_EU_C64 5
+#define OT_WAVES_PER_EU_C64 8  // quarter-unit workgroups, 64 VGPRs (5 / 6 / 8: 0.426 / 0.428 / 0.414 ms per launch)
 #endif
 #ifndef OT_RCP_TABLE
 #define OT_RCP_TABLE 1  // 0: never take the FAST (reciprocal table) kernel
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 // mean and a term quantised by the depth / camera-distance floats; colour: c*w + rgb >= 0 with c a mean of bytes).
 // Otherwise the IEEE divisions (FAST = false).
 #ifndef OT_RCP_N
-#define OT_RCP_N 2048  // 24 KiB of LDS per workgroup (float64 + float32 tables): 6 quarter-unit workgroups per CU
+#define OT_RCP_N 2048  // 16 KiB (float64) / 8 KiB (float32) of LDS per workgroup: 8 quarter-unit workgroups per CU
 #endif
 constexpr int RCP_N = OT_RCP_N;
 
@@ -648,15 +648,18 @@ constexpr int RCP_N = OT_RCP_N;
 // every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes
 template <bool C64, bool FAST>
-__global__ __launch_bounds__(64 * INT_WG, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_PER_EU) void k_batch_integrate(
+__global__ __launch_bounds__(64 * INT_WG, C64 ? (FAST ? OT_WAVES_PER_EU_C64 : 5) : OT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
     using CT = typename std::conditional<C64, double, float>::type;
-    __shared__ float s_r32[FAST ? RCP_N + 1 : 1];
+    // one table per kernel: float64 reciprocals for the float64-colour kernel (its float32 ones are their roundings:
+    // (float)RN64(1/n) == RN32(1/n) for every n <= 2^20, no double-rounding case -- tools/markstein_check.cpp),
+    // float32 ones otherwise
+    __shared__ float s_r32[(FAST && !C64) ? RCP_N + 1 : 1];
     __shared__ double s_r64[(FAST && C64) ? RCP_N + 1 : 1];
     if constexpr (FAST) {
         for (int n = threadIdx.x; n <= RCP_N; n += 64 * INT_WG) {
-            s_r32[n] = 1.0f / (float)n;  // IEEE (correctly rounded) quotients
-            if constexpr (C64) s_r64[n] = 1.0 / (double)n;
+            if constexpr (C64) s_r64[n] = 1.0 / (double)n;  // IEEE (correctly rounded) quotients
+            else s_r32[n] = 1.0f / (float)n;
         }
         __syncthreads();
     }
@@ -808,7 +811,7 @@ __global__ __launch_bounds__(64 * INT_WG, C64 ? OT_WAVES_PER_EU_C64 : OT_WAVES_P
                         const float ta = ts[k] * wv + tn;
                         float tsn;  // (tsdf * w + t) / (w + 1): the IEEE quotient, tsdf bit-exact
                         if constexpr (FAST) {
-                            const float y = s_r32[(int)w1];
+                            const float y = C64 ? (float)s_r64[(int)w1] : s_r32[(int)w1];
                             const float q0 = ta * y;
                             tsn = __builtin_fmaf(__builtin_fmaf(-w1, q0, ta), y, q0);
                         } else {
