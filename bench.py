@@ -341,7 +341,8 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
     rank r keeps the units with owner(key) == r), so N GPUs integrate one object together (strong scaling; at
     N = 1 this is the headline itself).  Timed like the headline (reset + all frames + flush, max over ranks).
     Then marching cubes over the shards with a border halo (distributed.extract_sharded_mesh: all-gather of the
-    units' 721 low-face voxels, halo import, own-unit extraction, all-gather + merge of the partial meshes) -- timed
+    units' 721 low-face voxels sent to the owners of their -x/-y/-z neighbours only, halo import, own-unit extraction,
+    all-gather + merge of the partial meshes) -- timed
     apart as the per-object cost before normals / sampling; assemble_bytes = border rows each rank receives (the
     old whole-unit all-gather's bytes beside it), and the merged mesh must equal rank 0's unsharded mesh."""
     import importlib
@@ -391,6 +392,9 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
 
     t_asm, (mesh, border_bytes) = _timed(torch, dist, world, assemble, 1)
     whole = sum(cnt) * (3 + 4096 * (2 + 6)) * 4  # the whole-unit all-gather (f64 colour rows) it replaces
+    nb = Dm.all_gather_rows(torch.tensor([[int(vol.export_border()[0].shape[0])]], dtype=torch.int64,
+                                         device=COLL_DEV)).flatten().tolist()
+    allgather_border = (sum(nb) - nb[rank]) * (3 + 721 * 8) * 4  # every rank's border rows to every rank (round 2)
     match = None
     if rank == 0:  # the unsharded volume of the same scan, extracted on rank 0 (untimed)
         ref = make(False)
@@ -404,7 +408,7 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
                         "cubes with a border halo",
             "scaling": "strong", "frames_per_s": round(args.frames * 1.0 / dt, 1), "ms_per_step": round(dt * 1e3, 3),
             "units_per_rank_min": min(cnt), "units_per_rank_max": max(cnt), "assemble_ms": round(t_asm * 1e3, 2),
-            "assemble_bytes": border_bytes, "whole_unit_bytes": whole,
+            "assemble_bytes": border_bytes, "allgather_border_bytes": allgather_border, "whole_unit_bytes": whole,
             "mesh_vertices": int(mesh._v.dev().shape[0]), "mesh_matches_unsharded": match}
 
 

@@ -223,8 +223,17 @@ ot_status ot_tsdf_import_units_color64(ot_tsdf* vol, int64_t n, const int32_t* k
 /* Spatial sharding of ONE object's volume over `world` GPUs (not an Open3D API): this volume
  * allocates and integrates only the units whose owner hash(key) mod world == rank.  Every rank integrates every
  * frame; each voxel still sees the frames in call order, so the union of the ranks' exported units is bit-identical
- * to one unsharded volume.  Call before the first integrate. */
+ * to one unsharded volume.  Call before the first integrate.  The hash is of the unit's ownership block (below). */
 ot_status ot_tsdf_set_shard(ot_tsdf* vol, int32_t rank, int32_t world);
+/* Ownership granularity of a sharded volume: blocks of 2^log2_units units per axis share one owner (the hash is taken
+ * of the block key).  Set by ot_tsdf_set_shard to 2 (4^3 units) up to 4 ranks and 1 beyond; call after it, before the
+ * first integrate. */
+ot_status ot_tsdf_set_shard_block(ot_tsdf* vol, int32_t log2_units);
+/* Border-halo routing: per border row key int32 [n][3] (export_border's), the bitmask (bit r = rank r,
+ * world <= 64) of the other ranks that own one of the unit's 7 -x/-y/-z neighbours -- the only ranks whose marching
+ * cubes can read the row.  Device pointers; ordered on `stream`. */
+ot_status ot_tsdf_border_destinations(const ot_tsdf* vol, int64_t n, const int32_t* keys, int64_t* dest_mask,
+                                      void* stream);
 
 /* Border halo of a spatially sharded volume (SURVEY §8(e) "all-gather of border faces"; not an Open3D API).
  * export_border: per OWN unit (sorted key order; halo units are not exported) its 721 low-face voxels (x == 0 ||

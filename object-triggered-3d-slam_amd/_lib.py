@@ -77,6 +77,8 @@ SIGNATURES = {
     "ot_tsdf_import_units": [_p, _i64, _p, _p, _p, _p, _p],
     "ot_tsdf_import_units_color64": [_p, _i64, _p, _p, _p, _p, _p],
     "ot_tsdf_set_shard": [_p, _i32, _i32],
+    "ot_tsdf_set_shard_block": [_p, _i32],
+    "ot_tsdf_border_destinations": [_p, _i64, _p, _p, _p],
     "ot_tsdf_mesh_serial": [_p, _pi64],
     "ot_tsdf_mesh_vertex_normals": [_p, _i64, _p, _i64, _p, _i64, _p, _p],
     "ot_tsdf_export_border": [_p, _i64, _p, _p, _p, _p, _pi64, _p],

@@ -54,13 +54,21 @@ struct TsdfDev {
     int max_units;
     int shard_rank;   // spatial sharding of one volume over `shard_world` GPUs: this volume keeps only the units
     int shard_world;  // with owner(key) == shard_rank (<= 1: no sharding)
+    int shard_shift;  // ownership granularity: blocks of 2^shift units per axis share an owner
 };
 
-// owner rank of a unit: a hash independent of the table's slot hash mix64(key), so a shard's keys
-// still spread over all slots
+// owner rank of a unit: a hash of its block key (unit key >> shard_shift per axis), independent of the
+// table's slot hash mix64(key), so a shard's keys still spread over all slots.  Blocks of units keep most marching-cubes
+// neighbours on one rank (the border halo only crosses block faces) while still balancing the ranks' units.
+__host__ __device__ inline int unit_owner(int shard_world, int shard_shift, int x, int y, int z) {
+    const unsigned long long bk = pack_key(x >> shard_shift, y >> shard_shift, z >> shard_shift);
+    return (int)((unsigned)(mix64(bk + 0x9E3779B97F4A7C15ull) >> 32) % (unsigned)shard_world);
+}
 __host__ __device__ inline bool unit_owned(const TsdfDev& d, unsigned long long key) {
     if (d.shard_world <= 1) return true;
-    return (int)((unsigned)(mix64(key + 0x9E3779B97F4A7C15ull) >> 32) % (unsigned)d.shard_world) == d.shard_rank;
+    int x, y, z;
+    unpack_key(key, x, y, z);
+    return unit_owner(d.shard_world, d.shard_shift, x, y, z) == d.shard_rank;
 }
 
 // a unit's record: tsdf plane, weight plane, then the colour planes r, g, b (4096 each, voxel vi = z*256 + x*16 + y)

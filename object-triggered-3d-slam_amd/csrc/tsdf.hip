@@ -1019,6 +1019,22 @@ __global__ __launch_bounds__(256) void k_import_border(TsdfDev d, const int32_t*
     }
 }
 
+// destinations of a border row (SURVEY §8(e) halo): the ranks owning the unit's 7 -x/-y/-z neighbours (the units whose
+// marching cubes read its low faces), this rank excluded -- a superset of the rows k_import_border keeps there
+__global__ __launch_bounds__(256) void k_border_dest(TsdfDev d, int64_t n, const int32_t* __restrict__ keys,
+                                                     unsigned long long* __restrict__ mask) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    const int x = keys[r * 3], y = keys[r * 3 + 1], z = keys[r * 3 + 2];
+    unsigned long long m = 0ull;
+    if (d.shard_world > 1)
+        for (int t = 1; t < 8; ++t) {
+            const int nx = x - ((t >> 2) & 1), ny = y - ((t >> 1) & 1), nz = z - (t & 1);
+            if (key_in_range(nx, ny, nz)) m |= 1ull << unit_owner(d.shard_world, d.shard_shift, nx, ny, nz);
+        }
+    mask[r] = m & ~(1ull << d.shard_rank);
+}
+
 // owned units of the sorted order (a sharded volume's own units; every unit when unsharded)
 struct OwnedPred {
     TsdfDev d;
@@ -1799,6 +1815,31 @@ ot_status ot_tsdf_set_shard(ot_tsdf* vol, int32_t rank, int32_t world) {
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] set the shard before the first integrate");
     vol->dev.shard_rank = rank;
     vol->dev.shard_world = world;
+    // ownership blocks: 4^3 units up to 4 ranks, 2^3 beyond (configs[1] scan, 5 mm: largest shard / mean 1.09 / 1.13 /
+    // 1.09 at 2 / 4 / 8 ranks; border rows sent 0.42 / 0.25 / 0.24 of an all-gather's)
+    vol->dev.shard_shift = world <= 4 ? 2 : 1;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_set_shard_block(ot_tsdf* vol, int32_t log2_units) {
+    if (!vol || log2_units < 0 || log2_units > 8)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] shard block must be 2^0 .. 2^8 units per axis");
+    int nu = 0;
+    OT_HIP_TRY(hipMemcpy(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost));
+    if (nu != 0 || !vol->pending.empty())
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] set the shard before the first integrate");
+    vol->dev.shard_shift = log2_units;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_border_destinations(const ot_tsdf* vol, int64_t n, const int32_t* keys, int64_t* dest_mask,
+                                      void* stream) {
+    if (!vol || n < 0 || (n > 0 && (!keys || !dest_mask)) || vol->dev.shard_world > 64)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] border_destinations: invalid arguments");
+    if (n == 0) return OT_OK;
+    hipLaunchKernelGGL(k_border_dest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(stream), vol->dev, n, keys,
+                       (unsigned long long*)dest_mask);
+    OT_LAUNCH_CHECK();
     return OT_OK;
 }
 

@@ -150,18 +150,45 @@ def merge_shard_meshes(parts):
     return Vm, VCm, Tm[order].to(torch.int32)
 
 
+def exchange_rows(rows, dest_mask, group=None):
+    """Send each row to the ranks whose bit is set in its dest_mask (int64 bitmask per row) and return the rows this
+    rank receives, grouped by source rank (one all_to_all of counts, one all_to_all of rows: RCCL on nccl, through host
+    memory on gloo).  Single process: nothing to exchange."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return rows[:0]
+    if dist.get_backend(group) == "gloo" and rows.is_cuda:  # gloo collectives run through host memory
+        return exchange_rows(rows.cpu(), dest_mask.cpu(), group).to(rows.device)
+    world = dist.get_world_size(group)
+    idx = [torch.nonzero((dest_mask >> r) & 1).flatten() for r in range(world)]
+    send = torch.cat([rows[i] for i in idx]) if rows.shape[0] else rows
+    splits = torch.tensor([int(i.numel()) for i in idx], dtype=torch.int64, device=rows.device)
+    rsplits = torch.empty_like(splits)
+    dist.all_to_all_single(rsplits, splits, group=group)
+    rs = rsplits.cpu().tolist()
+    out = rows.new_empty((sum(rs), rows.shape[1]))
+    dist.all_to_all_single(out, send.contiguous(), output_split_sizes=rs, input_split_sizes=splits.cpu().tolist(),
+                           group=group)
+    return out
+
+
 def extract_sharded_mesh(volume, group=None):
     """Marching cubes of ONE object whose volume is spatially sharded over the ranks (ot_tsdf_set_shard), with a
-    border halo instead of whole units: every rank all-gathers the ranks' border rows (721 low-face
-    voxels per unit, ~1/5.7 of a unit), imports the ones its own units' cubes read (halo units), extracts the own
-    units' cubes, and the partial meshes are all-gathered and merged (merge_shard_meshes) into the unsharded
-    volume's mesh on every rank.  Returns (TriangleMesh, bytes of border rows this rank received)."""
+    border halo instead of whole units: every rank sends its border rows (721 low-face voxels per unit,
+    ~1/5.7 of a unit) only to the ranks owning one of the unit's -x/-y/-z neighbours (ot_tsdf_border_destinations;
+    ownership is by blocks of units, so most neighbours are local), imports the ones its own units' cubes read (halo
+    units), extracts the own units' cubes, and the partial meshes are all-gathered and merged (merge_shard_meshes)
+    into the unsharded volume's mesh on every rank.  Returns (TriangleMesh, bytes of border rows this rank
+    received)."""
     import torch
 
     from .geometry import TriangleMesh, _Arr
 
-    rows = pack_border(*volume.export_border())
-    allrows = all_gather_rows(rows, group)
+    keys, tsdf, weight, color = volume.export_border()
+    rows = pack_border(keys, tsdf, weight, color)
+    allrows = exchange_rows(rows, volume.border_destinations(keys), group)
     volume.import_border(*unpack_border(allrows))
     mesh, vk, tk = volume.extract_triangle_mesh(with_keys=True)
     V = mesh._v.dev()

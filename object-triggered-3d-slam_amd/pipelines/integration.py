@@ -178,6 +178,17 @@ class ScalableTSDFVolume:
         """Keep only the units owned by `rank` of `world` (spatial sharding of one object)."""
         L.call("ot_tsdf_set_shard", self._h, int(rank), int(world))
 
+    def set_shard_block(self, log2_units):
+        """Ownership granularity of a sharded volume (ot_tsdf_set_shard_block): 2^log2_units units per axis."""
+        L.call("ot_tsdf_set_shard_block", self._h, int(log2_units))
+
+    def border_destinations(self, keys):
+        """Per border-row key (export_border's keys), the int64 bitmask of the other ranks whose units read it."""
+        keys = D.to_device(keys, "int32")
+        out = D.empty((int(keys.shape[0]),), "int64")
+        L.call("ot_tsdf_border_destinations", self._h, int(keys.shape[0]), D.ptr(keys), D.ptr(out), D.stream_ptr())
+        return out
+
     def export_border(self):
         """This shard's border (ot_tsdf_export_border): per own unit keys (U,3) int32, tsdf/weight (U,721) f32,
         colour (U,721,3) in the volume's colour precision -- the low-face voxels that neighbouring units' marching

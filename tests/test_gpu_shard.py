@@ -184,3 +184,69 @@ def test_assemble_after_halo_extraction_bitexact(pkg, seq16, gpu):
     m1 = merged.extract_triangle_mesh()
     assert_bitwise(np.asarray(m1.vertices), np.asarray(m0.vertices), "assembled mesh vertices")
     assert_bitwise(np.asarray(m1.vertex_colors), np.asarray(m0.vertex_colors), "assembled mesh colours")
+
+
+def _halo_worker(rank, world, port, q):
+    import os
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    from conftest import PKG, ROOT
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg = importlib.import_module(PKG)
+        synth = importlib.import_module(PKG + ".synth")
+        D = importlib.import_module(PKG + ".distributed")
+        seq = synth.make_sequence(n_frames=16, frames=[0, 3, 7, 12])
+        vol = _integrate_p(pkg, seq, 0.005, (rank, world), 64)
+        keys, _, _, _ = vol.export_border()
+        mesh, got = D.extract_sharded_mesh(vol)
+        n_rows = torch.tensor([[int(keys.shape[0])]], dtype=torch.int64)
+        counts = D.all_gather_rows(n_rows).flatten().tolist()
+        row_bytes = (3 + 721 * 8) * 4  # pack_border row, float64 colour
+        allgather = (sum(counts) - counts[rank]) * row_bytes  # what the all-gather of every border row delivered
+        q.put((rank, mesh._v.dev().cpu().numpy(), mesh._t.dev().cpu().numpy(), mesh._vc.dev().cpu().numpy(), got,
+               allgather))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_exchange_ranks_bitexact(pkg, seq16, gpu, world):
+    """`world` ranks (gloo, sharing this GPU) each integrate one object's frames into their shard
+    (ownership by blocks of units), exchange border rows only with the ranks owning a -x/-y/-z neighbour
+    (distributed.exchange_rows: all_to_all), extract and merge: every rank's mesh equals the unsharded mesh bit for
+    bit, and each rank receives at most half the border bytes an all-gather of every row delivers."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    full = _integrate_p(pkg, seq16, 0.005, None, 64)
+    m0 = full.extract_triangle_mesh()
+    V0, T0, C0 = (np.asarray(a) for a in (m0.vertices, m0.triangles, m0.vertex_colors))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict((r, rest) for r, *rest in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        V, T, VC, got, allgather = out[r]
+        assert_bitwise(V, V0, f"rank {r} merged vertices")
+        assert_bitwise(T, T0, f"rank {r} merged triangles")
+        assert_bitwise(VC, C0, f"rank {r} merged colours")
+        assert got <= 0.5 * allgather, f"rank {r}: {got} border bytes received vs {allgather} by all-gather"
