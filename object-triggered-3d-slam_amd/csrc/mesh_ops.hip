@@ -196,42 +196,89 @@ __global__ __launch_bounds__(256) void k_chain_chunk(const ChainJob* __restrict_
     }
 }
 
-// one chunk in Open3D's order from s (lane 0, operands staged in LDS); CDF values stored coalesced
+// One chunk from the exact s in Open3D's order, by integer segments: inside the binade of s every element that is
+// not a tie, stays below 2^53 grid steps and keeps the running integer below 2^53 is one step of an integer prefix
+// sum (the whole wave at once); the first element that breaks this is added by one exact float64 add (s + a) and the
+// next segment starts after it.  A chunk costs one wave prefix per binade crossing / tie / special value instead of
+// 256 dependent adds.  CDF values are stored as they are produced.
+__device__ inline long long wave_min_ll(long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const long long t = __shfl_xor(v, o);
+        v = t < v ? t : v;
+    }
+    return v;
+}
+
 template <bool CDF>
 __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, double* lds, int lane) {
+    (void)lds;
     double v[4];
     chunk_load4(j.x, j.n, b * CH, lane, v);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lds[4 * lane + k] = v[k];
-    __syncthreads();
     const int64_t base = b * CH;
     const int cnt = j.n - base < CH ? (int)(j.n - base) : CH;
-    if (lane == 0) {  // 8 staged operands read ahead of their dependent adds (one LDS round trip per 8)
-        double acc = s;
-        for (int k0 = 0; k0 < cnt; k0 += 8) {
-            double v[8];
+    int pos = 0;
+    while (pos < cnt) {  // wave-uniform
+        const int e = binade(s);
+        int stop = pos;
+        if (e != EX_NONE) {
+            const double scale = pow2(52 - e), u = pow2(e - 52);
+            const long long N = (long long)(s * scale);  // exact integer in [2^52, 2^53)
+            long long r[4], incl[4], loc = 0;
+            long long bad = CH;  // first element of this lane the integer step cannot take
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = lds[k0 + i];
+            for (int k = 0; k < 4; ++k) {
+                const int idx = 4 * lane + k;
+                const double m = v[k] * scale;  // exact: power-of-two scaling
+                const bool ok = m >= 0.0 && m < (double)R_MAX && m - floor(m) != 0.5;
+                const bool act = idx >= pos && idx < cnt;
+                r[k] = (act && ok) ? (long long)rint(m) : 0;
+                if (act && !ok && bad == CH) bad = idx;
+                if (idx >= cnt && bad == CH) bad = idx;
+            }
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (k0 + i < cnt) {
-                    acc = v[i] + acc;
-                    if (CDF) lds[k0 + i] = acc;
+            for (int k = 0; k < 4; ++k) {
+                loc += r[k];
+                incl[k] = loc;
+            }
+            long long pre = loc;  // inclusive wave prefix of the lanes' totals
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const long long t = __shfl_up(pre, d);
+                if (lane >= d) pre += t;
+            }
+            const long long excl = pre - loc;
+            const long long first_bad = wave_min_ll(bad);
+            long long cross = CH;  // first element whose running integer leaves the binade
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                incl[k] += excl;
+                const int idx = 4 * lane + k;
+                if (idx >= pos && idx < first_bad && N + incl[k] > R_MAX - 1 && cross == CH) cross = idx;
+            }
+            const long long first_cross = wave_min_ll(cross);
+            stop = (int)(first_bad < first_cross ? first_bad : first_cross);
+            stop = stop < cnt ? stop : cnt;
+            if (stop > pos) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int idx = 4 * lane + k;
+                    if (CDF && idx >= pos && idx < stop) j.out[base + idx] = (double)(N + incl[k]) * u;
                 }
+                const int last = stop - 1;
+                const long long mine = (last & 3) == 0 ? incl[0] : (last & 3) == 1 ? incl[1] : (last & 3) == 2 ? incl[2] : incl[3];
+                s = (double)(N + __shfl(mine, last >> 2)) * u;
+            }
         }
-        lds[CH] = acc;
-    }
-    __syncthreads();
-    const double out = lds[CH];
-    if (CDF) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t i = base + 4 * lane + k;
-            if (i < j.n) j.out[i] = lds[4 * lane + k];
+        if (stop < cnt) {  // one exact float64 add, in Open3D's order
+            const double mine = (stop & 3) == 0 ? v[0] : (stop & 3) == 1 ? v[1] : (stop & 3) == 2 ? v[2] : v[3];
+            s = __shfl(mine, stop >> 2) + s;
+            if (CDF && lane == 0) j.out[base + stop] = s;
+            ++stop;
         }
+        pos = stop;
     }
-    __syncthreads();
-    return out;
+    return s;
 }
 
 // one block per chain: run heads (b == 0, guessed binade changes, a flagged chunk or the chunk after one), the
@@ -241,56 +288,84 @@ __device__ inline bool run_head(const ChainJob& j, int64_t b) {
     return b == 0 || j.kind[b] != 0 || j.kind[b - 1] != 0 || j.ex[b] != j.ex[b - 1];
 }
 
-__global__ __launch_bounds__(256) void k_chain_runs(const ChainJob* __restrict__ jobs) {
-    __shared__ long long s_val[256];
-    __shared__ int s_head[256];
-    __shared__ int s_first[256];
+// segmented (flag, value) combine of the run prefix: a head restarts the sum; sums saturate at 2^53
+__device__ inline long long sat_add(long long a, long long b) {
+    const long long c = a + b;  // both <= 2^53: no overflow
+    return c < R_MAX ? c : R_MAX;
+}
+
+__global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict__ jobs) {
+    __shared__ long long s_wv[16];
+    __shared__ int s_wh[16];
+    __shared__ long long s_cin[16];
+    __shared__ int s_wn[16];
+    __shared__ int s_nin[16];
+    __shared__ long long s_carry;
+    __shared__ int s_next;
     const ChainJob j = jobs[blockIdx.x];
-    const int t = threadIdx.x;
-    const int64_t nb = (j.n + CH - 1) / CH, per = (nb + 255) / 256;
-    const int64_t lo = t * per, hi = lo + per < nb ? lo + per : nb;
-    long long acc = 0;
-    int has_head = 0, first = 0x7FFFFFFF;
-    for (int64_t b = lo; b < hi; ++b) {
-        if (run_head(j, b)) {
-            acc = 0;
-            has_head = 1;
-            first = first < (int)b ? first : (int)b;
-        }
-        acc = acc + j.msum[b];
-        acc = acc < R_MAX ? acc : R_MAX;
-    }
-    s_val[t] = acc;
-    s_head[t] = has_head;
-    s_first[t] = first;
-    __syncthreads();
-    if (t == 0) {  // carries: 256 serial steps over the threads' summaries (one block, a few microseconds)
-        long long c = 0;
-        for (int i = 0; i < 256; ++i) {
-            const long long v = s_val[i];
-            const int h = s_head[i];
-            s_val[i] = c;  // carry into thread i
-            c = h ? v : (c + v < R_MAX ? c + v : R_MAX);
-        }
-        int nxt = (int)nb;  // first head after thread i's range
-        for (int i = 255; i >= 0; --i) {
-            const int f = s_first[i];
-            s_first[i] = nxt;
-            nxt = f < nxt ? f : nxt;
-        }
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t nb = (j.n + CH - 1) / CH;
+    if (t == 0) {
+        s_carry = 0;
+        s_next = (int)nb;
     }
     __syncthreads();
-    acc = s_val[t];
-    for (int64_t b = lo; b < hi; ++b) {
-        if (run_head(j, b)) acc = 0;
-        acc = acc + j.msum[b];
-        acc = acc < R_MAX ? acc : R_MAX;
-        j.pre[b] = acc;
+    // forward: inclusive prefix of msum inside each run, tile by tile (wave scan by shuffles, 16 wave totals by one wave)
+    for (int64_t t0 = 0; t0 < nb; t0 += 1024) {
+        const int64_t b = t0 + t;
+        const bool in = b < nb;
+        int h = in ? (run_head(j, b) ? 1 : 0) : 1;
+        long long v = in ? j.msum[b] : 0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const long long tv = __shfl_up(v, d);
+            const int th = __shfl_up(h, d);
+            if (lane >= d) {
+                v = h ? v : sat_add(tv, v);
+                h = h | th;
+            }
+        }
+        if (lane == 63) {
+            s_wv[w] = v;
+            s_wh[w] = h;
+        }
+        __syncthreads();
+        if (t == 0) {  // carry into each wave: 16 serial combines
+            long long c = s_carry;
+            for (int i = 0; i < 16; ++i) {
+                s_cin[i] = c;
+                c = s_wh[i] ? s_wv[i] : sat_add(c, s_wv[i]);
+            }
+            s_carry = c;
+        }
+        __syncthreads();
+        if (in) j.pre[b] = h ? v : sat_add(s_cin[w], v);
+        __syncthreads();
     }
-    int nxt = s_first[t];
-    for (int64_t b = hi - 1; b >= lo; --b) {
-        j.rend[b] = nxt - 1;
-        if (run_head(j, b)) nxt = (int)b;
+    // backward: every chunk's run end = (first head after it) - 1, tile by tile from the end (suffix minimum)
+    const int64_t tiles = (nb + 1023) / 1024;
+    for (int64_t q = tiles - 1; q >= 0; --q) {
+        const int64_t b = q * 1024 + t;
+        int nx = (b + 1 < nb && run_head(j, b + 1)) ? (int)(b + 1) : 0x7FFFFFFF;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int tv = __shfl_down(nx, d);
+            if (lane + d < 64) nx = tv < nx ? tv : nx;
+        }
+        if (lane == 0) s_wn[w] = nx;
+        __syncthreads();
+        if (t == 0) {
+            int c = s_next;
+            for (int i = 15; i >= 0; --i) {
+                s_nin[i] = c;
+                c = s_wn[i] < c ? s_wn[i] : c;
+            }
+            s_next = c;
+        }
+        __syncthreads();
+        const int nxt = nx < s_nin[w] ? nx : s_nin[w];
+        if (b < nb) j.rend[b] = nxt - 1;
+        __syncthreads();
     }
 }
 
@@ -403,7 +478,7 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
     hipLaunchKernelGGL(k_chain_bsum, grid, dim3(256), 0, stream, djobs);
     hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(256), 0, stream, djobs);
     hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
-    hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(256), 0, stream, djobs);
+    hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
     hipLaunchKernelGGL(k_chain_walk<CDF>, dim3(n_jobs), dim3(64), 0, stream, djobs);
     if (CDF) hipLaunchKernelGGL(k_chain_emit, grid, dim3(256), 0, stream, djobs);
 }
