@@ -703,7 +703,10 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     ot_status st;
     int64_t K = 0;
     double* vox = nullptr;
-    if (vbits <= 32 && F <= 64) {  // 32-bit voxel keys, one sort segment per frame, pixel runs: 8 B per run per pass
+#ifndef OT_FB_RUNS
+#define OT_FB_RUNS 1
+#endif
+    if (OT_FB_RUNS && vbits <= 32 && F <= 64) {  // 32-bit voxel keys, one segment per frame, pixel runs: 8 B per run per pass
         unsigned* k32 = (unsigned*)kin;
         hipLaunchKernelGGL(k_fb_keys<unsigned>, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb, (const int*)d_tc,
                            k32, vin);
