@@ -12,9 +12,7 @@
 //   k_fb_setup    per frame: bounds -> voxel origin (min - vs/2), key widths; one block scans the tile counts
 //   k_fb_keys     the same pixels again: voxel key (frame | kx | ky | kz), written by stable compaction in pixel
 //                 (= point index) order, value = global pixel index
-//   pixel runs    (32-bit keys) consecutive points of a frame with one key and consecutive pixels -> one run (first
-//                 pixel, length): 1.5-1.8x fewer items to sort on the configs[2] stream
-//   radix sort    stable (one segment per frame) => every voxel's runs, and so its points, stay in point-index order
+//   radix sort    stable => every voxel's points stay in point-index order
 //   heads         voxel segment starts (stable compaction)
 //   k_fb_reduce   one lane per voxel: its points re-unprojected from the depth (no xyz/rgb intermediates in HBM),
 //                 summed in index order, divided by the count (Open3D AccumulatedPoint)
@@ -391,132 +389,15 @@ __global__ __launch_bounds__(256) void k_fb_gather(const int64_t* __restrict__ k
     oidx[t] = i - voff[lo];
 }
 
-// Pixel runs (u32-key path): consecutive points of one frame with the same voxel key and consecutive pixels form a run
-// (a voxel spans ~2-3 pixels of a row), so the voxel sort moves runs instead of points (1.5-1.8x fewer pairs on the
-// configs[2] stream).  A voxel's runs stay in point order under the stable sort, and a run's points are consecutive,
-// so the per-voxel sums still take the points in index order.
-struct RunHeadPred {
+// voxel heads of the segmented (u32-key) sort: a new key, or the first point of a frame
+struct SegHeadPred32 {
     const unsigned* keys;
-    const unsigned* pix;  // global pixel index per point
+    const unsigned* vals;
     unsigned npx;
     __device__ bool operator()(int64_t i) const {
-        return i == 0 || keys[i] != keys[i - 1] || pix[i] != pix[i - 1] + 1u || pix[i] / npx != pix[i - 1] / npx;
+        return i == 0 || keys[i] != keys[i - 1] || vals[i] / npx != vals[i - 1] / npx;
     }
 };
-struct RunEmit {
-    const unsigned* keys;
-    const unsigned* pix;
-    unsigned* rkey;    // run key
-    unsigned* ridx;    // run index (the sort value)
-    unsigned* rpix;    // first pixel (global index)
-    unsigned* rstart;  // first point
-    __device__ void operator()(int64_t i, int64_t pos) const {
-        rkey[pos] = keys[i];
-        ridx[pos] = (unsigned)pos;
-        rpix[pos] = pix[i];
-        rstart[pos] = (unsigned)i;
-    }
-};
-
-// run lengths from the run starts (in place: rstart -> length) and the per-frame first run (binary search on rpix)
-__global__ void k_fb_run_len(const unsigned* __restrict__ rstart, int64_t R, int64_t P, unsigned* __restrict__ rlen) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= R) return;
-    rlen[r] = (r + 1 < R ? rstart[r + 1] : (unsigned)P) - rstart[r];
-}
-
-__global__ void k_fb_run_frames(const unsigned* __restrict__ rpix, int64_t R, int npx, int F, int64_t* __restrict__ roff) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f > F) return;
-    int64_t lo = 0, hi = R;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int)(rpix[mid] / (unsigned)npx) < f) lo = mid + 1;
-        else hi = mid;
-    }
-    roff[f] = lo;
-}
-
-// voxel heads of the sorted runs: a new key, or a run of another frame
-struct RunVoxHeadPred {
-    const unsigned* keys;  // sorted run keys
-    const unsigned* vals;  // sorted run indices
-    const unsigned* rpix;
-    unsigned npx;
-    __device__ bool operator()(int64_t i) const {
-        return i == 0 || keys[i] != keys[i - 1] || rpix[vals[i]] / npx != rpix[vals[i - 1]] / npx;
-    }
-};
-
-// one lane per voxel: its runs (sorted run indices, in point order) and each run's consecutive pixels
-// re-unprojected and summed in index order
-__global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsigned* __restrict__ sval,
-                                                        const unsigned* __restrict__ rpix,
-                                                        const unsigned* __restrict__ rlen,
-                                                        const int* __restrict__ heads, int64_t K, int64_t R,
-                                                        double* __restrict__ vx, double* __restrict__ vc) {
-    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s >= K) return;
-    const int64_t beg = heads[s], end = (s + 1 < K) ? heads[s + 1] : R;
-    const int npx = p.w * p.h;
-    const unsigned g0 = rpix[sval[beg]];
-    const int f = (int)(g0 / (unsigned)npx);
-    double m[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
-    const uint16_t* dep = p.depth + (int64_t)f * npx;
-    const uint8_t* col = p.color + (int64_t)f * npx * 3;
-    double sp[3] = {0, 0, 0}, sc[3] = {0, 0, 0};
-    int64_t cnt = 0;
-    for (int64_t jr = beg; jr < end; ++jr) {
-        const unsigned r = sval[jr];
-        const int pix0 = (int)(rpix[r] - (unsigned)f * (unsigned)npx), len = (int)rlen[r];
-        cnt += len;
-        constexpr int VB = 4;  // a run's pixels in batches of 4: loads issued before the in-order sums
-        for (int j0 = 0; j0 < len; j0 += VB) {
-            float dd[VB];
-            unsigned cc[VB][3];
-#pragma unroll
-            for (int k = 0; k < VB; ++k) {
-                const int px = pix0 + (j0 + k < len ? j0 + k : j0);
-                dd[k] = (float)dep[px];
-                const uint8_t* cp = col + (int64_t)px * 3;
-                cc[k][0] = cp[0], cc[k][1] = cp[1], cc[k][2] = cp[2];
-            }
-#pragma unroll
-            for (int k = 0; k < VB; ++k) {
-                if (j0 + k >= len) break;
-                double xyz[3];
-                fb_point(p, m, div_rn(dd[k], p.scale_f, p.rscale_f), pix0 + j0 + k, xyz);  // valid by construction
-#pragma unroll
-                for (int a = 0; a < 3; ++a) sp[a] += xyz[a];
-                sc[0] += div_rn((double)cc[k][0], 255.0, 1.0 / 255.0);
-                sc[1] += div_rn((double)cc[k][1], 255.0, 1.0 / 255.0);
-                sc[2] += div_rn((double)cc[k][2], 255.0, 1.0 / 255.0);
-            }
-        }
-    }
-    const double cntd = (double)cnt, rc = 1.0 / cntd;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        vx[s * 3 + a] = div_rn(sp[a], cntd, rc);
-        vc[s * 3 + a] = div_rn(sc[a], cntd, rc);
-    }
-}
-
-// offs[f] = first voxel whose frame is >= f, voxels over sorted runs
-__global__ void k_fb_frame_offsets_runs(const unsigned* __restrict__ sval, const unsigned* __restrict__ rpix,
-                                        const int* __restrict__ heads, int64_t K, int npx, int F, int* __restrict__ offs) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f > F) return;
-    int64_t lo = 0, hi = K;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int)(rpix[sval[heads[mid]]] / (unsigned)npx) < f) lo = mid + 1;
-        else hi = mid;
-    }
-    offs[f] = (int)lo;
-}
 
 struct KeptEmit {
     int64_t* out;
@@ -559,7 +440,7 @@ struct ot_rgbd_filter {
     int F = 0;
     int64_t P = 0, K = 0, kept = 0;
     std::vector<int64_t> poff, voff, koff;  // host offsets [F + 1]
-    FbBuf b_frames, b_tiles, b_keys, b_vals, b_heads, b_vox, b_avg, b_out, b_misc, b_runs;
+    FbBuf b_frames, b_tiles, b_keys, b_vals, b_heads, b_vox, b_avg, b_out, b_misc;
     double* vx = nullptr;
     double* vc = nullptr;
     double* kx = nullptr;
@@ -702,54 +583,15 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     unsigned* vout = vin + P;
     ot_status st;
     int64_t K = 0;
-    double* vox = nullptr;
-#ifndef OT_FB_RUNS
-#define OT_FB_RUNS 1
-#endif
-    if (OT_FB_RUNS && vbits <= 32 && F <= 64) {  // 32-bit voxel keys, one segment per frame, pixel runs: 8 B per run per pass
+    if (vbits <= 32 && F <= 64) {  // 32-bit voxel keys, one sort segment per frame: 8 B per pair per pass
         unsigned* k32 = (unsigned*)kin;
+        unsigned* k32o = k32 + P;
         hipLaunchKernelGGL(k_fb_keys<unsigned>, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb, (const int*)d_tc,
                            k32, vin);
         OT_LAUNCH_CHECK();
-        // runs: key, index (sort value), first pixel, first point, length; sorted key / index; per-frame run offsets
-        unsigned* rkey = (unsigned*)fl->b_runs.get((size_t)P * 28 + (size_t)(F + 1) * 8 + 512);
-        if (!rkey) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
-        unsigned* rkey_o = rkey + P;
-        unsigned* ridx = rkey_o + P;
-        unsigned* ridx_o = ridx + P;
-        unsigned* rpix = ridx_o + P;
-        unsigned* rstart = rpix + P;
-        unsigned* rlen = rstart + P;
-        int64_t* d_roff = (int64_t*)(((uintptr_t)(rlen + P) + 63) & ~(uintptr_t)63);
-        int64_t R = 0;
-        st = compact(P, RunHeadPred{k32, vin, (unsigned)npx}, RunEmit{k32, vin, rkey, ridx, rpix, rstart}, stream, &R,
-                     7);  // sync 2
+        st = sort_segments_u32_u32(k32, k32o, vin, vout, fl->poff.data(), F, vbits, stream, 3);
         if (st != OT_OK) return st;
-        hipLaunchKernelGGL(k_fb_run_len, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream,
-                           (const unsigned*)rstart, R, P, rlen);
-        hipLaunchKernelGGL(k_fb_run_frames, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)rpix, R, npx, F,
-                           d_roff);
-        OT_LAUNCH_CHECK();
-        std::vector<int64_t> roff(F + 1);
-        OT_HIP_TRY(hipMemcpyAsync(roff.data(), d_roff, sizeof(int64_t) * (F + 1), hipMemcpyDeviceToHost, stream));
-        OT_HIP_TRY(hipStreamSynchronize(stream));  // sync 3: the sort's segments
-        st = sort_segments_u32_u32(rkey, rkey_o, ridx, ridx_o, roff.data(), F, vbits, stream, 3);
-        if (st != OT_OK) return st;
-        st = compact(R, RunVoxHeadPred{rkey_o, ridx_o, rpix, (unsigned)npx}, SegHeadEmit{heads}, stream, &K,
-                     7);  // sync 4
-        if (st != OT_OK) return st;
-        hipLaunchKernelGGL(k_fb_frame_offsets_runs, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)ridx_o,
-                           (const unsigned*)rpix, (const int*)heads, K, npx, F, d_voff);
-        fl->K = K;
-        // ---- voxel averages (frame-major, key order inside a frame) ------------------------------------------
-        vox = (double*)fl->b_vox.get((size_t)K * 48 + 256);
-        if (!vox) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
-        fl->vx = vox;
-        fl->vc = vox + K * 3;
-        hipLaunchKernelGGL(k_fb_reduce_runs, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
-                           (const unsigned*)ridx_o, (const unsigned*)rpix, (const unsigned*)rlen, (const int*)heads, K,
-                           R, fl->vx, fl->vc);
-        OT_LAUNCH_CHECK();
+        st = compact(P, SegHeadPred32{k32o, vout, (unsigned)npx}, SegHeadEmit{heads}, stream, &K, 7);  // sync 2
     } else {
         hipLaunchKernelGGL(k_fb_keys<unsigned long long>, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb,
                            (const int*)d_tc, kin, vin);
@@ -757,19 +599,19 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
         st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)P, end_bit, stream, 3);
         if (st != OT_OK) return st;
         st = compact(P, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises (sync 2)
-        if (st != OT_OK) return st;
-        hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)vout,
-                           (const int*)heads, K, npx, F, d_voff);
-        fl->K = K;
-        // ---- voxel averages (frame-major, key order inside a frame) ------------------------------------------
-        vox = (double*)fl->b_vox.get((size_t)K * 48 + 256);
-        if (!vox) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
-        fl->vx = vox;
-        fl->vc = vox + K * 3;
-        hipLaunchKernelGGL(k_fb_reduce, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
-                           (const unsigned*)vout, (const int*)heads, K, P, fl->vx, fl->vc);
-        OT_LAUNCH_CHECK();
     }
+    if (st != OT_OK) return st;
+    hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)vout,
+                       (const int*)heads, K, npx, F, d_voff);
+    fl->K = K;
+    // ---- voxel averages (frame-major, key order inside a frame) ----------------------------------------------
+    double* vox = (double*)fl->b_vox.get((size_t)K * 48 + 256);
+    if (!vox) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+    fl->vx = vox;
+    fl->vc = vox + K * 3;
+    hipLaunchKernelGGL(k_fb_reduce, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p, (const unsigned*)vout,
+                       (const int*)heads, K, P, fl->vx, fl->vc);
+    OT_LAUNCH_CHECK();
     std::vector<int> hvoff(F + 1);
     OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));
     // ---- statistical outlier removal over all frames' voxel clouds at once ----------------------------------
