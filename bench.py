@@ -217,8 +217,11 @@ def main():
         roofline["hbm_achieved"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9, 1)
         roofline["hbm_frac"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     ient, _ = _pmc_entry(args, L, kname, pmc_cfg)
-    if ient and ient.get("valu_busy_frac") is not None:  # the other ceiling: vector-ALU issue (PMC, same build)
-        roofline["valu_busy_frac"] = round(ient["valu_busy_frac"], 4)
+    if ient and ient.get("valu_busy_frac") is not None:  # the other ceilings: vector-ALU issue and the vector-memory
+        roofline["valu_busy_frac"] = round(ient["valu_busy_frac"], 4)  # address / data path (PMC, same build)
+    for key in ("ta_busy_frac", "td_busy_frac"):
+        if ient and ient.get(key) is not None:
+            roofline[key] = round(ient[key], 4)
     if ient:  # raw counters and the correction applied to them (calibrated on 8-B gathers, tools/fetch_calib.hip)
         roofline["traffic_raw"] = {k: ient.get(k) for k in ("raw_fetch_kib", "raw_write_kib", "fetch_correction",
                                                             "fetch_correction_source", "write_correction")}

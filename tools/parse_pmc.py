@@ -28,8 +28,9 @@ BASE_CFG = {"voxel": 0.005, "frames": 256, "batch": 0}
 
 def short_name(full):
     base = full.split("(")[0].split("::")[-1]
-    if base.startswith("k_batch_integrate<"):
-        return base
+    if base.startswith("k_batch_integrate<"):  # <C64, FAST>: the reciprocal-table kernel keeps the bench's name
+        args = [a.strip() for a in base[base.index("<") + 1:base.rindex(">")].split(",")]
+        return f"k_batch_integrate<{args[0]}>" + ("" if len(args) < 2 or args[1] == "true" else "[ieee]")
     return base.split("<")[0]
 
 
