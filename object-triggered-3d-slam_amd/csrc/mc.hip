@@ -510,9 +510,20 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     if (st != OT_OK) return st;
     m.vk = mb.vk;
     m.tk = mb.tk;
-    hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, stream, vol->dev, m, vol->voxel_length, mb.v,
+    // vertex positions / colours and triangle indices depend on the same edge bitmasks and bases but not on each
+    // other: the vertices run on the volume's side stream beside the triangles (fork / join by events)
+    if (!vol->side) {
+        OT_HIP_TRY(hipStreamCreateWithFlags(&vol->side, hipStreamNonBlocking));
+        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_fork, hipEventDisableTiming));
+        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_join, hipEventDisableTiming));
+    }
+    OT_HIP_TRY(hipEventRecord(vol->ev_fork, stream));
+    OT_HIP_TRY(hipStreamWaitEvent(vol->side, vol->ev_fork, 0));
+    hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, vol->side, vol->dev, m, vol->voxel_length, mb.v,
                        vol->color_type == OT_COLOR_RGB8 ? mb.c : nullptr);
+    OT_HIP_TRY(hipEventRecord(vol->ev_join, vol->side));
     hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, mb.t);
+    OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_join, 0));
     OT_LAUNCH_CHECK();  // the mesh is complete in stream order (fetch / normals / keys are ordered after it)
     mb.nv = nv;
     mb.nt = nt;

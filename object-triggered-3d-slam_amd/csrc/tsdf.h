@@ -30,6 +30,8 @@ constexpr int C_UNITS = 1;     // units allocated
 constexpr int C_OVERFLOW = 2;  // pool exhausted (units dropped)
 constexpr int C_HASHERR = 3;   // hash full or key out of range
 constexpr int C_BATCH_PAIRS = 4;  // (frame, unit) pairs of a batch: counters[4 + parity] (batches alternate, see k_batch_units)
+constexpr int C_KMAX = 8;   // [8, 11): max over allocated units of key_a + KEY_BIAS + 1 (0: no unit yet)
+constexpr int C_KNEG = 11;  // [11, 14): max over allocated units of KEY_BIAS - key_a + 1 (so min key_a = KEY_BIAS + 1 - it)
 constexpr int N_COUNTERS = 16;
 
 // stats[] slots (u64)
@@ -69,6 +71,17 @@ __host__ __device__ inline bool unit_owned(const TsdfDev& d, unsigned long long 
     int x, y, z;
     unpack_key(key, x, y, z);
     return unit_owner(d.shard_world, d.shard_shift, x, y, z) == d.shard_rank;
+}
+
+// a newly allocated unit widens the volume's key bounds (read back with the counters: the sorted-unit order packs keys
+// on their actual ranges without a bounds pass)
+__device__ inline void note_unit_key(const TsdfDev& d, int x, int y, int z) {
+    const int k[3] = {x, y, z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        atomicMax(&d.counters[C_KMAX + a], k[a] + KEY_BIAS + 1);
+        atomicMax(&d.counters[C_KNEG + a], KEY_BIAS - k[a] + 1);
+    }
 }
 
 // a unit's record: tsdf plane, weight plane, then the colour planes r, g, b (4096 each, voxel vi = z*256 + x*16 + y)
@@ -174,6 +187,9 @@ struct ot_tsdf {
     int sorted_frame = -1;
     // extracted mesh
     ot::MeshBuffers mesh;
+    // a second stream for independent extraction stages (vertex positions beside triangle indices), fork / join
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // kernel timing (events around the dominant integration kernel)
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;

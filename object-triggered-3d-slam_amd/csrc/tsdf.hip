@@ -121,6 +121,7 @@ __device__ inline void touch_unit(const TsdfDev& d, int frame, int x, int y, int
         d.unit_keys[id * 3 + 1] = y;
         d.unit_keys[id * 3 + 2] = z;
         fresh = 1;
+        note_unit_key(d, x, y, z);
     }
     const int pos = atomicAdd(&d.counters[C_TOUCHED], 1);
     d.touched[pos] = fresh ? (int)((unsigned)id | 0x80000000u) : id;
@@ -587,6 +588,7 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
                 d.unit_keys[id * 3 + 0] = kx;
                 d.unit_keys[id * 3 + 1] = ky;
                 d.unit_keys[id * 3 + 2] = kz;
+                note_unit_key(d, kx, ky, kz);
                 id |= (int)0x80000000u;
             }
         }
@@ -986,6 +988,7 @@ __global__ __launch_bounds__(256) void k_import_border(TsdfDev d, const int32_t*
                         d.unit_keys[id * 3 + 1] = y;
                         d.unit_keys[id * 3 + 2] = z;
                         fresh = 1;
+                        note_unit_key(d, x, y, z);
                     }
                 }
             }
@@ -1101,6 +1104,7 @@ __global__ __launch_bounds__(256) void k_import(TsdfDev d, const int32_t* __rest
                         d.unit_keys[id * 3 + 0] = x;
                         d.unit_keys[id * 3 + 1] = y;
                         d.unit_keys[id * 3 + 2] = z;
+                        note_unit_key(d, x, y, z);
                     }
                 }
             }
@@ -1120,33 +1124,6 @@ __global__ __launch_bounds__(256) void k_import(TsdfDev d, const int32_t* __rest
         cbase[vi] = color ? color[o * 3 + 0] : (CT)0;
         cbase[UNIT_VOX + vi] = color ? color[o * 3 + 1] : (CT)0;
         cbase[2 * UNIT_VOX + vi] = color ? color[o * 3 + 2] : (CT)0;
-    }
-}
-
-// per-axis min / max of the unit keys (one workgroup; a few thousand units)
-__global__ __launch_bounds__(256) void k_unit_bounds(TsdfDev d, int n, int* out6) {
-    __shared__ int mn[3], mx[3];
-    if (threadIdx.x < 3) {
-        mn[threadIdx.x] = 0x7FFFFFFF;
-        mx[threadIdx.x] = -0x7FFFFFFF;
-    }
-    __syncthreads();
-    int lo[3] = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF}, hi[3] = {-0x7FFFFFFF, -0x7FFFFFFF, -0x7FFFFFFF};
-    for (int i = threadIdx.x; i < n; i += 256)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = min(lo[a], d.unit_keys[i * 3 + a]);
-            hi[a] = max(hi[a], d.unit_keys[i * 3 + a]);
-        }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        atomicMin(&mn[a], lo[a]);
-        atomicMax(&mx[a], hi[a]);
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        out6[threadIdx.x] = mn[threadIdx.x];
-        out6[3 + threadIdx.x] = mx[threadIdx.x];
     }
 }
 
@@ -1464,14 +1441,14 @@ ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) 
     if (nu > 0) {
         char* ws = (char*)scratch((size_t)nu * 24 + 256, 5);
         if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-        int* b6 = (int*)ws;
         unsigned long long* kin = (unsigned long long*)(ws + 256);
         unsigned long long* kout = kin + nu;
         unsigned* vin = (unsigned*)(kout + nu);
-        hipLaunchKernelGGL(k_unit_bounds, dim3(1), dim3(256), 0, stream, vol->dev, nu, b6);
-        int hb[6];
-        OT_HIP_TRY(hipMemcpyAsync(hb, b6, sizeof(hb), hipMemcpyDeviceToHost, stream));
-        OT_HIP_TRY(hipStreamSynchronize(stream));
+        int hb[6];  // per-axis key bounds, kept by the allocating kernels (note_unit_key)
+        for (int a = 0; a < 3; ++a) {
+            hb[a] = KEY_BIAS + 1 - c[C_KNEG + a];
+            hb[3 + a] = c[C_KMAX + a] - KEY_BIAS - 1;
+        }
         int bits[3];
         for (int a = 0; a < 3; ++a) {
             const long long span = (long long)hb[3 + a] - hb[a];
@@ -1568,6 +1545,9 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (v->hbframes) (void)hipHostFree(v->hbframes);
+    if (v->ev_fork) (void)hipEventDestroy(v->ev_fork);
+    if (v->ev_join) (void)hipEventDestroy(v->ev_join);
+    if (v->side) (void)hipStreamDestroy(v->side);
     for (hipEvent_t ev : v->hb_event)
         if (ev) (void)hipEventDestroy(ev);
     delete v;
