@@ -79,6 +79,18 @@ __host__ __device__ inline unsigned long long mix64(unsigned long long z) {
     return z ^ (z >> 31);
 }
 
+// the frame holding element i of frame-major data with segment starts foff[0 .. nframes): the last f with
+// foff[f] <= i (empty frames are skipped over)
+__device__ inline int frame_of(const int* __restrict__ foff, int nframes, int64_t i) {
+    int lo = 0, hi = nframes;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (foff[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // fl(x / y) without a division, from r = fl(1 / y): q0 = fl(x r) lies within an ulp of x / y and r within half an
 // ulp of 1 / y, so fl(q0 + fl(x - q0 y) r) is the correctly rounded quotient (Markstein; both fma's exact in the
 // remainder) barring over/underflow, which the callers' ranges (pixel coordinates, depths, colours, counts) exclude.

@@ -10,12 +10,14 @@
 //   k_fb_pixels   tile of 2048 pixels of one frame: depth -> float (Open3D ConvertDepthToFloatImage), unprojection
 //                 of the valid pixels in float64 (camera_pose = inverse(extrinsic)), per-tile bounds + valid count
 //   k_fb_setup    per frame: bounds -> voxel origin (min - vs/2), key widths; one block scans the tile counts
-//   k_fb_keys     the same pixels again: voxel key (frame | kx | ky | kz), written by stable compaction in pixel
-//                 (= point index) order, value = global pixel index
+//   k_fb_keys     the same pixels again: voxel key (kx | ky | kz, one sort segment per frame), written by stable
+//                 compaction in pixel (= point index) order, value = point index, and the point's 8-B record (pixel,
+//                 raw depth, RGB8) at that index (the u64-key fallback for huge grids / batches: frame in the key,
+//                 value = global pixel index)
 //   radix sort    stable => every voxel's points stay in point-index order
 //   heads         voxel segment starts (stable compaction)
-//   k_fb_reduce   one lane per voxel: its points re-unprojected from the depth (no xyz/rgb intermediates in HBM),
-//                 summed in index order, divided by the count (Open3D AccumulatedPoint)
+//   k_fb_reduce   one lane per voxel: its points re-unprojected from their records (no xyz/rgb intermediates in HBM,
+//                 one 8-B gather per point), summed in index order, divided by the count (Open3D AccumulatedPoint)
 //   SOR           grid.h over all frames' voxel clouds at once (frame in the key's top bits) + sor_frames
 //   keep          stable compaction of avg > 0 && avg < threshold_f; rows gathered per frame
 #include <algorithm>
@@ -36,7 +38,7 @@ struct FbFrame {  // per-frame constants (device table)
     double pose[16];    // inverse(extrinsic), row-major
     double vmin[3];     // voxel grid origin: min_bound - vs / 2
     int err;
-    int pad;
+    int tag;            // u32-key chain: parity of the frame's rank among the batch's non-empty frames
 };
 
 struct FbParams {
@@ -80,25 +82,67 @@ __device__ inline double floor_div(double a, double b, double inv_b) {
     return floor(a / b);
 }
 
-// the lane's 8 depth values as Open3D's float image: f = (float)u16 / (float)scale; 0 when f >= trunc
-__device__ inline void fb_depth8(const FbParams& p, const uint16_t* __restrict__ dep, int pix0, int npx, float f[8]) {
+// the lane's 8 depth values as Open3D's float image: f = (float)u16 / (float)scale; 0 when f >= trunc (raw: the
+// u16 values themselves)
+__device__ inline void fb_depth8(const FbParams& p, const uint16_t* __restrict__ dep, int pix0, int npx, float f[8],
+                                 unsigned raw[8]) {
     if (pix0 + FB_PIX <= npx && ((reinterpret_cast<uintptr_t>(dep + pix0) & 15) == 0)) {
-        const uint4 raw = *reinterpret_cast<const uint4*>(dep + pix0);
-        const uint32_t wd[4] = {raw.x, raw.y, raw.z, raw.w};
+        const uint4 r4 = *reinterpret_cast<const uint4*>(dep + pix0);
+        const uint32_t wd[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            f[2 * k] = (float)(wd[k] & 0xFFFFu);
-            f[2 * k + 1] = (float)(wd[k] >> 16);
+            raw[2 * k] = wd[k] & 0xFFFFu;
+            raw[2 * k + 1] = wd[k] >> 16;
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < FB_PIX; ++k) f[k] = pix0 + k < npx ? (float)dep[pix0 + k] : 0.0f;
+        for (int k = 0; k < FB_PIX; ++k) raw[k] = pix0 + k < npx ? (unsigned)dep[pix0 + k] : 0u;
     }
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
-        f[k] = div_rn(f[k], p.scale_f, p.rscale_f);
+        f[k] = div_rn((float)raw[k], p.scale_f, p.rscale_f);
         if ((double)f[k] >= p.trunc) f[k] = 0.0f;
     }
+}
+__device__ inline void fb_depth8(const FbParams& p, const uint16_t* __restrict__ dep, int pix0, int npx, float f[8]) {
+    unsigned raw[8];
+    fb_depth8(p, dep, pix0, npx, f, raw);
+}
+
+// the lane's 8 RGB8 pixels as 24-bit words (r | g << 8 | b << 16): three 8-B loads when the 24 bytes are aligned
+__device__ inline void fb_color8(const uint8_t* __restrict__ col, int pix0, int npx, unsigned rgb[8]) {
+    const uint8_t* c = col + (int64_t)pix0 * 3;
+    if (pix0 + FB_PIX <= npx && ((reinterpret_cast<uintptr_t>(c) & 7) == 0)) {
+        const uint2* c8 = reinterpret_cast<const uint2*>(c);
+        const uint2 a = c8[0], b = c8[1], d = c8[2];
+        const unsigned long long w0 = ((unsigned long long)a.y << 32) | a.x, w1 = ((unsigned long long)b.y << 32) | b.x,
+                                 w2 = ((unsigned long long)d.y << 32) | d.x;
+        rgb[0] = (unsigned)(w0 & 0xFFFFFF);
+        rgb[1] = (unsigned)((w0 >> 24) & 0xFFFFFF);
+        rgb[2] = (unsigned)(((w0 >> 48) | (w1 << 16)) & 0xFFFFFF);
+        rgb[3] = (unsigned)((w1 >> 8) & 0xFFFFFF);
+        rgb[4] = (unsigned)((w1 >> 32) & 0xFFFFFF);
+        rgb[5] = (unsigned)(((w1 >> 56) | (w2 << 8)) & 0xFFFFFF);
+        rgb[6] = (unsigned)((w2 >> 16) & 0xFFFFFF);
+        rgb[7] = (unsigned)(w2 >> 40);
+    } else {
+#pragma unroll
+        for (int k = 0; k < FB_PIX; ++k)
+            rgb[k] = pix0 + k < npx ? (unsigned)c[3 * k] | ((unsigned)c[3 * k + 1] << 8) | ((unsigned)c[3 * k + 2] << 16)
+                                    : 0u;
+    }
+}
+
+// a valid point of the u32-key chain as one 8-B record, written in point order by k_fb_keys so the voxel reduce
+// gathers one word per point instead of a depth and three colour bytes: pixel within its frame (24 bits), raw depth
+// (16), RGB8 (24)
+constexpr int FB_PACK_PIX_BITS = 24;
+#ifndef OT_FB_PACK
+#define OT_FB_PACK 1
+#endif
+__device__ inline unsigned long long fb_pack(unsigned pix, unsigned raw_depth, unsigned rgb) {
+    return (unsigned long long)pix | ((unsigned long long)raw_depth << FB_PACK_PIX_BITS) |
+           ((unsigned long long)rgb << (FB_PACK_PIX_BITS + 16));
 }
 
 // per tile: valid count and bounds (order-preserving u64 encodings) of the valid pixels' points
@@ -239,13 +283,21 @@ __global__ __launch_bounds__(256) void k_fb_setup(FbParams p, int* __restrict__ 
 struct FbKeys {
     unsigned long long ny, nz;
     int vbits;
+    int tag;  // u32 keys: the frame tag in bit 31 (vbits <= 31), so that adjacent frames' keys always differ
 };
 
 // the tile again: voxel keys of the valid pixels, emitted in pixel order at the tile's scanned offset.  KeyT = u64:
-// the frame in the key's top bits (one sort over the batch); u32: the voxel index only (segmented sort by frame)
-template <typename KeyT>
+// the frame in the key's top bits (one sort over the batch), value = global pixel index; u32: the voxel index only
+// (segmented sort by frame) with the frame's tag bit (FbKeys::tag) on top, and, PACKED, value = the point's own index
+// with its record (fb_pack) stored at that index, else value = global pixel index.  The workgroup's outputs are one
+// contiguous range: staged in LDS and stored with consecutive lanes on consecutive entries
+#ifndef OT_FB_STAGE
+#define OT_FB_STAGE 1
+#endif
+template <typename KeyT, bool PACKED>
 __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, const int* __restrict__ toff,
-                                                        KeyT* __restrict__ keys, unsigned* __restrict__ vals) {
+                                                        KeyT* __restrict__ keys, unsigned* __restrict__ vals,
+                                                        unsigned long long* __restrict__ packed) {
     const int f = blockIdx.y, tile = blockIdx.x;
     const int npx = p.w * p.h;
     const int pix0 = tile * FB_TILE + threadIdx.x * FB_PIX;
@@ -255,7 +307,9 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
     for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
     const double vmin[3] = {p.frames[f].vmin[0], p.frames[f].vmin[1], p.frames[f].vmin[2]};
     float d[FB_PIX];
-    fb_depth8(p, dep, pix0, npx, d);
+    unsigned raw[FB_PIX], rgb[FB_PIX];
+    fb_depth8(p, dep, pix0, npx, d, raw);
+    if (PACKED) fb_color8(p.color + (int64_t)f * npx * 3, pix0, npx, rgb);
     int c = 0;
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) c += (pix0 + k < npx && d[k] > 0.0f) ? 1 : 0;
@@ -270,9 +324,16 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
     __shared__ int wsum[4];
     if (lane == 63) wsum[wid] = inc;
     __syncthreads();
-    int pos = toff[(int64_t)f * p.tpf + tile] + inc - c;
-    for (int w = 0; w < wid; ++w) pos += wsum[w];
-    const unsigned long long fkey = sizeof(KeyT) == 8 ? (unsigned long long)f << kb.vbits : 0ull;
+    const int base = toff[(int64_t)f * p.tpf + tile];
+    int loc = inc - c;
+    for (int w = 0; w < wid; ++w) loc += wsum[w];
+    const unsigned long long fkey = sizeof(KeyT) == 8 ? (unsigned long long)f << kb.vbits
+                                                      : (unsigned long long)(kb.tag ? p.frames[f].tag : 0) << 31;
+#if OT_FB_STAGE
+    __shared__ KeyT s_key[FB_TILE];
+    __shared__ unsigned long long s_rec[PACKED ? FB_TILE : 1];
+    __shared__ unsigned s_val[PACKED ? 1 : FB_TILE];
+#endif
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
         double xyz[3];
@@ -280,24 +341,54 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
             long long kk[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
-            keys[pos] = (KeyT)(fkey | (((unsigned long long)kk[0] * kb.ny + (unsigned long long)kk[1]) * kb.nz +
-                                       (unsigned long long)kk[2]));
-            vals[pos] = (unsigned)((int64_t)f * npx + pix0 + k);
-            ++pos;
+            const KeyT key = (KeyT)(fkey | (((unsigned long long)kk[0] * kb.ny + (unsigned long long)kk[1]) * kb.nz +
+                                            (unsigned long long)kk[2]));
+#if OT_FB_STAGE
+            s_key[loc] = key;
+            if (PACKED) s_rec[loc] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k]);
+            else s_val[loc] = (unsigned)((int64_t)f * npx + pix0 + k);
+#else
+            const int pos = base + loc;
+            keys[pos] = key;
+            if (PACKED) {
+                vals[pos] = (unsigned)pos;
+                packed[pos] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k]);
+            } else {
+                vals[pos] = (unsigned)((int64_t)f * npx + pix0 + k);
+            }
+#endif
+            ++loc;
         }
     }
+#if OT_FB_STAGE
+    __syncthreads();
+    const int n = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    for (int i = threadIdx.x; i < n; i += FB_THREADS) {
+        keys[base + i] = s_key[i];
+        if (PACKED) {
+            vals[base + i] = (unsigned)(base + i);
+            packed[base + i] = s_rec[i];
+        } else {
+            vals[base + i] = s_val[i];
+        }
+    }
+#endif
 }
 
-// one lane per voxel: its points (sorted values = global pixel indices, in index order) re-unprojected and summed
+// one lane per voxel: its points (sorted values, in index order) re-unprojected and summed.  PACKED: values are
+// point indices into the fb_pack records and the voxel's frame is found in the point offsets poff[0 .. F); else
+// values are global pixel indices into the depth / colour images
+template <bool PACKED>
 __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* __restrict__ sval,
-                                                   const int* __restrict__ heads, int64_t K, int64_t P,
-                                                   double* __restrict__ vx, double* __restrict__ vc) {
+                                                   const unsigned long long* __restrict__ packed,
+                                                   const int* __restrict__ poff, const int* __restrict__ heads,
+                                                   int64_t K, int64_t P, double* __restrict__ vx,
+                                                   double* __restrict__ vc) {
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (s >= K) return;
     const int64_t beg = heads[s], end = (s + 1 < K) ? heads[s + 1] : P;
     const int npx = p.w * p.h;
-    const unsigned g0 = sval[beg];
-    const int f = (int)(g0 / (unsigned)npx);
+    const int f = PACKED ? frame_of(poff, p.F, beg) : (int)(sval[beg] / (unsigned)npx);
     double m[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
@@ -308,15 +399,28 @@ __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* _
     constexpr int VB = 4;
     for (int64_t j0 = beg; j0 < end; j0 += VB) {
         int pix[VB];
-#pragma unroll
-        for (int k = 0; k < VB; ++k) pix[k] = (int)(sval[j0 + k < end ? j0 + k : j0] - (unsigned)f * (unsigned)npx);
         float dd[VB];
         unsigned cc[VB][3];
+        if (PACKED) {
+            unsigned long long rec[VB];
 #pragma unroll
-        for (int k = 0; k < VB; ++k) {
-            dd[k] = (float)dep[pix[k]];
-            const uint8_t* cp = col + (int64_t)pix[k] * 3;
-            cc[k][0] = cp[0], cc[k][1] = cp[1], cc[k][2] = cp[2];
+            for (int k = 0; k < VB; ++k) rec[k] = packed[sval[j0 + k < end ? j0 + k : j0]];
+#pragma unroll
+            for (int k = 0; k < VB; ++k) {
+                pix[k] = (int)(rec[k] & ((1u << FB_PACK_PIX_BITS) - 1));
+                dd[k] = (float)(unsigned)((rec[k] >> FB_PACK_PIX_BITS) & 0xFFFFu);
+                const unsigned rgb = (unsigned)(rec[k] >> (FB_PACK_PIX_BITS + 16));
+                cc[k][0] = rgb & 0xFF, cc[k][1] = (rgb >> 8) & 0xFF, cc[k][2] = rgb >> 16;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < VB; ++k) pix[k] = (int)(sval[j0 + k < end ? j0 + k : j0] - (unsigned)f * (unsigned)npx);
+#pragma unroll
+            for (int k = 0; k < VB; ++k) {
+                dd[k] = (float)dep[pix[k]];
+                const uint8_t* cp = col + (int64_t)pix[k] * 3;
+                cc[k][0] = cp[0], cc[k][1] = cp[1], cc[k][2] = cp[2];
+            }
         }
 #pragma unroll
         for (int k = 0; k < VB; ++k) {
@@ -348,6 +452,26 @@ __global__ void k_fb_frame_offsets(const unsigned* __restrict__ sval, const int*
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
         if ((int)(sval[heads[mid]] / (unsigned)npx) < f) lo = mid + 1;
+        else hi = mid;
+    }
+    offs[f] = (int)lo;
+}
+
+// the same from the point offsets (segmented sort: frame f's points stay in [poff[f], poff[f + 1]), and each frame's
+// first point is a voxel head): offs[f] = first voxel whose head is >= poff[f]
+__global__ void k_fb_frame_offsets_seg(const int* __restrict__ poff, const int* __restrict__ heads, int64_t K, int F,
+                                       int* __restrict__ offs) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f > F) return;
+    if (f == F) {
+        offs[F] = (int)K;
+        return;
+    }
+    const int target = poff[f];
+    int64_t lo = 0, hi = K;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (heads[mid] < target) lo = mid + 1;
         else hi = mid;
     }
     offs[f] = (int)lo;
@@ -389,8 +513,23 @@ __global__ __launch_bounds__(256) void k_fb_gather(const int64_t* __restrict__ k
     oidx[t] = i - voff[lo];
 }
 
-// voxel heads of the segmented (u32-key) sort: a new key, or the first point of a frame
-struct SegHeadPred32 {
+// voxel heads of the segmented (u32-key) sort: a new key, or the first point of a frame.  With the frame tags in the
+// keys (FbKeys::tag) adjacent frames' keys always differ; otherwise the frame starts are looked up: in the point
+// offsets poff[0 .. F) (PACKED values = point indices) or from the values' global pixel indices
+struct SegHeadPredTag {
+    const unsigned* keys;
+    __device__ bool operator()(int64_t i) const { return i == 0 || keys[i] != keys[i - 1]; }
+};
+struct SegHeadPredPoff {
+    const unsigned* keys;
+    const int* poff;
+    int F;
+    __device__ bool operator()(int64_t i) const {
+        if (i == 0 || keys[i] != keys[i - 1]) return true;
+        return poff[frame_of(poff, F, i)] == i;
+    }
+};
+struct SegHeadPredPix {
     const unsigned* keys;
     const unsigned* vals;
     unsigned npx;
@@ -440,7 +579,7 @@ struct ot_rgbd_filter {
     int F = 0;
     int64_t P = 0, K = 0, kept = 0;
     std::vector<int64_t> poff, voff, koff;  // host offsets [F + 1]
-    FbBuf b_frames, b_tiles, b_keys, b_vals, b_heads, b_vox, b_avg, b_out, b_misc;
+    FbBuf b_frames, b_tiles, b_keys, b_vals, b_heads, b_vox, b_avg, b_out, b_misc, b_packed;
     double* vx = nullptr;
     double* vc = nullptr;
     double* kx = nullptr;
@@ -573,7 +712,7 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     while (vbits < 64 && std::ldexp(1.0, vbits) < cells) ++vbits;
     const int end_bit = vbits + fbits;
     if (end_bit > 63) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel grid exceeds 64-bit key packing");
-    const FbKeys kb{ny, nz, vbits};
+    const FbKeys kb{ny, nz, vbits, 0};
     // ---- voxel keys in point order, stable sort ------------------------------------------------------------
     unsigned long long* kin = (unsigned long long*)fl->b_keys.get((size_t)P * 16 + 256);
     unsigned* vin = (unsigned*)fl->b_vals.get((size_t)P * 8 + 256);
@@ -583,34 +722,66 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     unsigned* vout = vin + P;
     ot_status st;
     int64_t K = 0;
-    if (vbits <= 32 && F <= 64) {  // 32-bit voxel keys, one sort segment per frame: 8 B per pair per pass
+    const bool seg32 = vbits <= 32 && F <= 64;
+    const bool pack = seg32 && OT_FB_PACK && npx <= (1 << FB_PACK_PIX_BITS);
+    unsigned long long* packed = nullptr;
+    if (seg32) {  // 32-bit voxel keys, one sort segment per frame: 8 B per pair per pass
         unsigned* k32 = (unsigned*)kin;
         unsigned* k32o = k32 + P;
-        hipLaunchKernelGGL(k_fb_keys<unsigned>, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb, (const int*)d_tc,
-                           k32, vin);
+        FbKeys kt = kb;
+        kt.tag = vbits <= 31;
+        if (kt.tag) {  // frame tags: parity of each frame's rank among the non-empty frames (frame table re-sent)
+            int r = 0;
+            for (int f = 0; f < F; ++f) {
+                fl->h_frames[f].tag = r & 1;
+                r += fl->poff[f + 1] > fl->poff[f] ? 1 : 0;
+            }
+            OT_HIP_TRY(hipMemcpyAsync(d_frames, fl->h_frames, sizeof(FbFrame) * F, hipMemcpyHostToDevice, stream));
+        }
+        if (pack) {
+            packed = (unsigned long long*)fl->b_packed.get((size_t)P * 8 + 256);
+            if (!packed) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+            hipLaunchKernelGGL((k_fb_keys<unsigned, true>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kt,
+                               (const int*)d_tc, k32, vin, packed);
+        } else {
+            hipLaunchKernelGGL((k_fb_keys<unsigned, false>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kt,
+                               (const int*)d_tc, k32, vin, nullptr);
+        }
         OT_LAUNCH_CHECK();
         st = sort_segments_u32_u32(k32, k32o, vin, vout, fl->poff.data(), F, vbits, stream, 3);
         if (st != OT_OK) return st;
-        st = compact(P, SegHeadPred32{k32o, vout, (unsigned)npx}, SegHeadEmit{heads}, stream, &K, 7);  // sync 2
+        if (kt.tag) st = compact(P, SegHeadPredTag{k32o}, SegHeadEmit{heads}, stream, &K, 7);  // sync 2
+        else if (pack) st = compact(P, SegHeadPredPoff{k32o, d_poff, F}, SegHeadEmit{heads}, stream, &K, 7);
+        else st = compact(P, SegHeadPredPix{k32o, vout, (unsigned)npx}, SegHeadEmit{heads}, stream, &K, 7);
+        if (st != OT_OK) return st;
     } else {
-        hipLaunchKernelGGL(k_fb_keys<unsigned long long>, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb,
-                           (const int*)d_tc, kin, vin);
+        hipLaunchKernelGGL((k_fb_keys<unsigned long long, false>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb,
+                           (const int*)d_tc, kin, vin, nullptr);
         OT_LAUNCH_CHECK();
         st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)P, end_bit, stream, 3);
         if (st != OT_OK) return st;
         st = compact(P, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises (sync 2)
+        if (st != OT_OK) return st;
     }
-    if (st != OT_OK) return st;
-    hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)vout,
-                       (const int*)heads, K, npx, F, d_voff);
+    if (pack)
+        hipLaunchKernelGGL(k_fb_frame_offsets_seg, dim3((F + 64) / 64), dim3(64), 0, stream, (const int*)d_poff,
+                           (const int*)heads, K, F, d_voff);
+    else
+        hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)vout,
+                           (const int*)heads, K, npx, F, d_voff);
     fl->K = K;
     // ---- voxel averages (frame-major, key order inside a frame) ----------------------------------------------
     double* vox = (double*)fl->b_vox.get((size_t)K * 48 + 256);
     if (!vox) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
     fl->vx = vox;
     fl->vc = vox + K * 3;
-    hipLaunchKernelGGL(k_fb_reduce, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p, (const unsigned*)vout,
-                       (const int*)heads, K, P, fl->vx, fl->vc);
+    if (pack)
+        hipLaunchKernelGGL(k_fb_reduce<true>, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
+                           (const unsigned*)vout, (const unsigned long long*)packed, (const int*)d_poff,
+                           (const int*)heads, K, P, fl->vx, fl->vc);
+    else
+        hipLaunchKernelGGL(k_fb_reduce<false>, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
+                           (const unsigned*)vout, nullptr, nullptr, (const int*)heads, K, P, fl->vx, fl->vc);
     OT_LAUNCH_CHECK();
     std::vector<int> hvoff(F + 1);
     OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));

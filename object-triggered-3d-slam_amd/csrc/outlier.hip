@@ -27,16 +27,6 @@
 
 namespace ot {
 
-__device__ inline int frame_of(const int* __restrict__ foff, int nframes, int64_t i) {
-    int lo = 0, hi = nframes;  // last f with foff[f] <= i (empty frames are skipped over)
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (foff[mid] <= i) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
 __device__ inline int cell_coord(double v, double origin, double h) { return (int)floor((v - origin) / h); }
 
 __device__ inline bool cell_valid(const GridDev& g, int x, int y, int z) {
