@@ -178,7 +178,7 @@ ot_status ot_tsdf_flush(ot_tsdf* vol, void* stream);
 /* Frames queued on the host for the next batch (their input buffers are still referenced; every frame queued before
  * them has been enqueued on its stream).  Host-only, no synchronisation. */
 ot_status ot_tsdf_pending_frames(const ot_tsdf* vol, int32_t* n_host);
-/* Batch size used by ot_tsdf_integrate_u16 (1 = integrate immediately, default 32). */
+/* Batch size used by ot_tsdf_integrate_u16 (1 = integrate immediately, default and maximum 64). */
 ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames);
 
 /* Number of allocated volume units.  Queued frames are integrated first, on `stream`; synchronises `stream`. */

@@ -14,6 +14,7 @@
 //                    colour (f1*c0 + f0*c1)/(f0+f1) with c = colour/255 — Open3D's float64 expressions
 //   k_mc_triangles : per-lane triangle offsets by block scan; vertex ids by popcount lookups
 #include <atomic>
+#include <cstring>
 #include <mutex>
 #include "../../include/otslam_mc_tables.h"
 #include "compact.h"
@@ -489,12 +490,17 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     if (st != OT_OK) return st;
     st = exclusive_scan_i64(m.vert_cnt, m.vert_base, (size_t)U, stream, 15);
     if (st != OT_OK) return st;
-    long long tails[4];
-    OT_HIP_TRY(hipMemcpyAsync(&tails[0], m.tri_base + U - 1, 8, hipMemcpyDeviceToHost, stream));
-    OT_HIP_TRY(hipMemcpyAsync(&tails[1], m.tri_cnt + U - 1, 8, hipMemcpyDeviceToHost, stream));
-    OT_HIP_TRY(hipMemcpyAsync(&tails[2], m.vert_base + U - 1, 8, hipMemcpyDeviceToHost, stream));
-    OT_HIP_TRY(hipMemcpyAsync(&tails[3], m.vert_cnt + U - 1, 8, hipMemcpyDeviceToHost, stream));
-    OT_HIP_TRY(hipStreamSynchronize(stream));
+    long long tails[4];  // the scans' last bases and counts: one mailbox read-back
+    MailSrc ms;
+    ms.n = 8;
+    const long long* tp[4] = {m.tri_base + U - 1, m.tri_cnt + U - 1, m.vert_base + U - 1, m.vert_cnt + U - 1};
+    for (int i = 0; i < 4; ++i) {
+        ms.p[2 * i] = (const unsigned*)tp[i];
+        ms.p[2 * i + 1] = (const unsigned*)tp[i] + 1;
+    }
+    st = mail_words(vol, ms, stream);
+    if (st != OT_OK) return st;
+    std::memcpy(tails, vol->hmail, sizeof(tails));
     const int64_t nt = tails[0] + tails[1], nv = tails[2] + tails[3];
     if (nv > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] more than 2^31 vertices");
     int64_t capc = mb.cap_v;

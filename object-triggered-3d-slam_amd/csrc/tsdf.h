@@ -107,7 +107,8 @@ __host__ __device__ inline void border_voxel(int b, int& x, int& y, int& z) {
     else y = r - 15, z = 0;
 }
 
-constexpr int MAX_BATCH = 64;  // frames per fused launch (one bit each in fmask)
+constexpr int MAX_BATCH = 64;
+constexpr int OT_MAIL_WORDS = 64;  // frames per fused launch (one bit each in fmask)
 
 // per-frame parameters of a batch (device resident)
 struct BatchFrame {
@@ -169,12 +170,17 @@ struct ot_tsdf {
     float* depth_f = nullptr;
     int64_t depth_f_cap = 0;
     // batching of integrate_u16
-    int batch_max = 32;
+#ifndef OT_DEFAULT_BATCH
+#define OT_DEFAULT_BATCH 64
+#endif
+    int batch_max = OT_DEFAULT_BATCH;  // frames per fused launch (ot_tsdf_set_batch)
     std::vector<ot::PendingFrame> pending;
     void* batch_ws = nullptr;       // unused (kept for ABI of the struct layout)
     size_t batch_ws_bytes = 0;
     ot::BatchFrame* bframes = nullptr;     // device [MAX_BATCH]
     ot::BatchFrame* hbframes = nullptr;    // pinned host staging [2][MAX_BATCH]
+    unsigned* hmail = nullptr;             // pinned coherent host mailbox [OT_MAIL_WORDS]: small read-backs stored
+                                           // by a one-wave kernel (mail_words) instead of staged D2H copies
     hipEvent_t hb_event[2] = {nullptr, nullptr};
     int hb_next = 0;
     int batch_pc = ot::C_BATCH_PAIRS;      // pair counter of the next batch (alternates 4, 5)
@@ -200,5 +206,11 @@ struct ot_tsdf {
 namespace ot {
 // shared between tsdf.hip and mc.hip
 ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units);
+// small read-back: the 4-byte words at p[0 .. n) copied to vol->hmail by one kernel, then the stream synchronised
+struct MailSrc {
+    const unsigned* p[ot::OT_MAIL_WORDS];
+    int n;
+};
+ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream);
 ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream);
 }  // namespace ot

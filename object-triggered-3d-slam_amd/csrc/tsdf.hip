@@ -1417,6 +1417,21 @@ static ot_status counter_errors(const int* c) {
     return OT_OK;
 }
 
+// one wave copies n <= OT_MAIL_WORDS 4-byte words into the volume's pinned coherent mailbox (plain vector stores over
+// PCIe); the caller synchronises the stream and reads vol->hmail.  One launch replaces a staged D2H copy per value
+__global__ void k_mail_words(MailSrc s, unsigned* __restrict__ out) {
+    const int i = threadIdx.x;
+    if (i < s.n) out[i] = *s.p[i];
+}
+
+ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
+    if (s.n > OT_MAIL_WORDS) return fail(OT_ERR_INVALID_ARGUMENT, "mailbox overflow");
+    hipLaunchKernelGGL(k_mail_words, dim3(1), dim3(64), 0, stream, s, vol->hmail);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
+}
+
 static ot_status check_errors(ot_tsdf* vol, hipStream_t stream) {
     int c[N_COUNTERS];
     OT_HIP_TRY(hipMemcpyAsync(c, vol->dev.counters, sizeof(c), hipMemcpyDeviceToHost, stream));
@@ -1430,9 +1445,13 @@ static ot_status check_errors(ot_tsdf* vol, hipStream_t stream) {
 ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) {
     ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
-    int c[N_COUNTERS];  // error flags and the unit count in one read-back
-    OT_HIP_TRY(hipMemcpyAsync(c, vol->dev.counters, sizeof(c), hipMemcpyDeviceToHost, stream));
-    OT_HIP_TRY(hipStreamSynchronize(stream));
+    int c[N_COUNTERS];  // error flags and the unit count in one read-back (the pinned mailbox)
+    MailSrc ms;
+    ms.n = N_COUNTERS;
+    for (int i = 0; i < N_COUNTERS; ++i) ms.p[i] = (const unsigned*)vol->dev.counters + i;
+    st = mail_words(vol, ms, stream);
+    if (st != OT_OK) return st;
+    std::memcpy(c, vol->hmail, sizeof(c));
     st = counter_errors(c);
     if (st != OT_OK) return st;
     int nu = (int)std::min<int64_t>(c[C_UNITS], vol->max_units);
@@ -1525,6 +1544,8 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
     if ((e = hipMalloc(&v->bframes, sizeof(BatchFrame) * MAX_BATCH)) != hipSuccess) return cleanup(e);
     if ((e = hipHostMalloc(&v->hbframes, sizeof(BatchFrame) * MAX_BATCH * 2, hipHostMallocDefault)) != hipSuccess)
         return cleanup(e);
+    if ((e = hipHostMalloc(&v->hmail, sizeof(unsigned) * OT_MAIL_WORDS, hipHostMallocCoherent)) != hipSuccess)
+        return cleanup(e);
     ot_status st = ot_tsdf_reset(v);
     if (st != OT_OK) {
         ot_tsdf_destroy(v);
@@ -1545,6 +1566,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (v->hbframes) (void)hipHostFree(v->hbframes);
+    if (v->hmail) (void)hipHostFree(v->hmail);
     if (v->ev_fork) (void)hipEventDestroy(v->ev_fork);
     if (v->ev_join) (void)hipEventDestroy(v->ev_join);
     if (v->side) (void)hipStreamDestroy(v->side);

@@ -26,7 +26,7 @@ class ScalableTSDFVolume:
     volume_unit_resolution=16, depth_sampling_stride=4).
 
     Extra keyword arguments (not in Open3D): `max_units` (block-pool capacity in HBM), `batch_frames`
-    (frames queued per fused integration launch, default 32, max 64; 1 = integrate immediately; results are
+    (frames queued per fused integration launch, default and max 64; 1 = integrate immediately; results are
     bit-identical for any value: a batch applies its frames to each voxel in call order) and `color_precision`
     (64, the default: the running colour mean in float64 with exact division, Open3D's TSDFVoxel::color_ --
     bit-exact colours; 32: float32 state with one reciprocal per update, |rel| <= 1e-4, faster)."""

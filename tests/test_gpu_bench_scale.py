@@ -1,5 +1,5 @@
 """GPU parity at the benchmark's full size (BASELINE.json configs[1]): the 256-frame 640x480 synthetic scan bench.py
-times, integrated at 5 mm through the same C-ABI entry point (ot_tsdf_integrate_u16, 32-frame fused batches), is
+times, integrated at 5 mm through the same C-ABI entry point (ot_tsdf_integrate_u16, 64-frame fused batches by default), is
 bit-exact against the CPU oracle on every unit key, voxel weight and tsdf value, and the exact voxel-update /
 unit-integration counters agree (they are the `roofline` accounting's inputs).  Colours: bit-exact in float64 with
 colour precision 64 (Open3D's TSDFVoxel::color_), within 1e-4 with the float32 headline setting.

@@ -155,10 +155,12 @@ def test_tsdf_float_path_batched(pkg, O, gpu, synth, seq16):
     _compare_volumes(vol, ref)
 
 
-def test_tsdf_many_batches_5mm(pkg, O, gpu, synth):
-    """70 frames of a 70-frame ring at 5 mm: two 32-frame batches, one 6-frame batch; full 360 deg coverage."""
+@pytest.mark.parametrize("batch", [None, 32])
+def test_tsdf_many_batches_5mm(pkg, O, gpu, synth, batch):
+    """70 frames of a 70-frame ring at 5 mm: one 64-frame batch (the default) and a 6-frame one, or two 32-frame
+    batches and a 6-frame one; full 360 deg coverage."""
     depth, color, ext = synth.make_sequence(n_frames=70)
-    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005)
+    vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005, batch=batch)
     n = _compare_volumes(vol, ref)
     assert n > 3000
 
