@@ -77,6 +77,11 @@ ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int
 ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_neighbors, double std_ratio,
                      double* avg, double* stats, hipStream_t stream, int slot0);
 
+// The statistics half of sor_frames: from the mean kNN distances avg[0 .. n) (frame-major, d_foff / h_foff: device /
+// host frame offsets) to stats[f] = {mean, std, valid, threshold}.  Scratch slot `slot`.  Synchronises once.
+ot_status sor_stats_frames(const double* avg, const int* d_foff, const int* h_foff, int F, double std_ratio,
+                           double* stats, hipStream_t stream, int slot);
+
 // keep predicate of frame f's points: avg > 0 && avg < stats[f].threshold
 struct SorKeep {
     const double* avg;

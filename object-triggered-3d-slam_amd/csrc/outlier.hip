@@ -894,6 +894,15 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
     else OT_SOR_LAUNCH(64);
 #undef OT_SOR_LAUNCH
     OT_LAUNCH_CHECK();
+    return sor_stats_frames(avg, gb.g.foff, h_foff, F, std_ratio, stats, stream, slot0);
+}
+
+ot_status sor_stats_frames(const double* avg, const int* d_foff, const int* h_foff, int F, double std_ratio,
+                           double* stats, hipStream_t stream, int slot) {
+    int64_t max_n = 0;
+    for (int f = 0; f < F; ++f) max_n = std::max<int64_t>(max_n, h_foff[f + 1] - h_foff[f]);
+    const int64_t n = h_foff[F];
+    const int slot0 = slot;
     // the two sequential float64 sums per frame (exact chains): x values, chain jobs, valid counts, sums
     const int nvb = (int)std::max<int64_t>((max_n + 255) / 256, 1);
     size_t aux = 0;
@@ -916,11 +925,11 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
     ChainJob* djobs = (ChainJob*)cur;
     OT_HIP_TRY(hipMemcpyAsync(djobs, jobs.data(), sizeof(ChainJob) * F, hipMemcpyHostToDevice, stream));
     const dim3 vgrid((unsigned)nvb, (unsigned)F);
-    hipLaunchKernelGGL(k_sor_values, vgrid, dim3(256), 0, stream, (const double*)avg, gb.g.foff, 0,
+    hipLaunchKernelGGL(k_sor_values, vgrid, dim3(256), 0, stream, (const double*)avg, d_foff, 0,
                        (const double*)stats, x, vpart);
     launch_sum_chains(djobs, F, max_n, stream);
     hipLaunchKernelGGL(k_sor_valid, dim3(F), dim3(256), 0, stream, (const int*)vpart, nvb, (const double*)sums, stats);
-    hipLaunchKernelGGL(k_sor_values, vgrid, dim3(256), 0, stream, (const double*)avg, gb.g.foff, 1,
+    hipLaunchKernelGGL(k_sor_values, vgrid, dim3(256), 0, stream, (const double*)avg, d_foff, 1,
                        (const double*)stats, x, vpart);
     launch_sum_chains(djobs, F, max_n, stream);
     hipLaunchKernelGGL(k_sor_stats, dim3((unsigned)((F + 63) / 64)), dim3(64), 0, stream, F, (const double*)sums,

@@ -198,3 +198,27 @@ def test_batch_tiny_images_many_frames(pkg, O, synth, gpu):
         assert_bitwise(davg, avg, f"tiny-image mean kNN distances (frame {f})")
         _, ind = flt.frame(f)
         assert_bitwise(np.asarray(ind, np.int64), idx, f"tiny-image kept indices (frame {f})")
+
+
+def test_batch_far_clusters(pkg, O, synth, gpu):
+    """Voxel-column SOR (outlier.hip sor_voxel_frames) at its limits: a 4-voxel cluster 3.5 m behind a 30x30-pixel
+    patch needs neighbours beyond every bounded box (the whole-frame scan of stage 3), a frame of one cluster whose
+    columns run along the viewing axis (identity pose: long kz runs, the binary-searched windows), and a frame of a
+    single pixel (k > points)."""
+    intr_t = synth.REF_INTRINSICS_640
+    depth = np.zeros((3, 480, 640), np.uint16)
+    depth[0, 200:230, 300:330] = 1000
+    depth[0, 0:2, 0:2] = 4500
+    rng = np.random.default_rng(9)
+    depth[1, 100:160, 200:260] = rng.integers(800, 1400, (60, 60)).astype(np.uint16)  # a noisy slab in depth
+    depth[2, 240, 320] = 2000
+    color = rng.integers(0, 256, (3, 480, 640, 3)).astype(np.uint8)
+    ext = np.stack([np.eye(4)] * 3)
+    flt = _run_batch(pkg, intr_t, depth, color, ext, max_frames=3, trunc=5.0)
+    for f in range(3):
+        P, v, vc, avg, idx = _oracle_chain(O, depth[f], color[f], ext[f], intr_t)
+        down, davg = flt.voxel_cloud(f)
+        assert_bitwise(np.asarray(down.points).reshape(-1, 3), v.reshape(-1, 3), f"far-cluster voxels (frame {f})")
+        assert_bitwise(davg, avg, f"far-cluster mean kNN distances (frame {f})")
+        _, ind = flt.frame(f)
+        assert_bitwise(np.asarray(ind, np.int64), idx, f"far-cluster kept indices (frame {f})")

@@ -18,6 +18,7 @@ run() {  # run <dir> <counters> -- <cmd...>
   timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/$d -o run -- "$@" \
       > gpurun_out/$d.log 2>&1 || { echo "pass $d failed"; tail -5 gpurun_out/$d.log; exit 1; }
 }
+[ -x tools/fetch_calib ] || /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -o tools/fetch_calib tools/fetch_calib.hip || exit 1
 cal=(); dirs=()
 for i in 0 1; do
   run pmc_c_$i "${TRAFFIC[$i]}" -- ./tools/fetch_calib 1024; cal+=("gpurun_out/pmc_c_$i")
