@@ -506,6 +506,7 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
     intr_t = synth.REF_INTRINSICS_640
     W, H = intr_t[0], intr_t[1]
     intr = L.ot_intrinsics(W, H, *intr_t[2:])
+    intr_ref = C.byref(intr)
     dev = []
     for depth, color, ext in scans:
         dev.append((torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous(),
@@ -530,10 +531,10 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
             for j in range(t, len(dev), T):
                 vol, (d16, col, ext) = vols[j], dev[j]
                 vol.reset()
+                dp, cp, ep = d16.data_ptr(), col.data_ptr(), ext.ctypes.data  # plain int addresses per call
                 for k in range(ext.shape[0]):
-                    st = lib.ot_tsdf_integrate_u16(vol._h, C.c_void_p(d16.data_ptr() + k * npx * 2),
-                                                   C.c_void_p(col.data_ptr() + k * npx * 3), C.byref(intr),
-                                                   ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
+                    st = lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128,
+                                                   1000.0, 3.0, stream)
                     if st:
                         raise RuntimeError(lib.ot_last_error().decode())
                 mesh = vol.extract_triangle_mesh()
@@ -564,12 +565,13 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
         vol, (d16, col, ext) = vols[0], dev[0]
         s_ = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
+        dp, cp, ep = d16.data_ptr(), col.data_ptr(), ext.ctypes.data
+
         def one():
             vol.reset()
             for k in range(ext.shape[0]):
-                if lib.ot_tsdf_integrate_u16(vol._h, C.c_void_p(d16.data_ptr() + k * npx * 2),
-                                             C.c_void_p(col.data_ptr() + k * npx * 3), C.byref(intr),
-                                             ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, s_):
+                if lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128,
+                                             1000.0, 3.0, s_):
                     raise RuntimeError(lib.ot_last_error().decode())
             mesh = vol.extract_triangle_mesh()
             mesh.compute_vertex_normals()

@@ -112,13 +112,13 @@ class ScalableTSDFVolume:
             d16, scale, trunc = raw
             self._queued((d16, cdev))
             L.call("ot_tsdf_integrate_u16", self._h, D.ptr(d16), D.ptr(cdev), C.byref(intr),
-                   ext.ctypes.data_as(C.c_void_p), scale, trunc, D.stream_ptr())
+                   ext.ctypes.data, scale, trunc, D.stream_ptr())  # int address: data_as costs ~2 us a call
             self._release()
         else:
             ddev = depth.dev()
             self._queued((ddev, cdev))
             L.call("ot_tsdf_integrate", self._h, D.ptr(ddev), D.ptr(cdev), C.byref(intr),
-                   ext.ctypes.data_as(C.c_void_p), D.stream_ptr())
+                   ext.ctypes.data, D.stream_ptr())
             self._release()
 
     def flush(self):

@@ -30,6 +30,7 @@ vol = pkg.pipelines.integration.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc
 if len(sys.argv) > 1:
     vol.set_batch(int(sys.argv[1]))  # frames per fused launch
 s_ = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+dp, cp, ep, intr_ref = d16.data_ptr(), col.data_ptr(), ext.ctypes.data, C.byref(intr)
 phases = {}
 
 
@@ -44,8 +45,7 @@ def one(record):
     t = time.perf_counter()
     vol.reset()
     for k in range(ext.shape[0]):
-        lib.ot_tsdf_integrate_u16(vol._h, C.c_void_p(d16.data_ptr() + k * npx * 2), C.c_void_p(col.data_ptr() + k * npx * 3),
-                                  C.byref(intr), ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, s_)
+        lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128, 1000.0, 3.0, s_)
     t_calls = time.perf_counter()
     lib.ot_tsdf_flush(vol._h, s_)
     t = mark("integrate (64 calls + flush)", t)
