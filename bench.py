@@ -593,7 +593,10 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
             "frames_per_s": round(args.objects * args.object_frames / dt, 1), "ms": round(dt * 1e3, 3),
             "objects_per_rank": len(ids), "merged_points": int(merged.shape[0]), "merge": merge,
             "single_object_ms": single,
-            "single_object_note": "median of 5, object 0 of this rank on one stream, same pipeline, no merge"}
+            "single_object_note": "median of 5, object 0 of this rank on one stream, same pipeline, no merge",
+            # this run's objects time over one object's latency: the most an objects-over-GPUs run (one object per
+            # GPU) can gain over this one, before its merge
+            "objects_over_single": round(dt * 1e3 / single, 2) if single else None}
 
 
 def _merge_label(world):
