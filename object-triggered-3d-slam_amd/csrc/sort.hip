@@ -27,7 +27,7 @@ using BigSortConfig = rocprim::radix_sort_config<
     0>;
 
 // ------------------------------------------------------------------------------------------------------------
-// Own stable LSD radix sort (8-bit digits), P + 2 launches for P passes:
+// Own stable LSD radix sort (8- or 9-bit digits, whichever needs fewer passes), P + 2 launches for P passes:
 //   k_rs_upsweep  per-tile digit histograms of every pass at once (original order)
 //   k_rs_reduce   per pass and segment: digit totals over the segment's tiles (the upsweep zeroed them, its
 //                 look-back flags, tickets)
@@ -40,9 +40,18 @@ using BigSortConfig = rocprim::radix_sort_config<
 // rocPRIM's onesweep needs 3 + 3P launches (histogram memset, per pass a look-back memset and a block-id reset);
 // sorts up to RS_OWN_MAX pairs are launch-bound, so the launch count is their cost; larger unsegmented ones go to
 // rocPRIM.
-constexpr int RS_THREADS = 256;
-constexpr int RS_BINS = 256;
+// D-bit digits: 2^D bins and 2^D threads per tile (one digit per thread in the histogram, scan and look-back);
+// D = 8 (256 threads) or 9 (512 threads: a 25..27-bit key in 3 passes instead of 4)
+template <int D>
+struct Rs {
+    static constexpr int BINS = 1 << D;
+    static constexpr int THREADS = BINS;
+    static constexpr int WAVES = THREADS / 64;
+};
 constexpr int RS_MAXP = 8;
+#ifndef OT_SEGSORT_D9
+#define OT_SEGSORT_D9 1  // 9-bit digits (512-thread tiles) whenever they need fewer passes than 8-bit ones
+#endif
 constexpr int RS_MAXSEG = 64;
 constexpr unsigned RS_AGG = 1u << 30, RS_PREFIX = 2u << 30, RS_VAL = (1u << 30) - 1;
 // above this size rocPRIM's onesweep (1024-thread tiles) moves the data faster than these 2048-item tiles; below
@@ -70,11 +79,12 @@ __device__ inline int rs_segment(const RsSegs& sg, int tile) {
     return s;
 }
 
-template <typename KeyT, int RS_ITEMS>
-__global__ __launch_bounds__(RS_THREADS) void k_rs_upsweep(const KeyT* __restrict__ keys, RsSegs sg, RsPasses ps,
+template <typename KeyT, int RS_ITEMS, int D>
+__global__ __launch_bounds__(Rs<D>::THREADS) void k_rs_upsweep(const KeyT* __restrict__ keys, RsSegs sg, RsPasses ps,
                                                            unsigned* __restrict__ tile_hist, int ntiles,
                                                            unsigned* __restrict__ look, unsigned* __restrict__ tickets,
                                                            unsigned* __restrict__ totals) {
+    constexpr int RS_THREADS = Rs<D>::THREADS, RS_BINS = Rs<D>::BINS;
     constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
     __shared__ unsigned h[RS_MAXP][RS_BINS];
     const int tid = threadIdx.x;
@@ -120,11 +130,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_upsweep(const KeyT* __restric
     for (int p = 0; p < ps.np; ++p) tile_hist[((size_t)p * ntiles + blockIdx.x) * RS_BINS + tid] = h[p][tid];
 }
 
-__device__ inline unsigned block_exclusive_scan_256(unsigned v, unsigned* sh) {
+template <int BINS>
+__device__ inline unsigned block_exclusive_scan(unsigned v, unsigned* sh) {
     const int tid = threadIdx.x;
     sh[tid] = v;
     __syncthreads();
-    for (int d = 1; d < RS_BINS; d <<= 1) {
+    for (int d = 1; d < BINS; d <<= 1) {
         const unsigned o = tid >= d ? sh[tid - d] : 0u;
         __syncthreads();
         sh[tid] += o;
@@ -138,8 +149,10 @@ __device__ inline unsigned block_exclusive_scan_256(unsigned v, unsigned* sh) {
 // per pass and segment: digit totals over the segment's tiles; grid (passes * segments, RS_RED_BLOCKS), each block
 // sums every RS_RED_BLOCKS-th tile of its segment and adds its partial totals atomically (the upsweep zeroed them)
 constexpr int RS_RED_BLOCKS = 64;
-__global__ __launch_bounds__(RS_THREADS) void k_rs_reduce(const unsigned* __restrict__ tile_hist, int ntiles, RsSegs sg,
+template <int D>
+__global__ __launch_bounds__(Rs<D>::THREADS) void k_rs_reduce(const unsigned* __restrict__ tile_hist, int ntiles, RsSegs sg,
                                                           unsigned* __restrict__ totals) {
+    constexpr int RS_BINS = Rs<D>::BINS;
     const int p = blockIdx.x / sg.nseg, s = blockIdx.x % sg.nseg, d = threadIdx.x;
     const unsigned* th = tile_hist + (size_t)p * ntiles * RS_BINS;
     const int t1 = sg.tile[s + 1];
@@ -154,13 +167,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_reduce(const unsigned* __rest
     if (sum) atomicAdd(&totals[(size_t)blockIdx.x * RS_BINS + d], sum);
 }
 
-constexpr int RS_WAVES = RS_THREADS / 64;
-
-template <typename KeyT, int RS_ITEMS>
-__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const KeyT* __restrict__ kin, const unsigned* __restrict__ vin,
+template <typename KeyT, int RS_ITEMS, int D>
+__global__ __launch_bounds__(Rs<D>::THREADS) void k_rs_scatter(const KeyT* __restrict__ kin, const unsigned* __restrict__ vin,
                                                            KeyT* __restrict__ kout, unsigned* __restrict__ vout,
                                                            RsSegs sg, RsPass ps, const unsigned* __restrict__ totals,
                                                            unsigned* look, unsigned* ticket) {
+    constexpr int RS_THREADS = Rs<D>::THREADS, RS_BINS = Rs<D>::BINS, RS_WAVES = Rs<D>::WAVES;
     constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
     constexpr int RS_CHUNK = RS_TILE / RS_WAVES;  // items per wave: a contiguous run of the tile
     __shared__ KeyT s_keys[RS_TILE];
@@ -200,7 +212,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const KeyT* __restric
         const bool ok = dig[r] < RS_BINS;
         unsigned long long eq = __ballot(ok);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
+        for (int b = 0; b < D; ++b) {
             const bool bit = (dig[r] >> b) & 1u;
             const unsigned long long bb = __ballot(bit);
             eq &= bit ? bb : ~bb;
@@ -223,9 +235,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const KeyT* __restric
     }
     __hip_atomic_store(&look[(size_t)tile * RS_BINS + tid], (tile == first ? RS_PREFIX : RS_AGG) | c, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned start = block_exclusive_scan_256(c, s_scan);  // contains barriers
+    const unsigned start = block_exclusive_scan<RS_BINS>(c, s_scan);  // contains barriers
     const unsigned goff = (unsigned)sg.start[sgi] +
-                          block_exclusive_scan_256(totals[(size_t)sgi * RS_BINS + tid], s_scan);  // digit tid's start
+                          block_exclusive_scan<RS_BINS>(totals[(size_t)sgi * RS_BINS + tid], s_scan);  // digit tid's start
     s_start[tid] = start;
 #pragma unroll
     for (int q = 0; q < RS_WAVES; ++q) s_wrun[q][tid] = start + wb[q];
@@ -269,20 +281,21 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const KeyT* __restric
 }
 
 // the own sort over segments (host segment offsets seg[0..nseg], seg[0] = 0, seg[nseg] = n)
-template <typename KeyT, int RS_ITEMS>
+template <typename KeyT, int RS_ITEMS, int D>
 static ot_status rs_sort(const KeyT* kin, KeyT* kout, const unsigned* vin, unsigned* vout, const int64_t* seg, int nseg,
                          int end_bit, hipStream_t stream, int scratch_slot) {
+    constexpr int RS_THREADS = Rs<D>::THREADS, RS_BINS = Rs<D>::BINS;
     constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
     const size_t n = (size_t)seg[nseg];
     if (n == 0) return OT_OK;
     if (nseg < 1 || nseg > RS_MAXSEG || n > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[sort] too many segments");
     if (end_bit < 1) end_bit = 1;
     RsPasses ps{};
-    ps.np = (end_bit + 7) / 8;
+    ps.np = (end_bit + D - 1) / D;
     if (ps.np > RS_MAXP) ps.np = RS_MAXP;
     for (int p = 0; p < ps.np; ++p) {
-        ps.p[p].shift = 8 * p;
-        const int bits = std::min(8, end_bit - 8 * p);
+        ps.p[p].shift = D * p;
+        const int bits = std::min(D, end_bit - D * p);
         ps.p[p].mask = (1u << bits) - 1u;
     }
     RsSegs sg{};
@@ -310,9 +323,9 @@ static ot_status rs_sort(const KeyT* kin, KeyT* kout, const unsigned* vin, unsig
     unsigned* look = tile_hist + hist_words;
     unsigned* totals = look + hist_words;
     unsigned* tickets = totals + (size_t)RS_MAXP * nseg * RS_BINS;
-    hipLaunchKernelGGL((k_rs_upsweep<KeyT, RS_ITEMS>), dim3(ntiles), dim3(RS_THREADS), 0, stream, kin, sg, ps, tile_hist, ntiles,
+    hipLaunchKernelGGL((k_rs_upsweep<KeyT, RS_ITEMS, D>), dim3(ntiles), dim3(RS_THREADS), 0, stream, kin, sg, ps, tile_hist, ntiles,
                        look, tickets, totals);
-    hipLaunchKernelGGL(k_rs_reduce, dim3(ps.np * nseg, RS_RED_BLOCKS), dim3(RS_THREADS), 0, stream,
+    hipLaunchKernelGGL(k_rs_reduce<D>, dim3(ps.np * nseg, RS_RED_BLOCKS), dim3(RS_THREADS), 0, stream,
                        (const unsigned*)tile_hist, ntiles, sg, totals);
     const KeyT* ks = kin;
     const unsigned* vs = vin;
@@ -320,7 +333,7 @@ static ot_status rs_sort(const KeyT* kin, KeyT* kout, const unsigned* vin, unsig
         const bool last = p == ps.np - 1;
         KeyT* kd = last ? kout : (p % 2 == 0 ? ka : kb);
         unsigned* vd = last ? vout : (p % 2 == 0 ? va : vb);
-        hipLaunchKernelGGL((k_rs_scatter<KeyT, RS_ITEMS>), dim3(maxt * nseg), dim3(RS_THREADS), 0, stream, ks, vs, kd, vd, sg, ps.p[p],
+        hipLaunchKernelGGL((k_rs_scatter<KeyT, RS_ITEMS, D>), dim3(maxt * nseg), dim3(RS_THREADS), 0, stream, ks, vs, kd, vd, sg, ps.p[p],
                            (const unsigned*)(totals + (size_t)p * nseg * RS_BINS), look + (size_t)p * ntiles * RS_BINS,
                            tickets + p);
         ks = kd;
@@ -335,7 +348,9 @@ ot_status sort_pairs_u64_u32(const unsigned long long* kin, unsigned long long* 
     if (n == 0) return OT_OK;
     if (n <= RS_OWN_MAX) {
         const int64_t seg[2] = {0, (int64_t)n};
-        return rs_sort<unsigned long long, 8>(kin, kout, vin, vout, seg, 1, end_bit, stream, scratch_slot);
+        if (OT_SEGSORT_D9 && (end_bit + 8) / 9 < (end_bit + 7) / 8)  // 9-bit digits when they save a pass
+            return rs_sort<unsigned long long, 4, 9>(kin, kout, vin, vout, seg, 1, end_bit, stream, scratch_slot);
+        return rs_sort<unsigned long long, 8, 8>(kin, kout, vin, vout, seg, 1, end_bit, stream, scratch_slot);
     }
     size_t tmp = 0;
     OT_HIP_TRY(rocprim::radix_sort_pairs<BigSortConfig>(nullptr, tmp, kin, kout, vin, vout, n, 0u, (unsigned)end_bit,
@@ -349,9 +364,13 @@ ot_status sort_pairs_u64_u32(const unsigned long long* kin, unsigned long long* 
 #ifndef OT_SEGSORT_ITEMS
 #define OT_SEGSORT_ITEMS 16  // items per thread of the segmented sort's tiles (4096-item tiles)
 #endif
+
 ot_status sort_segments_u32_u32(const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout,
                                 const int64_t* seg, int nseg, int end_bit, hipStream_t stream, int scratch_slot) {
-    return rs_sort<unsigned, OT_SEGSORT_ITEMS>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot);
+    // 9-bit digits (512-thread tiles of the same 4096 items) when they save a pass: 25..27-bit keys in 3 passes
+    if (OT_SEGSORT_D9 && (end_bit + 8) / 9 < (end_bit + 7) / 8)
+        return rs_sort<unsigned, OT_SEGSORT_ITEMS / 2, 9>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot);
+    return rs_sort<unsigned, OT_SEGSORT_ITEMS, 8>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot);
 }
 
 ot_status sort_pairs_u32_u32(const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout, size_t n,

@@ -29,6 +29,8 @@ def _sort(pkg, keys, end_bit):
 @pytest.mark.parametrize("n,end_bit,hi", [
     (1, 8, 4), (100, 8, 256), (2047, 13, 1 << 13), (2048, 16, 50), (2049, 30, 1 << 30), (100003, 30, 1 << 30),
     (1 << 20, 51, 1 << 51), (3000017, 24, 1 << 24), (250000, 64, None), (77777, 1, 2), (500000, 40, 1000),
+    # 9-bit digits where they save a pass (18, 27, 36 bits)
+    (2049, 18, 1 << 18), (100003, 27, 1 << 27), (500000, 36, 1 << 36),
 ])
 def test_sort_stable_bitexact(pkg, gpu, n, end_bit, hi):
     rng = np.random.default_rng(n + end_bit)
@@ -57,6 +59,8 @@ def test_sort_presorted_and_reversed(pkg, gpu):
 
 @pytest.mark.parametrize("sizes,end_bit", [
     ([0, 1, 2047, 2048, 2049, 0, 5], 12), ([812746, 810001, 0, 799999], 28), ([100000] * 33, 32), ([3] * 64, 2),
+    # 9-bit digits (3 passes for 25..27 bits, 2 for 17..18): the configs[2] voxel keys
+    ([812746, 810001, 0, 799999], 27), ([0, 1, 4095, 4096, 4097, 0, 5], 25), ([100000] * 33, 18),
 ])
 def test_segmented_sort_bitexact(pkg, gpu, sizes, end_bit):
     """sort_segments_u32_u32 (the batched configs[2] voxel sort): every segment sorted stably on its own, nothing
