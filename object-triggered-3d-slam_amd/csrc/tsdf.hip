@@ -628,12 +628,6 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 #ifndef OT_RCP_TABLE
 #define OT_RCP_TABLE 1  // 0: never take the FAST (reciprocal table) kernel
 #endif
-#ifndef OT_SHARED_RCP
-#define OT_SHARED_RCP 1  // the float64-colour kernel reads its reciprocal once per voxel for both quotients
-#endif
-#ifndef OT_C64_SKIP
-#define OT_C64_SKIP 0  // 1: float64 colour update only for voxels k with an updating lane (measured slower: 0.584 vs 0.564 ms)
-#endif
 // Reciprocal table: y[n] = RN(1/n) for n in [1, RCP_N].  For b = w + 1 an integer in that range, q0 = RN(a*y),
 // r = fma(-b, q0, a) (exact), q = RN(q0 + r*y) is RN(a/b) -- Markstein's theorem (y correctly rounded, q0 within one
 // ulp, no underflow in r; binary32 and binary64 alike): the IEEE quotient bit for bit with 3 operations and an LDS
@@ -815,16 +809,10 @@ __global__ __launch_bounds__(64 * INT_WG, C64 ? (FAST ? OT_WAVES_PER_EU_C64 : 5)
                         const float w1 = wv + 1.0f;
                         const float ta = ts[k] * wv + tn;
                         float tsn;  // (tsdf * w + t) / (w + 1): the IEEE quotient, tsdf bit-exact
-#if OT_SHARED_RCP
-                        // one table read per voxel for the tsdf and the colour quotients
+                        // one table read per voxel for the tsdf and the colour quotients (round 3: +0.8 %)
                         const double y64 = (FAST && C64) ? s_r64[(int)w1] : 0.0;
-#endif
                         if constexpr (FAST) {
-#if OT_SHARED_RCP
                             const float y = C64 ? (float)y64 : s_r32[(int)w1];
-#else
-                            const float y = C64 ? (float)s_r64[(int)w1] : s_r32[(int)w1];
-#endif
                             const float q0 = ta * y;
                             tsn = __builtin_fmaf(__builtin_fmaf(-w1, q0, ta), y, q0);
                         } else {
@@ -833,22 +821,14 @@ __global__ __launch_bounds__(64 * INT_WG, C64 ? (FAST ? OT_WAVES_PER_EU_C64 : 5)
                         ts[k] = doit ? tsn : ts[k];
                         if (use_color) {
                             if constexpr (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
-#if OT_C64_SKIP
-                                if (__any(doit)) {
-#else
-                                {
-#endif
+                                {  // every lane, in select form (skipping voxels without an updating lane: slower)
                                     const double wd = (double)wv, w1d = (double)w1;
                                     const double ar = cr[k] * wd + (double)(cv[k] & 0xFFu);
                                     const double ag = cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu);
                                     const double ab = cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu);
                                     double nr, ng, nb;
                                     if constexpr (FAST) {
-#if OT_SHARED_RCP
                                         const double y = y64;
-#else
-                                        const double y = s_r64[(int)w1];
-#endif
                                         const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
                                         nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
                                         ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
