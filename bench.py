@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--voxel", type=float, default=0.005)
     ap.add_argument("--sdf-trunc", type=float, default=0.04)
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
-    ap.add_argument("--cpu-frames", type=int, default=32, help="frames in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--sustain", type=float, default=1.5, help="seconds of sustained headline steps (0 = skip)")
     ap.add_argument("--color-bits", type=int, default=64, choices=(32, 64),
                     help="headline colour precision: 64 = Open3D's float64 TSDFVoxel::color_ (the C ABI and facade "
@@ -75,12 +75,66 @@ def parse():
     return ap.parse_args()
 
 
+def resolve_world(gpus, env):
+    """Reconcile --gpus with a launcher's environment.  Returns ("spawn", N) when this process must start N ranks
+    itself (no WORLD_SIZE, --gpus N > 1), ("run", world) when it is one rank of `world` (or the only process);
+    raises SystemExit when a launcher's WORLD_SIZE disagrees with --gpus."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return ("spawn", gpus) if gpus > 1 else ("run", 1)
+    if int(ws) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {gpus}")
+    return "run", int(ws)
+
+
+def launch_ranks(n, script, argv, env=None):
+    """Start n ranks of `script argv` as child processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on
+    127.0.0.1), before this process touches the GPU; rank 0 prints the JSON line.  If a rank fails the others are
+    terminated (they would wait in a collective forever).  Returns the worst exit status."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=e))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.send_signal(signal.SIGTERM)
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    return (max(bad, key=abs) if bad else 0), rcs
+
+
 def main():
     args = parse()
+    mode, world = resolve_world(args.gpus, os.environ)
+    if mode == "spawn":  # `python bench.py --gpus N` with no launcher: one child process per GPU
+        rc, _ = launch_ranks(world, os.path.abspath(__file__), sys.argv[1:])
+        sys.exit(rc if 0 <= rc < 256 else 1)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # configs[3] scans are rendered before this process touches the GPU (the render pool forks workers)
@@ -407,8 +461,9 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
                      torch.equal(mesh._vc.dev(), m0._vc.dev()))
         del ref
     return {"workload": f"configs[1] scan (seed 0) as ONE object spatially sharded over {world} GPU(s): unit owner = "
-                        f"hash(key) mod {world}, every rank integrates every frame into its own units; marching "
-                        "cubes with a border halo",
+                        f"hash(ownership block key) mod {world}, blocks of {4 if world <= 4 else 2}^3 units "
+                        "(tsdf.h unit_owner), every rank integrates every frame into its own units; marching cubes "
+                        "with a border halo routed to the owners of the -x/-y/-z neighbours",
             "scaling": "strong", "frames_per_s": round(args.frames * 1.0 / dt, 1), "ms_per_step": round(dt * 1e3, 3),
             "units_per_rank_min": min(cnt), "units_per_rank_max": max(cnt), "assemble_ms": round(t_asm * 1e3, 2),
             "assemble_bytes": border_bytes, "allgather_border_bytes": allgather_border, "whole_unit_bytes": whole,
@@ -842,8 +897,9 @@ def _traffic(args, L, kernel, config):
 
 
 def cpu_baseline(depth, color, ext, intr_t, args):
-    """CPU oracle (kind "port") on the first --cpu-frames frames of the same scan: 1 warm-up pass, then the median
-    of 5 timed passes (BASELINE.md / SURVEY 8(d) method), each into a fresh volume."""
+    """CPU oracle (kind "port") on the --cpu-frames first frames of the same scan (default: all 256, the headline's
+    whole step): 1 warm-up pass, then the median of 3 timed passes, each into a fresh volume; the per-pass spread is
+    reported beside the median (host load moves it by +-20 % across boxes)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -859,14 +915,15 @@ def cpu_baseline(depth, color, ext, intr_t, args):
         return time.perf_counter() - t0
 
     one_pass()
-    times = [one_pass() for _ in range(5)]
+    times = [one_pass() for _ in range(3)]
     dt = float(np.median(times))
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     return {"value": round(n / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} of the {args.frames} frames, same synthetic scan, one fresh volume per pass "
-                      f"(float64 colour state, as Open3D and the headline), 1 warm-up + median of 5 passes, "
-                      f"depth->float excluded (done before timing), OMP_NUM_THREADS={cores}",
-            "pass_seconds": [round(t, 3) for t in times]}
+            "sample": f"{'all' if n == depth.shape[0] else 'first'} {n} of the {args.frames} frames, same synthetic "
+                      f"scan, one fresh volume per pass (float64 colour state, as Open3D and the headline), 1 warm-up "
+                      f"+ median of 3 passes, depth->float excluded (done before timing), OMP_NUM_THREADS={cores}",
+            "pass_seconds": [round(t, 3) for t in times],
+            "frames_per_s_min_max": [round(n / max(times), 3), round(n / min(times), 3)]}
 
 
 if __name__ == "__main__":

@@ -154,6 +154,11 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"HIP extension missing: {LIB_PATH} (run __graft_entry__.build())")
         lib = C.CDLL(LIB_PATH)
+        lib.ot_version.argtypes, lib.ot_version.restype = [], C.c_char_p
+        built, src = library_source_hash(lib), source_hash()
+        if built != src:  # binary provenance: the .so must be the build of the sources beside it
+            raise RuntimeError(f"stale HIP library {LIB_PATH}: built from sources {built or '(no hash)'}, "
+                               f"sources here are {src} (run __graft_entry__.build())")
         missing = []
         for name, argtypes in {**SIGNATURES, **TEST_SIGNATURES}.items():
             try:
@@ -190,18 +195,15 @@ def intrinsics_struct(intr) -> ot_intrinsics:
 
 
 def source_hash() -> str:
-    """sha256 (16 hex) over the HIP sources, headers and Makefile the library is built from: tags measurements
-    (profiles/pmc_traffic.json) with the build they were taken on, independent of compiler output bytes."""
-    import hashlib
+    """sha256 (16 hex) over the HIP sources, headers and Makefile the library is built from (_srchash.py): tags
+    measurements (profiles/pmc_traffic.json) with the build they were taken on; the Makefile compiles the same hash
+    into the library (ot_version), and load() refuses a library built from other sources."""
+    from . import _srchash
 
-    h = hashlib.sha256()
-    csrc = os.path.join(_HERE, "csrc")
-    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h")) or f == "Makefile")
-    inc = os.path.join(os.path.dirname(_HERE), "include")
-    paths = [os.path.join(csrc, f) for f in files] + sorted(os.path.join(inc, f) for f in os.listdir(inc)
-                                                            if f.endswith(".h"))
-    for p in paths:
-        h.update(os.path.basename(p).encode())
-        with open(p, "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+    return _srchash.compute()
+
+
+def library_source_hash(lib) -> str:
+    """The source hash compiled into a loaded library (ot_version() ends with ' src=<hash>'), '' if absent."""
+    ver = lib.ot_version().decode(errors="replace")
+    return ver.rsplit(" src=", 1)[1].strip() if " src=" in ver else ""

@@ -107,8 +107,8 @@ __host__ __device__ inline void border_voxel(int b, int& x, int& y, int& z) {
     else y = r - 15, z = 0;
 }
 
-constexpr int MAX_BATCH = 64;
-constexpr int OT_MAIL_WORDS = 64;  // frames per fused launch (one bit each in fmask)
+constexpr int MAX_BATCH = 64;      // frames per fused launch (one bit each in fmask)
+constexpr int OT_MAIL_WORDS = 64;  // capacity of the pinned host mailbox (4-B words per read-back, mail_words)
 
 // per-frame parameters of a batch (device resident)
 struct BatchFrame {

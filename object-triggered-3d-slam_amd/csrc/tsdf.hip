@@ -268,8 +268,8 @@ __global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d)
 
 // ============================================================================ batched (temporal blocking)
 // One launch per batch of F <= 64 frames:
-//   k_batch_prep      : per-pixel (depth, multiplier) float2 + packed colour for every frame (grid.y = frame);
-//                       by default fused into k_batch_touch (each touch workgroup stages a pixel chunk)
+//   staging           : per-pixel (depth, multiplier) float2 + packed colour for every frame, done by k_batch_touch's
+//                       workgroups (each stages a contiguous pixel chunk of its frames)
 //   k_batch_touch     : stride samples of every frame; a unit touched by frame f gets bit f in its slot's
 //                       fmask (64-bit atomicOr); the first bit set in a batch appends the slot to bslots
 //   k_batch_units     : per touched slot: allocate the unit if new, move its frame mask into a 32-B header
@@ -336,10 +336,7 @@ __device__ inline void prep_quad(const BatchFrame& fr, const float* __restrict__
 
 // Quads [q, q1) with stride 256 (one lane's share of a chunk): on the common path (u16 depth, RGB8, aligned, W*H
 // a multiple of 4) PREP_K quads per step with all of their loads issued before any store.
-#ifndef OT_PREP_K
-#define OT_PREP_K 2
-#endif
-constexpr int PREP_K = OT_PREP_K;
+constexpr int PREP_K = 2;  // 3 or 4 (more VGPRs, fewer resident touch waves): step +2-3 %
 __device__ inline void prep_range(const BatchFrame& fr, const float* __restrict__ mult, int64_t q, int64_t q1,
                                   int64_t npx) {
     const bool fast = fr.depth16 && fr.color && (npx & 3) == 0 &&
@@ -377,12 +374,6 @@ __device__ inline void prep_range(const BatchFrame& fr, const float* __restrict_
     for (; q < q1; q += 256) prep_quad(fr, mult, q * 4, npx);
 }
 
-__global__ __launch_bounds__(256) void k_batch_prep(const BatchFrame* __restrict__ frames, const float* __restrict__ mult,
-                                                    int64_t npx) {
-    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (i0 < npx) prep_quad(frames[blockIdx.y], mult, i0, npx);
-}
-
 struct BatchTouchParams {
     int W, stride, ws, hs;
     double fx, fy, cx, cy;
@@ -391,6 +382,7 @@ struct BatchTouchParams {
     const float* mult;  // fused staging (k_batch_touch stages the batch's pixels too): ray multipliers
     int64_t npx;        // pixels per frame
     int pc;             // this batch's pair counter index
+    int stage;          // 1: stage the batch's (depth, multiplier) / colour pixels for the integrate; 0: it reads raw
 };
 
 __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int pc, int x, int y, int z) {
@@ -420,14 +412,8 @@ __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, i
 // every distinct unit of the tile does ONE global hash insert + ONE atomicOr of its merged mask.  A key that does
 // not fit the LDS table falls back to the direct global path.
 constexpr int TT = 16;          // tile edge in samples
-#ifndef OT_TF
-#define OT_TF 4  // 64-frame batches (round 3): 4 frames per workgroup +1 % step vs 2; 8 / 16: -0.7 / -9 %
-#endif
-constexpr int TF = OT_TF;       // frames per workgroup
-#ifndef OT_LTAB
-#define OT_LTAB 1024
-#endif
-constexpr int LTAB = OT_LTAB;   // LDS table entries (16 B each + a 4-B slot in the list of used entries)
+constexpr int TF = 4;        // frames per workgroup (64-frame batches: +1 % step vs 2; 8 / 16: -0.7 / -9 %)
+constexpr int LTAB = 1024;   // LDS table entries (16 B each + a 4-B slot in the list of used entries)
 
 __device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* masks, int* used, int* nused,
                                  unsigned long long key, unsigned long long bit) {
@@ -460,17 +446,16 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
         s_masks[e] = 0ull;
     }
     if (tid == 0) s_nused = 0;
-#ifndef OT_SPLIT_PREP
-    // Fused staging: this workgroup also stages a contiguous 1/gridDim.x of the pixels of each of its frames
-    // (k_batch_prep's work; the touch below reads raw depth itself, so nothing here waits on these stores).
-    {
+    // Fused staging: this workgroup also stages a contiguous 1/gridDim.x of the pixels of each of its frames (the
+    // touch below reads raw depth itself, so nothing here waits on these stores; as a separate launch the staging
+    // measured 7 us slower per 64 frames)
+    if (p.stage) {
         const int64_t quads = (p.npx + 3) >> 2;
         const int64_t per = (quads + gridDim.x - 1) / gridDim.x;
         const int64_t q0 = (int64_t)blockIdx.x * per, q1 = q0 + per < quads ? q0 + per : quads;
         for (int f = blockIdx.y * TF; f < blockIdx.y * TF + TF && f < nframes; ++f)
             prep_range(frames[f], p.mult, q0 + tid, q1, p.npx);
     }
-#endif
     __syncthreads();
     const int tiles_x = (p.ws + TT - 1) / TT;
     const int sx = (blockIdx.x % tiles_x) * TT + (tid & (TT - 1));
@@ -480,12 +465,8 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
         const int r = sy * p.stride, c = sx * p.stride;
         for (int f = f0; f < f0 + TF && f < nframes; ++f) {
             const BatchFrame& fr = frames[f];
-#ifndef OT_SPLIT_PREP
-            const int64_t pix = (int64_t)r * p.W + c;  // the staged depth, computed as k_batch_prep does
+            const int64_t pix = (int64_t)r * p.W + c;  // the staged depth, computed as the staging does
             const float df = fr.depth16 ? prep_depth(fr, fr.depth16[pix]) : fr.depthf[pix];
-#else
-            const float df = fr.dm[(int64_t)r * p.W + c].x;
-#endif
             if (!(df > 0.0f)) continue;
             const double z = (double)df;
             const double x = ((double)c - p.cx) * z / p.fx;
@@ -546,15 +527,11 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
 // camera-space position still advances by exactly z sequential additions of Es.col(2) from the column origin,
 // as in Open3D, so every slice reproduces the single-lane z walk bit for bit.  Waves never synchronise: the
 // unit header (id, key, frame mask) is resolved once by k_batch_units and read with scalar loads.
-#ifndef OT_BZ
-#define OT_BZ 4
-#endif
-constexpr int BZ = OT_BZ;                     // voxels per lane along z
+constexpr int BZ = 4;                         // voxels per lane along z (2: slower, profiles/r03w_*)
 constexpr int SLICES = 4 * (UNIT_RES / BZ);   // waves per unit
-#ifndef OT_INT_WG
-#define OT_INT_WG 4  // waves per integrate workgroup: a quarter unit (measured per 32-frame launch, float64 colour:
-#endif               // 16 waves 0.511 ms, 8 waves 0.452 ms, 4 waves 0.426 ms; float32 colour 0.402 / 0.383 / 0.378)
-constexpr int INT_WG = OT_INT_WG;
+// waves per integrate workgroup: a quarter unit (measured per 32-frame launch, float64 colour: 16 waves 0.511 ms,
+// 8 waves 0.452 ms, 4 waves 0.426 ms; float32 colour 0.402 / 0.383 / 0.378)
+constexpr int INT_WG = 4;
 constexpr int INT_PARTS = SLICES / INT_WG;  // workgroups per unit
 
 struct UnitWork {
@@ -1317,14 +1294,11 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     // batch pair count and the integrate's queue heads
     // this batch's pair counter: zeroed by reset, or by the previous batch's k_batch_units (no memset here)
     const int pc = vol->batch_pc;
-#ifdef OT_SPLIT_PREP
-    hipLaunchKernelGGL(k_batch_prep, dim3((unsigned)((npx / 4 + 255) / 256 + 1), n), dim3(256), 0, stream,
-                       (const BatchFrame*)vol->bframes, (const float*)vol->mult, npx);
-#endif
     BatchTouchParams tp;
     tp.mult = vol->mult;
     tp.npx = npx;
     tp.pc = pc;
+    tp.stage = 1;
     tp.W = in.width;
     tp.stride = vol->stride;
     tp.ws = (in.width + vol->stride - 1) / vol->stride;
@@ -1708,9 +1682,11 @@ ot_status ot_tsdf_set_color_precision(ot_tsdf* vol, int32_t bits) {
     if (c64 != vol->color64) {  // the record stride changes: reallocate the (still empty) pool
         const int uf = c64 ? UNIT_FLOATS_C64 : UNIT_FLOATS;
         OT_HIP_TRY(hipDeviceSynchronize());
-        OT_HIP_TRY(hipFree(vol->dev.vox));
-        vol->dev.vox = nullptr;
-        OT_HIP_TRY(hipMalloc(&vol->dev.vox, sizeof(float) * (size_t)uf * vol->max_units));
+        // the new pool first: if the allocation fails the volume keeps its old, consistent layout
+        float* pool = nullptr;
+        OT_HIP_TRY(hipMalloc(&pool, sizeof(float) * (size_t)uf * vol->max_units));
+        (void)hipFree(vol->dev.vox);
+        vol->dev.vox = pool;
         vol->dev.unit_floats = uf;
         vol->dev.color64 = c64 ? 1 : 0;
         vol->color64 = c64;

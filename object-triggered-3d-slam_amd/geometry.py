@@ -523,7 +523,11 @@ class TriangleMesh:
         out = D.empty((nv, 3), "float64")
         mc = getattr(self, "_mc", None)
         vol = mc[0]() if mc is not None else None
-        if vol is not None and getattr(vol, "_h", None) is not None and not self._v._viewed and not self._t._viewed:
+        fresh = vol is not None and not self._v._viewed and not self._t._viewed
+        if fresh:  # the very arrays the extraction wrote, unmodified since (no view, no in-place device edit)
+            V, T = self._v.dev(), self._t.dev()
+            fresh = (V.data_ptr(), V._version, T.data_ptr(), T._version) == tuple(mc[2:6])
+        if fresh and getattr(vol, "_h", None) is not None:
             st = L.load().ot_tsdf_mesh_vertex_normals(vol._h, mc[1], D.ptr(self._v.dev()), nv, D.ptr(self._t.dev()),
                                                        nt, D.ptr(out), D.stream_ptr())
             if st == L.OT_OK:

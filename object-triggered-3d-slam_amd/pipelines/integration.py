@@ -238,7 +238,10 @@ class ScalableTSDFVolume:
         serial = C.c_int64(-1)
         L.call("ot_tsdf_mesh_serial", self._h, C.byref(serial))
         # normals via the marching-cubes structure kept with this volume (weakly referenced: the mesh outlives it)
-        mesh._mc = (weakref.ref(self), serial.value) if serial.value >= 0 else None
+        # the device arrays' identity and torch version counters are recorded too: an in-place edit of V or T (same
+        # pointer, same counts) bumps the version and sends compute_vertex_normals to the generic path
+        mesh._mc = (weakref.ref(self), serial.value, V.data_ptr(), V._version, T.data_ptr(), T._version) \
+            if serial.value >= 0 else None
         if self.color_type == TSDFVolumeColorType.RGB8:
             mesh._vc = _Arr(dev=VC)
         if not with_keys:

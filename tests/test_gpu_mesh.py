@@ -153,6 +153,23 @@ def test_vertex_normals_mc_walk_bitexact(pkg, O, synth, seq16, gpu, voxel):
     assert_bitwise(np.asarray(stale.vertex_normals), rN, "fallback vertex normals")
 
 
+def test_vertex_normals_after_in_place_edit(pkg, O, synth, seq16, gpu):
+    """an in-place device edit of the triangle array (same pointer, same counts) must not take the
+    marching-cubes walk, whose triangle ids come from the stored structure: the facade sees the tensor's version bump
+    and takes the corner sort, which equals the oracle's normals of the EDITED mesh."""
+    depth, color, ext = seq16
+    vol, ref = _volumes(pkg, O, synth, depth, color, ext, 0.01)
+    mesh = vol.extract_triangle_mesh()
+    T = mesh._t.dev()
+    nt = T.shape[0]
+    assert nt > 10
+    T[: nt // 2] = T[: nt // 2].flip(1).clone()  # reverse the winding of half the triangles, in place
+    mesh.compute_vertex_normals()
+    V = np.asarray(mesh.vertices)
+    rN = O.vertex_normals(V, T.cpu().numpy())
+    assert_bitwise(np.asarray(mesh.vertex_normals), rN, "vertex normals after an in-place triangle edit")
+
+
 def test_vertex_normals_mc_walk_sharded(pkg, O, synth, seq16, gpu):
     """A spatially sharded volume's partial mesh (own cubes only; halo units supply neighbours): the walk equals the
     corner sort on the same partial mesh."""

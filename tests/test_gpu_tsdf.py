@@ -165,6 +165,98 @@ def test_tsdf_many_batches_5mm(pkg, O, gpu, synth, batch):
     assert n > 3000
 
 
+@pytest.mark.parametrize("bits", [64, 32])
+def test_ieee_division_kernel_after_import(pkg, O, gpu, synth, bits):
+    """after import_units the weights are arbitrary state, so the host launches the IEEE-division
+    integrate (k_batch_integrate<C64, false>) instead of the reciprocal-table one.  Volume A integrates the first
+    12 frames and exports; volume B imports A's units and integrates the next 12 frames in 5-frame batches; B must
+    equal the oracle that integrated all 24 frames (tsdf / weight / keys bitwise; colour bitwise at precision 64)."""
+    integ = _integration(pkg)
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=4), n_frames=48, frames=range(0, 48, 2))
+    ref = O.TSDF(0.01, 0.04, 1, 4)
+
+    def feed(vol, ks):
+        for k in ks:
+            rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+                pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+                convert_rgb_to_intensity=False)
+            vol.integrate(rgbd, intr, ext[k])
+            ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
+
+    a = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                 color_precision=bits)
+    feed(a, range(12))
+    keys, tsdf, weight, col = a.export_units()
+    b = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                 color_precision=bits, batch_frames=5)
+    b.import_units(keys, tsdf, weight, col)
+    feed(b, range(12, 24))
+    bk, bt, bw, bc = (t.cpu().numpy() for t in b.export_units())
+    rk, rt, rw, rc = ref.export()
+    assert_bitwise(bk, rk, "unit keys (import + IEEE kernel)")
+    assert_bitwise(bw, rw, "voxel weights (import + IEEE kernel)")
+    assert_bitwise(bt, rt, "voxel tsdf (import + IEEE kernel)")
+    if bits == 64:
+        assert_bitwise(bc, rc, "float64 colours (import + IEEE kernel)")
+    else:
+        np.testing.assert_allclose(bc, rc, rtol=1e-4, atol=1e-4 * 255)
+
+
+@pytest.mark.parametrize("bits", [64, 32])
+def test_long_scan_crosses_reciprocal_table(pkg, O, gpu, synth, bits):
+    """the reciprocal-table integrate serves weights below RCP_N = 2048; once frames since reset + the
+    batch reach it the host switches to the IEEE-division kernel.  2,200 frames (a 16-frame 80x60 ring cycled), so
+    weights run past 2048 and the scan crosses the switch part-way; bitwise vs the oracle at the end."""
+    L = pkg._lib
+    lib = L.load()
+    intr_t = (80, 60, 70.7, 70.7, 40.5, 30.5)
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=6), n_frames=16, intr=intr_t)
+    ext = np.ascontiguousarray(ext, dtype=np.float64)
+    n_total = 2200
+    d16 = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
+    col = torch.from_numpy(color).cuda().contiguous()
+    W, H = intr_t[0], intr_t[1]
+    intr = L.ot_intrinsics(W, H, *intr_t[2:])
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    vol = C.c_void_p()
+    L.call("ot_tsdf_create", 0.02, 0.08, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
+    ref = O.TSDF(0.02, 0.08, 1, 4)
+    dfs = [O.depth_to_float(depth[k], 1000.0, 3.0) for k in range(16)]
+    try:
+        L.call("ot_tsdf_set_color_precision", vol, bits)
+        for i in range(n_total):
+            k = i % 16
+            st = lib.ot_tsdf_integrate_u16(vol, C.c_void_p(d16.data_ptr() + k * W * H * 2),
+                                           C.c_void_p(col.data_ptr() + k * W * H * 3), C.byref(intr),
+                                           ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
+            assert st == 0, lib.ot_last_error()
+            ref.integrate(dfs[k], color[k], intr_t, ext[k])
+        nu = C.c_int64(0)
+        L.call("ot_tsdf_num_units", vol, C.byref(nu), stream)
+        n = nu.value
+        keys = torch.empty((n, 3), dtype=torch.int32, device="cuda")
+        tsdf = torch.empty((n, 4096), dtype=torch.float32, device="cuda")
+        weight = torch.empty((n, 4096), dtype=torch.float32, device="cuda")
+        colr = torch.empty((n, 4096, 3), dtype=torch.float64 if bits == 64 else torch.float32, device="cuda")
+        L.call("ot_tsdf_export_units", vol, n, C.c_void_p(keys.data_ptr()), C.c_void_p(tsdf.data_ptr()),
+               C.c_void_p(weight.data_ptr()), C.c_void_p(colr.data_ptr()) if bits == 32 else None, stream)
+        if bits == 64:
+            L.call("ot_tsdf_export_color64", vol, n, C.c_void_p(colr.data_ptr()), stream)
+    finally:
+        L.call("ot_tsdf_destroy", vol)
+    rk, rt, rw, rc = ref.export()
+    assert rw.max() > 2048, "the scan must drive weights past the reciprocal table"
+    assert_bitwise(keys.cpu().numpy(), rk, "unit keys (long scan)")
+    assert_bitwise(weight.cpu().numpy(), rw, "voxel weights (long scan)")
+    assert_bitwise(tsdf.cpu().numpy(), rt, "voxel tsdf (long scan)")
+    if bits == 64:
+        assert_bitwise(colr.cpu().numpy(), rc, "float64 colours (long scan)")
+    else:
+        np.testing.assert_allclose(colr.cpu().numpy(), rc, rtol=1e-4, atol=1e-4 * 255)
+
+
 def test_tsdf_lexical_order_matters(pkg, O, gpu, synth, seq16):
     """Running averages depend on frame order: the GPU must apply frames in call order."""
     depth, color, ext = seq16
