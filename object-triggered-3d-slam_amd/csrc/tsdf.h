@@ -121,6 +121,7 @@ struct BatchFrame {
     float E[12];              // rows 0..2 of (float)extrinsic
     float es[3];              // column 2 of (float)extrinsic * voxel_length
     float scale;              // (float)depth_scale
+    float rscale;             // fl(1 / scale): div_rn's reciprocal (RAW integrate)
     double trunc;             // depth_trunc
 };
 

@@ -588,23 +588,12 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
     }
 }
 
-// occupancy floor the integrate is compiled for: the float32-colour kernel allocates 64 VGPRs (8 waves
-// per SIMD) on its own; the float64-colour state wants more (C64 cap below)
-#ifndef OT_MASK_INVALID_LOADS
-#define OT_MASK_INVALID_LOADS 1  // lanes whose voxel projects outside the image issue no depth gather (with the
-#endif                           // 64-VGPR cap below: integrate 0.415-0.421 -> 0.409-0.412 ms; at 66 VGPRs 0.59)
-#ifndef OT_SKIP_IDLE_STORE
-#define OT_SKIP_IDLE_STORE 1  // slices with no update in the batch are not written back (-1.5 % integrate)
-#endif
-#ifndef OT_WAVES_PER_EU
-#define OT_WAVES_PER_EU 8  // float32 colour: 64 VGPRs, 8 waves per SIMD (the kernel lives on its occupancy)
-#endif
-#ifndef OT_WAVES_PER_EU_C64
-#define OT_WAVES_PER_EU_C64 8  // quarter-unit workgroups, 64 VGPRs (5 / 6 / 8: 0.426 / 0.428 / 0.414 ms per launch)
-#endif
-#ifndef OT_RCP_TABLE
-#define OT_RCP_TABLE 1  // 0: never take the FAST (reciprocal table) kernel
-#endif
+// Occupancy: the integrate lives on it: 64 VGPRs, 8 waves per SIMD for both colour precisions with
+// quarter-unit workgroups (float64 colour at 5 / 6 / 8 waves: 0.426 / 0.428 / 0.414 ms per 32-frame launch; the IEEE-
+// division float64 kernel needs more registers and runs at 5).  Measured and settled: lanes whose voxel
+// projects outside the image issue no depth gather (0.415-0.421 -> 0.409-0.412 ms); slices with no update in the
+// batch are not written back (-1.5 %).
+constexpr int INT_WAVES_PER_EU = 8;
 // Reciprocal table: y[n] = RN(1/n) for n in [1, RCP_N].  For b = w + 1 an integer in that range, q0 = RN(a*y),
 // r = fma(-b, q0, a) (exact), q = RN(q0 + r*y) is RN(a/b) -- Markstein's theorem (y correctly rounded, q0 within one
 // ulp, no underflow in r; binary32 and binary64 alike): the IEEE quotient bit for bit with 3 operations and an LDS
@@ -612,19 +601,22 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 // is an integer count of updates below RCP_N (frames since reset + the batch < RCP_N) and the state comes from
 // integration alone (no imported units): then |a| is 0 or far above the underflow range (tsdf: a sum of a running
 // mean and a term quantised by the depth / camera-distance floats; colour: c*w + rgb >= 0 with c a mean of bytes).
-// Otherwise the IEEE divisions (FAST = false).
-#ifndef OT_RCP_N
-#define OT_RCP_N 2048  // 16 KiB (float64) / 8 KiB (float32) of LDS per workgroup: 8 quarter-unit workgroups per CU
-#endif
-constexpr int RCP_N = OT_RCP_N;
+// Otherwise the IEEE divisions (FAST = false: tests/test_gpu_tsdf.py::test_long_scan_crosses_reciprocal_table and
+// ::test_ieee_division_kernel_after_import run both across the switch).
+constexpr int RCP_N = 2048;  // 16 KiB (float64) / 8 KiB (float32) of LDS per workgroup: 8 quarter-unit workgroups per CU
 
 // One workgroup of INT_WG waves per unit part (a quarter unit by default: small workgroups let the CU keep 6-8 of them
 // resident instead of one 16-wave unit -- a unit-sized workgroup left the float64-colour kernel at 4 waves per SIMD
 // whatever its registers); the parts of a unit run on one XCD.  Work items are assigned by a static grid stride that
 // every wave derives on its own: no atomics, one barrier (the reciprocal table).
-// C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes
-template <bool C64, bool FAST>
-__global__ __launch_bounds__(64 * INT_WG, C64 ? (FAST ? OT_WAVES_PER_EU_C64 : 5) : OT_WAVES_PER_EU) void k_batch_integrate(
+// C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes.
+// RAW: the frames were not staged (a spatially sharded volume: every rank would otherwise stage every pixel of every
+// frame for its share of the units); a voxel visit gathers the caller's u16 depth (converted as
+// Image::ConvertDepthToFloatImage: div_rn = the IEEE quotient, checked over every u16 value), the frame-independent
+// ray multiplier (the volume's cached table) and, for updating lanes, the caller's three RGB8 bytes.  Same values,
+// bit for bit, as the staged (depth, multiplier) / colour words.
+template <bool C64, bool FAST, bool RAW>
+__global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
     using CT = typename std::conditional<C64, double, float>::type;
     // one table per kernel: float64 reciprocals for the float64-colour kernel (its float32 ones are their roundings:
@@ -700,8 +692,11 @@ __global__ __launch_bounds__(64 * INT_WG, C64 ? (FAST ? OT_WAVES_PER_EU_C64 : 5)
                 for (unsigned long long m = mask; m; m &= m - 1) {
                     const int f = __ffsll((long long)m) - 1;
                     const BatchFrame& fr = frames[f];
-                    const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(fr.dm, npx * 8);
-                    const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
+                    // staged: (depth, multiplier) words and packed colours; RAW: the caller's u16 depth and RGB8
+                    // bytes plus the volume's multiplier table
+                    const __amdgpu_buffer_rsrc_t dm_rsrc = RAW ? make_rsrc(fr.depth16, npx * 2) : make_rsrc(fr.dm, npx * 8);
+                    const __amdgpu_buffer_rsrc_t rgba_rsrc = RAW ? make_rsrc(fr.color, npx * 3) : make_rsrc(fr.rgba, npx * 4);
+                    const __amdgpu_buffer_rsrc_t mult_rsrc = make_rsrc(p.mult, RAW ? npx * 4 : 0);
                     const bool use_color = fr.color != nullptr;
                     float pc[3];
 #pragma unroll
@@ -751,19 +746,25 @@ __global__ __launch_bounds__(64 * INT_WG, C64 ? (FAST ? OT_WAVES_PER_EU_C64 : 5)
                     float dv[BZ], mv[BZ];
 #pragma unroll
                     for (int k = 0; k < BZ; ++k) {
-#if OT_MASK_INVALID_LOADS
                         dv[k] = mv[k] = 0.0f;
-                        if (pixv[k] >= 0) {
-                            const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
-                            dv[k] = __uint_as_float(raw.x);
-                            mv[k] = __uint_as_float(raw.y);
+                        if (pixv[k] >= 0) {  // lanes projecting outside the image issue no gather
+                            if constexpr (RAW) {
+                                const unsigned short r16 = __builtin_amdgcn_raw_buffer_load_b16(dm_rsrc, pixv[k] * 2, 0, 0);
+                                mv[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(mult_rsrc, pixv[k] * 4, 0, 0));
+                                dv[k] = (float)r16;
+                            } else {
+                                const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
+                                dv[k] = __uint_as_float(raw.x);
+                                mv[k] = __uint_as_float(raw.y);
+                            }
                         }
-#else
-                        const int qx = pixv[k] < 0 ? 0 : pixv[k];
-                        const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, qx * 8, 0, 0);
-                        dv[k] = __uint_as_float(raw.x);
-                        mv[k] = __uint_as_float(raw.y);
-#endif
+                    }
+                    if constexpr (RAW) {  // Image::ConvertDepthToFloatImage, exactly as the staging computes it
+#pragma unroll
+                        for (int k = 0; k < BZ; ++k) {
+                            const float q = div_rn(dv[k], fr.scale, fr.rscale);
+                            dv[k] = ((double)q >= fr.trunc) ? 0.0f : q;
+                        }
                     }
                     // phase C: the depth test; colour gathered only by the lanes whose voxel updates
                     bool doitv[BZ];
@@ -774,7 +775,16 @@ __global__ __launch_bounds__(64 * INT_WG, C64 ? (FAST ? OT_WAVES_PER_EU_C64 : 5)
                         sdfv[k] = (dv[k] - pcz[k]) * mv[k];
                         doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
                         cv[k] = 0u;
-                        if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
+                        if (use_color && doitv[k]) {
+                            if constexpr (RAW) {
+                                const int o = pixv[k] * 3;
+                                cv[k] = (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rgba_rsrc, o, 0, 0) |
+                                        ((unsigned)__builtin_amdgcn_raw_buffer_load_b8(rgba_rsrc, o + 1, 0, 0) << 8) |
+                                        ((unsigned)__builtin_amdgcn_raw_buffer_load_b8(rgba_rsrc, o + 2, 0, 0) << 16);
+                            } else {
+                                cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
+                            }
+                        }
                     }
                     // phase D: updates in frame order (select form: identical values, no exec-mask branches)
 #pragma unroll
@@ -833,10 +843,8 @@ __global__ __launch_bounds__(64 * INT_WG, C64 ? (FAST ? OT_WAVES_PER_EU_C64 : 5)
                         upd += doit ? 1u : 0u;
                     }
                 }
-#if OT_SKIP_IDLE_STORE
                 // a slice none of whose voxels updated in this batch still holds its HBM values (fresh ones: zeros)
                 if (!fresh && !__any(upd != upd0)) continue;
-#endif
 #pragma unroll
                 for (int k = 0; k < BZ; ++k) {
                     const int vi = (z0 + k) * 256 + col;
@@ -1214,32 +1222,35 @@ static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t
     return OT_OK;
 }
 
-#ifndef OT_GRID_MULT
-#define OT_GRID_MULT 8
-#endif
-// Grid of k_batch_integrate: OT_GRID_MULT x the co-resident workgroups (cached per device; a benign race at worst
-// computes the same value twice).  A 64-frame batch of the configs[1] scan has ~12k (unit, quarter) items: at 8x
+// Grid of k_batch_integrate: INT_GRID_MULT x the co-resident workgroups (cached per device and kernel; a benign race at
+// worst computes the same value twice).  A 64-frame batch of the configs[1] scan has ~12k (unit, quarter) items: at 8x
 // (16k workgroups) nearly every workgroup takes one item and the dispatcher balances them; at 4x some take two in a
-// static stride (0.77 vs 0.72 ms per launch; 16x / 32x: 0.73 / 0.77).
-template <bool C64, bool FAST>
-static const void* integrate_kernel() {
-    return (const void*)k_batch_integrate<C64, FAST>;
+// static stride (0.77 vs 0.72 ms per launch; 6x / 12x / 16x / 32x: within 2 %, slower).
+constexpr int INT_GRID_MULT = 8;
+
+// the integrate instantiation of a batch: colour precision 64, reciprocal table, unstaged (sharded) frames
+static const void* integrate_kernel(int variant) {
+    static const void* const k[8] = {
+        (const void*)k_batch_integrate<false, false, false>, (const void*)k_batch_integrate<false, false, true>,
+        (const void*)k_batch_integrate<false, true, false>,  (const void*)k_batch_integrate<false, true, true>,
+        (const void*)k_batch_integrate<true, false, false>,  (const void*)k_batch_integrate<true, false, true>,
+        (const void*)k_batch_integrate<true, true, false>,   (const void*)k_batch_integrate<true, true, true>};
+    return k[variant & 7];
 }
 
-static int integrate_grid(bool c64, bool fast) {
-    static int cache[4][64] = {{0}};
+static int integrate_grid(int variant) {
+    static int cache[8][64] = {{0}};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 4096;
-    int* cache_c = cache[(c64 ? 2 : 0) + (fast ? 1 : 0)];
+    int* cache_c = cache[variant & 7];
     if (!cache_c[dev]) {
         int per_cu = 0, cus = 0;
-        const void* kern = c64 ? (fast ? integrate_kernel<true, true>() : integrate_kernel<true, false>())
-                               : (fast ? integrate_kernel<false, true>() : integrate_kernel<false, false>());
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * INT_WG, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, integrate_kernel(variant), 64 * INT_WG, 0) !=
+                hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 ||
             cus <= 0)
             return 4096;
-        cache_c[dev] = per_cu * cus * OT_GRID_MULT;
+        cache_c[dev] = per_cu * cus * INT_GRID_MULT;
     }
     return cache_c[dev];
 }
@@ -1249,7 +1260,11 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     ot_status st = ensure_mult(vol, &in, stream);
     if (st != OT_OK) return st;
     const int64_t npx = (int64_t)in.width * in.height;
-    if (vol->bdepth_cap < npx * n) {
+    // a spatially sharded volume integrates from the caller's raw frames (RAW kernel): no rank stages every pixel of
+    // every frame for its share of the units; needs the u16 depth path on every frame of the batch
+    bool raw = vol->dev.shard_world > 1;
+    for (int k = 0; k < n && raw; ++k) raw = frames[k].depth != nullptr;
+    if (!raw && vol->bdepth_cap < npx * n) {
         if (vol->bdm) {
             OT_HIP_TRY(hipStreamSynchronize(stream));
             OT_HIP_TRY(hipFree(vol->bdm));
@@ -1286,6 +1301,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         b.es[1] = E[1 * 4 + 2] * ip0.vl;
         b.es[2] = E[2 * 4 + 2] * ip0.vl;
         b.scale = (float)f.depth_scale;
+        b.rscale = 1.0f / b.scale;
         b.trunc = f.depth_trunc;
     }
     OT_HIP_TRY(hipMemcpyAsync(vol->bframes, host, sizeof(BatchFrame) * n, hipMemcpyHostToDevice, stream));
@@ -1298,7 +1314,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.mult = vol->mult;
     tp.npx = npx;
     tp.pc = pc;
-    tp.stage = 1;
+    tp.stage = raw ? 0 : 1;
     tp.W = in.width;
     tp.stride = vol->stride;
     tp.ws = (in.width + vol->stride - 1) / vol->stride;
@@ -1316,8 +1332,9 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc);
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
-    const bool fast = OT_RCP_TABLE && !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
-    const int grid = integrate_grid(vol->color64, fast);
+    const bool fast = !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
+    const int variant = (vol->color64 ? 4 : 0) + (fast ? 2 : 0) + (raw ? 1 : 0);
+    const int grid = integrate_grid(variant);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
         OT_HIP_TRY(hipEventCreate(&e0));
@@ -1326,14 +1343,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     }
     const BatchFrame* bf = vol->bframes;
     const UnitWork* uw = (const UnitWork*)vol->dev.work;
-    if (vol->color64 && fast)
-        hipLaunchKernelGGL((k_batch_integrate<true, true>), dim3(grid), dim3(64 * INT_WG), 0, stream, bf, ip0, vol->dev, uw, pc);
-    else if (vol->color64)
-        hipLaunchKernelGGL((k_batch_integrate<true, false>), dim3(grid), dim3(64 * INT_WG), 0, stream, bf, ip0, vol->dev, uw, pc);
-    else if (fast)
-        hipLaunchKernelGGL((k_batch_integrate<false, true>), dim3(grid), dim3(64 * INT_WG), 0, stream, bf, ip0, vol->dev, uw, pc);
-    else
-        hipLaunchKernelGGL((k_batch_integrate<false, false>), dim3(grid), dim3(64 * INT_WG), 0, stream, bf, ip0, vol->dev, uw, pc);
+    void* args[] = {(void*)&bf, (void*)&ip0, (void*)&vol->dev, (void*)&uw, (void*)&pc};
+    OT_HIP_TRY(hipLaunchKernel(integrate_kernel(variant), dim3(grid), dim3(64 * INT_WG), args, 0, stream));
     vol->batch_pc ^= 1;  // only once this batch's kernels are queued (its units kernel zeroes the other counter)
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
