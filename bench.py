@@ -242,6 +242,8 @@ def main():
     step()
     kms, klaunch = C.c_double(0.0), C.c_int64(0)
     L.call("ot_tsdf_kernel_time", vol, C.byref(kms), C.byref(klaunch))
+    fms, fbatches = C.c_double(0.0), C.c_int64(0)  # each batch's front end (staging + touch + unit headers)
+    L.call("ot_tsdf_frontend_time", vol, C.byref(fms), C.byref(fbatches))
     L.call("ot_tsdf_set_profiling", vol, 0)
 
     frames_total = world * args.frames * args.steps
@@ -276,6 +278,7 @@ def main():
     for key in ("ta_busy_frac", "td_busy_frac"):
         if ient and ient.get(key) is not None:
             roofline[key] = round(ient[key], 4)
+    roofline["frontend_ms_per_batch"] = round(fms.value / max(fbatches.value, 1), 5)
     if ient:  # raw counters and the correction applied to them (calibrated on 8-B gathers, tools/fetch_calib.hip)
         roofline["traffic_raw"] = {k: ient.get(k) for k in ("raw_fetch_kib", "raw_write_kib", "fetch_correction",
                                                             "fetch_correction_source", "write_correction")}
@@ -332,6 +335,7 @@ def main():
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
            "roofline": roofline, "cpu_baseline": cpu, "sustained": sustained, "color32": color32,
+           "spatial_amdahl": spatial_amdahl(fms.value / max(fbatches.value, 1), kernel_ms_avg),
            "filtered": filt, "objects": objects,
            "hybrid_map": hybrid, "single_frame": single, "spatial": spatial, "source_hash": L.source_hash()}
     if rank == 0:
@@ -440,6 +444,16 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
         L.call("ot_tsdf_flush", v._h, stream)
 
     dt, _ = _timed(torch, dist, world, step, args.steps)
+    # this rank's per-batch front end (undivided: staging + touch + unit headers) and integrate (divided), one step
+    L.call("ot_tsdf_set_profiling", vol._h, 1)
+    step()
+    fe, fb, ik, il = C.c_double(0.0), C.c_int64(0), C.c_double(0.0), C.c_int64(0)
+    L.call("ot_tsdf_frontend_time", vol._h, C.byref(fe), C.byref(fb))
+    L.call("ot_tsdf_kernel_time", vol._h, C.byref(ik), C.byref(il))
+    L.call("ot_tsdf_set_profiling", vol._h, 0)
+    per = torch.tensor([[fe.value / max(fb.value, 1), ik.value / max(il.value, 1)]], dtype=torch.float64,
+                       device=COLL_DEV)
+    per = Dm.all_gather_rows(per).cpu().numpy()
     nu = vol.num_units()
     cnt = Dm.all_gather_rows(torch.tensor([[nu]], dtype=torch.int64, device=COLL_DEV)).flatten().tolist()
     group = None
@@ -467,7 +481,26 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
             "scaling": "strong", "frames_per_s": round(args.frames * 1.0 / dt, 1), "ms_per_step": round(dt * 1e3, 3),
             "units_per_rank_min": min(cnt), "units_per_rank_max": max(cnt), "assemble_ms": round(t_asm * 1e3, 2),
             "assemble_bytes": border_bytes, "allgather_border_bytes": allgather_border, "whole_unit_bytes": whole,
-            "mesh_vertices": int(mesh._v.dev().shape[0]), "mesh_matches_unsharded": match}
+            "mesh_vertices": int(mesh._v.dev().shape[0]), "mesh_matches_unsharded": match,
+            "frontend_ms_per_batch_max": round(float(per[:, 0].max()), 5),
+            "integrate_ms_per_batch_max": round(float(per[:, 1].max()), 5),
+            "frontend_note": "every rank stages and unprojects every frame (undivided); the integrate divides by units"}
+
+
+def spatial_amdahl(frontend_ms, integrate_ms):
+    """Amdahl bound of ONE object spatially sharded over N GPUs, from this run's per-batch device times:
+    every rank stages every pixel of every frame and unprojects every stride sample (the front end: staging + touch +
+    unit headers; only the touch's hash inserts divide), while the integrate divides by the units each rank owns.
+    Speed-up cap at N = (F + I) / (F + I / N).  Integrating from the raw frames instead of staging them (no per-rank
+    staging) was measured: the integrate gets 1.9x slower per unit (two gathers per voxel visit instead of one), more
+    than the staging it saves."""
+    F, I = frontend_ms, integrate_ms
+    if F <= 0 or I <= 0:
+        return None
+    return {"frontend_ms_per_batch": round(F, 5), "integrate_ms_per_batch": round(I, 5),
+            "undivided_fraction": round(F / (F + I), 4),
+            "speedup_cap": {str(n): round((F + I) / (F + I / n), 2) for n in (2, 4, 8)},
+            "note": "one object over N GPUs; the weak-scaling headline (one object per GPU) is not bounded by this"}
 
 
 def single_frame(L, synth, torch, depth, color, ext, intr_t, reps=50):

@@ -199,6 +199,9 @@ ot_status ot_tsdf_get_color_precision(const ot_tsdf* vol, int32_t* bits_host);
  * number of timed launches since profiling was enabled (synchronises). */
 ot_status ot_tsdf_set_profiling(ot_tsdf* vol, int32_t enable);
 ot_status ot_tsdf_kernel_time(ot_tsdf* vol, double* total_ms_host, int64_t* launches_host);
+/* The same for each batch's front end (frame staging + unit touch + unit headers): the work every rank of a
+ * spatially sharded volume repeats for all pixels (bench.py's Amdahl bound of single-object sharding). */
+ot_status ot_tsdf_frontend_time(ot_tsdf* vol, double* total_ms_host, int64_t* batches_host);
 
 /* Dump every unit sorted by key (kx, ky, kz): keys int32 [U][3]; per unit 4096 voxels in Open3D
  * IndexOf order (x*256 + y*16 + z): tsdf f32, weight f32, color f32 [3] (0..255).  Any pointer may be

@@ -73,6 +73,7 @@ SIGNATURES = {
     "ot_tsdf_export_color64": [_p, _i64, _p, _p],
     "ot_tsdf_set_profiling": [_p, _i32],
     "ot_tsdf_kernel_time": [_p, C.POINTER(C.c_double), _pi64],
+    "ot_tsdf_frontend_time": [_p, C.POINTER(C.c_double), _pi64],
     "ot_tsdf_export_units": [_p, _i64, _p, _p, _p, _p, _p],
     "ot_tsdf_import_units": [_p, _i64, _p, _p, _p, _p, _p],
     "ot_tsdf_import_units_color64": [_p, _i64, _p, _p, _p, _p, _p],

@@ -10,15 +10,23 @@
 //   k_fb_pixels   tile of 2048 pixels of one frame: depth -> float (Open3D ConvertDepthToFloatImage), unprojection
 //                 of the valid pixels in float64 (camera_pose = inverse(extrinsic)), per-tile bounds + valid count
 //   k_fb_setup    per frame: bounds -> voxel origin (min - vs/2), key widths; one block scans the tile counts
-//   k_fb_keys     the same pixels again: voxel key (kx | ky | kz, one sort segment per frame), written by stable
+//   k_fb_keys     the same pixels again: CELL-MAJOR voxel key (the SOR cell (kx, ky, kz) >> m, then the voxel inside
+//                 the cell; one sort segment per frame), written by stable
 //                 compaction in pixel (= point index) order, value = point index, and the point's 8-B record (pixel,
 //                 raw depth, RGB8) at that index (the u64-key fallback for huge grids / batches: frame in the key,
 //                 value = global pixel index)
 //   radix sort    stable => every voxel's points stay in point-index order
 //   heads         voxel segment starts (stable compaction)
 //   k_fb_reduce   one lane per voxel: its points re-unprojected from their records (no xyz/rgb intermediates in HBM,
-//                 one 8-B gather per point), summed in index order, divided by the count (Open3D AccumulatedPoint)
-//   SOR           grid.h over all frames' voxel clouds at once (frame in the key's top bits) + sor_frames
+//                 one 8-B gather per point), summed in index order, divided by the count (Open3D AccumulatedPoint);
+//                 also the voxel's SOR cell key
+//   SOR           grid.h over all frames' voxel clouds at once (frame in the key's top bits) + sor_frames.  The SOR
+//                 cells are blocks of 2^m x 2^m x 2^m voxels on the voxel lattice (m from nb_neighbors: ~0.9 k points
+//                 per occupied cell of a surface), so the voxel order IS the grid's cell order: the grid is built
+//                 from the voxel list directly (cell heads, column hash, neighbour ranges) -- no cell keys from the
+//                 coordinates, no second sort, no re-laid-out copy of the cloud.  A frame's voxel cloud therefore
+//                 comes out in cell-major key order (Open3D's is hash order: any fixed order is as valid); the SOR
+//                 statistics sum in that order
 //   keep          stable compaction of avg > 0 && avg < threshold_f; rows gathered per frame
 #include <algorithm>
 #include <cmath>
@@ -278,13 +286,23 @@ __global__ __launch_bounds__(256) void k_fb_setup(FbParams p, int* __restrict__ 
     }
 }
 
-// voxel key = frame << vbits | (kx * ny + ky) * nz + kz: mixed radix (lexicographic (kx, ky, kz) order) over the
-// batch's largest per-axis ranges, so the radix sort runs over as few bits as the extents need
+// voxel key = frame << vbits | cell << 3m | local: cell = ((kx >> m) << (by + bz)) | ((ky >> m) << bz) | (kz >> m) on
+// the batch's largest per-axis cell ranges (bx, by, bz bits), local = (kx & M) << 2m | (ky & M) << m | (kz & M) --
+// lexicographic (cell x, y, z, then voxel x, y, z inside the cell).  key >> 3m is the SOR grid's cell key (grid.h:
+// z in the low bits), so the sorted voxels are already grouped by cell, cells of one (frame, x, y) column in z order
 struct FbKeys {
-    unsigned long long ny, nz;
-    int vbits;
-    int tag;  // u32 keys: the frame tag in bit 31 (vbits <= 31), so that adjacent frames' keys always differ
+    int m;       // log2 of the SOR cell edge in voxels
+    int by, bz;  // bits of the cell y / z fields
+    int vbits;   // key bits: bx + by + bz + 3m
+    int tag;     // u32 keys: the frame tag in bit 31 (vbits <= 31), so that adjacent frames' keys always differ
 };
+__device__ inline unsigned long long fb_voxel_key(const FbKeys& kb, unsigned long long kx, unsigned long long ky,
+                                                  unsigned long long kz) {
+    const int m = kb.m;
+    const unsigned long long M = (1ull << m) - 1ull;
+    const unsigned long long cell = ((kx >> m) << (kb.by + kb.bz)) | ((ky >> m) << kb.bz) | (kz >> m);
+    return (cell << (3 * m)) | ((kx & M) << (2 * m)) | ((ky & M) << m) | (kz & M);
+}
 
 // the tile again: voxel keys of the valid pixels, emitted in pixel order at the tile's scanned offset.  KeyT = u64:
 // the frame in the key's top bits (one sort over the batch), value = global pixel index; u32: the voxel index only
@@ -341,8 +359,8 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
             long long kk[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
-            const KeyT key = (KeyT)(fkey | (((unsigned long long)kk[0] * kb.ny + (unsigned long long)kk[1]) * kb.nz +
-                                            (unsigned long long)kk[2]));
+            const KeyT key = (KeyT)(fkey | fb_voxel_key(kb, (unsigned long long)kk[0], (unsigned long long)kk[1],
+                                                        (unsigned long long)kk[2]));
 #if OT_FB_STAGE
             s_key[loc] = key;
             if (PACKED) s_rec[loc] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k]);
@@ -378,17 +396,34 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
 // one lane per voxel: its points (sorted values, in index order) re-unprojected and summed.  PACKED: values are
 // point indices into the fb_pack records and the voxel's frame is found in the point offsets poff[0 .. F); else
 // values are global pixel indices into the depth / colour images
+// the voxel's SOR grid cell key (grid.h layout: frame << sf | cell): sorted keys k32 (u32 chain, frame tag in bit 31
+// when vbits <= 31) or k64 (frame << vbits | voxel key)
+struct FbCellKeys {
+    const unsigned* k32;
+    const unsigned long long* k64;
+    int shift;  // 3m
+    int vbits;
+    int sf;     // grid frame shift (u32 chain: the cell bits)
+    unsigned long long* out;
+};
+
 template <bool PACKED>
 __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* __restrict__ sval,
                                                    const unsigned long long* __restrict__ packed,
                                                    const int* __restrict__ poff, const int* __restrict__ heads,
                                                    int64_t K, int64_t P, double* __restrict__ vx,
-                                                   double* __restrict__ vc) {
+                                                   double* __restrict__ vc, FbCellKeys ck) {
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (s >= K) return;
     const int64_t beg = heads[s], end = (s + 1 < K) ? heads[s + 1] : P;
     const int npx = p.w * p.h;
     const int f = PACKED ? frame_of(poff, p.F, beg) : (int)(sval[beg] / (unsigned)npx);
+    if (ck.k32) {
+        const unsigned vk = ck.vbits < 32 ? (ck.k32[beg] & ((1u << ck.vbits) - 1u)) : ck.k32[beg];
+        ck.out[s] = ((unsigned long long)f << ck.sf) | (unsigned long long)(vk >> ck.shift);
+    } else {
+        ck.out[s] = ck.k64[beg] >> ck.shift;
+    }
     double m[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
@@ -703,16 +738,23 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     fl->P = P;
     fl->poff[F] = P;
     if (P == 0) return OT_OK;
-    const unsigned long long nx = (unsigned long long)hs.kbits[0] + 1, ny = (unsigned long long)hs.kbits[1] + 1,
-                             nz = (unsigned long long)hs.kbits[2] + 1;
+    // SOR cells of 2^m voxels per axis: ~0.9 k points per occupied cell of a surface sampled once per voxel
+    // (cell edge vs * sqrt(target) rounded to a power of two in ratio, ties up: the largest m <= 4 with
+    // 4^m <= 2 target; m = 2 for nb_neighbors 20; oracle.batch_cell_shift)
+    const double ctarget = sor_cell_target(fl->nb_neighbors);
+    int m = 0;
+    while (m < 4 && std::ldexp(1.0, 2 * (m + 1)) <= 2.0 * ctarget) ++m;
+    int cbits[3];
+    for (int a = 0; a < 3; ++a) {
+        cbits[a] = 0;
+        while (cbits[a] < 31 && ((hs.kbits[a] >> m) >> cbits[a]) != 0) ++cbits[a];  // bits of the largest cell index
+    }
     int fbits = 0;
     while ((1 << fbits) < F) ++fbits;
-    const double cells = (double)nx * (double)ny * (double)nz;
-    int vbits = 1;
-    while (vbits < 64 && std::ldexp(1.0, vbits) < cells) ++vbits;
+    const int vbits = std::max(1, cbits[0] + cbits[1] + cbits[2] + 3 * m);
     const int end_bit = vbits + fbits;
     if (end_bit > 63) return fail(OT_ERR_INVALID_ARGUMENT, "[VoxelDownSample] voxel grid exceeds 64-bit key packing");
-    const FbKeys kb{ny, nz, vbits, 0};
+    const FbKeys kb{m, cbits[1], cbits[2], vbits, 0};
     // ---- voxel keys in point order, stable sort ------------------------------------------------------------
     unsigned long long* kin = (unsigned long long*)fl->b_keys.get((size_t)P * 16 + 256);
     unsigned* vin = (unsigned*)fl->b_vals.get((size_t)P * 8 + 256);
@@ -770,41 +812,39 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
         hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)vout,
                            (const int*)heads, K, npx, F, d_voff);
     fl->K = K;
-    // ---- voxel averages (frame-major, key order inside a frame) ----------------------------------------------
-    double* vox = (double*)fl->b_vox.get((size_t)K * 48 + 256);
+    // ---- voxel averages (frame-major, cell-major key order inside a frame) and their SOR cell keys ------------
+    double* vox = (double*)fl->b_vox.get((size_t)K * 56 + 256);
     if (!vox) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
     fl->vx = vox;
     fl->vc = vox + K * 3;
+    unsigned long long* ckeys = (unsigned long long*)(vox + K * 6);
+    const int gsf = cbits[0] + cbits[1] + cbits[2];  // grid key: frame << gsf | cell (z in the low cbits[2] bits)
+    // sorted keys: the u32 chain's are at (unsigned*)kin + P (k32o), the u64 path's at kout
+    const FbCellKeys ck{seg32 ? (const unsigned*)kin + P : nullptr, seg32 ? nullptr : (const unsigned long long*)kout,
+                        3 * m, vbits, gsf, ckeys};
     if (pack)
         hipLaunchKernelGGL(k_fb_reduce<true>, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
                            (const unsigned*)vout, (const unsigned long long*)packed, (const int*)d_poff,
-                           (const int*)heads, K, P, fl->vx, fl->vc);
+                           (const int*)heads, K, P, fl->vx, fl->vc, ck);
     else
         hipLaunchKernelGGL(k_fb_reduce<false>, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
-                           (const unsigned*)vout, nullptr, nullptr, (const int*)heads, K, P, fl->vx, fl->vc);
+                           (const unsigned*)vout, nullptr, nullptr, (const int*)heads, K, P, fl->vx, fl->vc, ck);
     OT_LAUNCH_CHECK();
     std::vector<int> hvoff(F + 1);
     OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));
     // ---- statistical outlier removal over all frames' voxel clouds at once ----------------------------------
-    // grid origin per frame = its voxel origin (every centroid lies above it); cell h from the voxel size
-    // (~target points per occupied cell of a surface sampled once per voxel: h = vs * sqrt(target))
+    // grid origin per frame = its voxel origin, cell edge 2^m voxels: the cells are the keys' cell fields
     double* d_org = (double*)fl->b_misc.get(sizeof(double) * 3 * F + 64);
     if (!d_org) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
-    const double hcell = vs * std::sqrt(sor_cell_target(fl->nb_neighbors));
+    const double hcell = vs * (double)(1 << m);  // exact (power-of-two scaling)
     std::vector<double> horg((size_t)F * 3);
-    int dims[3] = {1, 1, 1};
     for (int f = 0; f < F; ++f)
-        for (int a = 0; a < 3; ++a) {
-            horg[f * 3 + a] = fl->h_frames[f].vmin[a];
-            if (hfb[f * 6] == ~0ull) continue;  // empty frame
-            const double span = ordered_to_dbl(hfb[f * 6 + 3 + a]) - horg[f * 3 + a];
-            dims[a] = std::max(dims[a], (int)std::floor(span / hcell) + 2);
-        }
+        for (int a = 0; a < 3; ++a) horg[f * 3 + a] = fl->h_frames[f].vmin[a];
     OT_HIP_TRY(hipMemcpyAsync(d_org, horg.data(), sizeof(double) * 3 * F, hipMemcpyHostToDevice, stream));
     GridBuild gb;
     OT_HIP_TRY(hipStreamSynchronize(stream));  // hvoff (copied above) is needed on the host from here
-    st = build_grid_frames(fl->vx, K, F, d_voff, d_org, hcell, dims, SOR_GRID_NBR, stream, gb, 25,
-                           hvoff.data());  // synchronises
+    st = build_grid_sorted(fl->vx, ckeys, K, F, d_voff, d_org, hcell, cbits, SOR_GRID_NBR, stream, gb,
+                           25);  // synchronises
     if (st != OT_OK) return st;
     for (int f = 0; f <= F; ++f) fl->voff[f] = hvoff[f];
     double* avg = (double*)fl->b_avg.get((size_t)K * 8 + (size_t)F * 32 + 256);

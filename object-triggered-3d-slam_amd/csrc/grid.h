@@ -39,7 +39,8 @@ constexpr int SOR_GRID_NBR = GRID_NBR3 | ((OT_SOR_R == 2 || OT_SOR_NBR5) ? GRID_
 
 struct GridDev {
     const double* sxyz;        // [n][3] points in sorted (frame, cell) order
-    const unsigned* sidx;      // sorted position -> point index
+    const unsigned* sidx;      // sorted position -> point index (nullptr: the identity, a presorted cloud)
+    const unsigned long long* pkey;  // sorted position -> its cell key (the cell a query's guards are measured from)
     const int* pcell;          // sorted position -> cell (position in the sorted cell list)
     const int2* nbr3;          // per cell: NBR3 column ranges
     const int2* nbr5;          // per cell: NBR5 column ranges (nullptr unless built)
@@ -69,6 +70,14 @@ struct GridBuild {
 ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int* d_foff, const double* d_origin,
                             double h, const int dims[3], int nbr, hipStream_t stream, GridBuild& out, int slot0,
                             const int* h_foff = nullptr);
+
+// The grid of a cloud already in cell order (filter_batch.hip: voxels sorted by cell-major keys): ckeys[i] = point i's
+// cell key (frame << (bits[0] + bits[1] + bits[2]) | x << (bits[1] + bits[2]) | y << bits[2] | z, non-decreasing),
+// cells of edge h at the per-frame origins; no sort, no copy (the grid reads xyz in place).  Scratch slots slot0 ..
+// slot0 + 2.  Synchronises (cell count).
+ot_status build_grid_sorted(const double* xyz, const unsigned long long* ckeys, int64_t n, int nframes,
+                            const int* d_foff, const double* d_origin, double h, const int bits[3], int nbr,
+                            hipStream_t stream, GridBuild& out, int slot0);
 
 // Statistical outlier removal over a built grid (Open3D RemoveStatisticalOutliers per frame):
 // avg[i] = mean kNN distance of point i (-1 when none); per frame the cloud mean and squared-deviation sum are

@@ -75,6 +75,16 @@ __device__ inline int2 grid_find(const GridDev& g, int f, int x, int y, int z) {
     return column_range(g, grid_column(g, f, x, y), z, z);
 }
 
+// the cell the grid assigned to sorted point j (its key): SOR measures every guard from this cell's faces, so a
+// point the rounding of its coordinates puts a hair outside its cell still gets correct (conservative) bounds
+__device__ inline void query_cell(const GridDev& g, int64_t j, int& cx, int& cy, int& cz) {
+    const unsigned long long key = g.pkey[j];
+    cz = (int)(key & ((1ull << g.sy) - 1));
+    cy = (int)((key >> g.sy) & ((1ull << (g.sx - g.sy)) - 1));
+    cx = (int)((key >> g.sx) & ((1ull << (g.sf - g.sx)) - 1));
+}
+__device__ inline int64_t sor_out(const GridDev& g, int64_t j) { return g.sidx ? (int64_t)g.sidx[j] : j; }
+
 template <typename KeyT>
 __global__ __launch_bounds__(256) void k_cell_keys(const double* __restrict__ xyz, int64_t n, GridDev g, KeyT* keys,
                                                    unsigned* idx, int* err) {
@@ -227,13 +237,14 @@ __device__ inline void topk_reset(double (&best)[KMAX], int kk) {
 
 constexpr int SOR_RMAX = 8;  // beyond this ring a query falls back to an exact scan of its frame
 
-// distance from q to the faces of its (2R+1)^3 cell block, minus a rounding margin
-__device__ inline double block_guard(const GridDev& g, const double q[3], const double* o, double R) {
+// distance from q to the faces of the (2R+1)^3 cell block around cell c, minus a rounding margin (f = q's position
+// inside c: in [0, 1) up to rounding; outside it the formula is still q's distance to the block's faces)
+__device__ inline double block_guard(const GridDev& g, const double q[3], const double* o, const int c[3], double R) {
     double guard = (R + 1.0) * g.h;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const double u = (q[a] - o[a]) / g.h;
-        const double f = u - floor(u);
+        const double f = u - (double)c[a];
         guard = fmin(guard, fmin(R + f, R + 1.0 - f) * g.h);
     }
     return guard - 1e-6 * g.h;
@@ -242,9 +253,9 @@ __device__ inline double block_guard(const GridDev& g, const double q[3], const 
 // Continue an unsettled query through the Chebyshev rings r0 .. SOR_RMAX of its cell (rings < r0 are already in the
 // list) until the k-th distance lies inside the scanned cube, else scan the whole frame from scratch.
 template <int KMAX>
-__device__ inline void sor_rings(const GridDev& g, const double q[3], const double* o, int f, int r0, int64_t fbeg,
-                                 int64_t fend, int kk, long long have, double (&best)[KMAX]) {
-    const int cx = cell_coord(q[0], o[0], g.h), cy = cell_coord(q[1], o[1], g.h), cz = cell_coord(q[2], o[2], g.h);
+__device__ inline void sor_rings(const GridDev& g, const double q[3], const double* o, int f, const int c[3], int r0,
+                                 int64_t fbeg, int64_t fend, int kk, long long have, double (&best)[KMAX]) {
+    const int cx = c[0], cy = c[1], cz = c[2];
     for (int r = r0; r <= SOR_RMAX; ++r) {
         for (int dx = -r; dx <= r; ++dx)
             for (int dy = -r; dy <= r; ++dy) {
@@ -255,7 +266,7 @@ __device__ inline void sor_rings(const GridDev& g, const double q[3], const doub
                     have += se.y - se.x;
                 }
             }
-        const double guard = block_guard(g, q, o, (double)r);
+        const double guard = block_guard(g, q, o, c, (double)r);
         if (have >= fend - fbeg || (best[KMAX - 1] < INFINITY && best[KMAX - 1] <= guard * guard)) return;
     }
     topk_reset<KMAX>(best, kk);
@@ -294,11 +305,12 @@ __device__ inline double sor_mean(const double (&best)[KMAX], int kk) {
 __device__ inline double face_gap(double lo, double hi, int d, double h) {
     return d < 0 ? lo + (double)(-d - 1) * h : (d > 0 ? hi + (double)(d - 1) * h : 0.0);
 }
-__device__ inline void cell_fracs(const GridDev& g, const double q[3], const double* o, double lo[3], double hi[3]) {
+__device__ inline void cell_fracs(const GridDev& g, const double q[3], const double* o, const int c[3], double lo[3],
+                                  double hi[3]) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const double uu = (q[a] - o[a]) / g.h;
-        const double fr = uu - floor(uu);
+        const double fr = uu - (double)c[a];  // q's place in its cell c (distances below clamp at 0 outside it)
         lo[a] = fmax(fr * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
         hi[a] = fmax((1.0 - fr) * g.h * (1.0 - 1e-9) - 1e-12 * g.h, 0.0);
     }
@@ -332,8 +344,10 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     topk_reset<KMAX>(best, kk);
     const int c = g.pcell[j];
     const int2* rr = (R == 1 ? g.nbr3 + (int64_t)c * NBR3 : g.nbr5 + (int64_t)c * NBR5);
+    int cc[3];
+    query_cell(g, j, cc[0], cc[1], cc[2]);
     double lo[3], hi[3];
-    cell_fracs(g, q, o, lo, hi);
+    cell_fracs(g, q, o, cc, lo, hi);
     long long have = 0;
     for (int u = 0; u < W * W; ++u) {
         const int t = R == 1 ? c_cols3[u] : c_cols5[u];
@@ -343,9 +357,9 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
         if (!(ex * ex + ey * ey >= best[KMAX - 1])) scan_range<KMAX>(g.sxyz, q, se.x, se.y, best);
         have += se.y - se.x;
     }
-    const double guard = block_guard(g, q, o, (double)R);
+    const double guard = block_guard(g, q, o, cc, (double)R);
     if (have >= fend - fbeg || (have >= kk && best[KMAX - 1] <= guard * guard)) {
-        avg[g.sidx[j]] = sor_mean<KMAX>(best, kk);
+        avg[sor_out(g, j)] = sor_mean<KMAX>(best, kk);
         return;
     }
     const unsigned long long m = __ballot(1);  // the wave's unsettled lanes: one atomic per wave
@@ -379,11 +393,13 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
         long long have = pd.have[s];
         bool settled = false;
         int rnext = R + 1;
+        int cc[3];
+        query_cell(g, j, cc[0], cc[1], cc[2]);
         if (R == 1) {
             const int c = g.pcell[j];
-            const int cx = cell_coord(q[0], o[0], g.h), cy = cell_coord(q[1], o[1], g.h), cz = g.cz[c];
+            const int cx = cc[0], cy = cc[1], cz = cc[2];
             double lo[3], hi[3];
-            cell_fracs(g, q, o, lo, hi);
+            cell_fracs(g, q, o, cc, lo, hi);
             const int2* r5 = g.nbr5 ? g.nbr5 + (int64_t)c * NBR5 : nullptr;
             const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
             bool counted_all = true;  // have counts every point of the 5x5x5 block
@@ -417,7 +433,7 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
                     have += full.y - full.x;
                 }
             }
-            const double guard = block_guard(g, q, o, 2.0);
+            const double guard = block_guard(g, q, o, cc, 2.0);
             // the list is full exactly when kk points were scanned (nothing is skipped while the k-th distance is
             // infinite); a skipped column lies beyond the k-th distance
             settled = (counted_all && have >= fend - fbeg) ||
@@ -435,9 +451,9 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
                 for (int i = 0; i < KMAX; ++i) pd3.best[(int64_t)i * pd3.cap + s3] = best[i];
                 continue;
             }
-            sor_rings<KMAX>(g, q, o, f, rnext, fbeg, fend, kk, have, best);
+            sor_rings<KMAX>(g, q, o, f, cc, rnext, fbeg, fend, kk, have, best);
         }
-        avg[g.sidx[j]] = sor_mean<KMAX>(best, kk);
+        avg[sor_out(g, j)] = sor_mean<KMAX>(best, kk);
     }
 }
 
@@ -498,9 +514,11 @@ __global__ __launch_bounds__(64) void k_sor_knn_wave(GridDev g, int k, double* a
             for (int i = 64; i < KMAX; ++i) gl[i] = pd3.best[(int64_t)i * pd3.cap + s];
         __syncthreads();
         long long have = pd3.have[s];  // < 0: not every point of the scanned cube was counted
-        const int cx = cell_coord(q[0], o[0], g.h), cy = cell_coord(q[1], o[1], g.h), cz = cell_coord(q[2], o[2], g.h);
+        int cc[3];
+        query_cell(g, j, cc[0], cc[1], cc[2]);
+        const int cx = cc[0], cy = cc[1], cz = cc[2];
         double lo[3], hi[3];
-        cell_fracs(g, q, o, lo, hi);
+        cell_fracs(g, q, o, cc, lo, hi);
         double L[KMAX];
         bool settled = false;
         for (int r = 3; r <= SOR_RMAX3 && !settled; ++r) {
@@ -548,7 +566,7 @@ __global__ __launch_bounds__(64) void k_sor_knn_wave(GridDev g, int k, double* a
             wave_merge<KMAX>(lds, gl, L, kk);
             if (__any(cull)) have = -1;
             if (have >= 0) have += wave_sum(hl);
-            const double guard = block_guard(g, q, o, (double)r);
+            const double guard = block_guard(g, q, o, cc, (double)r);
             const double kth = gl[KMAX - 1];
             settled = have >= fend - fbeg || (kth < INFINITY && kth <= guard * guard);
         }
@@ -564,7 +582,7 @@ __global__ __launch_bounds__(64) void k_sor_knn_wave(GridDev g, int k, double* a
             double best[KMAX];
 #pragma unroll
             for (int i = 0; i < KMAX; ++i) best[i] = gl[i];
-            avg[g.sidx[j]] = sor_mean<KMAX>(best, kk);
+            avg[sor_out(g, j)] = sor_mean<KMAX>(best, kk);
         }
         __syncthreads();  // gl is reloaded for the next query
     }
@@ -608,6 +626,7 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
     bool settled = false;
     const int cx = cell_coord(qc[0], g.origin[0], g.h), cy = cell_coord(qc[1], g.origin[1], g.h),
               cz = cell_coord(qc[2], g.origin[2], g.h);
+    const int cq[3] = {cx, cy, cz};  // q's own cell (a query, not a grid point: its cell is computed, as the grid's)
     if (off2 == 0.0) {
         int c;
         grid_cell_range(g, cx, cy, cz, c);
@@ -617,7 +636,7 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
                 const int2 se = r3[(u + 4) % NBR3];
                 nn_range(g, q, se.x, se.y, best);
             }
-            double guard = block_guard(g, q, g.origin, 1.0);
+            double guard = block_guard(g, q, g.origin, cq, 1.0);
             settled = best <= guard * guard;
             if (!settled) {
                 const int czc = g.cz[c];
@@ -634,7 +653,7 @@ __global__ __launch_bounds__(256) void k_nn_dist(GridDev g, const double* __rest
                         nn_range(g, q, r.x, r.y, best);
                     }
                 }
-                guard = block_guard(g, q, g.origin, 2.0);
+                guard = block_guard(g, q, g.origin, cq, 2.0);
                 settled = best <= guard * guard;
             }
         }
@@ -840,6 +859,68 @@ ot_status build_grid_frames(const double* xyz, int64_t n, int nframes, const int
     OT_LAUNCH_CHECK();
     g.sxyz = sxyz;
     g.sidx = vout;
+    g.pkey = kout;
+    g.pcell = pcell;
+    g.nbr3 = nbr3;
+    g.nbr5 = nbr5;
+    out.ncells = ncells;
+    return OT_OK;
+}
+
+ot_status build_grid_sorted(const double* xyz, const unsigned long long* ckeys, int64_t n, int nframes,
+                            const int* d_foff, const double* d_origin, double h, const int bits[3], int nbr,
+                            hipStream_t stream, GridBuild& out, int slot0) {
+    GridDev& g = out.g;
+    g.h = h;
+    g.origin = d_origin;
+    g.foff = d_foff;
+    g.nframes = nframes;
+    for (int a = 0; a < 3; ++a) {
+        if (bits[a] < 0 || bits[a] > 20)
+            return fail(OT_ERR_INVALID_ARGUMENT, "neighbour grid out of range (radius too small for the extent)");
+        g.dim[a] = 1 << bits[a];
+    }
+    g.sy = bits[2];
+    g.sx = bits[1] + bits[2];
+    g.sf = bits[0] + bits[1] + bits[2];
+    char* ws = (char*)scratch(256 + (size_t)n * 8, slot0);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    int* heads = (int*)ws;
+    int* pcell = heads + n;
+    int64_t ncells = 0;
+    ot_status st = compact_segments(n, ckeys, heads, pcell, stream, &ncells, slot0 + 1);  // synchronises
+    if (st != OT_OK) return st;
+    int64_t cap = 1;
+    while (cap < 2 * ncells + 2) cap <<= 1;
+    const bool w3 = nbr & GRID_NBR3, w5 = nbr & GRID_NBR5;
+    const size_t per_cell = (w3 ? NBR3 * 8 : 0) + (w5 ? NBR5 * 8 : 0) + 12;
+    char* hs = (char*)scratch((size_t)cap * (8 + 8) + (size_t)ncells * per_cell + 128, slot0 + 2);
+    if (!hs) return fail(OT_ERR_HIP, "scratch allocation failed");
+    g.hkeys = (unsigned long long*)hs;
+    g.hval = (int2*)(g.hkeys + cap);
+    int2* cur = g.hval + cap;
+    int2* nbr3 = w3 ? cur : nullptr;
+    cur += w3 ? ncells * NBR3 : 0;
+    int2* nbr5 = w5 ? cur : nullptr;
+    cur += w5 ? ncells * NBR5 : 0;
+    g.crange = cur;
+    g.cz = (int*)(g.crange + ncells);
+    g.hash_mask = (int)(cap - 1);
+    OT_HIP_TRY(hipMemsetAsync(g.hkeys, 0xFF, sizeof(unsigned long long) * cap, stream));
+    if (ncells > 0) {
+        hipLaunchKernelGGL(k_grid_insert, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, stream, ckeys, heads,
+                           ncells, n, g);
+        if (w5)
+            hipLaunchKernelGGL(k_cell_nbr<2>, dim3((unsigned)((ncells * NBR5 + 255) / 256)), dim3(256), 0, stream,
+                               ckeys, heads, ncells, g, nbr3, nbr5);
+        else if (w3)
+            hipLaunchKernelGGL(k_cell_nbr<1>, dim3((unsigned)((ncells * NBR3 + 255) / 256)), dim3(256), 0, stream,
+                               ckeys, heads, ncells, g, nbr3, nbr5);
+        OT_LAUNCH_CHECK();
+    }
+    g.sxyz = xyz;
+    g.sidx = nullptr;
+    g.pkey = ckeys;
     g.pcell = pcell;
     g.nbr3 = nbr3;
     g.nbr5 = nbr5;

@@ -115,13 +115,12 @@ struct BatchFrame {
     const uint16_t* depth16;  // raw depth (u16 path) or nullptr
     const float* depthf;      // caller's float depth (float path) or nullptr
     const uint8_t* color;     // caller's RGB8 or nullptr
-    float2* dm;               // packed per-pixel (depth, ray multiplier) written by k_batch_prep
-    uint32_t* rgba;           // packed per-pixel colour r | g << 8 | b << 16 written by k_batch_prep
+    float2* dm;               // packed per-pixel (depth, ray multiplier) staged by k_batch_touch
+    uint32_t* rgba;           // packed per-pixel colour r | g << 8 | b << 16 staged by k_batch_touch
     double pose[12];          // rows 0..2 of inverse(extrinsic) (stride unprojection, float64)
     float E[12];              // rows 0..2 of (float)extrinsic
     float es[3];              // column 2 of (float)extrinsic * voxel_length
     float scale;              // (float)depth_scale
-    float rscale;             // fl(1 / scale): div_rn's reciprocal (RAW integrate)
     double trunc;             // depth_trunc
 };
 
@@ -202,6 +201,10 @@ struct ot_tsdf {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
     double prof_ms = 0.0;
     int64_t prof_launches = 0;
+    // and around each batch's front end (staging + touch + units), the part a sharded volume does not divide
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_fe_events;
+    double prof_fe_ms = 0.0;
+    int64_t prof_fe_batches = 0;
 };
 
 namespace ot {

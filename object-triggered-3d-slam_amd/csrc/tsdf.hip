@@ -382,7 +382,6 @@ struct BatchTouchParams {
     const float* mult;  // fused staging (k_batch_touch stages the batch's pixels too): ray multipliers
     int64_t npx;        // pixels per frame
     int pc;             // this batch's pair counter index
-    int stage;          // 1: stage the batch's (depth, multiplier) / colour pixels for the integrate; 0: it reads raw
 };
 
 __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int pc, int x, int y, int z) {
@@ -448,8 +447,10 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
     if (tid == 0) s_nused = 0;
     // Fused staging: this workgroup also stages a contiguous 1/gridDim.x of the pixels of each of its frames (the
     // touch below reads raw depth itself, so nothing here waits on these stores; as a separate launch the staging
-    // measured 7 us slower per 64 frames)
-    if (p.stage) {
+    // measured 7 us slower per 64 frames).  Every rank of a spatially sharded volume stages every pixel:
+    // integrating from the raw frames instead (a u16 depth + a multiplier-table gather per voxel visit) made the
+    // integrate 1.9x slower per unit (round 4, tools/shard_frontend.py), more than the staging it saves
+    {
         const int64_t quads = (p.npx + 3) >> 2;
         const int64_t per = (quads + gridDim.x - 1) / gridDim.x;
         const int64_t q0 = (int64_t)blockIdx.x * per, q1 = q0 + per < quads ? q0 + per : quads;
@@ -610,12 +611,7 @@ constexpr int RCP_N = 2048;  // 16 KiB (float64) / 8 KiB (float32) of LDS per wo
 // whatever its registers); the parts of a unit run on one XCD.  Work items are assigned by a static grid stride that
 // every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes.
-// RAW: the frames were not staged (a spatially sharded volume: every rank would otherwise stage every pixel of every
-// frame for its share of the units); a voxel visit gathers the caller's u16 depth (converted as
-// Image::ConvertDepthToFloatImage: div_rn = the IEEE quotient, checked over every u16 value), the frame-independent
-// ray multiplier (the volume's cached table) and, for updating lanes, the caller's three RGB8 bytes.  Same values,
-// bit for bit, as the staged (depth, multiplier) / colour words.
-template <bool C64, bool FAST, bool RAW>
+template <bool C64, bool FAST>
 __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
     using CT = typename std::conditional<C64, double, float>::type;
@@ -692,11 +688,8 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                 for (unsigned long long m = mask; m; m &= m - 1) {
                     const int f = __ffsll((long long)m) - 1;
                     const BatchFrame& fr = frames[f];
-                    // staged: (depth, multiplier) words and packed colours; RAW: the caller's u16 depth and RGB8
-                    // bytes plus the volume's multiplier table
-                    const __amdgpu_buffer_rsrc_t dm_rsrc = RAW ? make_rsrc(fr.depth16, npx * 2) : make_rsrc(fr.dm, npx * 8);
-                    const __amdgpu_buffer_rsrc_t rgba_rsrc = RAW ? make_rsrc(fr.color, npx * 3) : make_rsrc(fr.rgba, npx * 4);
-                    const __amdgpu_buffer_rsrc_t mult_rsrc = make_rsrc(p.mult, RAW ? npx * 4 : 0);
+                    const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(fr.dm, npx * 8);
+                    const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
                     const bool use_color = fr.color != nullptr;
                     float pc[3];
 #pragma unroll
@@ -748,22 +741,9 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                     for (int k = 0; k < BZ; ++k) {
                         dv[k] = mv[k] = 0.0f;
                         if (pixv[k] >= 0) {  // lanes projecting outside the image issue no gather
-                            if constexpr (RAW) {
-                                const unsigned short r16 = __builtin_amdgcn_raw_buffer_load_b16(dm_rsrc, pixv[k] * 2, 0, 0);
-                                mv[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(mult_rsrc, pixv[k] * 4, 0, 0));
-                                dv[k] = (float)r16;
-                            } else {
-                                const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
-                                dv[k] = __uint_as_float(raw.x);
-                                mv[k] = __uint_as_float(raw.y);
-                            }
-                        }
-                    }
-                    if constexpr (RAW) {  // Image::ConvertDepthToFloatImage, exactly as the staging computes it
-#pragma unroll
-                        for (int k = 0; k < BZ; ++k) {
-                            const float q = div_rn(dv[k], fr.scale, fr.rscale);
-                            dv[k] = ((double)q >= fr.trunc) ? 0.0f : q;
+                            const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
+                            dv[k] = __uint_as_float(raw.x);
+                            mv[k] = __uint_as_float(raw.y);
                         }
                     }
                     // phase C: the depth test; colour gathered only by the lanes whose voxel updates
@@ -775,16 +755,7 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                         sdfv[k] = (dv[k] - pcz[k]) * mv[k];
                         doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
                         cv[k] = 0u;
-                        if (use_color && doitv[k]) {
-                            if constexpr (RAW) {
-                                const int o = pixv[k] * 3;
-                                cv[k] = (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rgba_rsrc, o, 0, 0) |
-                                        ((unsigned)__builtin_amdgcn_raw_buffer_load_b8(rgba_rsrc, o + 1, 0, 0) << 8) |
-                                        ((unsigned)__builtin_amdgcn_raw_buffer_load_b8(rgba_rsrc, o + 2, 0, 0) << 16);
-                            } else {
-                                cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
-                            }
-                        }
+                        if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
                     }
                     // phase D: updates in frame order (select form: identical values, no exec-mask branches)
 #pragma unroll
@@ -1228,21 +1199,18 @@ static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t
 // static stride (0.77 vs 0.72 ms per launch; 6x / 12x / 16x / 32x: within 2 %, slower).
 constexpr int INT_GRID_MULT = 8;
 
-// the integrate instantiation of a batch: colour precision 64, reciprocal table, unstaged (sharded) frames
+// the integrate instantiation of a batch: colour precision 64 (bit 1), reciprocal table (bit 0)
 static const void* integrate_kernel(int variant) {
-    static const void* const k[8] = {
-        (const void*)k_batch_integrate<false, false, false>, (const void*)k_batch_integrate<false, false, true>,
-        (const void*)k_batch_integrate<false, true, false>,  (const void*)k_batch_integrate<false, true, true>,
-        (const void*)k_batch_integrate<true, false, false>,  (const void*)k_batch_integrate<true, false, true>,
-        (const void*)k_batch_integrate<true, true, false>,   (const void*)k_batch_integrate<true, true, true>};
-    return k[variant & 7];
+    static const void* const k[4] = {(const void*)k_batch_integrate<false, false>, (const void*)k_batch_integrate<false, true>,
+                                     (const void*)k_batch_integrate<true, false>, (const void*)k_batch_integrate<true, true>};
+    return k[variant & 3];
 }
 
 static int integrate_grid(int variant) {
-    static int cache[8][64] = {{0}};
+    static int cache[4][64] = {{0}};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 4096;
-    int* cache_c = cache[variant & 7];
+    int* cache_c = cache[variant & 3];
     if (!cache_c[dev]) {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, integrate_kernel(variant), 64 * INT_WG, 0) !=
@@ -1260,11 +1228,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     ot_status st = ensure_mult(vol, &in, stream);
     if (st != OT_OK) return st;
     const int64_t npx = (int64_t)in.width * in.height;
-    // a spatially sharded volume integrates from the caller's raw frames (RAW kernel): no rank stages every pixel of
-    // every frame for its share of the units; needs the u16 depth path on every frame of the batch
-    bool raw = vol->dev.shard_world > 1;
-    for (int k = 0; k < n && raw; ++k) raw = frames[k].depth != nullptr;
-    if (!raw && vol->bdepth_cap < npx * n) {
+    if (vol->bdepth_cap < npx * n) {
         if (vol->bdm) {
             OT_HIP_TRY(hipStreamSynchronize(stream));
             OT_HIP_TRY(hipFree(vol->bdm));
@@ -1301,7 +1265,6 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         b.es[1] = E[1 * 4 + 2] * ip0.vl;
         b.es[2] = E[2 * 4 + 2] * ip0.vl;
         b.scale = (float)f.depth_scale;
-        b.rscale = 1.0f / b.scale;
         b.trunc = f.depth_trunc;
     }
     OT_HIP_TRY(hipMemcpyAsync(vol->bframes, host, sizeof(BatchFrame) * n, hipMemcpyHostToDevice, stream));
@@ -1314,7 +1277,6 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.mult = vol->mult;
     tp.npx = npx;
     tp.pc = pc;
-    tp.stage = raw ? 0 : 1;
     tp.W = in.width;
     tp.stride = vol->stride;
     tp.ws = (in.width + vol->stride - 1) / vol->stride;
@@ -1327,16 +1289,24 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.unit_len = vol->unit_length;
     tp.slot_cap = (int)vol->hash_cap;
     const unsigned tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
+    hipEvent_t f0 = nullptr, f1 = nullptr;  // front end (staging + touch + units): the part a sharded volume repeats
+    if (vol->profiling) {
+        OT_HIP_TRY(hipEventCreate(&f0));
+        OT_HIP_TRY(hipEventCreate(&f1));
+        OT_HIP_TRY(hipEventRecord(f0, stream));
+    }
     hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, tp, vol->dev, n);
     hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc);
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
     const bool fast = !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
-    const int variant = (vol->color64 ? 4 : 0) + (fast ? 2 : 0) + (raw ? 1 : 0);
+    const int variant = (vol->color64 ? 2 : 0) + (fast ? 1 : 0);
     const int grid = integrate_grid(variant);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
+        OT_HIP_TRY(hipEventRecord(f1, stream));
+        vol->prof_fe_events.emplace_back(f0, f1);
         OT_HIP_TRY(hipEventCreate(&e0));
         OT_HIP_TRY(hipEventCreate(&e1));
         OT_HIP_TRY(hipEventRecord(e0, stream));
@@ -1714,13 +1684,30 @@ ot_status ot_tsdf_get_color_precision(const ot_tsdf* vol, int32_t* bits) {
 ot_status ot_tsdf_set_profiling(ot_tsdf* vol, int32_t enable) {
     if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     vol->profiling = enable != 0;
-    vol->prof_ms = 0.0;
-    vol->prof_launches = 0;
-    for (auto& e : vol->prof_events) {
+    vol->prof_ms = vol->prof_fe_ms = 0.0;
+    vol->prof_launches = vol->prof_fe_batches = 0;
+    for (auto* lst : {&vol->prof_events, &vol->prof_fe_events}) {
+        for (auto& e : *lst) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        lst->clear();
+    }
+    return OT_OK;
+}
+
+// accumulate (and release) an event-pair list into (ms, count)
+static ot_status drain_events(std::vector<std::pair<hipEvent_t, hipEvent_t>>& lst, double& ms_acc, int64_t& n_acc) {
+    for (auto& e : lst) {
+        OT_HIP_TRY(hipEventSynchronize(e.second));
+        float ms = 0.0f;
+        OT_HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second));
+        ms_acc += ms;
+        n_acc += 1;
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
-    vol->prof_events.clear();
+    lst.clear();
     return OT_OK;
 }
 
@@ -1728,18 +1715,19 @@ ot_status ot_tsdf_kernel_time(ot_tsdf* vol, double* total_ms, int64_t* launches)
     if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     ot_status st = tsdf_flush(vol, nullptr);
     if (st != OT_OK) return st;
-    for (auto& e : vol->prof_events) {
-        OT_HIP_TRY(hipEventSynchronize(e.second));
-        float ms = 0.0f;
-        OT_HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second));
-        vol->prof_ms += ms;
-        vol->prof_launches += 1;
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
-    }
-    vol->prof_events.clear();
+    if ((st = drain_events(vol->prof_events, vol->prof_ms, vol->prof_launches)) != OT_OK) return st;
     if (total_ms) *total_ms = vol->prof_ms;
     if (launches) *launches = vol->prof_launches;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_frontend_time(ot_tsdf* vol, double* total_ms, int64_t* batches) {
+    if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    ot_status st = tsdf_flush(vol, nullptr);
+    if (st != OT_OK) return st;
+    if ((st = drain_events(vol->prof_fe_events, vol->prof_fe_ms, vol->prof_fe_batches)) != OT_OK) return st;
+    if (total_ms) *total_ms = vol->prof_fe_ms;
+    if (batches) *batches = vol->prof_fe_batches;
     return OT_OK;
 }
 

@@ -213,6 +213,26 @@ def filter_min_z(xyz, rgb, zmin):
     return ox[:k].copy(), (oc[:k].copy() if oc is not None else None)
 
 
+def batch_cell_shift(nb_neighbors):
+    """log2 of the SOR cell edge in voxels of the batched configs[2] chain (filter_batch.hip fb_cell_shift): the
+    largest m <= 4 with 4^m <= 2 t, t = max(0.9 k, 2) -- the power of two nearest sqrt(t) in ratio (ties up); 2 for
+    nb_neighbors = 20."""
+    t = max(0.9 * nb_neighbors, 2.0)
+    m = 0
+    while m < 4 and 4.0 ** (m + 1) <= 2.0 * t:
+        m += 1
+    return m
+
+
+def cell_major_order(keys, m):
+    """Permutation that puts a voxel cloud (voxel_down_sample's integer keys (kx, ky, kz), any order) in the batched
+    chain's canonical order: lexicographic by the cell (kx, ky, kz) >> m, then by the voxel inside the cell.  Open3D
+    emits its voxels in hash-map order; the batch's order is the SOR grid's cell order (filter_batch.hip)."""
+    k = np.asarray(keys, np.int64).reshape(-1, 3)
+    c, l = k >> m, k & ((1 << m) - 1)
+    return np.lexsort((l[:, 2], l[:, 1], l[:, 0], c[:, 2], c[:, 1], c[:, 0]))
+
+
 def remove_statistical_outlier(xyz, nb_neighbors, std_ratio):
     p = _c(xyz, np.float64)
     n = p.shape[0]

@@ -17,9 +17,15 @@ from conftest import assert_bitwise
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_chain(O, depth, color, ext, intr_t, trunc=5.0, vs=0.005, k=20, ratio=2.0, scale=1000.0):
+def _oracle_chain(O, depth, color, ext, intr_t, trunc=5.0, vs=0.005, k=20, ratio=2.0, scale=1000.0, batch=True):
+    """The oracle's per-frame chain.  batch=True: the voxel cloud in the batched chain's canonical order (cell-major
+    keys, oracle.cell_major_order; Open3D's own order is hash-map order), the SOR run on that order (its cloud
+    statistics sum in cloud order); batch=False: voxel_down_sample's key order, as the per-call facade."""
     xyz, rgb = O.unproject(O.depth_to_float(depth, scale, trunc), color, intr_t, ext)
-    v, vc, _, _ = O.voxel_down_sample(xyz, rgb, vs)
+    v, vc, keys, _ = O.voxel_down_sample(xyz, rgb, vs)
+    if batch:
+        perm = O.cell_major_order(keys, O.batch_cell_shift(k))
+        v, vc = v[perm], vc[perm]
     idx, avg = O.remove_statistical_outlier(v, k, ratio)
     return xyz.shape[0], v, vc, avg, idx
 
@@ -36,9 +42,10 @@ def hd_oracle(O, synth, hd_frames):
     return [_oracle_chain(O, depth[f], color[f], ext[f], synth.REF_INTRINSICS_1280) for f in range(depth.shape[0])]
 
 
-def test_hd_chain_per_call_bitexact(pkg, synth, hd_frames, hd_oracle, gpu):
+def test_hd_chain_per_call_bitexact(pkg, O, synth, hd_frames, gpu):
     """VERDICT r1 'Next' 1: the HIP unproject -> voxel -> SOR chain on one full 1280x720 frame, Open3D-shaped calls."""
     depth, color, ext = hd_frames
+    hd_oracle = [_oracle_chain(O, depth[0], color[0], ext[0], synth.REF_INTRINSICS_1280, batch=False)]
     intr = pkg.camera.PinholeCameraIntrinsic(*synth.REF_INTRINSICS_1280)
     rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
         pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), depth_scale=1000.0, depth_trunc=5.0,
@@ -171,35 +178,37 @@ def test_batch_matches_per_call_ragged(pkg, O, synth, gpu):
             pkg.geometry.Image(color[f]), pkg.geometry.Image(depth[f]), depth_scale=1000.0, depth_trunc=3.0,
             convert_rgb_to_intensity=False)
         down = pkg.geometry.PointCloud.create_from_rgbd_image(rgbd, intr, ext[f]).voxel_down_sample(0.005)
-        kept, ind = down.remove_statistical_outlier(20, 2.0)
+        P, v, vc, avg, idx = _oracle_chain(O, depth[f], color[f], ext[f], intr_t, trunc=3.0)
         bdown, _ = flt.voxel_cloud(f)
         bkept, bind = flt.frame(f)
-        assert_bitwise(np.asarray(bdown.points), np.asarray(down.points).reshape(-1, 3), f"ragged voxels (frame {f})")
-        assert bind == ind, f"ragged kept indices (frame {f})"
-        assert_bitwise(np.asarray(bkept.points), np.asarray(kept.points).reshape(-1, 3), f"ragged kept (frame {f})")
+        # the same voxels as the per-call chain (as a set: the batch emits them in cell-major order) ...
+        dp = np.asarray(down.points).reshape(-1, 3)
+        bp = np.asarray(bdown.points).reshape(-1, 3)
+        assert_bitwise(bp[np.lexsort(bp.T[::-1])], dp[np.lexsort(dp.T[::-1])], f"ragged voxel set (frame {f})")
+        # ... and in that order exactly the oracle chain's
+        assert_bitwise(bp, v.reshape(-1, 3), f"ragged voxels (frame {f})")
+        assert bind == idx.tolist(), f"ragged kept indices (frame {f})"
+        assert_bitwise(np.asarray(bkept.points).reshape(-1, 3), v.reshape(-1, 3)[idx], f"ragged kept (frame {f})")
     assert flt.voxel_offsets[3] == flt.voxel_offsets[2]  # the empty frame
     # a second run on 2 frames reuses the handle
     flt.run(depth[:2], color[:2], ext[:2])
     assert flt.n_frames == 2 and flt.kept_offsets[2] == flt.kept
 
 
-def test_batch_wide_keys_match_per_call(pkg, synth, gpu):
+def test_batch_wide_keys_match_per_call(pkg, O, synth, gpu):
     """A 0.4 mm voxel makes the voxel key wider than 32 bits: the batch takes its 64-bit-key path (frame in the
     key) and must still equal the per-frame calls."""
     intr_t = synth.REF_INTRINSICS_640
     depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=16, frames=[2, 11])
-    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
-    flt = pkg.filters.RGBDFilterBatch(intr, max_frames=2, depth_trunc=5.0, voxel_size=0.0004).run(depth, color, ext)
+    flt = pkg.filters.RGBDFilterBatch(pkg.camera.PinholeCameraIntrinsic(*intr_t), max_frames=2, depth_trunc=5.0,
+                                      voxel_size=0.0004).run(depth, color, ext)
     for f in range(2):
-        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
-            pkg.geometry.Image(color[f]), pkg.geometry.Image(depth[f]), depth_scale=1000.0, depth_trunc=5.0,
-            convert_rgb_to_intensity=False)
-        down = pkg.geometry.PointCloud.create_from_rgbd_image(rgbd, intr, ext[f]).voxel_down_sample(0.0004)
-        kept, ind = down.remove_statistical_outlier(20, 2.0)
-        bdown, _ = flt.voxel_cloud(f)
+        P, v, vc, avg, idx = _oracle_chain(O, depth[f], color[f], ext[f], intr_t, vs=0.0004)
+        bdown, davg = flt.voxel_cloud(f)
         bkept, bind = flt.frame(f)
-        assert_bitwise(np.asarray(bdown.points), np.asarray(down.points), f"wide-key voxels (frame {f})")
-        assert bind == ind, f"wide-key kept indices (frame {f})"
+        assert_bitwise(np.asarray(bdown.points), v, f"wide-key voxels (frame {f})")
+        assert_bitwise(davg, avg, f"wide-key mean kNN distances (frame {f})")
+        assert bind == idx.tolist(), f"wide-key kept indices (frame {f})"
 
 
 def test_batch_sparse_tail(pkg, O, synth, gpu):
@@ -280,10 +289,9 @@ def test_batch_tiny_images_many_frames(pkg, O, synth, gpu):
 
 
 def test_batch_far_clusters(pkg, O, synth, gpu):
-    """Voxel-column SOR (outlier.hip sor_voxel_frames) at its limits: a 4-voxel cluster 3.5 m behind a 30x30-pixel
-    patch needs neighbours beyond every bounded box (the whole-frame scan of stage 3), a frame of one cluster whose
-    columns run along the viewing axis (identity pose: long kz runs, the binary-searched windows), and a frame of a
-    single pixel (k > points)."""
+    """SOR at its limits: a 4-voxel cluster 3.5 m behind a 30x30-pixel patch needs neighbours beyond every bounded
+    box (the whole-frame scan of stage 3), a frame of one cluster stretched along the viewing axis (identity pose: long
+    z columns of cells), and a frame of a single pixel (k > points)."""
     intr_t = synth.REF_INTRINSICS_640
     depth = np.zeros((3, 480, 640), np.uint16)
     depth[0, 200:230, 300:330] = 1000

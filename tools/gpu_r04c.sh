@@ -1,0 +1,23 @@
+#!/bin/bash
+# r04c: configs[2] with cell-major voxel keys (the SOR grid built from the voxel order): filter parity tests, the
+# isolated chain timing + rocprofv3 breakdown, then every -m gpu test and the bench line.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+T=${TAG:-r04c}
+timeout -k 10 600 python -u -m pytest tests/test_gpu_filter_batch.py tests/test_gpu_filters.py -m gpu -x -q --timeout 300 \
+  --timeout-method thread > gpurun_out/${T}_filter_tests.log 2>&1 || { echo FILTER_TESTS_FAILED; tail -40 gpurun_out/${T}_filter_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_filter_tests.log
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+timeout -k 10 240 python3 -u tools/filter_batch_time.py --frames 64 --batches 32 --reps 3 > gpurun_out/${T}_fb_time.log 2>&1 || { echo FBTIME_FAILED; tail -20 gpurun_out/${T}_fb_time.log; exit 1; }
+cat gpurun_out/${T}_fb_time.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_fb_prof -o run -- python3 -u tools/filter_batch_time.py --frames 64 --batches 32 --reps 3 > gpurun_out/${T}_fb_prof.log 2>&1 || { echo FBPROF_FAILED; tail -20 gpurun_out/${T}_fb_prof.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  --deselect tests/test_gpu_filter_batch.py --deselect tests/test_gpu_filters.py > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${T}_gpu_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_gpu_tests.log
+timeout -k 10 400 python bench.py > gpurun_out/${T}_bench.log 2>&1 || { echo BENCH_FAILED; tail -30 gpurun_out/${T}_bench.log; exit 1; }
+python3 -c "
+import json; d=json.loads(open('gpurun_out/${T}_bench.log').read().strip().splitlines()[-1])
+print('value', d['value'], 'filtered', d['filtered']['ms_per_frame'], 'objects', d['objects']['ms'], d['objects']['single_object_ms'], d['objects']['objects_over_single'])
+print('amdahl', d['spatial_amdahl'])"
+echo DONE
