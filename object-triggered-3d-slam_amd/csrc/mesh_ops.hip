@@ -369,20 +369,50 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
     }
 }
 
+// The walk's per-chunk metadata (ex, run end, run prefix, kind), staged in LDS by the whole workgroup before the one
+// walking wave starts: every walk step then reads LDS instead of making dependent global round trips (the walk is a
+// single wave's latency chain: one object's sampling waits on it, round 4: sum / CDF walks 86 / 118 us per configs[3]
+// mesh).  Chains with more chunks than WALK_LDS_CHUNKS read global memory as before.
+constexpr int WALK_LDS_CHUNKS = 7168;  // 16 B + 1 B per chunk: 119 KiB of LDS (1.8 M values)
+struct WalkMeta {
+    const ChainJob* j;
+    const int4* m;        // LDS: {ex, rend, pre lo, pre hi} per chunk, or nullptr
+    const signed char* k; // LDS: kind per chunk
+    __device__ int ex(int64_t b) const { return m ? m[b].x : j->ex[b]; }
+    __device__ int rend(int64_t b) const { return m ? m[b].y : j->rend[b]; }
+    __device__ long long pre(int64_t b) const {
+        return m ? (long long)(((unsigned long long)(unsigned)m[b].w << 32) | (unsigned)m[b].z) : j->pre[b];
+    }
+    __device__ int kind(int64_t b) const { return m ? (int)k[b] : j->kind[b]; }
+};
+
 template <bool CDF>
-__global__ __launch_bounds__(64) void k_chain_walk(const ChainJob* __restrict__ jobs) {
+__global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict__ jobs, int lds_chunks) {
+    extern __shared__ int4 s_meta[];
     __shared__ double lds[CH + 2];
     const ChainJob j = jobs[blockIdx.x];
-    const int lane = threadIdx.x;
     const int64_t nb = (j.n + CH - 1) / CH;
+    const bool staged = nb <= lds_chunks;
+    signed char* s_kind = reinterpret_cast<signed char*>(s_meta + (staged ? nb : 0));
+    if (staged) {  // the whole workgroup stages the metadata, then one wave walks
+        for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
+            const unsigned long long pv = (unsigned long long)j.pre[b];
+            s_meta[b] = make_int4(j.ex[b], j.rend[b], (int)(unsigned)pv, (int)(unsigned)(pv >> 32));
+            s_kind[b] = (signed char)j.kind[b];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const WalkMeta M{&j, staged ? s_meta : nullptr, staged ? s_kind : nullptr};
+    const int lane = threadIdx.x;
     double s = 0.0;  // sum: 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0
     int nseg = 0;
     int64_t b = 0;
     while (b < nb) {  // wave-uniform control flow: every lane holds the same s and b
-        const int k_b = j.kind[b], e_b = j.ex[b], re = j.rend[b];
-        const bool head = b == 0 || j.rend[b - 1] < b;
-        const long long base = head ? 0 : j.pre[b - 1];
-        const long long p_re = j.pre[re];
+        const int k_b = M.kind(b), e_b = M.ex(b), re = M.rend(b);
+        const bool head = b == 0 || M.rend(b - 1) < b;
+        const long long base = head ? 0 : M.pre(b - 1);
+        const long long p_re = M.pre(re);
         const int e = binade(s);
         if (e != EX_NONE && k_b == 0 && e_b == e && base < R_MAX) {  // (a saturated base proves nothing)
             const long long N = (long long)(s * pow2(52 - e));  // exact integer in [2^52, 2^53)
@@ -393,7 +423,7 @@ __global__ __launch_bounds__(64) void k_chain_walk(const ChainJob* __restrict__ 
                 while (hi - lo > 1) {
                     const int64_t step = (hi - lo - 1 + 63) / 64;
                     const int64_t c = lo + 1 + (int64_t)lane * step;
-                    const bool ok = c < hi && j.pre[c] <= lim;
+                    const bool ok = c < hi && M.pre(c) <= lim;
                     const unsigned long long m = __ballot(ok);
                     const int L = __popcll(m);  // the accepted probes are a prefix (pre is monotone)
                     const int64_t nlo = L ? lo + 1 + (int64_t)(L - 1) * step : lo;
@@ -410,7 +440,7 @@ __global__ __launch_bounds__(64) void k_chain_walk(const ChainJob* __restrict__ 
                     j.seg_base[nseg] = base;
                 }
                 ++nseg;
-                s = (double)(N + j.pre[k] - base) * pow2(e - 52);
+                s = (double)(N + M.pre(k) - base) * pow2(e - 52);
                 b = k + 1;
                 continue;
             }
@@ -479,7 +509,16 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
     hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(256), 0, stream, djobs);
     hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
     hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
-    hipLaunchKernelGGL(k_chain_walk<CDF>, dim3(n_jobs), dim3(64), 0, stream, djobs);
+    // metadata staged in LDS when every job's chunks fit (max_n bounds them all)
+    const int lds_chunks = nb <= WALK_LDS_CHUNKS ? (int)nb : 0;
+    const size_t lds_bytes = (size_t)lds_chunks * 17 + 16;
+    static bool attr_set[2] = {false, false};
+    if (!attr_set[CDF]) {  // above 64 KiB of dynamic LDS the kernel must opt in (once per process)
+        (void)hipFuncSetAttribute((const void*)k_chain_walk<CDF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)((size_t)WALK_LDS_CHUNKS * 17 + 16));
+        attr_set[CDF] = true;
+    }
+    hipLaunchKernelGGL(k_chain_walk<CDF>, dim3(n_jobs), dim3(1024), lds_bytes, stream, djobs, lds_chunks);
     if (CDF) hipLaunchKernelGGL(k_chain_emit, grid, dim3(256), 0, stream, djobs);
 }
 
