@@ -317,6 +317,13 @@ typedef struct ot_mesh_sample_job {
 } ot_mesh_sample_job;
 ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs_host, int32_t n_jobs,
                                                 int64_t n_points, uint64_t seed, void* stream);
+/* The same, with a hipEvent_t (nullable) that the point emission waits for: the area sums and CDFs read only the
+ * vertices and triangles and start at once, while the vertex normals (or colours) the emission interpolates may
+ * still be computed on another stream (the facade's compute_vertex_normals of a fresh mesh,
+ * reconstruct_rgbd_filter.py:113 -> :123). */
+ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs_host, int32_t n_jobs,
+                                                int64_t n_points, uint64_t seed, void* inputs_ready_event,
+                                                void* stream);
 
 /* ---------------------------------------------------------------------------------------------------
  * Hybrid map — fusion/hybrid_map.py

@@ -627,11 +627,16 @@ ot_status ot_mesh_sample_points_uniformly(const double* V, const double* VN, con
                                           const int32_t* T, int64_t nt, int64_t n_points, uint64_t seed, double* P,
                                           double* PN, double* PC, void* stream) {
     const ot_mesh_sample_job job{V, VN, VC, nv, T, nt, P, PN, PC};
-    return ot_mesh_sample_points_uniformly_batch(&job, 1, n_points, seed, stream);
+    return ot_mesh_sample_points_uniformly_after(&job, 1, n_points, seed, nullptr, stream);
 }
 
 ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points,
-                                                uint64_t seed, void* stream_) {
+                                                uint64_t seed, void* stream) {
+    return ot_mesh_sample_points_uniformly_after(jobs, n_jobs, n_points, seed, nullptr, stream);
+}
+
+ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points,
+                                                uint64_t seed, void* inputs_ready, void* stream_) {
     hipStream_t stream = S(stream_);
     if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
     if (n_jobs < 0 || (n_jobs > 0 && !jobs)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
@@ -679,6 +684,9 @@ ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, 
                            nt, (const double*)sums[j], qs[j]);
     }
     launch_chains<true>(djobs + n_jobs, n_jobs, max_nt, stream);
+    // the vertex normals / colours the emission interpolates may still be in flight on another stream (the facade
+    // computes the normals of a fresh mesh beside the area chains above, which read only V and T)
+    if (inputs_ready) OT_HIP_TRY(hipStreamWaitEvent(stream, (hipEvent_t)inputs_ready, 0));
     for (int j = 0; j < n_jobs; ++j) {
         const ot_mesh_sample_job& m = jobs[j];
         const int64_t nt = m.n_triangles;

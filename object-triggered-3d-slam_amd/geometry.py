@@ -8,6 +8,7 @@ Every compute method calls the C ABI; none has a CPU implementation.
 from __future__ import annotations
 
 import ctypes as C
+import importlib
 
 import numpy as np
 
@@ -19,11 +20,18 @@ from .utility import DoubleVector, Vector3dVector, Vector3iVector
 class _Arr:
     """An (N, k) array living on the host (numpy) and/or the device (torch)."""
 
-    __slots__ = ("_h", "_d", "_viewed")
+    __slots__ = ("_h", "_d", "_viewed", "_ready")
 
-    def __init__(self, host=None, dev=None):
+    def __init__(self, host=None, dev=None, ready=None):
         self._h, self._d = host, dev
         self._viewed = False  # a writable host view was handed out: the host copy is authoritative
+        self._ready = ready   # torch.cuda.Event: the device data is complete once it fires (written on another stream)
+
+    def _join(self):
+        """Make the current stream wait for the producer of the device data (once)."""
+        if self._ready is not None:
+            D.torch.cuda.current_stream().wait_event(self._ready)
+            self._ready = None
 
     @staticmethod
     def wrap(a, dtype, cols):
@@ -42,6 +50,7 @@ class _Arr:
 
     def host(self):
         if self._h is None:
+            self._join()
             self._h = D.to_host(self._d)
         return self._h
 
@@ -54,6 +63,7 @@ class _Arr:
         return h
 
     def dev(self):
+        self._join()
         if self._d is None:
             self._d = D.to_device(self._h)
         elif self._viewed:  # refresh IN PLACE: pointers handed out earlier (queued kernels, job tables) stay valid
@@ -65,6 +75,7 @@ class _Arr:
         return self._d
 
     def copy(self):
+        self._join()
         if self._viewed or self._d is None:
             return _Arr(host=self.host().copy())
         return _Arr(dev=self._d.clone())
@@ -528,11 +539,23 @@ class TriangleMesh:
             V, T = self._v.dev(), self._t.dev()
             fresh = (V.data_ptr(), V._version, T.data_ptr(), T._version) == tuple(mc[2:6])
         if fresh and getattr(vol, "_h", None) is not None:
-            st = L.load().ot_tsdf_mesh_vertex_normals(vol._h, mc[1], D.ptr(self._v.dev()), nv, D.ptr(self._t.dev()),
-                                                       nt, D.ptr(out), D.stream_ptr())
+            # the marching-cubes walk runs on a side stream: the caller's next step (sample_points_uniformly) starts
+            # its area chains, which read only V and T, while the normals are computed; any reader of the normals
+            # waits for them (_Arr ready event; the sampler passes it to ot_mesh_sample_points_uniformly_after)
+            torch = D.torch
+            cur = torch.cuda.current_stream()
+            side = importlib.import_module(__package__ + ".streams").side_stream()
+            side.wait_stream(cur)
+            st = L.load().ot_tsdf_mesh_vertex_normals(vol._h, mc[1], D.ptr(V), nv, D.ptr(T), nt, D.ptr(out),
+                                                       C.c_void_p(side.cuda_stream))
             if st == L.OT_OK:
-                self._vn = _Arr(dev=out)
+                for t in (V, T, out):  # allocated on the caller's stream, used on the side stream
+                    t.record_stream(side)
+                done = torch.cuda.Event()
+                done.record(side)
+                self._vn = _Arr(dev=out, ready=done)
                 return self
+            cur.wait_stream(side)
         L.call("ot_mesh_compute_vertex_normals", D.ptr(self._v.dev()), nv, D.ptr(self._t.dev()), nt, D.ptr(out),
                D.stream_ptr())
         self._vn = _Arr(dev=out)
@@ -560,10 +583,18 @@ class TriangleMesh:
         P = D.empty((n, 3), "float64")
         PN = D.empty((n, 3), "float64") if self.has_vertex_normals() else None
         PC = D.empty((n, 3), "float64") if self.has_vertex_colors() else None
-        L.call("ot_mesh_sample_points_uniformly", D.ptr(self._v.dev()),
-               D.ptr(self._vn.dev()) if PN is not None else None, D.ptr(self._vc.dev()) if PC is not None else None,
-               len(self._v), D.ptr(self._t.dev()), len(self._t), n, C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF),
-               D.ptr(P), D.ptr(PN), D.ptr(PC), D.stream_ptr())
+        # normals still in flight on the side stream (compute_vertex_normals of a fresh mesh): the C side waits for
+        # them after the area chains, right before the emission that interpolates them
+        ready = self._vn._ready if (PN is not None and not self._vn._viewed and self._vn._d is not None) else None
+        VN = (self._vn._d if ready is not None else self._vn.dev()) if PN is not None else None
+        job = (L.ot_mesh_sample_job * 1)(L.ot_mesh_sample_job(
+            D.ptr(self._v.dev()), D.ptr(VN), D.ptr(self._vc.dev()) if PC is not None else None, len(self._v),
+            D.ptr(self._t.dev()), len(self._t), D.ptr(P), D.ptr(PN), D.ptr(PC)))
+        L.call("ot_mesh_sample_points_uniformly_after", C.cast(job, C.c_void_p), 1, n,
+               C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), C.c_void_p(ready.cuda_event) if ready is not None else None,
+               D.stream_ptr())
+        if ready is not None:
+            self._vn._ready = None  # the caller's stream has waited for it (inside the call)
         pcd = PointCloud()
         pcd._xyz = _Arr(dev=P)
         pcd._nrm = _Arr(dev=PN) if PN is not None else None

@@ -24,3 +24,20 @@ def worker_streams(n: int) -> list:
         while len(lst) < n:
             lst.append(torch.cuda.Stream(device=dev))
         return lst[:n]
+
+
+_side: dict = {}
+
+
+def side_stream():
+    """A second stream paired with the current one (created once per stream): independent work of the same caller
+    -- a fresh mesh's vertex normals beside its sampling's area chains -- runs there, joined by an event."""
+    import torch
+
+    cur = torch.cuda.current_stream()
+    key = (cur.device_index, cur.cuda_stream)
+    with _lock:
+        st = _side.get(key)
+        if st is None:
+            st = _side[key] = torch.cuda.Stream(device=cur.device_index)
+        return st

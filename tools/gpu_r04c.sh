@@ -20,4 +20,6 @@ python3 -c "
 import json; d=json.loads(open('gpurun_out/${T}_bench.log').read().strip().splitlines()[-1])
 print('value', d['value'], 'filtered', d['filtered']['ms_per_frame'], 'objects', d['objects']['ms'], d['objects']['single_object_ms'], d['objects']['objects_over_single'])
 print('amdahl', d['spatial_amdahl'])"
+timeout -k 10 200 python3 tools/single_object_phases.py > gpurun_out/${T}_obj_phases.log 2>&1 || { echo PHASES_FAILED; tail -20 gpurun_out/${T}_obj_phases.log; exit 1; }
+cat gpurun_out/${T}_obj_phases.log
 echo DONE
