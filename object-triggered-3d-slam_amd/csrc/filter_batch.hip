@@ -145,9 +145,6 @@ __device__ inline void fb_color8(const uint8_t* __restrict__ col, int pix0, int 
 // gathers one word per point instead of a depth and three colour bytes: pixel within its frame (24 bits), raw depth
 // (16), RGB8 (24)
 constexpr int FB_PACK_PIX_BITS = 24;
-#ifndef OT_FB_PACK
-#define OT_FB_PACK 1
-#endif
 __device__ inline unsigned long long fb_pack(unsigned pix, unsigned raw_depth, unsigned rgb) {
     return (unsigned long long)pix | ((unsigned long long)raw_depth << FB_PACK_PIX_BITS) |
            ((unsigned long long)rgb << (FB_PACK_PIX_BITS + 16));
@@ -155,8 +152,10 @@ __device__ inline unsigned long long fb_pack(unsigned pix, unsigned raw_depth, u
 
 // per tile: valid count and bounds (order-preserving u64 encodings) of the valid pixels' points
 __global__ __launch_bounds__(FB_THREADS) void k_fb_pixels(FbParams p, int* __restrict__ tcount,
-                                                          unsigned long long* __restrict__ tbounds) {
+                                                          unsigned long long* __restrict__ tbounds,
+                                                          unsigned long long* __restrict__ run_status) {
     const int f = blockIdx.y, tile = blockIdx.x;
+    if (threadIdx.x == 0) run_status[(int64_t)f * p.tpf + tile] = 0ull;  // k_fb_runs' look-back word of this tile
     const int npx = p.w * p.h;
     const int pix0 = tile * FB_TILE + threadIdx.x * FB_PIX;
     const uint16_t* dep = p.depth + (int64_t)f * npx;
@@ -218,8 +217,10 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_pixels(FbParams p, int* __res
 __global__ __launch_bounds__(256) void k_fb_setup(FbParams p, int* __restrict__ tcount,
                                                   const unsigned long long* __restrict__ tbounds,
                                                   unsigned long long* __restrict__ fbounds, int* __restrict__ kbits,
-                                                  long long* __restrict__ totals, int* __restrict__ poff) {
+                                                  long long* __restrict__ totals, int* __restrict__ poff,
+                                                  int* __restrict__ run_ticket) {
     const int f = blockIdx.x;
+    if (f < p.F && threadIdx.x == 0) run_ticket[f] = 0;  // k_fb_runs' tile tickets of frame f
     if (f == p.F) {  // scan
         __shared__ int wsum[4];
         __shared__ long long carry_s;
@@ -309,9 +310,6 @@ __device__ inline unsigned long long fb_voxel_key(const FbKeys& kb, unsigned lon
 // (segmented sort by frame) with the frame's tag bit (FbKeys::tag) on top, and, PACKED, value = the point's own index
 // with its record (fb_pack) stored at that index, else value = global pixel index.  The workgroup's outputs are one
 // contiguous range: staged in LDS and stored with consecutive lanes on consecutive entries
-#ifndef OT_FB_STAGE
-#define OT_FB_STAGE 1
-#endif
 template <typename KeyT, bool PACKED>
 __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, const int* __restrict__ toff,
                                                         KeyT* __restrict__ keys, unsigned* __restrict__ vals,
@@ -347,11 +345,9 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
     for (int w = 0; w < wid; ++w) loc += wsum[w];
     const unsigned long long fkey = sizeof(KeyT) == 8 ? (unsigned long long)f << kb.vbits
                                                       : (unsigned long long)(kb.tag ? p.frames[f].tag : 0) << 31;
-#if OT_FB_STAGE
     __shared__ KeyT s_key[FB_TILE];
     __shared__ unsigned long long s_rec[PACKED ? FB_TILE : 1];
     __shared__ unsigned s_val[PACKED ? 1 : FB_TILE];
-#endif
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
         double xyz[3];
@@ -361,24 +357,12 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
             for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
             const KeyT key = (KeyT)(fkey | fb_voxel_key(kb, (unsigned long long)kk[0], (unsigned long long)kk[1],
                                                         (unsigned long long)kk[2]));
-#if OT_FB_STAGE
             s_key[loc] = key;
             if (PACKED) s_rec[loc] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k]);
             else s_val[loc] = (unsigned)((int64_t)f * npx + pix0 + k);
-#else
-            const int pos = base + loc;
-            keys[pos] = key;
-            if (PACKED) {
-                vals[pos] = (unsigned)pos;
-                packed[pos] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k]);
-            } else {
-                vals[pos] = (unsigned)((int64_t)f * npx + pix0 + k);
-            }
-#endif
             ++loc;
         }
     }
-#if OT_FB_STAGE
     __syncthreads();
     const int n = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     for (int i = threadIdx.x; i < n; i += FB_THREADS) {
@@ -390,12 +374,8 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
             vals[base + i] = s_val[i];
         }
     }
-#endif
 }
 
-// one lane per voxel: its points (sorted values, in index order) re-unprojected and summed.  PACKED: values are
-// point indices into the fb_pack records and the voxel's frame is found in the point offsets poff[0 .. F); else
-// values are global pixel indices into the depth / colour images
 // the voxel's SOR grid cell key (grid.h layout: frame << sf | cell): sorted keys k32 (u32 chain, frame tag in bit 31
 // when vbits <= 31) or k64 (frame << vbits | voxel key)
 struct FbCellKeys {
@@ -407,6 +387,232 @@ struct FbCellKeys {
     unsigned long long* out;
 };
 
+// ---- runs (the u32 chain with packed point records) ---------------------------------------------------------
+// A run = consecutive pixels of one image row whose points fall in the same voxel (at 5 mm and 1280x720 a voxel spans
+// ~1.7 pixels of a row: 813k points -> ~480k runs per configs[2] frame).  The sort groups RUNS instead of points:
+// runs of one voxel keep their emission order, which is row-major pixel order, and a run's points are consecutive
+// in point order -- so a voxel's points are still summed in point-index order (Open3D's AddPoint order), the sort
+// moves ~0.6x the pairs and the head / reduce passes walk ~0.6x the items.
+// Each tile of a frame emits its runs at the frame's point offset poff[f] + (runs of the frame's earlier tiles),
+// found by a decoupled look-back inside the frame (tiles take tickets in start order, so a tile only waits on running
+// ones); rlen[f] = the frame's run count (its segment of the sort holds that many, the rest is capacity).
+constexpr unsigned long long FB_LB_AGG = 1ull << 62, FB_LB_PRE = 2ull << 62, FB_LB_VAL = (1ull << 62) - 1;
+
+// key of pixel pix of frame f (false: no point), as k_fb_keys computes it
+__device__ inline bool fb_pixel_key(const FbParams& p, const FbKeys& kb, const double* m, const double vmin[3],
+                                    const uint16_t* __restrict__ dep, int pix, unsigned& key) {
+    float d = div_rn((float)dep[pix], p.scale_f, p.rscale_f);
+    if ((double)d >= p.trunc) d = 0.0f;
+    double xyz[3];
+    if (!fb_point(p, m, d, pix, xyz)) return false;
+    long long kk[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
+    key = (unsigned)fb_voxel_key(kb, (unsigned long long)kk[0], (unsigned long long)kk[1], (unsigned long long)kk[2]);
+    return true;
+}
+
+__global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, const int* __restrict__ toff,
+                                                        const int* __restrict__ poff, unsigned* __restrict__ rkeys,
+                                                        unsigned* __restrict__ rvals, int* __restrict__ rstart,
+                                                        unsigned long long* __restrict__ packed,
+                                                        unsigned long long* status, int* ticket, int* __restrict__ rlen) {
+    const int f = blockIdx.y;
+    __shared__ int s_tile;
+    __shared__ int wsum[4];
+    __shared__ unsigned s_lastkey[4];
+    __shared__ int s_lastval[4];
+    __shared__ unsigned s_prevkey;
+    __shared__ int s_prevval;
+    __shared__ int s_excl;
+    __shared__ unsigned long long s_rec[FB_TILE];
+    __shared__ unsigned s_rkey[FB_TILE];
+    __shared__ int s_rstart[FB_TILE];
+    if (threadIdx.x == 0) s_tile = atomicAdd(&ticket[f], 1);
+    __syncthreads();
+    const int tile = s_tile;  // tiles start in ticket order: the look-back below only waits on running tiles
+    const int npx = p.w * p.h;
+    const int pix0 = tile * FB_TILE + threadIdx.x * FB_PIX;
+    const uint16_t* dep = p.depth + (int64_t)f * npx;
+    double m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
+    const double vmin[3] = {p.frames[f].vmin[0], p.frames[f].vmin[1], p.frames[f].vmin[2]};
+    if (threadIdx.x == 0) {  // the pixel before the tile (the previous tile's last one)
+        unsigned pk = 0u;
+        const int pp = tile * FB_TILE - 1;
+        s_prevval = (pp >= 0 && fb_pixel_key(p, kb, m, vmin, dep, pp, pk)) ? 1 : 0;
+        s_prevkey = pk;
+    }
+    float d[FB_PIX];
+    unsigned raw[FB_PIX], rgb[FB_PIX], key[FB_PIX];
+    bool val[FB_PIX];
+    fb_depth8(p, dep, pix0, npx, d, raw);
+    fb_color8(p.color + (int64_t)f * npx * 3, pix0, npx, rgb);
+#pragma unroll
+    for (int k = 0; k < FB_PIX; ++k) {
+        double xyz[3];
+        val[k] = pix0 + k < npx && fb_point(p, m, d[k], pix0 + k, xyz);
+        key[k] = 0u;
+        if (val[k]) {
+            long long kk[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
+            key[k] = (unsigned)fb_voxel_key(kb, (unsigned long long)kk[0], (unsigned long long)kk[1],
+                                            (unsigned long long)kk[2]);
+        }
+    }
+    // the previous pixel of the lane's first: the previous lane's last (a shuffle), the previous wave's last (LDS) or
+    // the previous tile's last (thread 0 above)
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+    unsigned pk = __shfl_up(key[FB_PIX - 1], 1, 64);
+    int pv = __shfl_up(val[FB_PIX - 1] ? 1 : 0, 1, 64);
+    if (lane == 63) {
+        s_lastkey[wid] = key[FB_PIX - 1];
+        s_lastval[wid] = val[FB_PIX - 1] ? 1 : 0;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        pk = wid == 0 ? s_prevkey : s_lastkey[wid - 1];
+        pv = wid == 0 ? s_prevval : s_lastval[wid - 1];
+    }
+    int c = 0, nr = 0;
+    bool head[FB_PIX];
+#pragma unroll
+    for (int k = 0; k < FB_PIX; ++k) {
+        const bool pvk = k == 0 ? pv != 0 : val[k - 1];
+        const unsigned pkk = k == 0 ? pk : key[k - 1];
+        const bool row_start = ((pix0 + k) % p.w) == 0;
+        head[k] = val[k] && !(pvk && !row_start && pkk == key[k]);
+        c += val[k] ? 1 : 0;
+        nr += head[k] ? 1 : 0;
+    }
+    // exclusive prefixes of the lanes' point and run counts over the workgroup (packed: both <= 2048)
+    const int both = (nr << 16) | c;
+    int inc = both;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int loc = inc - both;
+    for (int w = 0; w < wid; ++w) loc += wsum[w];
+    const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    const int n_pts = tot & 0xFFFF, n_runs = tot >> 16;
+    int ploc = loc & 0xFFFF, rloc = loc >> 16;
+    const int base = toff[(int64_t)f * p.tpf + tile];  // this tile's first point
+    // the frame's runs before this tile: decoupled look-back (thread 0)
+    if (threadIdx.x == 0) {
+        unsigned long long* st = status + (int64_t)f * p.tpf;
+        long long excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(&st[0], FB_LB_PRE | (unsigned long long)n_runs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&st[tile], FB_LB_AGG | (unsigned long long)n_runs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int t = tile - 1; t >= 0;) {
+                const unsigned long long v = __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v == 0ull) continue;  // tile t has not published yet (it took an earlier ticket: it is running)
+                excl += (long long)(v & FB_LB_VAL);
+                if ((v & ~FB_LB_VAL) == FB_LB_PRE) break;
+                --t;
+            }
+            __hip_atomic_store(&st[tile], FB_LB_PRE | (unsigned long long)(excl + n_runs), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_excl = (int)excl;
+        if (tile == p.tpf - 1) rlen[f] = (int)excl + n_runs;
+    }
+#pragma unroll
+    for (int k = 0; k < FB_PIX; ++k) {
+        if (!val[k]) continue;
+        s_rec[ploc] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k]);
+        if (head[k]) {
+            s_rkey[rloc] = key[k];
+            s_rstart[rloc] = base + ploc;
+            ++rloc;
+        }
+        ++ploc;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n_pts; i += FB_THREADS) packed[base + i] = s_rec[i];
+    const int rbase = poff[f] + s_excl;
+    for (int i = threadIdx.x; i < n_runs; i += FB_THREADS) {
+        rkeys[rbase + i] = s_rkey[i];
+        rvals[rbase + i] = (unsigned)(rbase + i);
+        rstart[rbase + i] = s_rstart[i];
+    }
+}
+
+// voxel heads over the runs (segment f = [poff[f], poff[f] + rlen[f]), the rest of its range is capacity): a frame's
+// first run or a new key
+struct SegHeadPredRuns {
+    const unsigned* keys;
+    const int* poff;
+    const int* rlen;
+    int F;
+    __device__ bool operator()(int64_t i) const {
+        const int f = frame_of(poff, F, i);
+        if (i - poff[f] >= rlen[f]) return false;
+        return i == poff[f] || keys[i] != keys[i - 1];
+    }
+};
+
+// one lane per voxel: its runs (sorted values = run positions, in emission order) and each run's points (consecutive
+// point records) re-unprojected and summed in point order
+__global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsigned* __restrict__ sval,
+                                                        const int* __restrict__ rstart,
+                                                        const unsigned long long* __restrict__ packed,
+                                                        const int* __restrict__ poff, const int* __restrict__ rlen,
+                                                        const int* __restrict__ heads, int64_t K, int64_t P,
+                                                        double* __restrict__ vx, double* __restrict__ vc,
+                                                        FbCellKeys ck) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= K) return;
+    const int beg = heads[s];
+    const int f = frame_of(poff, p.F, beg);
+    const int fend = poff[f] + rlen[f];                      // the frame's runs end
+    const int pend = f + 1 < p.F ? poff[f + 1] : (int)P;     // the frame's points end
+    const int end = (s + 1 < K && heads[s + 1] < fend) ? heads[s + 1] : fend;
+    {
+        const unsigned vk = ck.vbits < 32 ? (ck.k32[beg] & ((1u << ck.vbits) - 1u)) : ck.k32[beg];
+        ck.out[s] = ((unsigned long long)f << ck.sf) | (unsigned long long)(vk >> ck.shift);
+    }
+    double m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
+    double sp[3] = {0, 0, 0}, sc[3] = {0, 0, 0};
+    int cnt = 0;
+    for (int r = beg; r < end; ++r) {
+        const int ri = (int)sval[r];
+        const int q0 = rstart[ri], q1 = ri + 1 < fend ? rstart[ri + 1] : pend;
+        for (int q = q0; q < q1; ++q) {
+            const unsigned long long rec = packed[q];
+            const int pix = (int)(rec & ((1u << FB_PACK_PIX_BITS) - 1));
+            const float dd = (float)(unsigned)((rec >> FB_PACK_PIX_BITS) & 0xFFFFu);
+            const unsigned rgb = (unsigned)(rec >> (FB_PACK_PIX_BITS + 16));
+            double xyz[3];
+            fb_point(p, m, div_rn(dd, p.scale_f, p.rscale_f), pix, xyz);  // valid by construction
+#pragma unroll
+            for (int a = 0; a < 3; ++a) sp[a] += xyz[a];
+            sc[0] += div_rn((double)(rgb & 0xFF), 255.0, 1.0 / 255.0);
+            sc[1] += div_rn((double)((rgb >> 8) & 0xFF), 255.0, 1.0 / 255.0);
+            sc[2] += div_rn((double)(rgb >> 16), 255.0, 1.0 / 255.0);
+            ++cnt;
+        }
+    }
+    const double cntd = (double)cnt, rc = 1.0 / cntd;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        vx[s * 3 + a] = div_rn(sp[a], cntd, rc);
+        vc[s * 3 + a] = div_rn(sc[a], cntd, rc);
+    }
+}
+
+// one lane per voxel: its points (sorted values, in index order) re-unprojected and summed.  PACKED: values are
+// point indices into the fb_pack records and the voxel's frame is found in the point offsets poff[0 .. F); else
+// values are global pixel indices into the depth / colour images
 template <bool PACKED>
 __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* __restrict__ sval,
                                                    const unsigned long long* __restrict__ packed,
@@ -683,9 +889,10 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     for (int f = 0; f < F; ++f) inverse4(extrinsics_host + 16 * f, fl->h_frames[f].pose);
     FbFrame* d_frames = (FbFrame*)fl->b_frames.get(sizeof(FbFrame) * F);
     // layout: tile counts i32 [F*tpf] | align 64 | tile bounds u64 [F*tpf][6] | frame bounds u64 [F][6] | kbits i32 [4]
-    // | totals i64 [2] | voff i32 [F+1] | poff i32 [F]
+    // | totals i64 [2] | voff i32 [F+1] | poff i32 [F] | run tickets i32 [F] | run counts i32 [F] | align 8 |
+    // run look-back status u64 [F*tpf]
     const size_t tiles_bytes = (size_t)F * tpf * 4 + 63 + (size_t)F * tpf * 48 + (size_t)F * 48 + 16 + 16 +
-                               (size_t)(F + 1) * 4 + (size_t)F * 4;
+                               (size_t)(F + 1) * 4 + (size_t)F * 12 + 8 + (size_t)F * tpf * 8;
     int* d_tc = (int*)fl->b_tiles.get(tiles_bytes);
     if (!d_frames || !d_tc) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
     unsigned long long* d_tb = (unsigned long long*)(((uintptr_t)(d_tc + (size_t)F * tpf) + 63) & ~(uintptr_t)63);
@@ -694,6 +901,9 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     long long* d_tot = (long long*)(d_kbits + 4);
     int* d_voff = (int*)(d_tot + 2);
     int* d_poff = d_voff + (F + 1);
+    int* d_ticket = d_poff + F;
+    int* d_rlen = d_ticket + F;
+    unsigned long long* d_status = (unsigned long long*)(((uintptr_t)(d_rlen + F) + 7) & ~(uintptr_t)7);
     OT_HIP_TRY(hipMemcpyAsync(d_frames, fl->h_frames, sizeof(FbFrame) * F, hipMemcpyHostToDevice, stream));
     OT_HIP_TRY(hipMemsetAsync(d_kbits, 0, sizeof(int) * 4, stream));
     FbParams p;
@@ -715,9 +925,9 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     p.inv_vs = 1.0 / vs;
     p.frames = d_frames;
     p.F = F;
-    hipLaunchKernelGGL(k_fb_pixels, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, d_tc, d_tb);
+    hipLaunchKernelGGL(k_fb_pixels, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, d_tc, d_tb, d_status);
     hipLaunchKernelGGL(k_fb_setup, dim3(F + 1), dim3(256), 0, stream, p, d_tc, (const unsigned long long*)d_tb, d_fb,
-                       d_kbits, d_tot, d_poff);
+                       d_kbits, d_tot, d_poff, d_ticket);
     OT_LAUNCH_CHECK();
     // ---- sync 1: point count, key widths, frame bounds / origins -------------------------------------------
     struct {
@@ -765,9 +975,24 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     ot_status st;
     int64_t K = 0;
     const bool seg32 = vbits <= 32 && F <= 64;
-    const bool pack = seg32 && OT_FB_PACK && npx <= (1 << FB_PACK_PIX_BITS);
+    // the bench / production path: u32 keys, frames up to 2^24 pixels -> runs of pixels sorted (packed point records)
+    const bool pack = seg32 && npx <= (1 << FB_PACK_PIX_BITS);
     unsigned long long* packed = nullptr;
-    if (seg32) {  // 32-bit voxel keys, one sort segment per frame: 8 B per pair per pass
+    int* rstart = nullptr;
+    if (pack) {  // runs: one sort segment per frame, [poff[f], poff[f] + rlen[f]) of each frame's point range
+        unsigned* k32 = (unsigned*)kin;
+        unsigned* k32o = k32 + P;
+        packed = (unsigned long long*)fl->b_packed.get((size_t)P * 12 + 256);
+        if (!packed) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+        rstart = (int*)(packed + P);
+        hipLaunchKernelGGL(k_fb_runs, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb, (const int*)d_tc,
+                           (const int*)d_poff, k32, vin, rstart, packed, d_status, d_ticket, d_rlen);
+        OT_LAUNCH_CHECK();
+        st = sort_segments_u32_u32(k32, k32o, vin, vout, fl->poff.data(), F, vbits, stream, 3, d_rlen);
+        if (st != OT_OK) return st;
+        st = compact(P, SegHeadPredRuns{k32o, d_poff, d_rlen, F}, SegHeadEmit{heads}, stream, &K, 7);  // sync 2
+        if (st != OT_OK) return st;
+    } else if (seg32) {  // 32-bit voxel keys of single points, one sort segment per frame: 8 B per pair per pass
         unsigned* k32 = (unsigned*)kin;
         unsigned* k32o = k32 + P;
         FbKeys kt = kb;
@@ -780,20 +1005,12 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
             }
             OT_HIP_TRY(hipMemcpyAsync(d_frames, fl->h_frames, sizeof(FbFrame) * F, hipMemcpyHostToDevice, stream));
         }
-        if (pack) {
-            packed = (unsigned long long*)fl->b_packed.get((size_t)P * 8 + 256);
-            if (!packed) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
-            hipLaunchKernelGGL((k_fb_keys<unsigned, true>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kt,
-                               (const int*)d_tc, k32, vin, packed);
-        } else {
-            hipLaunchKernelGGL((k_fb_keys<unsigned, false>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kt,
-                               (const int*)d_tc, k32, vin, nullptr);
-        }
+        hipLaunchKernelGGL((k_fb_keys<unsigned, false>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kt,
+                           (const int*)d_tc, k32, vin, nullptr);
         OT_LAUNCH_CHECK();
         st = sort_segments_u32_u32(k32, k32o, vin, vout, fl->poff.data(), F, vbits, stream, 3);
         if (st != OT_OK) return st;
         if (kt.tag) st = compact(P, SegHeadPredTag{k32o}, SegHeadEmit{heads}, stream, &K, 7);  // sync 2
-        else if (pack) st = compact(P, SegHeadPredPoff{k32o, d_poff, F}, SegHeadEmit{heads}, stream, &K, 7);
         else st = compact(P, SegHeadPredPix{k32o, vout, (unsigned)npx}, SegHeadEmit{heads}, stream, &K, 7);
         if (st != OT_OK) return st;
     } else {
@@ -823,9 +1040,9 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     const FbCellKeys ck{seg32 ? (const unsigned*)kin + P : nullptr, seg32 ? nullptr : (const unsigned long long*)kout,
                         3 * m, vbits, gsf, ckeys};
     if (pack)
-        hipLaunchKernelGGL(k_fb_reduce<true>, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
-                           (const unsigned*)vout, (const unsigned long long*)packed, (const int*)d_poff,
-                           (const int*)heads, K, P, fl->vx, fl->vc, ck);
+        hipLaunchKernelGGL(k_fb_reduce_runs, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
+                           (const unsigned*)vout, (const int*)rstart, (const unsigned long long*)packed,
+                           (const int*)d_poff, (const int*)d_rlen, (const int*)heads, K, P, fl->vx, fl->vc, ck);
     else
         hipLaunchKernelGGL(k_fb_reduce<false>, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
                            (const unsigned*)vout, nullptr, nullptr, (const int*)heads, K, P, fl->vx, fl->vc, ck);

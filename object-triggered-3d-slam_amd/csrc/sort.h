@@ -16,9 +16,11 @@ ot_status sort_pairs_u32_u32(const unsigned* kin, unsigned* kout, const unsigned
                              int end_bit, hipStream_t stream, int scratch_slot);
 
 // Segmented form (own onesweep): the input is nseg <= 64 concatenated segments, seg[0..nseg] host offsets (seg[0] = 0,
-// seg[nseg] = n); each segment is sorted stably on its own (pairs never cross a segment boundary).
+// seg[nseg] = n); each segment is sorted stably on its own (pairs never cross a segment boundary).  dlen (device,
+// nullable): segment s holds only its first dlen[s] pairs, the rest of its range is capacity (left untouched).
 ot_status sort_segments_u32_u32(const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout,
-                                const int64_t* seg, int nseg, int end_bit, hipStream_t stream, int scratch_slot);
+                                const int64_t* seg, int nseg, int end_bit, hipStream_t stream, int scratch_slot,
+                                const int* dlen = nullptr);
 
 // Device-wide exclusive prefix sum of int64.
 ot_status exclusive_scan_i64(const long long* in, long long* out, size_t n, hipStream_t stream, int scratch_slot);

@@ -17,12 +17,9 @@ using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::
                                               rocprim::default_config, 0>;
 // large (u64 key, u32 value) sorts: 8-bit digits with a 256-thread histogram kernel (measured: 10-bit digits, 4 passes
 // instead of 5 for a 33-bit key, are slower; 11 bits do not fit the onesweep histograms of a 64-bit key in LDS)
-#ifndef OT_SORT_BITS
-#define OT_SORT_BITS 8
-#endif
 using BigSortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 16>, rocprim::kernel_config<512, 16>, OT_SORT_BITS,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 16>, rocprim::kernel_config<512, 16>, 8,
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
 
@@ -49,9 +46,6 @@ struct Rs {
     static constexpr int WAVES = THREADS / 64;
 };
 constexpr int RS_MAXP = 8;
-#ifndef OT_SEGSORT_D9
-#define OT_SEGSORT_D9 1  // 9-bit digits (512-thread tiles) whenever they need fewer passes than 8-bit ones
-#endif
 constexpr int RS_MAXSEG = 64;
 constexpr unsigned RS_AGG = 1u << 30, RS_PREFIX = 2u << 30, RS_VAL = (1u << 30) - 1;
 // above this size rocPRIM's onesweep (1024-thread tiles) moves the data faster than these 2048-item tiles; below
@@ -66,12 +60,17 @@ struct RsPasses {
     RsPass p[RS_MAXP];
     int np;
 };
-// segments: [start[s], start[s + 1]) of the input; their tiles [tile[s], tile[s + 1])
+// segments: [start[s], start[s + 1]) of the input; their tiles [tile[s], tile[s + 1]).  dlen (device, nullable): the
+// segment holds only its first dlen[s] items (the rest of its range is capacity; tiles past the end sort nothing)
 struct RsSegs {
     int nseg;
     int start[RS_MAXSEG + 1];
     int tile[RS_MAXSEG + 1];
+    const int* dlen;
 };
+__device__ inline int rs_seg_end(const RsSegs& sg, int s) {
+    return sg.dlen ? sg.start[s] + sg.dlen[s] : sg.start[s + 1];
+}
 
 __device__ inline int rs_segment(const RsSegs& sg, int tile) {
     int s = 0;
@@ -99,7 +98,7 @@ __global__ __launch_bounds__(Rs<D>::THREADS) void k_rs_upsweep(const KeyT* __res
     __syncthreads();
     const int s = rs_segment(sg, blockIdx.x);
     const int base = sg.start[s] + (blockIdx.x - sg.tile[s]) * RS_TILE;
-    const int end = sg.start[s + 1];
+    const int end = rs_seg_end(sg, s);
     // per lane and pass a run of equal digits, flushed into the LDS histogram when the digit changes: a tile's keys
     // are spatially coherent (its high digits rarely change), and same-bin LDS atomics from a whole wave serialise
     unsigned cur[RS_MAXP], cnt[RS_MAXP];
@@ -192,7 +191,7 @@ __global__ __launch_bounds__(Rs<D>::THREADS) void k_rs_scatter(const KeyT* __res
     const int tile = first + s_tile / sg.nseg;
     if (tile >= sg.tile[sgi + 1]) return;  // past the end of a shorter segment (block-uniform)
     const int base = sg.start[sgi] + (tile - first) * RS_TILE;
-    const int n = sg.start[sgi + 1];  // end of the segment
+    const int n = rs_seg_end(sg, sgi);  // end of the segment's items
     const int wbase = base + w * RS_CHUNK;  // this wave's contiguous run: items wbase + r * 64 + lane
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     KeyT key[RS_ITEMS];
@@ -283,7 +282,7 @@ __global__ __launch_bounds__(Rs<D>::THREADS) void k_rs_scatter(const KeyT* __res
 // the own sort over segments (host segment offsets seg[0..nseg], seg[0] = 0, seg[nseg] = n)
 template <typename KeyT, int RS_ITEMS, int D>
 static ot_status rs_sort(const KeyT* kin, KeyT* kout, const unsigned* vin, unsigned* vout, const int64_t* seg, int nseg,
-                         int end_bit, hipStream_t stream, int scratch_slot) {
+                         int end_bit, hipStream_t stream, int scratch_slot, const int* dlen = nullptr) {
     constexpr int RS_THREADS = Rs<D>::THREADS, RS_BINS = Rs<D>::BINS;
     constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
     const size_t n = (size_t)seg[nseg];
@@ -300,6 +299,7 @@ static ot_status rs_sort(const KeyT* kin, KeyT* kout, const unsigned* vin, unsig
     }
     RsSegs sg{};
     sg.nseg = nseg;
+    sg.dlen = dlen;
     int ntiles = 0;
     for (int s = 0; s < nseg; ++s) {
         sg.start[s] = (int)seg[s];
@@ -348,7 +348,7 @@ ot_status sort_pairs_u64_u32(const unsigned long long* kin, unsigned long long* 
     if (n == 0) return OT_OK;
     if (n <= RS_OWN_MAX) {
         const int64_t seg[2] = {0, (int64_t)n};
-        if (OT_SEGSORT_D9 && (end_bit + 8) / 9 < (end_bit + 7) / 8)  // 9-bit digits when they save a pass
+        if ((end_bit + 8) / 9 < (end_bit + 7) / 8)  // 9-bit digits when they save a pass
             return rs_sort<unsigned long long, 4, 9>(kin, kout, vin, vout, seg, 1, end_bit, stream, scratch_slot);
         return rs_sort<unsigned long long, 8, 8>(kin, kout, vin, vout, seg, 1, end_bit, stream, scratch_slot);
     }
@@ -361,16 +361,17 @@ ot_status sort_pairs_u64_u32(const unsigned long long* kin, unsigned long long* 
     return OT_OK;
 }
 
-#ifndef OT_SEGSORT_ITEMS
-#define OT_SEGSORT_ITEMS 16  // items per thread of the segmented sort's tiles (4096-item tiles)
-#endif
+constexpr int SEGSORT_ITEMS = 16;  // items per thread of the segmented sort's tiles (4096-item tiles; 2048 / 6144
+                                   // measured slower)
 
 ot_status sort_segments_u32_u32(const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout,
-                                const int64_t* seg, int nseg, int end_bit, hipStream_t stream, int scratch_slot) {
+                                const int64_t* seg, int nseg, int end_bit, hipStream_t stream, int scratch_slot,
+                                const int* dlen) {
     // 9-bit digits (512-thread tiles of the same 4096 items) when they save a pass: 25..27-bit keys in 3 passes
-    if (OT_SEGSORT_D9 && (end_bit + 8) / 9 < (end_bit + 7) / 8)
-        return rs_sort<unsigned, OT_SEGSORT_ITEMS / 2, 9>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot);
-    return rs_sort<unsigned, OT_SEGSORT_ITEMS, 8>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot);
+    if ((end_bit + 8) / 9 < (end_bit + 7) / 8)
+        return rs_sort<unsigned, SEGSORT_ITEMS / 2, 9>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot,
+                                                       dlen);
+    return rs_sort<unsigned, SEGSORT_ITEMS, 8>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot, dlen);
 }
 
 ot_status sort_pairs_u32_u32(const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout, size_t n,

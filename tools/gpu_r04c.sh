@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 T=${TAG:-r04c}
-timeout -k 10 600 python -u -m pytest tests/test_gpu_filter_batch.py tests/test_gpu_filters.py -m gpu -x -q --timeout 300 \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_filter_batch.py tests/test_gpu_filters.py tests/test_gpu_chain.py tests/test_gpu_mesh.py tests/test_gpu_sort.py -m gpu -x -q --timeout 300 \
   --timeout-method thread > gpurun_out/${T}_filter_tests.log 2>&1 || { echo FILTER_TESTS_FAILED; tail -40 gpurun_out/${T}_filter_tests.log; exit 1; }
 tail -1 gpurun_out/${T}_filter_tests.log
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -13,7 +13,7 @@ timeout -k 10 240 python3 -u tools/filter_batch_time.py --frames 64 --batches 32
 cat gpurun_out/${T}_fb_time.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_fb_prof -o run -- python3 -u tools/filter_batch_time.py --frames 64 --batches 32 --reps 3 > gpurun_out/${T}_fb_prof.log 2>&1 || { echo FBPROF_FAILED; tail -20 gpurun_out/${T}_fb_prof.log; exit 1; }
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-  --deselect tests/test_gpu_filter_batch.py --deselect tests/test_gpu_filters.py > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${T}_gpu_tests.log; exit 1; }
+  --deselect tests/test_gpu_filter_batch.py --deselect tests/test_gpu_filters.py --deselect tests/test_gpu_chain.py --deselect tests/test_gpu_mesh.py --deselect tests/test_gpu_sort.py > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${T}_gpu_tests.log; exit 1; }
 tail -1 gpurun_out/${T}_gpu_tests.log
 timeout -k 10 400 python bench.py > gpurun_out/${T}_bench.log 2>&1 || { echo BENCH_FAILED; tail -30 gpurun_out/${T}_bench.log; exit 1; }
 python3 -c "
