@@ -639,7 +639,8 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
         # the objects' 100k-point samplings in one call: their serial area-CDF chains run side by side
         pcds = pkg.geometry.TriangleMesh.sample_points_uniformly_batch(meshes, number_of_points=100000)
         clouds = [p.filter_min_z(0.03)._xyz.dev() for p in pcds]
-        merged = D.merge_object_clouds(clouds)
+        # one collective, counts in-band: every rank holds <= ceil(objects / N) objects of <= 100k points
+        merged = D.merge_object_clouds(clouds, capacity=((args.objects + world - 1) // world) * 100000)
         sizes["local"] = sum(int(c.shape[0]) for c in clouds)
         return merged
 
@@ -691,7 +692,8 @@ def _merge_label(world):
     """the collective a merge actually runs at this world size / backend"""
     if world == 1:
         return "local concatenation (N=1: no process group, no collective)"
-    return "RCCL all-gather over xGMI" if COLL_DEV == "cuda" else "gloo all-gather"
+    return ("one RCCL all-gather over xGMI (counts in-band)" if COLL_DEV == "cuda"
+            else "one gloo all-gather (counts in-band)")
 
 
 def hybrid_fusion(args, L, synth, torch, dist, rank, world):
@@ -723,6 +725,7 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
     cat_old = torch.cat(saved, 0).contiguous() if saved else empty
     off_new = np.concatenate([[0], np.cumsum([int(o.shape[0]) for o in objs])]).astype(np.int64)
     off_old = np.concatenate([[0], np.cumsum([int(o.shape[0]) for o in saved])]).astype(np.int64)
+    cap = ((args.hybrid_objects + world - 1) // world) * 100000  # synth.object_cloud: 100k points per object
     keys_a = torch.empty((int(off_new[-1]) + 1, 4), dtype=torch.int32, device="cuda")
     keys_r = torch.empty((int(off_old[-1]) + 1, 4), dtype=torch.int32, device="cuda")
 
@@ -743,7 +746,7 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
             L.call("ot_occupancy_to_points", C.c_void_p(d_base.data_ptr()), 1024, 1024, 100, 0.05, -25.6, -25.6,
                    C.c_void_p(occ.data_ptr()), C.byref(nq), stream)
             stats["changed_cells"] = ch.value
-        merged = Dm.merge_object_clouds(objs)
+        merged = Dm.merge_object_clouds(objs, capacity=cap)  # one collective, counts in-band
         if rank == 0:
             merged = torch.cat([occ[:nq.value], merged], 0)
         stats.update(added=added, removed=removed)

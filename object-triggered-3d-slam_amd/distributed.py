@@ -215,9 +215,39 @@ def extract_sharded_mesh(volume, group=None):
     return out, int(allrows.numel()) * 4
 
 
-def merge_object_clouds(local_clouds, group=None):
+def all_gather_rows_capped(local, capacity, group=None):
+    """all_gather_rows in ONE collective when every rank knows a common bound on the rows (capacity): each rank sends
+    [capacity + 1, k] float64 rows -- row 0 carries its row count in-band (exact below 2^53), the rest its rows
+    zero-padded -- so there is no separate count exchange and no host read between two collectives; one read of the
+    world's counts afterwards trims the padding.  A rank above the bound raises (the bound is the caller's contract:
+    no rank could otherwise learn that another one fell back)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return local
+    if dist.get_backend(group) == "gloo" and local.is_cuda:  # gloo collectives run through host memory
+        return all_gather_rows_capped(local.cpu(), capacity, group).to(local.device)
+    world = dist.get_world_size(group)
+    n, k = int(local.shape[0]), int(local.shape[1])
+    cap = int(capacity)
+    if n > cap:
+        raise ValueError(f"all_gather_rows_capped: {n} rows exceed the capacity {cap}")
+    buf = local.new_zeros((cap + 1, k), dtype=torch.float64)
+    buf[0, 0] = float(n)
+    buf[1:n + 1] = local
+    out = local.new_empty((world * (cap + 1), k), dtype=torch.float64)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    out = out.view(world, cap + 1, k)
+    counts = out[:, 0, 0].cpu().tolist()
+    return torch.cat([out[r, 1:int(c) + 1] for r, c in enumerate(counts)], dim=0)
+
+
+def merge_object_clouds(local_clouds, group=None, capacity=None):
     """Rank-ordered concatenation of this rank's object clouds with everyone else's (points only: colours are
-    repainted uniformly by the hybrid map, hybrid_map.py:88)."""
+    repainted uniformly by the hybrid map, hybrid_map.py:88).  capacity: a bound on any rank's total rows that every
+    rank knows (objects per rank x samples per object): then one collective with the counts in-band
+    (all_gather_rows_capped) instead of a count exchange, a host read and a second collective."""
     import torch
 
     dev = local_clouds[0].device if local_clouds else None
@@ -228,6 +258,8 @@ def merge_object_clouds(local_clouds, group=None):
                                                                    dist.get_backend(group) == "nccl") else \
             torch.device("cpu")
     local = torch.cat(local_clouds, 0) if local_clouds else torch.zeros((0, 3), dtype=torch.float64, device=dev)
+    if capacity is not None:
+        return all_gather_rows_capped(local.to(torch.float64), capacity, group)
     return all_gather_rows(local.to(torch.float64), group)
 
 
@@ -272,7 +304,9 @@ def reconstruct_and_merge(cfg, yaml_file=None, pgm_file=None, save_path=None, ob
                 done.update(part)
         results = [done[j] for j in range(len(mine))]
     clouds = [pts for pts in results if pts is not None]
-    merged = merge_object_clouds(clouds)
+    # every rank's objects: ceil(len(labels) / world) at most, each <= n_samples points after the Z mask
+    cap = ((len(labels) + world - 1) // world) * int(cfg.n_samples)
+    merged = merge_object_clouds(clouds, capacity=cap)
     if rank != 0:
         return None
     objs = o3d.geometry.PointCloud()

@@ -31,7 +31,8 @@ def _worker(rank, world, port, sizes, q):
     rng = np.random.default_rng(rank)
     clouds = [torch.from_numpy(rng.standard_normal((n, 3))) for n in sizes[rank]]
     merged = D.merge_object_clouds(clouds)
-    q.put((rank, merged.numpy()))
+    capped = D.merge_object_clouds(clouds, capacity=max(sum(ns) for ns in sizes) + 1)  # one collective, counts in-band
+    q.put((rank, merged.numpy(), capped.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -52,13 +53,17 @@ def test_all_gather_merge_gloo(sizes):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, sizes, q)) for r in range(2)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=120) for _ in range(2))
+    out = {}
+    for _ in range(2):
+        r, merged, capped = q.get(timeout=120)
+        out[r] = (merged, capped)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     exp = _expected(sizes)
     for r in range(2):
-        assert np.array_equal(out[r], exp)
+        assert np.array_equal(out[r][0], exp)
+        assert np.array_equal(out[r][1], exp)
 
 
 def test_shard_contiguous_sorted():
