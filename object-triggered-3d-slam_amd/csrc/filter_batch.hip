@@ -754,21 +754,12 @@ __global__ __launch_bounds__(256) void k_fb_gather(const int64_t* __restrict__ k
     oidx[t] = i - voff[lo];
 }
 
-// voxel heads of the segmented (u32-key) sort: a new key, or the first point of a frame.  With the frame tags in the
-// keys (FbKeys::tag) adjacent frames' keys always differ; otherwise the frame starts are looked up: in the point
-// offsets poff[0 .. F) (PACKED values = point indices) or from the values' global pixel indices
+// voxel heads of the segmented (u32-key, unpacked) sort: a new key, or the first point of a frame.  With the frame tags
+// in the keys (FbKeys::tag) adjacent frames' keys always differ; otherwise the frame starts are found from the values'
+// global pixel indices
 struct SegHeadPredTag {
     const unsigned* keys;
     __device__ bool operator()(int64_t i) const { return i == 0 || keys[i] != keys[i - 1]; }
-};
-struct SegHeadPredPoff {
-    const unsigned* keys;
-    const int* poff;
-    int F;
-    __device__ bool operator()(int64_t i) const {
-        if (i == 0 || keys[i] != keys[i - 1]) return true;
-        return poff[frame_of(poff, F, i)] == i;
-    }
 };
 struct SegHeadPredPix {
     const unsigned* keys;

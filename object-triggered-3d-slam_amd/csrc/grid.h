@@ -17,25 +17,17 @@ constexpr int NBR3 = 9;   // 3x3 columns, z-1 .. z+1
 constexpr int NBR5 = 25;  // 5x5 columns, z-2 .. z+2
 
 // SOR (outlier.hip): radius (in cells) of the block a query scans first, and the matching cell occupancy target
-// (points per occupied cell of a surface-like cloud); both only change speed, never a result.
-#ifndef OT_SOR_R
-#define OT_SOR_R 1
-#endif
-#ifndef OT_SOR_OCC
-#define OT_SOR_OCC (OT_SOR_R == 1 ? 0.9 : 0.45)
-#endif
-#ifndef OT_SOR_NBR5
-#define OT_SOR_NBR5 0  // R = 1: precompute the 5x5 column ranges of every cell for stage 2 (default: probe on the fly)
-#endif
-constexpr int SOR_BLOCK_R = OT_SOR_R;
+// (points per occupied cell of a surface-like cloud); both only change speed, never a result.  Measured and settled
+// (DESIGN.md §4): R = 2 with finer cells, occupancies 0.6-1.3 k, precomputed 5x5 ranges for stage 2 -- all slower.
+constexpr int SOR_BLOCK_R = 1;
 inline double sor_cell_target(int nb_neighbors) {
-    const double t = (OT_SOR_OCC) * (double)nb_neighbors;
+    const double t = 0.9 * (double)nb_neighbors;
     return t > 2.0 ? t : 2.0;
 }
 
 // neighbour structures a grid build can precompute (bit mask)
 enum { GRID_NBR3 = 1, GRID_NBR5 = 2 };
-constexpr int SOR_GRID_NBR = GRID_NBR3 | ((OT_SOR_R == 2 || OT_SOR_NBR5) ? GRID_NBR5 : 0);
+constexpr int SOR_GRID_NBR = GRID_NBR3;
 
 struct GridDev {
     const double* sxyz;        // [n][3] points in sorted (frame, cell) order

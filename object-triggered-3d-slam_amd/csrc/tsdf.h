@@ -169,11 +169,8 @@ struct ot_tsdf {
     // float depth staging for the u16 path
     float* depth_f = nullptr;
     int64_t depth_f_cap = 0;
-    // batching of integrate_u16
-#ifndef OT_DEFAULT_BATCH
-#define OT_DEFAULT_BATCH 64
-#endif
-    int batch_max = OT_DEFAULT_BATCH;  // frames per fused launch (ot_tsdf_set_batch)
+    // batching of integrate_u16: frames per fused launch (ot_tsdf_set_batch; 64 = MAX_BATCH, measured best, §4)
+    int batch_max = ot::MAX_BATCH;
     std::vector<ot::PendingFrame> pending;
     void* batch_ws = nullptr;       // unused (kept for ABI of the struct layout)
     size_t batch_ws_bytes = 0;
