@@ -141,13 +141,15 @@ __device__ inline void fb_color8(const uint8_t* __restrict__ col, int pix0, int 
     }
 }
 
-// a valid point of the u32-key chain as one 8-B record, written in point order by k_fb_keys so the voxel reduce
-// gathers one word per point instead of a depth and three colour bytes: pixel within its frame (24 bits), raw depth
-// (16), RGB8 (24)
-constexpr int FB_PACK_PIX_BITS = 24;
-__device__ inline unsigned long long fb_pack(unsigned pix, unsigned raw_depth, unsigned rgb) {
-    return (unsigned long long)pix | ((unsigned long long)raw_depth << FB_PACK_PIX_BITS) |
-           ((unsigned long long)rgb << (FB_PACK_PIX_BITS + 16));
+// a valid point of the u32-key chain as one 8-B record, written in point order by k_fb_runs so the voxel reduce
+// gathers one word per point instead of a depth and three colour bytes: pixel within its frame
+// (23), run head (1: the first point of a run, below), raw depth (16), RGB8 (24)
+constexpr int FB_PACK_PIX_BITS = 23;
+constexpr unsigned long long FB_PACK_HEAD = 1ull << FB_PACK_PIX_BITS;
+constexpr int FB_PACK_DEPTH_SHIFT = FB_PACK_PIX_BITS + 1;
+__device__ inline unsigned long long fb_pack(unsigned pix, unsigned raw_depth, unsigned rgb, bool head) {
+    return (unsigned long long)pix | (head ? FB_PACK_HEAD : 0ull) | ((unsigned long long)raw_depth << FB_PACK_DEPTH_SHIFT) |
+           ((unsigned long long)rgb << (FB_PACK_DEPTH_SHIFT + 16));
 }
 
 // per tile: valid count and bounds (order-preserving u64 encodings) of the valid pixels' points
@@ -305,15 +307,14 @@ __device__ inline unsigned long long fb_voxel_key(const FbKeys& kb, unsigned lon
     return (cell << (3 * m)) | ((kx & M) << (2 * m)) | ((ky & M) << m) | (kz & M);
 }
 
-// the tile again: voxel keys of the valid pixels, emitted in pixel order at the tile's scanned offset.  KeyT = u64:
-// the frame in the key's top bits (one sort over the batch), value = global pixel index; u32: the voxel index only
-// (segmented sort by frame) with the frame's tag bit (FbKeys::tag) on top, and, PACKED, value = the point's own index
-// with its record (fb_pack) stored at that index, else value = global pixel index.  The workgroup's outputs are one
-// contiguous range: staged in LDS and stored with consecutive lanes on consecutive entries
-template <typename KeyT, bool PACKED>
+// the tile again: voxel keys of the valid pixels, emitted in pixel order at the tile's scanned offset, value = global
+// pixel index (the unpacked paths: frames above 2^23 pixels, or keys wider than 32 bits).  KeyT = u64: the frame in
+// the key's top bits (one sort over the batch); u32: the voxel key only (segmented sort by frame) with the frame's tag
+// bit (FbKeys::tag) on top.  The workgroup's outputs are one contiguous range: staged in LDS and stored with
+// consecutive lanes on consecutive entries
+template <typename KeyT>
 __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, const int* __restrict__ toff,
-                                                        KeyT* __restrict__ keys, unsigned* __restrict__ vals,
-                                                        unsigned long long* __restrict__ packed) {
+                                                        KeyT* __restrict__ keys, unsigned* __restrict__ vals) {
     const int f = blockIdx.y, tile = blockIdx.x;
     const int npx = p.w * p.h;
     const int pix0 = tile * FB_TILE + threadIdx.x * FB_PIX;
@@ -323,9 +324,8 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
     for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
     const double vmin[3] = {p.frames[f].vmin[0], p.frames[f].vmin[1], p.frames[f].vmin[2]};
     float d[FB_PIX];
-    unsigned raw[FB_PIX], rgb[FB_PIX];
+    unsigned raw[FB_PIX];
     fb_depth8(p, dep, pix0, npx, d, raw);
-    if (PACKED) fb_color8(p.color + (int64_t)f * npx * 3, pix0, npx, rgb);
     int c = 0;
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) c += (pix0 + k < npx && d[k] > 0.0f) ? 1 : 0;
@@ -346,8 +346,7 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
     const unsigned long long fkey = sizeof(KeyT) == 8 ? (unsigned long long)f << kb.vbits
                                                       : (unsigned long long)(kb.tag ? p.frames[f].tag : 0) << 31;
     __shared__ KeyT s_key[FB_TILE];
-    __shared__ unsigned long long s_rec[PACKED ? FB_TILE : 1];
-    __shared__ unsigned s_val[PACKED ? 1 : FB_TILE];
+    __shared__ unsigned s_val[FB_TILE];
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
         double xyz[3];
@@ -355,11 +354,9 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
             long long kk[3];
 #pragma unroll
             for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
-            const KeyT key = (KeyT)(fkey | fb_voxel_key(kb, (unsigned long long)kk[0], (unsigned long long)kk[1],
-                                                        (unsigned long long)kk[2]));
-            s_key[loc] = key;
-            if (PACKED) s_rec[loc] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k]);
-            else s_val[loc] = (unsigned)((int64_t)f * npx + pix0 + k);
+            s_key[loc] = (KeyT)(fkey | fb_voxel_key(kb, (unsigned long long)kk[0], (unsigned long long)kk[1],
+                                                    (unsigned long long)kk[2]));
+            s_val[loc] = (unsigned)((int64_t)f * npx + pix0 + k);
             ++loc;
         }
     }
@@ -367,12 +364,7 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_keys(FbParams p, FbKeys kb, c
     const int n = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     for (int i = threadIdx.x; i < n; i += FB_THREADS) {
         keys[base + i] = s_key[i];
-        if (PACKED) {
-            vals[base + i] = (unsigned)(base + i);
-            packed[base + i] = s_rec[i];
-        } else {
-            vals[base + i] = s_val[i];
-        }
+        vals[base + i] = s_val[i];
     }
 }
 
@@ -391,14 +383,15 @@ struct FbCellKeys {
 // A run = consecutive pixels of one image row whose points fall in the same voxel (at 5 mm and 1280x720 a voxel spans
 // ~1.7 pixels of a row: 813k points -> ~480k runs per configs[2] frame).  The sort groups RUNS instead of points:
 // runs of one voxel keep their emission order, which is row-major pixel order, and a run's points are consecutive
-// in point order -- so a voxel's points are still summed in point-index order (Open3D's AddPoint order), the sort
-// moves ~0.6x the pairs and the head / reduce passes walk ~0.6x the items.
+// in point order -- so a voxel's points are still summed in point-index order (Open3D's AddPoint order), while the
+// sort moves ~0.6x the pairs.  A run's sort value is the point index of its first point; its other points follow in
+// the packed records until the next record flagged as a run head (FB_PACK_HEAD) or the frame's end.
 // Each tile of a frame emits its runs at the frame's point offset poff[f] + (runs of the frame's earlier tiles),
 // found by a decoupled look-back inside the frame (tiles take tickets in start order, so a tile only waits on running
 // ones); rlen[f] = the frame's run count (its segment of the sort holds that many, the rest is capacity).
 constexpr unsigned long long FB_LB_AGG = 1ull << 62, FB_LB_PRE = 2ull << 62, FB_LB_VAL = (1ull << 62) - 1;
 
-// key of pixel pix of frame f (false: no point), as k_fb_keys computes it
+// key of pixel pix of frame f (false: no point), as the tiles compute it
 __device__ inline bool fb_pixel_key(const FbParams& p, const FbKeys& kb, const double* m, const double vmin[3],
                                     const uint16_t* __restrict__ dep, int pix, unsigned& key) {
     float d = div_rn((float)dep[pix], p.scale_f, p.rscale_f);
@@ -414,7 +407,7 @@ __device__ inline bool fb_pixel_key(const FbParams& p, const FbKeys& kb, const d
 
 __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, const int* __restrict__ toff,
                                                         const int* __restrict__ poff, unsigned* __restrict__ rkeys,
-                                                        unsigned* __restrict__ rvals, int* __restrict__ rstart,
+                                                        unsigned* __restrict__ rvals,
                                                         unsigned long long* __restrict__ packed,
                                                         unsigned long long* status, int* ticket, int* __restrict__ rlen) {
     const int f = blockIdx.y;
@@ -427,7 +420,7 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
     __shared__ int s_excl;
     __shared__ unsigned long long s_rec[FB_TILE];
     __shared__ unsigned s_rkey[FB_TILE];
-    __shared__ int s_rstart[FB_TILE];
+    __shared__ unsigned s_rval[FB_TILE];
     if (threadIdx.x == 0) s_tile = atomicAdd(&ticket[f], 1);
     __syncthreads();
     const int tile = s_tile;  // tiles start in ticket order: the look-back below only waits on running tiles
@@ -478,14 +471,15 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
     }
     int c = 0, nr = 0;
     bool head[FB_PIX];
+    int col = pix0 % p.w;  // column of the lane's first pixel; a row starts where it wraps to 0
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
         const bool pvk = k == 0 ? pv != 0 : val[k - 1];
         const unsigned pkk = k == 0 ? pk : key[k - 1];
-        const bool row_start = ((pix0 + k) % p.w) == 0;
-        head[k] = val[k] && !(pvk && !row_start && pkk == key[k]);
+        head[k] = val[k] && !(pvk && col != 0 && pkk == key[k]);
         c += val[k] ? 1 : 0;
         nr += head[k] ? 1 : 0;
+        if (++col >= p.w) col = 0;
     }
     // exclusive prefixes of the lanes' point and run counts over the workgroup (packed: both <= 2048)
     const int both = (nr << 16) | c;
@@ -527,10 +521,10 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {
         if (!val[k]) continue;
-        s_rec[ploc] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k]);
+        s_rec[ploc] = fb_pack((unsigned)(pix0 + k), raw[k], rgb[k], head[k]);
         if (head[k]) {
             s_rkey[rloc] = key[k];
-            s_rstart[rloc] = base + ploc;
+            s_rval[rloc] = (unsigned)(base + ploc);
             ++rloc;
         }
         ++ploc;
@@ -540,29 +534,61 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
     const int rbase = poff[f] + s_excl;
     for (int i = threadIdx.x; i < n_runs; i += FB_THREADS) {
         rkeys[rbase + i] = s_rkey[i];
-        rvals[rbase + i] = (unsigned)(rbase + i);
-        rstart[rbase + i] = s_rstart[i];
+        rvals[rbase + i] = s_rval[i];
     }
 }
 
-// voxel heads over the runs (segment f = [poff[f], poff[f] + rlen[f]), the rest of its range is capacity): a frame's
-// first run or a new key
-struct SegHeadPredRuns {
-    const unsigned* keys;
-    const int* poff;
-    const int* rlen;
-    int F;
-    __device__ bool operator()(int64_t i) const {
-        const int f = frame_of(poff, F, i);
-        if (i - poff[f] >= rlen[f]) return false;
-        return i == poff[f] || keys[i] != keys[i - 1];
+// Voxel heads over the sorted runs, frame by frame (segment f = [poff[f], poff[f] + rlen[f]); the rest of the frame's
+// range is capacity the sort left untouched): a frame's first run or a new key.  Grid (chunks, F): the block knows its
+// frame; per block the head count, then (after the scan) the heads in order.
+constexpr int FB_HEAD_CHUNK = 2048;  // runs per block (256 threads x 8)
+__device__ inline bool fb_run_head(const unsigned* __restrict__ keys, int i, int beg) {
+    return i == beg || keys[i] != keys[i - 1];
+}
+__global__ __launch_bounds__(256) void k_fb_heads_count(const unsigned* __restrict__ keys, const int* __restrict__ poff,
+                                                        const int* __restrict__ rlen, int chunks, int* __restrict__ counts) {
+    const int f = blockIdx.y, b = blockIdx.x;
+    const int beg = poff[f], n = rlen[f];
+    int c = 0;
+    for (int k = 0; k < FB_HEAD_CHUNK / 256; ++k) {
+        const int j = b * FB_HEAD_CHUNK + k * 256 + threadIdx.x;
+        c += (j < n && fb_run_head(keys, beg + j, beg)) ? 1 : 0;
     }
-};
+    c = wave_sum(c);
+    __shared__ int ws[4];
+    if (lane_id() == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[f * chunks + b] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+__global__ __launch_bounds__(256) void k_fb_heads_emit(const unsigned* __restrict__ keys, const int* __restrict__ poff,
+                                                       const int* __restrict__ rlen, int chunks,
+                                                       const int* __restrict__ offs, int* __restrict__ heads) {
+    const int f = blockIdx.y, b = blockIdx.x;
+    const int beg = poff[f], n = rlen[f];
+    int out = offs[f * chunks + b];
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+    __shared__ int ws[4];
+    for (int k = 0; k < FB_HEAD_CHUNK / 256; ++k) {  // 256 consecutive runs per round, emitted in order
+        const int j = b * FB_HEAD_CHUNK + k * 256 + threadIdx.x;
+        const bool h = j < n && fb_run_head(keys, beg + j, beg);
+        int tot = 0;
+        const int ex = wave_excl_count(h, tot);
+        if (lane == 0) ws[wid] = tot;
+        __syncthreads();
+        int before = 0, all = 0;
+        for (int w = 0; w < 4; ++w) {
+            before += w < wid ? ws[w] : 0;
+            all += ws[w];
+        }
+        if (h) heads[out + before + ex] = beg + j;
+        out += all;
+        __syncthreads();
+    }
+}
 
-// one lane per voxel: its runs (sorted values = run positions, in emission order) and each run's points (consecutive
-// point records) re-unprojected and summed in point order
+// one lane per voxel: its runs (sorted values = the runs' first point indices, in emission order) and each run's points
+// (consecutive packed records up to the next run head) re-unprojected and summed in point order
 __global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsigned* __restrict__ sval,
-                                                        const int* __restrict__ rstart,
                                                         const unsigned long long* __restrict__ packed,
                                                         const int* __restrict__ poff, const int* __restrict__ rlen,
                                                         const int* __restrict__ heads, int64_t K, int64_t P,
@@ -585,13 +611,13 @@ __global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsign
     double sp[3] = {0, 0, 0}, sc[3] = {0, 0, 0};
     int cnt = 0;
     for (int r = beg; r < end; ++r) {
-        const int ri = (int)sval[r];
-        const int q0 = rstart[ri], q1 = ri + 1 < fend ? rstart[ri + 1] : pend;
-        for (int q = q0; q < q1; ++q) {
-            const unsigned long long rec = packed[q];
+        int q = (int)sval[r];
+        unsigned long long rec = packed[q];
+        while (true) {
+            const unsigned long long nxt = q + 1 < pend ? packed[q + 1] : FB_PACK_HEAD;  // issued before the sums
             const int pix = (int)(rec & ((1u << FB_PACK_PIX_BITS) - 1));
-            const float dd = (float)(unsigned)((rec >> FB_PACK_PIX_BITS) & 0xFFFFu);
-            const unsigned rgb = (unsigned)(rec >> (FB_PACK_PIX_BITS + 16));
+            const float dd = (float)(unsigned)((rec >> FB_PACK_DEPTH_SHIFT) & 0xFFFFu);
+            const unsigned rgb = (unsigned)(rec >> (FB_PACK_DEPTH_SHIFT + 16));
             double xyz[3];
             fb_point(p, m, div_rn(dd, p.scale_f, p.rscale_f), pix, xyz);  // valid by construction
 #pragma unroll
@@ -600,6 +626,9 @@ __global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsign
             sc[1] += div_rn((double)((rgb >> 8) & 0xFF), 255.0, 1.0 / 255.0);
             sc[2] += div_rn((double)(rgb >> 16), 255.0, 1.0 / 255.0);
             ++cnt;
+            if (nxt & FB_PACK_HEAD) break;  // the next record starts another run (or the frame ended)
+            rec = nxt;
+            ++q;
         }
     }
     const double cntd = (double)cnt, rc = 1.0 / cntd;
@@ -610,20 +639,16 @@ __global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsign
     }
 }
 
-// one lane per voxel: its points (sorted values, in index order) re-unprojected and summed.  PACKED: values are
-// point indices into the fb_pack records and the voxel's frame is found in the point offsets poff[0 .. F); else
-// values are global pixel indices into the depth / colour images
-template <bool PACKED>
+// one lane per voxel: its points (sorted values = global pixel indices, in index order) re-unprojected from the
+// depth / colour images and summed
 __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* __restrict__ sval,
-                                                   const unsigned long long* __restrict__ packed,
-                                                   const int* __restrict__ poff, const int* __restrict__ heads,
-                                                   int64_t K, int64_t P, double* __restrict__ vx,
-                                                   double* __restrict__ vc, FbCellKeys ck) {
+                                                   const int* __restrict__ heads, int64_t K, int64_t P,
+                                                   double* __restrict__ vx, double* __restrict__ vc, FbCellKeys ck) {
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (s >= K) return;
     const int64_t beg = heads[s], end = (s + 1 < K) ? heads[s + 1] : P;
     const int npx = p.w * p.h;
-    const int f = PACKED ? frame_of(poff, p.F, beg) : (int)(sval[beg] / (unsigned)npx);
+    const int f = (int)(sval[beg] / (unsigned)npx);
     if (ck.k32) {
         const unsigned vk = ck.vbits < 32 ? (ck.k32[beg] & ((1u << ck.vbits) - 1u)) : ck.k32[beg];
         ck.out[s] = ((unsigned long long)f << ck.sf) | (unsigned long long)(vk >> ck.shift);
@@ -642,26 +667,13 @@ __global__ __launch_bounds__(256) void k_fb_reduce(FbParams p, const unsigned* _
         int pix[VB];
         float dd[VB];
         unsigned cc[VB][3];
-        if (PACKED) {
-            unsigned long long rec[VB];
 #pragma unroll
-            for (int k = 0; k < VB; ++k) rec[k] = packed[sval[j0 + k < end ? j0 + k : j0]];
+        for (int k = 0; k < VB; ++k) pix[k] = (int)(sval[j0 + k < end ? j0 + k : j0] - (unsigned)f * (unsigned)npx);
 #pragma unroll
-            for (int k = 0; k < VB; ++k) {
-                pix[k] = (int)(rec[k] & ((1u << FB_PACK_PIX_BITS) - 1));
-                dd[k] = (float)(unsigned)((rec[k] >> FB_PACK_PIX_BITS) & 0xFFFFu);
-                const unsigned rgb = (unsigned)(rec[k] >> (FB_PACK_PIX_BITS + 16));
-                cc[k][0] = rgb & 0xFF, cc[k][1] = (rgb >> 8) & 0xFF, cc[k][2] = rgb >> 16;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < VB; ++k) pix[k] = (int)(sval[j0 + k < end ? j0 + k : j0] - (unsigned)f * (unsigned)npx);
-#pragma unroll
-            for (int k = 0; k < VB; ++k) {
-                dd[k] = (float)dep[pix[k]];
-                const uint8_t* cp = col + (int64_t)pix[k] * 3;
-                cc[k][0] = cp[0], cc[k][1] = cp[1], cc[k][2] = cp[2];
-            }
+        for (int k = 0; k < VB; ++k) {
+            dd[k] = (float)dep[pix[k]];
+            const uint8_t* cp = col + (int64_t)pix[k] * 3;
+            cc[k][0] = cp[0], cc[k][1] = cp[1], cc[k][2] = cp[2];
         }
 #pragma unroll
         for (int k = 0; k < VB; ++k) {
@@ -700,22 +712,11 @@ __global__ void k_fb_frame_offsets(const unsigned* __restrict__ sval, const int*
 
 // the same from the point offsets (segmented sort: frame f's points stay in [poff[f], poff[f + 1]), and each frame's
 // first point is a voxel head): offs[f] = first voxel whose head is >= poff[f]
-__global__ void k_fb_frame_offsets_seg(const int* __restrict__ poff, const int* __restrict__ heads, int64_t K, int F,
-                                       int* __restrict__ offs) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f > F) return;
-    if (f == F) {
-        offs[F] = (int)K;
-        return;
-    }
-    const int target = poff[f];
-    int64_t lo = 0, hi = K;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (heads[mid] < target) lo = mid + 1;
-        else hi = mid;
-    }
-    offs[f] = (int)lo;
+__global__ void k_fb_voxel_offsets(const int* __restrict__ hc, int chunks, int F, const int64_t* __restrict__ total,
+                                   int* __restrict__ offs) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;  // the scanned head counts: frame f's first chunk's offset
+    if (f < F) offs[f] = hc[f * chunks];
+    else if (f == F) offs[F] = (int)*total;
 }
 
 // kept_off[f] = first kept entry whose voxel index is >= voff[f]
@@ -969,20 +970,34 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     // the bench / production path: u32 keys, frames up to 2^24 pixels -> runs of pixels sorted (packed point records)
     const bool pack = seg32 && npx <= (1 << FB_PACK_PIX_BITS);
     unsigned long long* packed = nullptr;
-    int* rstart = nullptr;
     if (pack) {  // runs: one sort segment per frame, [poff[f], poff[f] + rlen[f]) of each frame's point range
         unsigned* k32 = (unsigned*)kin;
         unsigned* k32o = k32 + P;
-        packed = (unsigned long long*)fl->b_packed.get((size_t)P * 12 + 256);
+        packed = (unsigned long long*)fl->b_packed.get((size_t)P * 8 + 256);
         if (!packed) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
-        rstart = (int*)(packed + P);
         hipLaunchKernelGGL(k_fb_runs, dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb, (const int*)d_tc,
-                           (const int*)d_poff, k32, vin, rstart, packed, d_status, d_ticket, d_rlen);
+                           (const int*)d_poff, k32, vin, packed, d_status, d_ticket, d_rlen);
         OT_LAUNCH_CHECK();
         st = sort_segments_u32_u32(k32, k32o, vin, vout, fl->poff.data(), F, vbits, stream, 3, d_rlen);
         if (st != OT_OK) return st;
-        st = compact(P, SegHeadPredRuns{k32o, d_poff, d_rlen, F}, SegHeadEmit{heads}, stream, &K, 7);  // sync 2
-        if (st != OT_OK) return st;
+        // voxel heads frame by frame: count per (chunk, frame), one scan, emit; sync 2 reads the total
+        int maxpts = 0;
+        for (int f = 0; f < F; ++f) maxpts = std::max(maxpts, (int)(fl->poff[f + 1] - fl->poff[f]));
+        const int chunks = std::max(1, (maxpts + FB_HEAD_CHUNK - 1) / FB_HEAD_CHUNK);
+        char* ws = (char*)scratch(sizeof(int) * (size_t)chunks * F + 64, 7);
+        if (!ws) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
+        int64_t* d_total = (int64_t*)ws;
+        int* d_hc = (int*)(ws + 64);
+        hipLaunchKernelGGL(k_fb_heads_count, dim3(chunks, F), dim3(256), 0, stream, (const unsigned*)k32o,
+                           (const int*)d_poff, (const int*)d_rlen, chunks, d_hc);
+        hipLaunchKernelGGL(k_scan_inplace, dim3(1), dim3(1024), 0, stream, d_hc, chunks * F, d_total);
+        hipLaunchKernelGGL(k_fb_heads_emit, dim3(chunks, F), dim3(256), 0, stream, (const unsigned*)k32o,
+                           (const int*)d_poff, (const int*)d_rlen, chunks, (const int*)d_hc, heads);
+        hipLaunchKernelGGL(k_fb_voxel_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const int*)d_hc, chunks, F,
+                           (const int64_t*)d_total, d_voff);
+        OT_LAUNCH_CHECK();
+        OT_HIP_TRY(hipMemcpyAsync(&K, d_total, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+        OT_HIP_TRY(hipStreamSynchronize(stream));
     } else if (seg32) {  // 32-bit voxel keys of single points, one sort segment per frame: 8 B per pair per pass
         unsigned* k32 = (unsigned*)kin;
         unsigned* k32o = k32 + P;
@@ -996,8 +1011,8 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
             }
             OT_HIP_TRY(hipMemcpyAsync(d_frames, fl->h_frames, sizeof(FbFrame) * F, hipMemcpyHostToDevice, stream));
         }
-        hipLaunchKernelGGL((k_fb_keys<unsigned, false>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kt,
-                           (const int*)d_tc, k32, vin, nullptr);
+        hipLaunchKernelGGL((k_fb_keys<unsigned>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kt, (const int*)d_tc,
+                           k32, vin);
         OT_LAUNCH_CHECK();
         st = sort_segments_u32_u32(k32, k32o, vin, vout, fl->poff.data(), F, vbits, stream, 3);
         if (st != OT_OK) return st;
@@ -1005,18 +1020,15 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
         else st = compact(P, SegHeadPredPix{k32o, vout, (unsigned)npx}, SegHeadEmit{heads}, stream, &K, 7);
         if (st != OT_OK) return st;
     } else {
-        hipLaunchKernelGGL((k_fb_keys<unsigned long long, false>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb,
-                           (const int*)d_tc, kin, vin, nullptr);
+        hipLaunchKernelGGL((k_fb_keys<unsigned long long>), dim3(tpf, F), dim3(FB_THREADS), 0, stream, p, kb,
+                           (const int*)d_tc, kin, vin);
         OT_LAUNCH_CHECK();
         st = sort_pairs_u64_u32(kin, kout, vin, vout, (size_t)P, end_bit, stream, 3);
         if (st != OT_OK) return st;
         st = compact(P, SegHeadPred{kout}, SegHeadEmit{heads}, stream, &K, 7);  // synchronises (sync 2)
         if (st != OT_OK) return st;
     }
-    if (pack)
-        hipLaunchKernelGGL(k_fb_frame_offsets_seg, dim3((F + 64) / 64), dim3(64), 0, stream, (const int*)d_poff,
-                           (const int*)heads, K, F, d_voff);
-    else
+    if (!pack)
         hipLaunchKernelGGL(k_fb_frame_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const unsigned*)vout,
                            (const int*)heads, K, npx, F, d_voff);
     fl->K = K;
@@ -1032,11 +1044,11 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
                         3 * m, vbits, gsf, ckeys};
     if (pack)
         hipLaunchKernelGGL(k_fb_reduce_runs, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
-                           (const unsigned*)vout, (const int*)rstart, (const unsigned long long*)packed,
+                           (const unsigned*)vout, (const unsigned long long*)packed,
                            (const int*)d_poff, (const int*)d_rlen, (const int*)heads, K, P, fl->vx, fl->vc, ck);
     else
-        hipLaunchKernelGGL(k_fb_reduce<false>, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
-                           (const unsigned*)vout, nullptr, nullptr, (const int*)heads, K, P, fl->vx, fl->vc, ck);
+        hipLaunchKernelGGL(k_fb_reduce, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
+                           (const unsigned*)vout, (const int*)heads, K, P, fl->vx, fl->vc, ck);
     OT_LAUNCH_CHECK();
     std::vector<int> hvoff(F + 1);
     OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));

@@ -192,6 +192,9 @@ __global__ __launch_bounds__(Rs<D>::THREADS) void k_rs_scatter(const KeyT* __res
     if (tile >= sg.tile[sgi + 1]) return;  // past the end of a shorter segment (block-uniform)
     const int base = sg.start[sgi] + (tile - first) * RS_TILE;
     const int n = rs_seg_end(sg, sgi);  // end of the segment's items
+    // a tile wholly in a segment's unused capacity (dlen): nothing to move, and no tile of the segment with items
+    // looks back past it (block-uniform)
+    if (base >= n && tile > first) return;
     const int wbase = base + w * RS_CHUNK;  // this wave's contiguous run: items wbase + r * 64 + lane
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     KeyT key[RS_ITEMS];
