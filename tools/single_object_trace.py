@@ -1,0 +1,90 @@
+"""One configs[3] object end to end on one stream, unsynchronised between phases (exactly bench.py's single_object
+leg), repeated: run it under `rocprofv3 --kernel-trace` and feed the trace to `--report` for the kernel timeline of
+the last repetition (durations and the idle gaps between kernels).  Tool only.
+
+  rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 tools/single_object_trace.py
+  python3 tools/single_object_trace.py --report DIR/run_kernel_trace.csv
+"""
+import csv
+import ctypes as C
+import importlib
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "object-triggered-3d-slam_amd"
+REPS = 8
+
+
+def report(path):
+    rows = []
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], int(r.get("Stream_Id", 0) or 0)))
+    rows.sort()
+    # every repetition launches the same kernels: the last REPS-th of the trace is the last repetition
+    last = rows[len(rows) - len(rows) // REPS:]
+    t0 = last[0][0]
+    busy = {}
+    prev_end = t0
+    print(f"{'start_us':>9} {'dur_us':>8} {'gap_us':>8} stream kernel")
+    for s, e, name, sid in last:
+        gap = (s - prev_end) / 1e3
+        print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {gap:8.1f} {sid:6d} {name[:90]}")
+        prev_end = max(prev_end, e)
+        short = name.split("(")[0][:60]
+        busy[short] = busy.get(short, 0.0) + (e - s) / 1e3
+    span = (max(r[1] for r in last) - t0) / 1e3
+    print(f"span {span:.1f} us over {len(last)} kernels")
+    for k, v in sorted(busy.items(), key=lambda kv: -kv[1])[:25]:
+        print(f"{v:9.1f} us  {k}")
+
+
+def main():
+    synth = importlib.import_module(PKG + ".synth")
+    depth, color, ext = synth.make_sequence(synth.object_scene(0), n_frames=64)
+    import torch
+
+    pkg = importlib.import_module(PKG)
+    L = importlib.import_module(PKG + "._lib")
+    lib = L.load()
+    intr_t = synth.REF_INTRINSICS_640
+    W, H = intr_t[0], intr_t[1]
+    intr = L.ot_intrinsics(W, H, *intr_t[2:])
+    npx = W * H
+    d16 = torch.from_numpy(depth.view(np.int16)).cuda().view(torch.uint16).contiguous()
+    col = torch.from_numpy(color).cuda().contiguous()
+    ext = np.ascontiguousarray(ext, dtype=np.float64)
+    vol = pkg.pipelines.integration.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04,
+                                                       color_type=pkg.pipelines.integration.TSDFVolumeColorType.RGB8)
+    s_ = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    dp, cp, ep, intr_ref = d16.data_ptr(), col.data_ptr(), ext.ctypes.data, C.byref(intr)
+
+    def one():
+        vol.reset()
+        for k in range(ext.shape[0]):
+            lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128, 1000.0,
+                                      3.0, s_)
+        mesh = vol.extract_triangle_mesh()
+        mesh.compute_vertex_normals()
+        return mesh.sample_points_uniformly(number_of_points=100000).filter_min_z(0.03)
+
+    ts = []
+    for _ in range(REPS):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        one()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t) * 1e3)
+    print("single object ms (median of last 5):", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--report":
+        report(sys.argv[2])
+    else:
+        main()
