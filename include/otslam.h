@@ -324,6 +324,14 @@ ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs_h
 ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs_host, int32_t n_jobs,
                                                 int64_t n_points, uint64_t seed, void* inputs_ready_event,
                                                 void* stream);
+/* reconstruct_rgbd_filter.py:123-132 in one pass per mesh: sample_points_uniformly(n_points) (the same points as
+ * ot_mesh_sample_points_uniformly with this seed), then the Z mask points[:, 2] >= z_min (NaN fails) applied in
+ * the sampling order.  The reference rebuilds its cloud from the points and colours alone, so the kept rows are written
+ * to out_xyz / out_colors (each with room for n_points rows; out_colors may be NULL) and normals are not interpolated
+ * (out_normals and vertex_normals are ignored: the vertex normals need not be ready).  n_kept_host: host int64_t
+ * [n_jobs], the kept row count of each job.  Synchronises the stream. */
+ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs_host, int32_t n_jobs, int64_t n_points,
+                                      uint64_t seed, double z_min, int64_t* n_kept_host, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------
  * Hybrid map — fusion/hybrid_map.py

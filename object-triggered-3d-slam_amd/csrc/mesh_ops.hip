@@ -10,6 +10,7 @@
 // then generated in parallel, one lane per output point: binary search of its triangle in the n_t array,
 // r1/r2 from a counter-based RNG (splitmix64 of seed + counter; Open3D's mt19937 is unseeded), barycentric
 // a = 1 - sqrt(r1), b = sqrt(r1)(1 - r2), c = sqrt(r1) r2.
+#include <functional>
 #include <vector>
 
 #include "chain.h"
@@ -548,38 +549,154 @@ __device__ inline double rng_u01(unsigned long long seed, unsigned long long ctr
     return (double)(z >> 11) * (1.0 / 9007199254740992.0);
 }
 
-__global__ __launch_bounds__(256) void k_sample(const double* __restrict__ V, const double* __restrict__ VN,
-                                                const double* __restrict__ VC, const int32_t* __restrict__ T,
-                                                const long long* __restrict__ ncum, int64_t nt, int64_t N,
-                                                unsigned long long seed, double* P, double* PN, double* PC) {
-    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (k >= N) return;
-    // triangle t: first index with ncum[t] > k (the CPU loop fills points [ncum[t-1], ncum[t]) from t)
+// point k of the sampling: triangle t = first index with ncum[t] > k (the CPU loop fills points [ncum[t-1], ncum[t])
+// from t), barycentric weights from the counter RNG; false: rounding shortfall (Open3D leaves those points zero)
+__device__ inline bool sample_triangle(const long long* __restrict__ ncum, int64_t nt, int64_t k,
+                                       unsigned long long seed, int64_t& t, double& a, double& b, double& c) {
     int64_t lo = 0, hi = nt;
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
         if (ncum[mid] > k) hi = mid;
         else lo = mid + 1;
     }
-    if (lo >= nt) {  // rounding shortfall: left zero like Open3D's zero-initialised storage
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            P[k * 3 + d] = 0.0;
-            if (PN) PN[k * 3 + d] = 0.0;
-            if (PC) PC[k * 3 + d] = 0.0;
-        }
-        return;
-    }
-    const int64_t t = lo;
+    if (lo >= nt) return false;
+    t = lo;
     const double r1 = rng_u01(seed, (unsigned long long)(2 * k)), r2 = rng_u01(seed, (unsigned long long)(2 * k + 1));
     const double s1 = sqrt(r1);
-    const double a = 1.0 - s1, b = s1 * (1.0 - r2), c = s1 * r2;
-    const int64_t i0 = T[t * 3], i1 = T[t * 3 + 1], i2 = T[t * 3 + 2];
+    a = 1.0 - s1, b = s1 * (1.0 - r2), c = s1 * r2;
+    return true;
+}
+__device__ inline void interp3(const double* __restrict__ A, int64_t i0, int64_t i1, int64_t i2, double a, double b,
+                               double c, double out[3]) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) out[d] = (a * A[i0 * 3 + d] + b * A[i1 * 3 + d]) + c * A[i2 * 3 + d];
+}
+
+__global__ __launch_bounds__(256) void k_sample(const double* __restrict__ V, const double* __restrict__ VN,
+                                                const double* __restrict__ VC, const int32_t* __restrict__ T,
+                                                const long long* __restrict__ ncum, int64_t nt, int64_t N,
+                                                unsigned long long seed, double* P, double* PN, double* PC) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= N) return;
+    int64_t t;
+    double a, b, c;
+    double x[3] = {0, 0, 0}, n[3] = {0, 0, 0}, col[3] = {0, 0, 0};
+    if (sample_triangle(ncum, nt, k, seed, t, a, b, c)) {
+        const int64_t i0 = T[t * 3], i1 = T[t * 3 + 1], i2 = T[t * 3 + 2];
+        interp3(V, i0, i1, i2, a, b, c, x);
+        if (PN) interp3(VN, i0, i1, i2, a, b, c, n);
+        if (PC) interp3(VC, i0, i1, i2, a, b, c, col);
+    }
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-        P[k * 3 + d] = (a * V[i0 * 3 + d] + b * V[i1 * 3 + d]) + c * V[i2 * 3 + d];
-        if (PN) PN[k * 3 + d] = (a * VN[i0 * 3 + d] + b * VN[i1 * 3 + d]) + c * VN[i2 * 3 + d];
-        if (PC) PC[k * 3 + d] = (a * VC[i0 * 3 + d] + b * VC[i1 * 3 + d]) + c * VC[i2 * 3 + d];
+        P[k * 3 + d] = x[d];
+        if (PN) PN[k * 3 + d] = n[d];
+        if (PC) PC[k * 3 + d] = col[d];
+    }
+}
+
+// The sampling and the Z mask of reconstruct_rgbd_filter.py:123-132 in one pass: the points with z >= z_min (NaN
+// fails, as numpy's mask) in sampling order, xyz and colours only (the reference rebuilds its cloud from those two, so
+// normals are not interpolated).  A workgroup takes MZ_TILE consecutive points in a ticket order, counts the kept
+// ones and finds its output offset by a decoupled look-back over the job's earlier workgroups; grid (tiles, jobs).
+constexpr int MZ_ITEMS = 4, MZ_TILE = 256 * MZ_ITEMS;
+constexpr unsigned long long MZ_AGG = 1ull << 62, MZ_PRE = 2ull << 62, MZ_VAL = (1ull << 62) - 1;
+struct MinZJob {
+    const double* V;
+    const double* VC;
+    const int32_t* T;
+    const long long* ncum;
+    int64_t nt;
+    double* P;
+    double* PC;
+};
+__global__ __launch_bounds__(256) void k_round_counts_jobs(const MinZJob* __restrict__ jobs, const double* const* cdfs,
+                                                           int64_t N, long long* const* ncums) {
+    const int j = blockIdx.y;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= jobs[j].nt) return;
+    const long long v = (long long)round(cdfs[j][t] * (double)N);
+    ncums[j][t] = v < N ? v : N;
+}
+__global__ __launch_bounds__(256) void k_sample_min_z(const MinZJob* __restrict__ jobs, int64_t N,
+                                                      unsigned long long seed, double z_min, int tiles,
+                                                      unsigned long long* status, int* ticket,
+                                                      long long* __restrict__ kept) {
+    const int j = blockIdx.y;
+    const MinZJob jb = jobs[j];
+    __shared__ int s_tile;
+    __shared__ int wsum[MZ_ITEMS][4];
+    __shared__ long long s_excl;
+    if (threadIdx.x == 0) s_tile = atomicAdd(&ticket[j], 1);
+    __syncthreads();
+    const int tile = s_tile;  // tiles start in ticket order: the look-back only waits on running workgroups
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+    double x[MZ_ITEMS][3], col[MZ_ITEMS][3];
+    bool keep[MZ_ITEMS];
+    int pre[MZ_ITEMS];
+#pragma unroll
+    for (int i = 0; i < MZ_ITEMS; ++i) {
+        const int64_t k = (int64_t)tile * MZ_TILE + i * 256 + threadIdx.x;
+        int64_t t;
+        double a, b, c;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) x[i][d] = col[i][d] = 0.0;
+        keep[i] = false;
+        if (k < N) {
+            if (sample_triangle(jb.ncum, jb.nt, k, seed, t, a, b, c)) {
+                const int64_t i0 = jb.T[t * 3], i1 = jb.T[t * 3 + 1], i2 = jb.T[t * 3 + 2];
+                interp3(jb.V, i0, i1, i2, a, b, c, x[i]);
+                if (jb.PC) interp3(jb.VC, i0, i1, i2, a, b, c, col[i]);
+            }
+            keep[i] = x[i][2] >= z_min;
+        }
+        int tot;
+        pre[i] = wave_excl_count(keep[i], tot);
+        if (lane == 0) wsum[i][wid] = tot;
+    }
+    __syncthreads();
+    int n_keep = 0;
+#pragma unroll
+    for (int i = 0; i < MZ_ITEMS; ++i) n_keep += wsum[i][0] + wsum[i][1] + wsum[i][2] + wsum[i][3];
+    if (threadIdx.x == 0) {
+        unsigned long long* st = status + (int64_t)j * tiles;
+        long long excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(&st[0], MZ_PRE | (unsigned long long)n_keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&st[tile], MZ_AGG | (unsigned long long)n_keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int t = tile - 1; t >= 0;) {
+                const unsigned long long v = __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v == 0ull) continue;  // not published yet (an earlier ticket: running)
+                excl += (long long)(v & MZ_VAL);
+                if ((v & ~MZ_VAL) == MZ_PRE) break;
+                --t;
+            }
+            __hip_atomic_store(&st[tile], MZ_PRE | (unsigned long long)(excl + n_keep), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_excl = excl;
+        if (tile == tiles - 1) kept[j] = excl + n_keep;
+    }
+    __syncthreads();
+    long long pos = s_excl;
+#pragma unroll
+    for (int i = 0; i < MZ_ITEMS; ++i) {
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            off += w < wid ? wsum[i][w] : 0;
+            tot += wsum[i][w];
+        }
+        if (keep[i]) {
+            const long long o = pos + off + pre[i];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                jb.P[o * 3 + d] = x[i][d];
+                if (jb.PC) jb.PC[o * 3 + d] = col[i][d];
+            }
+        }
+        pos += tot;
     }
 }
 
@@ -635,12 +752,16 @@ ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, 
     return ot_mesh_sample_points_uniformly_after(jobs, n_jobs, n_points, seed, nullptr, stream);
 }
 
-ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points,
-                                                uint64_t seed, void* inputs_ready, void* stream_) {
-    hipStream_t stream = S(stream_);
-    if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
-    if (n_jobs < 0 || (n_jobs > 0 && !jobs)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
-    if (n_jobs == 0) return OT_OK;
+}  // extern "C"
+
+namespace ot {
+// The area sums and CDFs of every job (SamplePointsUniformly's two serial float64 chains, run side by side) into
+// scratch slot 17, followed by `extra` bytes for the caller, whose leading `upload` bytes travel to the device with the
+// chain table in one copy: fill(host, dev) writes them once the layout is known.  cdf[j]: the job's CDF (device);
+// ncum[j]: room for its rounded counts; *extra_dev: the caller's device region.
+static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, size_t extra, size_t upload,
+                             const std::function<void(char*, char*)>& fill, hipStream_t stream,
+                             std::vector<double*>& cdf, std::vector<long long*>& ncum, char** extra_dev) {
     size_t bytes = 256;
     int64_t max_nt = 0;
     for (int j = 0; j < n_jobs; ++j) {
@@ -652,53 +773,133 @@ ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs, 
         bytes += (size_t)m.n_triangles * 32 + 256 + chain_aux_bytes(m.n_triangles);
         max_nt = m.n_triangles > max_nt ? m.n_triangles : max_nt;
     }
-    char* ws = (char*)scratch(bytes + sizeof(ChainJob) * 2 * (size_t)n_jobs + 256, 17);
+    const size_t table = sizeof(ChainJob) * 2 * (size_t)n_jobs;
+    char* ws = (char*)scratch(bytes + table + extra + 512, 17);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-    std::vector<ChainJob> chain(2 * (size_t)n_jobs);  // [sum chains | CDF chains]
-    std::vector<double*> areas(n_jobs), qs(n_jobs), sums(n_jobs);
-    std::vector<long long*> ncums(n_jobs);
+    std::vector<char> up(table + upload);  // [sum chains | CDF chains | caller's upload]
+    ChainJob* chain = (ChainJob*)up.data();
+    std::vector<double*> sums(n_jobs), qs(n_jobs);
+    cdf.assign(n_jobs, nullptr);
+    ncum.assign(n_jobs, nullptr);
     char* cur = ws;
     for (int j = 0; j < n_jobs; ++j) {
         const int64_t nt = jobs[j].n_triangles, nt2 = (nt + 1) & ~(int64_t)1;
         sums[j] = (double*)cur;
-        areas[j] = sums[j] + 8;  // 64-B offset: 16-B aligned rows for the chains' double2 loads
-        qs[j] = areas[j] + nt2;
-        ncums[j] = (long long*)(qs[j] + nt2);
-        cur = (char*)(ncums[j] + nt2) + 64;
+        cdf[j] = sums[j] + 8;  // 64-B offset: 16-B aligned rows for the chains' double2 loads
+        qs[j] = cdf[j] + nt2;
+        ncum[j] = (long long*)(qs[j] + nt2);
+        cur = (char*)(ncum[j] + nt2) + 64;
         cur = (char*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
-        ChainJob& cs = chain[j];
-        cs.x = areas[j], cs.n = nt, cs.out = sums[j];
+        ChainJob cs{};
+        cs.x = cdf[j], cs.n = nt, cs.out = sums[j];
         cur = chain_aux(cur, nt, cs);
-        ChainJob& cc = chain[n_jobs + j];
-        cc = cs;
-        cc.x = qs[j], cc.out = areas[j];  // the CDF overwrites the areas once q = a / s is formed
+        ChainJob cc = cs;
+        cc.x = qs[j], cc.out = cdf[j];  // the CDF overwrites the areas once q = a / s is formed
+        chain[j] = cs;
+        chain[n_jobs + j] = cc;
         hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, jobs[j].vertices,
-                           jobs[j].triangles, nt, areas[j]);
+                           jobs[j].triangles, nt, cdf[j]);
     }
     ChainJob* djobs = (ChainJob*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
-    OT_HIP_TRY(hipMemcpyAsync(djobs, chain.data(), sizeof(ChainJob) * 2 * n_jobs, hipMemcpyHostToDevice, stream));
+    *extra_dev = (char*)djobs + table;
+    if (upload) fill(up.data() + table, *extra_dev);
+    // pageable source: the copy is complete in stream order; the callers synchronise before returning
+    OT_HIP_TRY(hipMemcpyAsync(djobs, up.data(), up.size(), hipMemcpyHostToDevice, stream));
     launch_chains<false>(djobs, n_jobs, max_nt, stream);
     for (int j = 0; j < n_jobs; ++j) {
         const int64_t nt = jobs[j].n_triangles;
-        hipLaunchKernelGGL(k_area_div, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, (const double*)areas[j],
+        hipLaunchKernelGGL(k_area_div, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, (const double*)cdf[j],
                            nt, (const double*)sums[j], qs[j]);
     }
     launch_chains<true>(djobs + n_jobs, n_jobs, max_nt, stream);
+    OT_LAUNCH_CHECK();
+    return OT_OK;
+}
+}  // namespace ot
+
+extern "C" {
+
+ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points,
+                                                uint64_t seed, void* inputs_ready, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
+    if (n_jobs < 0 || (n_jobs > 0 && !jobs)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
+    if (n_jobs == 0) return OT_OK;
+    std::vector<double*> cdf;
+    std::vector<long long*> ncum;
+    char* extra = nullptr;
+    ot_status st = sample_cdfs(jobs, n_jobs, 0, 0, nullptr, stream, cdf, ncum, &extra);
+    if (st != OT_OK) return st;
     // the vertex normals / colours the emission interpolates may still be in flight on another stream (the facade
     // computes the normals of a fresh mesh beside the area chains above, which read only V and T)
     if (inputs_ready) OT_HIP_TRY(hipStreamWaitEvent(stream, (hipEvent_t)inputs_ready, 0));
     for (int j = 0; j < n_jobs; ++j) {
         const ot_mesh_sample_job& m = jobs[j];
         const int64_t nt = m.n_triangles;
-        hipLaunchKernelGGL(k_round_counts, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, areas[j], nt,
-                           n_points, ncums[j]);
+        hipLaunchKernelGGL(k_round_counts, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, cdf[j], nt,
+                           n_points, ncum[j]);
         hipLaunchKernelGGL(k_sample, dim3((unsigned)((n_points + 255) / 256)), dim3(256), 0, stream, m.vertices,
                            m.out_normals ? m.vertex_normals : nullptr, m.out_colors ? m.vertex_colors : nullptr,
-                           m.triangles, ncums[j], nt, n_points, (unsigned long long)seed, m.out_xyz, m.out_normals,
+                           m.triangles, ncum[j], nt, n_points, (unsigned long long)seed, m.out_xyz, m.out_normals,
                            m.out_colors);
     }
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(stream));  // the host job table is released on return
+    return OT_OK;
+}
+
+ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
+                                      double z_min, int64_t* n_kept_host, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
+    if (n_jobs < 0 || (n_jobs > 0 && (!jobs || !n_kept_host)))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
+    if (n_jobs == 0) return OT_OK;
+    if (n_points > ((int64_t)1 << 40)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many points");
+    const int64_t tiles64 = (n_points + MZ_TILE - 1) / MZ_TILE;
+    if (tiles64 > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many points");
+    const int tiles = (int)tiles64;
+    // caller region: [MinZJob x n | cdf ptrs | ncum ptrs] (uploaded) | align 64 | kept i64 [n] | ticket i32 [n] |
+    // align 64 | status u64 [n][tiles] (zeroed)
+    const size_t up_bytes = (sizeof(MinZJob) + 16) * (size_t)n_jobs;
+    const size_t zero_off = (up_bytes + 63) & ~(size_t)63;
+    const size_t status_off = zero_off + (((size_t)n_jobs * 12 + 63) & ~(size_t)63);
+    const size_t total = status_off + (size_t)n_jobs * tiles * 8;
+    std::vector<double*> cdf;
+    std::vector<long long*> ncum;
+    char* extra = nullptr;
+    auto fill = [&](char* h, char*) {
+        MinZJob* mj = (MinZJob*)h;
+        const double** cp = (const double**)(mj + n_jobs);
+        long long** np = (long long**)(cp + n_jobs);
+        for (int j = 0; j < n_jobs; ++j) {
+            const ot_mesh_sample_job& m = jobs[j];
+            mj[j] = MinZJob{m.vertices, m.out_colors ? m.vertex_colors : nullptr, m.triangles, ncum[j],
+                            m.n_triangles, m.out_xyz, m.out_colors};
+            cp[j] = cdf[j];
+            np[j] = ncum[j];
+        }
+    };
+    ot_status st = sample_cdfs(jobs, n_jobs, total, up_bytes, fill, stream, cdf, ncum, &extra);
+    if (st != OT_OK) return st;
+    const MinZJob* djobs = (const MinZJob*)extra;
+    const double* const* dcdf = (const double* const*)(djobs + n_jobs);
+    long long* const* dncum = (long long* const*)(dcdf + n_jobs);
+    long long* kept = (long long*)(extra + zero_off);
+    int* ticket = (int*)(kept + n_jobs);
+    unsigned long long* status = (unsigned long long*)(extra + status_off);
+    OT_HIP_TRY(hipMemsetAsync(extra + zero_off, 0, total - zero_off, stream));
+    int64_t max_nt = 0;
+    for (int j = 0; j < n_jobs; ++j) max_nt = jobs[j].n_triangles > max_nt ? jobs[j].n_triangles : max_nt;
+    hipLaunchKernelGGL(k_round_counts_jobs, dim3((unsigned)((max_nt + 255) / 256), n_jobs), dim3(256), 0, stream, djobs,
+                       dcdf, n_points, dncum);
+    hipLaunchKernelGGL(k_sample_min_z, dim3(tiles, n_jobs), dim3(256), 0, stream, djobs, n_points,
+                       (unsigned long long)seed, z_min, tiles, status, ticket, kept);
+    OT_LAUNCH_CHECK();
+    std::vector<long long> hk(n_jobs);
+    OT_HIP_TRY(hipMemcpyAsync(hk.data(), kept, sizeof(long long) * n_jobs, hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));  // the kept counts, and the host job table is released on return
+    for (int j = 0; j < n_jobs; ++j) n_kept_host[j] = hk[j];
     return OT_OK;
 }
 

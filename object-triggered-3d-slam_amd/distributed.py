@@ -342,5 +342,5 @@ def _reconstruct_points(R, cfg, label, o3d):
     mesh.compute_vertex_normals()
     if len(mesh.vertices) == 0:
         return None
-    pcd = mesh.sample_points_uniformly(number_of_points=cfg.n_samples)
-    return pcd.filter_min_z(cfg.z_filter)._xyz.dev()
+    # sample_points_uniformly + the Z mask (reconstruct_rgbd_filter.py:123-132) in one pass
+    return mesh.sample_points_min_z(cfg.n_samples, cfg.z_filter)._xyz.dev()

@@ -601,6 +601,42 @@ class TriangleMesh:
         pcd._rgb = _Arr(dev=PC) if PC is not None else None
         return pcd
 
+    def sample_points_min_z(self, number_of_points, z_min, seed=0):
+        """reconstruct_rgbd_filter.py:123-132 fused (not an Open3D API): sample_points_uniformly(number_of_points)
+        with this seed, then the rows with z >= z_min, points and colours only (the reference rebuilds its cloud from
+        those two) -- the same cloud as sample_points_uniformly(...).filter_min_z(z_min), in one pass over the
+        samples (ot_mesh_sample_points_min_z).  Vertex normals are not read, so any still in flight are not waited for."""
+        return TriangleMesh.sample_points_min_z_batch([self], number_of_points, z_min, seed)[0]
+
+    @staticmethod
+    def sample_points_min_z_batch(meshes, number_of_points, z_min, seed=0):
+        """sample_points_min_z for several meshes in one call: their area-CDF chains run side by side."""
+        if number_of_points <= 0:
+            raise RuntimeError("[SamplePointsUniformly] number_of_points <= 0")
+        n = int(number_of_points)
+        jobs = (L.ot_mesh_sample_job * max(len(meshes), 1))()
+        outs = []
+        for j, m in enumerate(meshes):
+            if len(m._t) == 0:
+                raise RuntimeError("[SamplePointsUniformly] Input mesh has no triangles.")
+            P = D.empty((n, 3), "float64")
+            PC = D.empty((n, 3), "float64") if m.has_vertex_colors() else None
+            jobs[j] = L.ot_mesh_sample_job(
+                D.ptr(m._v.dev()), None, D.ptr(m._vc.dev()) if PC is not None else None, len(m._v), D.ptr(m._t.dev()),
+                len(m._t), D.ptr(P), None, D.ptr(PC))
+            outs.append((P, PC))
+        kept = (C.c_int64 * max(len(meshes), 1))()
+        if meshes:
+            L.call("ot_mesh_sample_points_min_z", C.cast(jobs, C.c_void_p), len(meshes), n,
+                   C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), float(z_min), kept, D.stream_ptr())
+        clouds = []
+        for j, (P, PC) in enumerate(outs):
+            pcd = PointCloud()
+            pcd._xyz = _Arr(dev=P[:kept[j]])
+            pcd._rgb = _Arr(dev=PC[:kept[j]]) if PC is not None else None
+            clouds.append(pcd)
+        return clouds
+
     @staticmethod
     def sample_points_uniformly_batch(meshes, number_of_points=100, seed=0):
         """sample_points_uniformly for several meshes in one call (not an Open3D API): the same clouds as one

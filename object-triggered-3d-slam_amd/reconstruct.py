@@ -110,7 +110,11 @@ def _integrate_frame(o3d, cfg, volume, intrinsic, colors, depths, poses, i):
 
 
 def _filtered_cloud(o3d, cfg, mesh):
-    """sample_points_uniformly(N) then keep z >= threshold, points and colours only (:123-132)."""
+    """sample_points_uniformly(N) then keep z >= threshold, points and colours only (:123-132).  This package's
+    facade does both in one pass (TriangleMesh.sample_points_min_z: the same cloud); Open3D takes the reference's
+    steps."""
+    if hasattr(mesh, "sample_points_min_z"):
+        return mesh.sample_points_min_z(cfg.n_samples, cfg.z_filter)
     pcd = mesh.sample_points_uniformly(number_of_points=cfg.n_samples)
     pts = np.asarray(pcd.points)
     cols = np.asarray(pcd.colors)

@@ -90,6 +90,50 @@ def test_z_filter_tail(O, meshes):
     assert not out.has_normals()
 
 
+@pytest.mark.parametrize("z_min", [0.03, -np.inf, np.inf, 0.0])
+def test_sample_min_z_fused(pkg, O, synth, seq16, meshes, z_min):
+    """TriangleMesh.sample_points_min_z (ot_mesh_sample_points_min_z: sampling and Z mask in one pass) = the two steps
+    (sample_points_uniformly(...).filter_min_z) = the oracle, for one mesh and for meshes of different sizes in one
+    batch; -inf keeps every sample (the last tile partial: 100003 points), +inf none."""
+    mesh, (V, VC, T) = meshes
+    n = 100003
+    out = mesh.sample_points_min_z(n, z_min, seed=3)
+    two = mesh.sample_points_uniformly(number_of_points=n, seed=3).filter_min_z(z_min)
+    P, _, PC = O.sample_points_uniformly(V, T, n, 3, VC=VC)
+    rx, rc = O.filter_min_z(P, PC, z_min)
+    assert_bitwise(np.asarray(out.points), rx, "fused points vs oracle")
+    assert_bitwise(np.asarray(out.colors), rc, "fused colours vs oracle")
+    assert_bitwise(np.asarray(out.points), np.asarray(two.points), "fused vs two steps")
+    assert not out.has_normals()
+    if z_min == -np.inf:
+        assert len(out.points) == n
+    if z_min == np.inf:
+        assert len(out.points) == 0
+    depth, color, ext = seq16
+    vol2, _ = _volumes(pkg, O, synth, depth[:1], color[:1], ext[:1], 0.02)
+    mesh2 = vol2.extract_triangle_mesh()
+    batch = pkg.geometry.TriangleMesh.sample_points_min_z_batch([mesh2, mesh, mesh2], 5000, z_min, seed=9)
+    for m, c in zip([mesh2, mesh, mesh2], batch):
+        one = m.sample_points_uniformly(number_of_points=5000, seed=9).filter_min_z(z_min)
+        assert_bitwise(np.asarray(c.points), np.asarray(one.points), "fused batch vs two steps")
+        assert_bitwise(np.asarray(c.colors), np.asarray(one.colors), "fused batch colours")
+
+
+def test_sample_min_z_with_normals_in_flight(pkg, O, synth, seq16):
+    """The fused sampler on a fresh mesh whose vertex normals are still running on the side stream: it does not read
+    them (no wait), and the normals stay correct for a later reader."""
+    depth, color, ext = seq16
+    vol, ref = _volumes(pkg, O, synth, depth[:4], color[:4], ext[:4], 0.01)
+    mesh = vol.extract_triangle_mesh()
+    V, VC, T = ref.extract_triangle_mesh()
+    mesh.compute_vertex_normals()
+    out = mesh.sample_points_min_z(100000, 0.03, seed=1)
+    P, _, PC = O.sample_points_uniformly(V, T, 100000, 1, VC=VC)
+    rx, _ = O.filter_min_z(P, PC, 0.03)
+    assert_bitwise(np.asarray(out.points), rx, "fused points")
+    assert_bitwise(np.asarray(mesh.vertex_normals), O.vertex_normals(V, T), "normals after the fused sampler")
+
+
 def test_sampling_batch_matches_single(pkg, O, synth, seq16, meshes):
     """TriangleMesh.sample_points_uniformly_batch: the per-mesh clouds equal the single-mesh calls (and the oracle)
     for meshes of different sizes sampled together."""

@@ -71,7 +71,7 @@ def main():
                                       3.0, s_)
         mesh = vol.extract_triangle_mesh()
         mesh.compute_vertex_normals()
-        return mesh.sample_points_uniformly(number_of_points=100000).filter_min_z(0.03)
+        return mesh.sample_points_min_z(100000, 0.03)
 
     ts = []
     for _ in range(REPS):
