@@ -154,4 +154,40 @@ __device__ inline T wave_sum(T v) {
     return v;
 }
 
+// Decoupled look-back (single-pass prefix over the tiles of one chain), run by ONE whole wave of the tile's
+// workgroup: publishes the tile's aggregate, reads its predecessors' status words 64 at a time (lane i: tile - 1 - i),
+// folds every aggregate up to the nearest inclusive prefix, publishes its own inclusive prefix and returns the
+// exclusive one (all lanes).  Status word: 0 = not yet published, LB_AGG | count, LB_PRE | inclusive prefix; the
+// caller zeroes the words and starts tiles in order (tickets), so every predecessor is running or done.  A window is
+// folded up to its first unpublished word and re-read from there, so a tile waits only on running predecessors.
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_PRE = 2ull << 62, LB_VAL = (1ull << 62) - 1;
+__device__ inline long long lookback_wave(unsigned long long* st, int tile, unsigned long long agg) {
+    const int lane = (int)lane_id();
+    if (tile == 0) {
+        if (lane == 0) __hip_atomic_store(&st[0], LB_PRE | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(&st[tile], LB_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long excl = 0;
+    int top = tile - 1;  // the highest predecessor not folded in yet
+    while (true) {
+        const int t = top - lane;
+        const unsigned long long v =
+            t >= 0 ? __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : LB_PRE;  // below 0: stop
+        const unsigned long long pre = __ballot((v & ~LB_VAL) == LB_PRE), zero = __ballot(v == 0ull);
+        const int first_pre = pre ? __ffsll((long long)pre) - 1 : 64;
+        const int first_zero = zero ? __ffsll((long long)zero) - 1 : 64;
+        if (first_zero < first_pre) {  // fold the published aggregates above the first gap, then wait on it
+            excl += wave_sum(lane < first_zero ? (v & LB_VAL) : 0ull);
+            top -= first_zero;
+            continue;
+        }
+        excl += wave_sum(lane <= first_pre ? (v & LB_VAL) : 0ull);  // up to and including the inclusive prefix
+        if (first_pre < 64) break;
+        top -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(&st[tile], LB_PRE | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (long long)excl;
+}
+
 }  // namespace ot

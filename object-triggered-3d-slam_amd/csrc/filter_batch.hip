@@ -389,7 +389,6 @@ struct FbCellKeys {
 // Each tile of a frame emits its runs at the frame's point offset poff[f] + (runs of the frame's earlier tiles),
 // found by a decoupled look-back inside the frame (tiles take tickets in start order, so a tile only waits on running
 // ones); rlen[f] = the frame's run count (its segment of the sort holds that many, the rest is capacity).
-constexpr unsigned long long FB_LB_AGG = 1ull << 62, FB_LB_PRE = 2ull << 62, FB_LB_VAL = (1ull << 62) - 1;
 
 // key of pixel pix of frame f (false: no point), as the tiles compute it
 __device__ inline bool fb_pixel_key(const FbParams& p, const FbKeys& kb, const double* m, const double vmin[3],
@@ -497,26 +496,13 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
     const int n_pts = tot & 0xFFFF, n_runs = tot >> 16;
     int ploc = loc & 0xFFFF, rloc = loc >> 16;
     const int base = toff[(int64_t)f * p.tpf + tile];  // this tile's first point
-    // the frame's runs before this tile: decoupled look-back (thread 0)
-    if (threadIdx.x == 0) {
-        unsigned long long* st = status + (int64_t)f * p.tpf;
-        long long excl = 0;
-        if (tile == 0) {
-            __hip_atomic_store(&st[0], FB_LB_PRE | (unsigned long long)n_runs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&st[tile], FB_LB_AGG | (unsigned long long)n_runs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int t = tile - 1; t >= 0;) {
-                const unsigned long long v = __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v == 0ull) continue;  // tile t has not published yet (it took an earlier ticket: it is running)
-                excl += (long long)(v & FB_LB_VAL);
-                if ((v & ~FB_LB_VAL) == FB_LB_PRE) break;
-                --t;
-            }
-            __hip_atomic_store(&st[tile], FB_LB_PRE | (unsigned long long)(excl + n_runs), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    // the frame's runs before this tile: decoupled look-back by wave 0
+    if (threadIdx.x < 64) {
+        const long long excl = lookback_wave(status + (int64_t)f * p.tpf, tile, (unsigned long long)n_runs);
+        if (threadIdx.x == 0) {
+            s_excl = (int)excl;
+            if (tile == p.tpf - 1) rlen[f] = (int)excl + n_runs;
         }
-        s_excl = (int)excl;
-        if (tile == p.tpf - 1) rlen[f] = (int)excl + n_runs;
     }
 #pragma unroll
     for (int k = 0; k < FB_PIX; ++k) {

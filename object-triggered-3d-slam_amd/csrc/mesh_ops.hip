@@ -600,7 +600,6 @@ __global__ __launch_bounds__(256) void k_sample(const double* __restrict__ V, co
 // normals are not interpolated).  A workgroup takes MZ_TILE consecutive points in a ticket order, counts the kept
 // ones and finds its output offset by a decoupled look-back over the job's earlier workgroups; grid (tiles, jobs).
 constexpr int MZ_ITEMS = 4, MZ_TILE = 256 * MZ_ITEMS;
-constexpr unsigned long long MZ_AGG = 1ull << 62, MZ_PRE = 2ull << 62, MZ_VAL = (1ull << 62) - 1;
 struct MinZJob {
     const double* V;
     const double* VC;
@@ -658,25 +657,12 @@ __global__ __launch_bounds__(256) void k_sample_min_z(const MinZJob* __restrict_
     int n_keep = 0;
 #pragma unroll
     for (int i = 0; i < MZ_ITEMS; ++i) n_keep += wsum[i][0] + wsum[i][1] + wsum[i][2] + wsum[i][3];
-    if (threadIdx.x == 0) {
-        unsigned long long* st = status + (int64_t)j * tiles;
-        long long excl = 0;
-        if (tile == 0) {
-            __hip_atomic_store(&st[0], MZ_PRE | (unsigned long long)n_keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&st[tile], MZ_AGG | (unsigned long long)n_keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int t = tile - 1; t >= 0;) {
-                const unsigned long long v = __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v == 0ull) continue;  // not published yet (an earlier ticket: running)
-                excl += (long long)(v & MZ_VAL);
-                if ((v & ~MZ_VAL) == MZ_PRE) break;
-                --t;
-            }
-            __hip_atomic_store(&st[tile], MZ_PRE | (unsigned long long)(excl + n_keep), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {  // decoupled look-back by wave 0
+        const long long excl = lookback_wave(status + (int64_t)j * tiles, tile, (unsigned long long)n_keep);
+        if (threadIdx.x == 0) {
+            s_excl = excl;
+            if (tile == tiles - 1) kept[j] = excl + n_keep;
         }
-        s_excl = excl;
-        if (tile == tiles - 1) kept[j] = excl + n_keep;
     }
     __syncthreads();
     long long pos = s_excl;
