@@ -573,20 +573,23 @@ __global__ __launch_bounds__(256) void k_fb_heads_emit(const unsigned* __restric
 }
 
 // one lane per voxel: its runs (sorted values = the runs' first point indices, in emission order) and each run's points
-// (consecutive packed records up to the next run head) re-unprojected and summed in point order
+// (consecutive packed records up to the next run head) re-unprojected and summed in point order.  Grid (chunks, F): the
+// block knows its frame (voxels voff[f] .. voff[f+1]); the next run's first index is loaded before the current run's
+// walk, and each record's successor before its sums.
 __global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsigned* __restrict__ sval,
                                                         const unsigned long long* __restrict__ packed,
                                                         const int* __restrict__ poff, const int* __restrict__ rlen,
-                                                        const int* __restrict__ heads, int64_t K, int64_t P,
-                                                        double* __restrict__ vx, double* __restrict__ vc,
+                                                        const int* __restrict__ heads, const int* __restrict__ voff,
+                                                        int64_t P, double* __restrict__ vx, double* __restrict__ vc,
                                                         FbCellKeys ck) {
-    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s >= K) return;
+    const int f = blockIdx.y;
+    const int v1 = voff[f + 1];
+    const int s = voff[f] + blockIdx.x * 256 + threadIdx.x;
+    if (s >= v1) return;
+    const int fend = poff[f] + rlen[f];                   // the frame's runs end
+    const int pend = f + 1 < p.F ? poff[f + 1] : (int)P;  // the frame's points end
     const int beg = heads[s];
-    const int f = frame_of(poff, p.F, beg);
-    const int fend = poff[f] + rlen[f];                      // the frame's runs end
-    const int pend = f + 1 < p.F ? poff[f + 1] : (int)P;     // the frame's points end
-    const int end = (s + 1 < K && heads[s + 1] < fend) ? heads[s + 1] : fend;
+    const int end = s + 1 < v1 ? heads[s + 1] : fend;
     {
         const unsigned vk = ck.vbits < 32 ? (ck.k32[beg] & ((1u << ck.vbits) - 1u)) : ck.k32[beg];
         ck.out[s] = ((unsigned long long)f << ck.sf) | (unsigned long long)(vk >> ck.shift);
@@ -596,8 +599,9 @@ __global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsign
     for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
     double sp[3] = {0, 0, 0}, sc[3] = {0, 0, 0};
     int cnt = 0;
+    int q = (int)sval[beg];
     for (int r = beg; r < end; ++r) {
-        int q = (int)sval[r];
+        const int qn = r + 1 < end ? (int)sval[r + 1] : 0;  // the next run's first point
         unsigned long long rec = packed[q];
         while (true) {
             const unsigned long long nxt = q + 1 < pend ? packed[q + 1] : FB_PACK_HEAD;  // issued before the sums
@@ -616,12 +620,13 @@ __global__ __launch_bounds__(256) void k_fb_reduce_runs(FbParams p, const unsign
             rec = nxt;
             ++q;
         }
+        q = qn;
     }
     const double cntd = (double)cnt, rc = 1.0 / cntd;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        vx[s * 3 + a] = div_rn(sp[a], cntd, rc);
-        vc[s * 3 + a] = div_rn(sc[a], cntd, rc);
+        vx[(int64_t)s * 3 + a] = div_rn(sp[a], cntd, rc);
+        vc[(int64_t)s * 3 + a] = div_rn(sc[a], cntd, rc);
     }
 }
 
@@ -956,6 +961,7 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     // the bench / production path: u32 keys, frames up to 2^24 pixels -> runs of pixels sorted (packed point records)
     const bool pack = seg32 && npx <= (1 << FB_PACK_PIX_BITS);
     unsigned long long* packed = nullptr;
+    std::vector<int> hvoff(F + 1);
     if (pack) {  // runs: one sort segment per frame, [poff[f], poff[f] + rlen[f]) of each frame's point range
         unsigned* k32 = (unsigned*)kin;
         unsigned* k32o = k32 + P;
@@ -983,6 +989,7 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
                            (const int64_t*)d_total, d_voff);
         OT_LAUNCH_CHECK();
         OT_HIP_TRY(hipMemcpyAsync(&K, d_total, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+        OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));
         OT_HIP_TRY(hipStreamSynchronize(stream));
     } else if (seg32) {  // 32-bit voxel keys of single points, one sort segment per frame: 8 B per pair per pass
         unsigned* k32 = (unsigned*)kin;
@@ -1028,16 +1035,17 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     // sorted keys: the u32 chain's are at (unsigned*)kin + P (k32o), the u64 path's at kout
     const FbCellKeys ck{seg32 ? (const unsigned*)kin + P : nullptr, seg32 ? nullptr : (const unsigned long long*)kout,
                         3 * m, vbits, gsf, ckeys};
-    if (pack)
-        hipLaunchKernelGGL(k_fb_reduce_runs, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
-                           (const unsigned*)vout, (const unsigned long long*)packed,
-                           (const int*)d_poff, (const int*)d_rlen, (const int*)heads, K, P, fl->vx, fl->vc, ck);
-    else
+    if (pack) {
+        int maxv = 1;
+        for (int f = 0; f < F; ++f) maxv = std::max(maxv, hvoff[f + 1] - hvoff[f]);
+        hipLaunchKernelGGL(k_fb_reduce_runs, dim3((unsigned)((maxv + 255) / 256), F), dim3(256), 0, stream, p,
+                           (const unsigned*)vout, (const unsigned long long*)packed, (const int*)d_poff,
+                           (const int*)d_rlen, (const int*)heads, (const int*)d_voff, P, fl->vx, fl->vc, ck);
+    } else
         hipLaunchKernelGGL(k_fb_reduce, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, p,
                            (const unsigned*)vout, (const int*)heads, K, P, fl->vx, fl->vc, ck);
     OT_LAUNCH_CHECK();
-    std::vector<int> hvoff(F + 1);
-    OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));
+    if (!pack) OT_HIP_TRY(hipMemcpyAsync(hvoff.data(), d_voff, sizeof(int) * (F + 1), hipMemcpyDeviceToHost, stream));
     // ---- statistical outlier removal over all frames' voxel clouds at once ----------------------------------
     // grid origin per frame = its voxel origin, cell edge 2^m voxels: the cells are the keys' cell fields
     double* d_org = (double*)fl->b_misc.get(sizeof(double) * 3 * F + 64);
