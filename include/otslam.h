@@ -262,6 +262,15 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices_host, 
  * complete in stream order, before any later work on that stream). */
 ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors,
                                       int32_t* triangles, void* stream);
+/* The extraction in two phases, writing the mesh straight into the caller's arrays (no copy out of the volume's own
+ * buffers): _count classifies, counts and returns the vertex / triangle totals (one read-back); _emit then writes
+ * vertices [nv][3], vertex colours [nv][3] (may be NULL; zeros for NoColor) and triangles [nt][3] into device arrays
+ * sized from those totals, in stream order.  _emit fails once the volume has changed since _count.  After a _count,
+ * ot_tsdf_fetch_triangle_mesh emits again into its arguments (same bits) while the volume is unchanged;
+ * ot_tsdf_fetch_mesh_keys needs one emission first. */
+ot_status ot_tsdf_extract_triangle_mesh_count(ot_tsdf* vol, int64_t* n_vertices, int64_t* n_triangles, void* stream);
+ot_status ot_tsdf_emit_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors, int32_t* triangles,
+                                     void* stream);
 /* Serial of the last extraction (ot_tsdf_extract_triangle_mesh), or -1 once the volume has changed since (frames
  * integrated, reset, units imported). */
 ot_status ot_tsdf_mesh_serial(const ot_tsdf* vol, int64_t* serial_host);

@@ -28,9 +28,12 @@ ot_status fail(ot_status code, const std::string& msg);
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ----------------------------------------------------------------------------- per-device scratch
-// Grow-only scratch arena (one per device).  Not thread-safe: the facade is single-threaded per process
-// (Open3D's calls are synchronous from one Python thread, SURVEY.md §8(b) Threading).
+// Grow-only scratch arena per host thread and device (capi.hip): threads driving their own streams never share a
+// buffer.
 void* scratch(size_t bytes, int slot);
+// pinned host counterpart (per thread and device, grow-only): small tables uploaded with hipMemcpyAsync without the
+// pageable staging copy; the caller must have synchronised on its previous upload from the slot before rewriting it
+void* pinned_scratch(size_t bytes, int slot);
 // device allocations made by the library's grow-only buffers so far (scratch arenas, filter handles): a timed
 // region that allocates shows up as a change (bench.py reports it; test hook otx_alloc_count)
 void note_alloc();

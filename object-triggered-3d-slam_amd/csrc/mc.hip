@@ -449,20 +449,26 @@ using namespace ot;
 
 extern "C" {
 
-ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64_t* n_triangles, void* stream_) {
-    hipStream_t stream = S(stream_);
-    if (!vol || !n_vertices || !n_triangles) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+}  // extern "C"
+
+namespace ot {
+// Marching cubes, phase 1: classify, count and scan (one read-back for the vertex / triangle totals); the structure
+// (cube bytes, bases, merge-key buffers) is kept with the volume.  Phase 2 (mc_emit) writes the mesh to any
+// destination while the structure is valid.
+static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices, int64_t* n_triangles) {
     ot_status st = upload_tables();
     if (st != OT_OK) return st;
     int64_t U = 0;
     st = tsdf_sorted_units(vol, stream, &U);
     if (st != OT_OK) return st;
-    vol->mesh.nv = vol->mesh.nt = 0;
+    MeshBuffers& mb = vol->mesh;
+    mb.nv = mb.nt = 0;
+    mb.valid = false;
+    mb.internal = false;
+    mb.emitted = false;
     *n_vertices = *n_triangles = 0;
     if (U == 0) return OT_OK;
     // workspace (ids are dense in [0, U)), kept with the volume after the extraction (MeshBuffers::ws)
-    MeshBuffers& mb = vol->mesh;
-    mb.valid = false;
     const size_t bytes = mc_ws_bytes(U);
     if (mb.ws_bytes < bytes) {
         if (mb.ws) {
@@ -503,34 +509,10 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     std::memcpy(tails, vol->hmail, sizeof(tails));
     const int64_t nt = tails[0] + tails[1], nv = tails[2] + tails[3];
     if (nv > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] more than 2^31 vertices");
-    int64_t capc = mb.cap_v;
-    st = grow(mb.v, mb.cap_v, nv * 3);
-    if (st != OT_OK) return st;
-    st = grow(mb.c, capc, nv * 3);
-    if (st != OT_OK) return st;
-    st = grow(mb.t, mb.cap_t, nt * 3);
-    if (st != OT_OK) return st;
     st = grow(mb.vk, mb.cap_vk, nv);  // merge keys: 16 B per vertex, 12 B per triangle
     if (st != OT_OK) return st;
     st = grow(mb.tk, mb.cap_tk, nt * 3);
     if (st != OT_OK) return st;
-    m.vk = mb.vk;
-    m.tk = mb.tk;
-    // vertex positions / colours and triangle indices depend on the same edge bitmasks and bases but not on each
-    // other: the vertices run on the volume's side stream beside the triangles (fork / join by events)
-    if (!vol->side) {
-        OT_HIP_TRY(hipStreamCreateWithFlags(&vol->side, hipStreamNonBlocking));
-        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_fork, hipEventDisableTiming));
-        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_join, hipEventDisableTiming));
-    }
-    OT_HIP_TRY(hipEventRecord(vol->ev_fork, stream));
-    OT_HIP_TRY(hipStreamWaitEvent(vol->side, vol->ev_fork, 0));
-    hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, vol->side, vol->dev, m, vol->voxel_length, mb.v,
-                       vol->color_type == OT_COLOR_RGB8 ? mb.c : nullptr);
-    OT_HIP_TRY(hipEventRecord(vol->ev_join, vol->side));
-    hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, mb.t);
-    OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_join, 0));
-    OT_LAUNCH_CHECK();  // the mesh is complete in stream order (fetch / normals / keys are ordered after it)
     mb.nv = nv;
     mb.nt = nt;
     mb.ws_units = U;
@@ -539,6 +521,77 @@ ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64
     *n_vertices = nv;
     *n_triangles = nt;
     return OT_OK;
+}
+
+// Phase 2: vertex positions / colours and triangle indices (and the merge keys) into the given device arrays.  They
+// depend on the same edge bitmasks and bases but not on each other: the vertices run on the volume's side stream
+// beside the triangles (fork / join by events); the mesh is complete in stream order on return.
+static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStream_t stream) {
+    MeshBuffers& mb = vol->mesh;
+    if (mb.nv == 0 && mb.nt == 0) return OT_OK;
+    McDev m;
+    m.sorted_ids = vol->sorted_ids;
+    mc_layout((char*)mb.ws, mb.ws_units, m);
+    m.vk = mb.vk;
+    m.tk = mb.tk;
+    const unsigned g = (unsigned)mb.ws_units;
+    if (!vol->side) {
+        OT_HIP_TRY(hipStreamCreateWithFlags(&vol->side, hipStreamNonBlocking));
+        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_fork, hipEventDisableTiming));
+        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_join, hipEventDisableTiming));
+    }
+    OT_HIP_TRY(hipEventRecord(vol->ev_fork, stream));
+    OT_HIP_TRY(hipStreamWaitEvent(vol->side, vol->ev_fork, 0));
+    hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, vol->side, vol->dev, m, vol->voxel_length, V,
+                       vol->color_type == OT_COLOR_RGB8 ? VC : nullptr);
+    OT_HIP_TRY(hipEventRecord(vol->ev_join, vol->side));
+    hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, T);
+    OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_join, 0));
+    OT_LAUNCH_CHECK();
+    if (VC && vol->color_type != OT_COLOR_RGB8)
+        OT_HIP_TRY(hipMemsetAsync(VC, 0, sizeof(double) * 3 * mb.nv, stream));
+    mb.emitted = true;
+    return OT_OK;
+}
+}  // namespace ot
+
+extern "C" {
+
+ot_status ot_tsdf_extract_triangle_mesh(ot_tsdf* vol, int64_t* n_vertices, int64_t* n_triangles, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!vol || !n_vertices || !n_triangles) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    ot_status st = mc_count(vol, stream, n_vertices, n_triangles);
+    if (st != OT_OK || *n_vertices + *n_triangles == 0) return st;
+    MeshBuffers& mb = vol->mesh;
+    int64_t capc = mb.cap_v;
+    st = grow(mb.v, mb.cap_v, mb.nv * 3);
+    if (st != OT_OK) return st;
+    st = grow(mb.c, capc, mb.nv * 3);
+    if (st != OT_OK) return st;
+    st = grow(mb.t, mb.cap_t, mb.nt * 3);
+    if (st != OT_OK) return st;
+    st = mc_emit(vol, mb.v, vol->color_type == OT_COLOR_RGB8 ? mb.c : nullptr, mb.t, stream);
+    if (st != OT_OK) return st;
+    mb.internal = true;  // ot_tsdf_fetch_triangle_mesh copies from the volume's buffers
+    return OT_OK;
+}
+
+ot_status ot_tsdf_extract_triangle_mesh_count(ot_tsdf* vol, int64_t* n_vertices, int64_t* n_triangles,
+                                              void* stream_) {
+    if (!vol || !n_vertices || !n_triangles) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    return mc_count(vol, S(stream_), n_vertices, n_triangles);
+}
+
+ot_status ot_tsdf_emit_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors, int32_t* triangles,
+                                     void* stream_) {
+    if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    const MeshBuffers& mb = vol->mesh;
+    if (mb.nv == 0 && mb.nt == 0) return OT_OK;  // an empty mesh (also before any extraction)
+    if (!mb.valid)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ExtractTriangleMesh] the volume changed since the extraction");
+    if ((mb.nv > 0 && !vertices) || (mb.nt > 0 && !triangles))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ExtractTriangleMesh] invalid arguments");
+    return mc_emit(vol, vertices, vertex_colors, triangles, S(stream_));
 }
 
 ot_status ot_tsdf_mesh_serial(const ot_tsdf* vol, int64_t* serial_host) {
@@ -572,6 +625,13 @@ ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* ve
     hipStream_t stream = S(stream_);
     if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     const MeshBuffers& mb = vol->mesh;
+    if (!mb.internal && (mb.nv > 0 || mb.nt > 0)) {  // counted and emitted elsewhere: emit again from the structure
+        if (!mb.valid)
+            return fail(OT_ERR_INVALID_ARGUMENT, "[ExtractTriangleMesh] the volume changed since the extraction");
+        if ((mb.nv > 0 && !vertices) || (mb.nt > 0 && !triangles))
+            return fail(OT_ERR_INVALID_ARGUMENT, "[ExtractTriangleMesh] invalid arguments");
+        return mc_emit(vol, vertices, vertex_colors, triangles, stream);
+    }
     if (mb.nv > 0 && vertices)
         OT_HIP_TRY(hipMemcpyAsync(vertices, mb.v, sizeof(double) * 3 * mb.nv, hipMemcpyDefault, stream));
     if (mb.nv > 0 && vertex_colors) {
@@ -591,6 +651,8 @@ ot_status ot_tsdf_fetch_mesh_keys(ot_tsdf* vol, int32_t* vertex_keys, int32_t* t
     hipStream_t stream = S(stream_);
     if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     const MeshBuffers& mb = vol->mesh;
+    if (!mb.emitted && (mb.nv > 0 || mb.nt > 0))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ExtractTriangleMesh] the mesh of the last extraction was not emitted yet");
     if (mb.nv > 0 && vertex_keys)
         OT_HIP_TRY(hipMemcpyAsync(vertex_keys, mb.vk, sizeof(int4) * mb.nv, hipMemcpyDefault, stream));
     if (mb.nt > 0 && triangle_units)

@@ -762,8 +762,11 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
     const size_t table = sizeof(ChainJob) * 2 * (size_t)n_jobs;
     char* ws = (char*)scratch(bytes + table + extra + 512, 17);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-    std::vector<char> up(table + upload);  // [sum chains | CDF chains | caller's upload]
-    ChainJob* chain = (ChainJob*)up.data();
+    // [sum chains | CDF chains | caller's upload] in pinned host memory (a pageable source costs a staging copy:
+    // ~35 us on one object's critical path); the callers synchronise before returning, so the slot is free again
+    char* up = (char*)pinned_scratch(table + upload, 0);
+    if (!up) return fail(OT_ERR_HIP, "pinned allocation failed");
+    ChainJob* chain = (ChainJob*)up;
     std::vector<double*> sums(n_jobs), qs(n_jobs);
     cdf.assign(n_jobs, nullptr);
     ncum.assign(n_jobs, nullptr);
@@ -788,9 +791,8 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
     }
     ChainJob* djobs = (ChainJob*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
     *extra_dev = (char*)djobs + table;
-    if (upload) fill(up.data() + table, *extra_dev);
-    // pageable source: the copy is complete in stream order; the callers synchronise before returning
-    OT_HIP_TRY(hipMemcpyAsync(djobs, up.data(), up.size(), hipMemcpyHostToDevice, stream));
+    if (upload) fill(up + table, *extra_dev);
+    OT_HIP_TRY(hipMemcpyAsync(djobs, up, table + upload, hipMemcpyHostToDevice, stream));
     launch_chains<false>(djobs, n_jobs, max_nt, stream);
     for (int j = 0; j < n_jobs; ++j) {
         const int64_t nt = jobs[j].n_triangles;

@@ -141,6 +141,8 @@ struct MeshBuffers {
     int64_t ws_units = 0;
     int64_t serial = 0;   // extraction count; the structure is valid for `serial` while `valid`
     bool valid = false;   // cleared by anything that changes the volume (integrate, reset, import)
+    bool internal = false;  // the last extraction's mesh sits in v / c / t (else it was emitted to the caller)
+    bool emitted = false;   // the merge keys vk / tk of the last extraction are written (by an emission)
     double* v = nullptr;
     double* c = nullptr;
     int32_t* t = nullptr;

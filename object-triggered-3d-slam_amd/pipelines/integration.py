@@ -226,12 +226,13 @@ class ScalableTSDFVolume:
         keys (vertex (U,4) int32 = owner unit key + edge bit, triangle (T,3) int32 = its cube's unit key) that
         distributed.merge_shard_meshes uses."""
         nv, nt = C.c_int64(0), C.c_int64(0)
-        L.call("ot_tsdf_extract_triangle_mesh", self._h, C.byref(nv), C.byref(nt), D.stream_ptr())
+        # count, then emit straight into the mesh's own arrays (no copy out of the volume's buffers)
+        L.call("ot_tsdf_extract_triangle_mesh_count", self._h, C.byref(nv), C.byref(nt), D.stream_ptr())
         self._keep.clear()
         V = D.empty((nv.value, 3), "float64")
-        VC = D.empty((nv.value, 3), "float64")
+        VC = D.empty((nv.value, 3), "float64") if self.color_type == TSDFVolumeColorType.RGB8 else None
         T = D.empty((nt.value, 3), "int32")
-        L.call("ot_tsdf_fetch_triangle_mesh", self._h, D.ptr(V), D.ptr(VC), D.ptr(T), D.stream_ptr())
+        L.call("ot_tsdf_emit_triangle_mesh", self._h, D.ptr(V), D.ptr(VC), D.ptr(T), D.stream_ptr())
         mesh = TriangleMesh()
         mesh._v = _Arr(dev=V)
         mesh._t = _Arr(dev=T)
@@ -242,7 +243,7 @@ class ScalableTSDFVolume:
         # pointer, same counts) bumps the version and sends compute_vertex_normals to the generic path
         mesh._mc = (weakref.ref(self), serial.value, V.data_ptr(), V._version, T.data_ptr(), T._version) \
             if serial.value >= 0 else None
-        if self.color_type == TSDFVolumeColorType.RGB8:
+        if VC is not None:
             mesh._vc = _Arr(dev=VC)
         if not with_keys:
             return mesh

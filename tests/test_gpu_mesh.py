@@ -53,6 +53,63 @@ def test_marching_cubes_5mm(pkg, O, synth, seq16):
     assert_bitwise(np.asarray(mesh.vertices), V, "vertices 5mm")
 
 
+def test_extraction_phases_c_abi(pkg, O, synth, seq16):
+    """The facade's count + emit (straight into the mesh arrays) and the one-call ot_tsdf_extract_triangle_mesh +
+    ot_tsdf_fetch_triangle_mesh give the same bits; after a count, fetch emits again; emitting after the volume changed
+    fails, and so do merge keys before any emission."""
+    import ctypes as C
+
+    import torch
+
+    L = pkg._lib
+    lib = L.load()
+    depth, color, ext = seq16
+    vol, ref = _volumes(pkg, O, synth, depth[:3], color[:3], ext[:3], 0.01)
+    V, VC, T = ref.extract_triangle_mesh()
+    mesh = vol.extract_triangle_mesh()
+    assert_bitwise(np.asarray(mesh.vertices), V, "count + emit vertices")
+    assert_bitwise(np.asarray(mesh.triangles), T, "count + emit triangles")
+    assert_bitwise(np.asarray(mesh.vertex_colors), VC, "count + emit colours")
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    nv, nt = C.c_int64(0), C.c_int64(0)
+
+    def fetch():
+        dv = torch.empty((nv.value, 3), dtype=torch.float64, device="cuda")
+        dc = torch.empty((nv.value, 3), dtype=torch.float64, device="cuda")
+        dt = torch.empty((nt.value, 3), dtype=torch.int32, device="cuda")
+        assert lib.ot_tsdf_fetch_triangle_mesh(vol._h, C.c_void_p(dv.data_ptr()), C.c_void_p(dc.data_ptr()),
+                                               C.c_void_p(dt.data_ptr()), s) == 0, lib.ot_last_error()
+        torch.cuda.synchronize()
+        return dv.cpu().numpy(), dc.cpu().numpy(), dt.cpu().numpy()
+
+    # one-call extraction (the volume's own buffers), then fetch copies
+    assert lib.ot_tsdf_extract_triangle_mesh(vol._h, C.byref(nv), C.byref(nt), s) == 0
+    dv, dc, dt = fetch()
+    assert_bitwise(dv, V, "one-call vertices")
+    assert_bitwise(dt, T, "one-call triangles")
+    assert_bitwise(dc, VC, "one-call colours")
+    # count only: keys refuse until an emission, fetch emits from the kept structure
+    assert lib.ot_tsdf_extract_triangle_mesh_count(vol._h, C.byref(nv), C.byref(nt), s) == 0
+    vk = torch.empty((nv.value, 4), dtype=torch.int32, device="cuda")
+    tk = torch.empty((nt.value, 3), dtype=torch.int32, device="cuda")
+    assert lib.ot_tsdf_fetch_mesh_keys(vol._h, C.c_void_p(vk.data_ptr()), C.c_void_p(tk.data_ptr()), s) != 0
+    dv, dc, dt = fetch()
+    assert_bitwise(dv, V, "count + fetch vertices")
+    assert_bitwise(dt, T, "count + fetch triangles")
+    assert lib.ot_tsdf_fetch_mesh_keys(vol._h, C.c_void_p(vk.data_ptr()), C.c_void_p(tk.data_ptr()), s) == 0
+    # the volume changes: emission from the stale structure is refused
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[3]), pkg.geometry.Image(depth[3]), depth_scale=1000.0, depth_trunc=3.0,
+        convert_rgb_to_intensity=False)
+    vol.integrate(rgbd, pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth)), ext[3])
+    vol.flush()
+    dv = torch.empty((nv.value, 3), dtype=torch.float64, device="cuda")
+    dt = torch.empty((nt.value, 3), dtype=torch.int32, device="cuda")
+    assert lib.ot_tsdf_emit_triangle_mesh(vol._h, C.c_void_p(dv.data_ptr()), None, C.c_void_p(dt.data_ptr()),
+                                          s) != 0
+    assert "changed" in lib.ot_last_error().decode()
+
+
 def test_empty_volume_mesh(pkg, gpu):
     integ = pkg.pipelines.integration
     vol = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
