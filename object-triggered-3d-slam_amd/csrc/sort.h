@@ -22,7 +22,5 @@ ot_status sort_segments_u32_u32(const unsigned* kin, unsigned* kout, const unsig
                                 const int64_t* seg, int nseg, int end_bit, hipStream_t stream, int scratch_slot,
                                 const int* dlen = nullptr);
 
-// Device-wide exclusive prefix sum of int64.
-ot_status exclusive_scan_i64(const long long* in, long long* out, size_t n, hipStream_t stream, int scratch_slot);
 
 }  // namespace ot

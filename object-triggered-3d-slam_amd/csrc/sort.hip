@@ -416,16 +416,4 @@ extern "C" ot_status otx_sort_segments_u32_u32(const unsigned* kin, unsigned* ko
     return OT_OK;
 }
 
-namespace ot {
 
-ot_status exclusive_scan_i64(const long long* in, long long* out, size_t n, hipStream_t stream, int scratch_slot) {
-    if (n == 0) return OT_OK;
-    size_t tmp = 0;
-    OT_HIP_TRY(rocprim::exclusive_scan(nullptr, tmp, in, out, 0ll, n, rocprim::plus<long long>(), stream));
-    void* ws = scratch(tmp + 16, scratch_slot);
-    if (!ws) return fail(OT_ERR_HIP, "scan scratch allocation failed");
-    OT_HIP_TRY(rocprim::exclusive_scan(ws, tmp, in, out, 0ll, n, rocprim::plus<long long>(), stream));
-    return OT_OK;
-}
-
-}  // namespace ot
