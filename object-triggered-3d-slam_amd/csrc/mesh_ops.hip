@@ -164,7 +164,9 @@ __global__ __launch_bounds__(256) void k_chain_guess(const ChainJob* __restrict_
     double p = sh[t] - loc;  // approximate exclusive prefix (only a guess)
     for (int64_t i = lo; i < hi; ++i) {
         j.ex[i] = binade(p);
-        p += j.bsum[i];
+        const double bi = j.bsum[i];
+        j.bsum[i] = p;  // kept: the sampler's CDF chain guesses its binades from it (k_chain_cdf_prep)
+        p += bi;
     }
 }
 
@@ -197,25 +199,91 @@ __global__ __launch_bounds__(256) void k_chain_chunk(const ChainJob* __restrict_
     }
 }
 
+// The sampler's CDF chain prologue in one launch, after the area sum's walk: q_t = a_t / S (IEEE division, Open3D's
+// triangle_areas[t] / surface_area), the chunk's binade guess from the SUM chain's approximate prefix at the chunk
+// start over S (cdf at a chunk start ~ prefix / S: a guess only, the walk proves every accepted value), then
+// k_chain_chunk's integer sum and flags -- instead of a division pass plus the chunk-sum, guess and chunk passes.
+__global__ __launch_bounds__(256) void k_chain_cdf_prep(const ChainJob* __restrict__ sum_jobs,
+                                                        const ChainJob* __restrict__ cdf_jobs) {
+    const ChainJob js = sum_jobs[blockIdx.y], jc = cdf_jobs[blockIdx.y];
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nb = (jc.n + CH - 1) / CH;
+    if (b >= nb) return;
+    const int lane = threadIdx.x & 63;
+    const double S = js.out[0];
+    double v[4];
+    chunk_load4(js.x, js.n, b * CH, lane, v);
+    const int64_t i = b * CH + 4 * lane;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = v[k] / S;
+    double* q = const_cast<double*>(jc.x);
+    if (i + 3 < jc.n && ((reinterpret_cast<uintptr_t>(q) & 15) == 0)) {
+        *reinterpret_cast<double2*>(q + i) = make_double2(v[0], v[1]);
+        *reinterpret_cast<double2*>(q + i + 2) = make_double2(v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i + k < jc.n) q[i + k] = v[k];
+    }
+    const int e = binade(js.bsum[b] / S);
+    bool bad = e == EX_NONE;
+    long long r = 0;
+    if (!bad) {
+        const double scale = pow2(52 - e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (i + k >= jc.n) v[k] = 0.0;
+            const double m = v[k] * scale;  // exact: power-of-two scaling
+            const bool ok = m >= 0.0 && m < (double)R_MAX && m - floor(m) != 0.5;
+            bad |= !ok;
+            r += ok ? (long long)rint(m) : 0;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    const bool any_bad = __ballot(bad) != 0;
+    if (lane == 0) {
+        jc.ex[b] = e;
+        jc.msum[b] = r < R_MAX ? r : R_MAX;
+        jc.kind[b] = any_bad ? 1 : 0;
+    }
+}
+
 // One chunk from the exact s in Open3D's order, by integer segments: inside the binade of s every element that is
 // not a tie, stays below 2^53 grid steps and keeps the running integer below 2^53 is one step of an integer prefix
 // sum (the whole wave at once); the first element that breaks this is added by one exact float64 add (s + a) and the
 // next segment starts after it.  A chunk costs one wave prefix per binade crossing / tie / special value instead of
-// 256 dependent adds.  CDF values are stored as they are produced.
-__device__ inline long long wave_min_ll(long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const long long t = __shfl_xor(v, o);
-        v = t < v ? t : v;
-    }
-    return v;
+// 256 dependent adds.  CDF values are stored as they are produced.  The segment is a single wave's latency chain, so
+// its cross-lane steps avoid LDS: the prefix is a DPP scan inside rows of 16 plus the row totals read by readlane,
+// the first bad / crossing element is found by a ballot and one readlane, and broadcasts are readlanes.
+__device__ inline long long readlane64(long long v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)v, l), hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ inline double readlane_f64(double v, int l) { return __longlong_as_double(readlane64(__double_as_longlong(v), l)); }
+template <int CTRL>
+__device__ inline long long dpp_row_shr64(long long v) {  // lanes without a source in their row of 16 read 0
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, true);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ inline long long wave_incl_scan_i64(long long v, int lane) {
+    v += dpp_row_shr64<0x111>(v);  // row_shr:1
+    v += dpp_row_shr64<0x112>(v);  // row_shr:2
+    v += dpp_row_shr64<0x114>(v);  // row_shr:4
+    v += dpp_row_shr64<0x118>(v);  // row_shr:8 -> inclusive scan inside each row of 16
+    const long long r0 = readlane64(v, 15), r1 = readlane64(v, 31), r2 = readlane64(v, 47);
+    const int row = lane >> 4;
+    return v + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
+}
+// the smallest per-lane index (CH when no lane has one): lanes hold ascending index ranges, so it is the value of the
+// first lane that has one
+__device__ inline int wave_first_idx(int idx) {
+    const unsigned long long m = __ballot(idx < CH);
+    return m ? __builtin_amdgcn_readlane(idx, __ffsll((long long)m) - 1) : CH;
 }
 
 template <bool CDF>
-__device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, double* lds, int lane) {
-    (void)lds;
-    double v[4];
-    chunk_load4(j.x, j.n, b * CH, lane, v);
+__device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, const double v[4], int lane) {
     const int64_t base = b * CH;
     const int cnt = j.n - base < CH ? (int)(j.n - base) : CH;
     int pos = 0;
@@ -226,7 +294,7 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
             const double scale = pow2(52 - e), u = pow2(e - 52);
             const long long N = (long long)(s * scale);  // exact integer in [2^52, 2^53)
             long long r[4], incl[4], loc = 0;
-            long long bad = CH;  // first element of this lane the integer step cannot take
+            int bad = CH;  // first element of this lane the integer step cannot take
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int idx = 4 * lane + k;
@@ -242,23 +310,17 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
                 loc += r[k];
                 incl[k] = loc;
             }
-            long long pre = loc;  // inclusive wave prefix of the lanes' totals
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const long long t = __shfl_up(pre, d);
-                if (lane >= d) pre += t;
-            }
-            const long long excl = pre - loc;
-            const long long first_bad = wave_min_ll(bad);
-            long long cross = CH;  // first element whose running integer leaves the binade
+            const long long excl = wave_incl_scan_i64(loc, lane) - loc;
+            const int first_bad = wave_first_idx(bad);
+            int cross = CH;  // first element whose running integer leaves the binade
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 incl[k] += excl;
                 const int idx = 4 * lane + k;
                 if (idx >= pos && idx < first_bad && N + incl[k] > R_MAX - 1 && cross == CH) cross = idx;
             }
-            const long long first_cross = wave_min_ll(cross);
-            stop = (int)(first_bad < first_cross ? first_bad : first_cross);
+            const int first_cross = wave_first_idx(cross);
+            stop = first_bad < first_cross ? first_bad : first_cross;
             stop = stop < cnt ? stop : cnt;
             if (stop > pos) {
 #pragma unroll
@@ -268,12 +330,12 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
                 }
                 const int last = stop - 1;
                 const long long mine = (last & 3) == 0 ? incl[0] : (last & 3) == 1 ? incl[1] : (last & 3) == 2 ? incl[2] : incl[3];
-                s = (double)(N + __shfl(mine, last >> 2)) * u;
+                s = (double)(N + readlane64(mine, last >> 2)) * u;
             }
         }
         if (stop < cnt) {  // one exact float64 add, in Open3D's order
             const double mine = (stop & 3) == 0 ? v[0] : (stop & 3) == 1 ? v[1] : (stop & 3) == 2 ? v[2] : v[3];
-            s = __shfl(mine, stop >> 2) + s;
+            s = readlane_f64(mine, stop >> 2) + s;
             if (CDF && lane == 0) j.out[base + stop] = s;
             ++stop;
         }
@@ -390,7 +452,6 @@ struct WalkMeta {
 template <bool CDF>
 __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict__ jobs, int lds_chunks) {
     extern __shared__ int4 s_meta[];
-    __shared__ double lds[CH + 2];
     const ChainJob j = jobs[blockIdx.x];
     const int64_t nb = (j.n + CH - 1) / CH;
     const bool staged = nb <= lds_chunks;
@@ -409,6 +470,8 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
     double s = 0.0;  // sum: 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0
     int nseg = 0;
     int64_t b = 0;
+    double pv[4] = {0.0, 0.0, 0.0, 0.0};  // prefetched values of chunk pf
+    int64_t pf = -1;
     while (b < nb) {  // wave-uniform control flow: every lane holds the same s and b
         const int k_b = M.kind(b), e_b = M.ex(b), re = M.rend(b);
         const bool head = b == 0 || M.rend(b - 1) < b;
@@ -446,8 +509,18 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
                 continue;
             }
         }
-        // not provable from s: walk this chunk serially
-        s = chain_serial_chunk<CDF>(j, b, s, lds, lane);
+        // not provable from s: walk this chunk serially (its values prefetched by the previous serial chunk when that
+        // was chunk b - 1 -- serial chunks cluster where the running value is small -- and chunk b + 1's fetched now)
+        double v[4];
+        if (pf == b) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = pv[q];
+        } else {
+            chunk_load4(j.x, j.n, b * CH, lane, v);
+        }
+        if (b + 1 < nb) chunk_load4(j.x, j.n, (b + 1) * CH, lane, pv);
+        pf = b + 1;
+        s = chain_serial_chunk<CDF>(j, b, s, v, lane);
         if (lane == 0) j.kind[b] = 2;
         ++b;
     }
@@ -502,13 +575,17 @@ __global__ __launch_bounds__(256) void k_chain_emit(const ChainJob* __restrict__
 }
 
 // the chains of n_jobs independent inputs (device job table), side by side
+// prologue (true): chunk sums, binade guesses, integer chunk sums and flags; false: the caller produced those
+// (k_chain_cdf_prep)
 template <bool CDF>
-void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream) {
+void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream, bool prologue = true) {
     const int64_t nb = (max_n + CH - 1) / CH;
     const dim3 grid((unsigned)((nb + 3) / 4), (unsigned)n_jobs);
-    hipLaunchKernelGGL(k_chain_bsum, grid, dim3(256), 0, stream, djobs);
-    hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(256), 0, stream, djobs);
-    hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
+    if (prologue) {
+        hipLaunchKernelGGL(k_chain_bsum, grid, dim3(256), 0, stream, djobs);
+        hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(256), 0, stream, djobs);
+        hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
+    }
     hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
     // metadata staged in LDS when every job's chunks fit (max_n bounds them all)
     const int lds_chunks = nb <= WALK_LDS_CHUNKS ? (int)nb : 0;
@@ -525,12 +602,6 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
 
 void launch_sum_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream) {
     launch_chains<false>(djobs, n_jobs, max_n > 0 ? max_n : 1, stream);
-}
-
-__global__ __launch_bounds__(256) void k_area_div(const double* __restrict__ area, int64_t nt,
-                                                  const double* __restrict__ sum, double* __restrict__ q) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t < nt) q[t] = area[t] / sum[0];
 }
 
 __global__ __launch_bounds__(256) void k_round_counts(const double* __restrict__ cdf, int64_t nt, int64_t N,
@@ -794,12 +865,10 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
     if (upload) fill(up + table, *extra_dev);
     OT_HIP_TRY(hipMemcpyAsync(djobs, up, table + upload, hipMemcpyHostToDevice, stream));
     launch_chains<false>(djobs, n_jobs, max_nt, stream);
-    for (int j = 0; j < n_jobs; ++j) {
-        const int64_t nt = jobs[j].n_triangles;
-        hipLaunchKernelGGL(k_area_div, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, (const double*)cdf[j],
-                           nt, (const double*)sums[j], qs[j]);
-    }
-    launch_chains<true>(djobs + n_jobs, n_jobs, max_nt, stream);
+    const int64_t max_nb = (max_nt + CH - 1) / CH;
+    hipLaunchKernelGGL(k_chain_cdf_prep, dim3((unsigned)((max_nb + 3) / 4), (unsigned)n_jobs), dim3(256), 0, stream,
+                       (const ChainJob*)djobs, (const ChainJob*)(djobs + n_jobs));
+    launch_chains<true>(djobs + n_jobs, n_jobs, max_nt, stream, false);
     OT_LAUNCH_CHECK();
     return OT_OK;
 }
