@@ -3,6 +3,7 @@
 #include "srchash.h"  // generated in $(BUILD) by the Makefile
 
 #include <atomic>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -84,6 +85,27 @@ void* pinned_scratch(size_t bytes, int slot) {
         note_alloc();
     }
     return a.ptr[slot];
+}
+
+struct ArgBlob {
+    unsigned long long w[UPLOAD_ARG_BYTES / 8];
+};
+__global__ __launch_bounds__(64) void k_store_blob(ArgBlob b, unsigned long long* dst, int words) {
+    for (int i = threadIdx.x; i < words; i += 64) dst[i] = b.w[i];
+}
+
+ot_status upload_small(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+    if (bytes == 0) return OT_OK;
+    if (bytes > UPLOAD_ARG_BYTES || ((uintptr_t)dst & 7)) {
+        OT_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+        return OT_OK;
+    }
+    ArgBlob b;
+    std::memcpy(b.w, src, bytes);
+    const int words = (int)((bytes + 7) / 8);  // whole words: the destination region is padded to 8 B
+    hipLaunchKernelGGL(k_store_blob, dim3(1), dim3(64), 0, stream, b, (unsigned long long*)dst, words);
+    OT_LAUNCH_CHECK();
+    return OT_OK;
 }
 
 static inline double det3_helper(const double* m, int i1, int i2, int i3, int j1, int j2, int j3) {

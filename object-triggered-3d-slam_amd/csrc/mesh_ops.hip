@@ -145,23 +145,28 @@ __global__ __launch_bounds__(256) void k_chain_bsum(const ChainJob* __restrict__
     if (lane == 0) j.bsum[b] = s;
 }
 
-__global__ __launch_bounds__(256) void k_chain_guess(const ChainJob* __restrict__ jobs) {
-    __shared__ double sh[256];
+// approximate exclusive prefix of the chunk sums -> guessed binade per chunk (and the prefix itself, kept in bsum):
+// one 1024-thread block per chain, each thread a contiguous stretch of chunks, a wave-shuffle scan of the stretch
+// totals and one of the 16 wave totals
+__global__ __launch_bounds__(1024) void k_chain_guess(const ChainJob* __restrict__ jobs) {
+    __shared__ double s_w[16];
     const ChainJob j = jobs[blockIdx.x];
-    const int t = threadIdx.x;
-    const int64_t nb = (j.n + CH - 1) / CH, per = (nb + 255) / 256;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t nb = (j.n + CH - 1) / CH, per = (nb + 1023) / 1024;
     const int64_t lo = t * per, hi = lo + per < nb ? lo + per : nb;
     double loc = 0.0;
     for (int64_t i = lo; i < hi; ++i) loc += j.bsum[i];
-    sh[t] = loc;
-    __syncthreads();
-    for (int d = 1; d < 256; d <<= 1) {  // Hillis-Steele inclusive scan
-        const double o = t >= d ? sh[t - d] : 0.0;
-        __syncthreads();
-        sh[t] += o;
-        __syncthreads();
+    double inc = loc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const double o = __shfl_up(inc, d);
+        if (lane >= d) inc += o;
     }
-    double p = sh[t] - loc;  // approximate exclusive prefix (only a guess)
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    double off = 0.0;
+    for (int q = 0; q < w; ++q) off += s_w[q];
+    double p = off + inc - loc;  // approximate exclusive prefix (only a guess)
     for (int64_t i = lo; i < hi; ++i) {
         j.ex[i] = binade(p);
         const double bi = j.bsum[i];
@@ -357,6 +362,7 @@ __device__ inline long long sat_add(long long a, long long b) {
     return c < R_MAX ? c : R_MAX;
 }
 
+constexpr int RUN_ITEMS = 4;  // consecutive chunks per thread: a 1024-thread tile covers 4096 chunks
 __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict__ jobs) {
     __shared__ long long s_wv[16];
     __shared__ int s_wh[16];
@@ -368,29 +374,48 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
     const ChainJob j = jobs[blockIdx.x];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int64_t nb = (j.n + CH - 1) / CH;
+    constexpr int TILE = 1024 * RUN_ITEMS;
     if (t == 0) {
         s_carry = 0;
         s_next = (int)nb;
     }
     __syncthreads();
-    // forward: inclusive prefix of msum inside each run, tile by tile (wave scan by shuffles, 16 wave totals by one wave)
-    for (int64_t t0 = 0; t0 < nb; t0 += 1024) {
-        const int64_t b = t0 + t;
-        const bool in = b < nb;
-        int h = in ? (run_head(j, b) ? 1 : 0) : 1;
-        long long v = in ? j.msum[b] : 0;
+    // forward: inclusive prefix of msum inside each run (segmented scan: a head restarts the sum)
+    for (int64_t t0 = 0; t0 < nb; t0 += TILE) {
+        const int64_t b0 = t0 + (int64_t)t * RUN_ITEMS;
+        long long lv[RUN_ITEMS];
+        int lh[RUN_ITEMS];
+        long long v = 0;
+        int h = 0;  // a head seen so far inside this thread's chunks
+#pragma unroll
+        for (int k = 0; k < RUN_ITEMS; ++k) {
+            const int64_t b = b0 + k;
+            const bool in = b < nb;
+            const bool hd = !in || run_head(j, b);
+            const long long x = in ? j.msum[b] : 0;
+            v = hd ? x : sat_add(v, x);
+            h |= hd ? 1 : 0;
+            lv[k] = v;
+            lh[k] = h;
+        }
+        // exclusive segmented prefix of the thread aggregates (v, h) inside the wave
+        long long iv = v;
+        int ih = h;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-            const long long tv = __shfl_up(v, d);
-            const int th = __shfl_up(h, d);
+            const long long tv = __shfl_up(iv, d);
+            const int th = __shfl_up(ih, d);
             if (lane >= d) {
-                v = h ? v : sat_add(tv, v);
-                h = h | th;
+                iv = ih ? iv : sat_add(tv, iv);
+                ih = ih | th;
             }
         }
+        long long ev = __shfl_up(iv, 1);
+        int eh = __shfl_up(ih, 1);
+        if (lane == 0) ev = 0, eh = 0;
         if (lane == 63) {
-            s_wv[w] = v;
-            s_wh[w] = h;
+            s_wv[w] = iv;
+            s_wh[w] = ih;
         }
         __syncthreads();
         if (t == 0) {  // carry into each wave: 16 serial combines
@@ -402,20 +427,35 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
             s_carry = c;
         }
         __syncthreads();
-        if (in) j.pre[b] = h ? v : sat_add(s_cin[w], v);
+        const long long cin = eh ? ev : sat_add(s_cin[w], ev);  // the running value entering this thread's chunks
+#pragma unroll
+        for (int k = 0; k < RUN_ITEMS; ++k)
+            if (b0 + k < nb) j.pre[b0 + k] = lh[k] ? lv[k] : sat_add(cin, lv[k]);
         __syncthreads();
     }
     // backward: every chunk's run end = (first head after it) - 1, tile by tile from the end (suffix minimum)
-    const int64_t tiles = (nb + 1023) / 1024;
+    const int64_t tiles = (nb + TILE - 1) / TILE;
     for (int64_t q = tiles - 1; q >= 0; --q) {
-        const int64_t b = q * 1024 + t;
-        int nx = (b + 1 < nb && run_head(j, b + 1)) ? (int)(b + 1) : 0x7FFFFFFF;
+        const int64_t b0 = q * TILE + (int64_t)t * RUN_ITEMS;
+        int ln[RUN_ITEMS];
+        int nx = 0x7FFFFFFF;  // first head after each chunk, from this thread's chunks (suffix)
+#pragma unroll
+        for (int k = RUN_ITEMS - 1; k >= 0; --k) {
+            ln[k] = nx;  // heads after chunk b0 + k inside this thread, excluding b0 + k + 1 (added next)
+            const int64_t b1 = b0 + k + 1;
+            if (b1 < nb && run_head(j, b1)) ln[k] = (int)b1;
+            nx = ln[k];
+        }
+        // nx = first head after chunk b0 within this thread; wave exclusive suffix minimum from later lanes
+        int sm = nx;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-            const int tv = __shfl_down(nx, d);
-            if (lane + d < 64) nx = tv < nx ? tv : nx;
+            const int tv = __shfl_down(sm, d);
+            if (lane + d < 64) sm = tv < sm ? tv : sm;
         }
-        if (lane == 0) s_wn[w] = nx;
+        int later = __shfl_down(sm, 1);
+        if (lane == 63) later = 0x7FFFFFFF;
+        if (lane == 0) s_wn[w] = sm;
         __syncthreads();
         if (t == 0) {
             int c = s_next;
@@ -426,8 +466,12 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
             s_next = c;
         }
         __syncthreads();
-        const int nxt = nx < s_nin[w] ? nx : s_nin[w];
-        if (b < nb) j.rend[b] = nxt - 1;
+        const int after = later < s_nin[w] ? later : s_nin[w];  // first head after this thread's last chunk
+#pragma unroll
+        for (int k = 0; k < RUN_ITEMS; ++k) {
+            const int nxt = ln[k] < after ? ln[k] : after;
+            if (b0 + k < nb) j.rend[b0 + k] = nxt - 1;
+        }
         __syncthreads();
     }
 }
@@ -583,7 +627,7 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
     const dim3 grid((unsigned)((nb + 3) / 4), (unsigned)n_jobs);
     if (prologue) {
         hipLaunchKernelGGL(k_chain_bsum, grid, dim3(256), 0, stream, djobs);
-        hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(256), 0, stream, djobs);
+        hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(1024), 0, stream, djobs);
         hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
     }
     hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
@@ -833,8 +877,8 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
     const size_t table = sizeof(ChainJob) * 2 * (size_t)n_jobs;
     char* ws = (char*)scratch(bytes + table + extra + 512, 17);
     if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-    // [sum chains | CDF chains | caller's upload] in pinned host memory (a pageable source costs a staging copy:
-    // ~35 us on one object's critical path); the callers synchronise before returning, so the slot is free again
+    // [sum chains | CDF chains | caller's upload], sent by upload_small (kernel arguments; pinned memory serves the
+    // copy fallback of large tables, and the callers synchronise before returning, so the slot is free again)
     char* up = (char*)pinned_scratch(table + upload, 0);
     if (!up) return fail(OT_ERR_HIP, "pinned allocation failed");
     ChainJob* chain = (ChainJob*)up;
@@ -863,7 +907,8 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
     ChainJob* djobs = (ChainJob*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
     *extra_dev = (char*)djobs + table;
     if (upload) fill(up + table, *extra_dev);
-    OT_HIP_TRY(hipMemcpyAsync(djobs, up, table + upload, hipMemcpyHostToDevice, stream));
+    ot_status ust = upload_small(djobs, up, table + upload, stream);
+    if (ust != OT_OK) return ust;
     launch_chains<false>(djobs, n_jobs, max_nt, stream);
     const int64_t max_nb = (max_nt + CH - 1) / CH;
     hipLaunchKernelGGL(k_chain_cdf_prep, dim3((unsigned)((max_nb + 3) / 4), (unsigned)n_jobs), dim3(256), 0, stream,

@@ -1442,6 +1442,21 @@ ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) 
 
 using namespace ot;
 
+namespace ot {
+__global__ __launch_bounds__(256) void k_tsdf_clear(TsdfDev d, int64_t cap) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cap; i += (int64_t)gridDim.x * 256) {
+        d.hkeys[i] = ~0ull;
+        d.hvals[i] = -1;
+        d.stamp[i] = -1;
+        d.fmask[i] = 0ull;
+    }
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < N_COUNTERS) d.counters[threadIdx.x] = 0;
+        if (threadIdx.x < 4) d.stats[threadIdx.x] = 0ull;
+    }
+}
+}  // namespace ot
+
 extern "C" {
 
 ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_type, int32_t unit_res, int32_t stride,
@@ -1554,13 +1569,11 @@ ot_status ot_tsdf_reset_async(ot_tsdf* v, void* stream_) {
     hipStream_t stream = S(stream_);
     ot_status st = tsdf_flush(v, stream);  // queued frames belong to the old contents: apply, then clear
     if (st != OT_OK) return st;
-    TsdfDev& d = v->dev;
-    OT_HIP_TRY(hipMemsetAsync(d.hkeys, 0xFF, sizeof(unsigned long long) * v->hash_cap, stream));
-    OT_HIP_TRY(hipMemsetAsync(d.hvals, 0xFF, sizeof(int) * v->hash_cap, stream));
-    OT_HIP_TRY(hipMemsetAsync(d.stamp, 0xFF, sizeof(int) * v->hash_cap, stream));
-    OT_HIP_TRY(hipMemsetAsync(d.fmask, 0, sizeof(unsigned long long) * v->hash_cap, stream));
-    OT_HIP_TRY(hipMemsetAsync(d.counters, 0, sizeof(int) * N_COUNTERS, stream));
-    OT_HIP_TRY(hipMemsetAsync(d.stats, 0, sizeof(unsigned long long) * 4, stream));
+    // the hash table, frame masks, counters and statistics in one launch (six fill commands cost ~5 us of host time
+    // each, on one object's critical path)
+    const unsigned blocks = (unsigned)std::min<int64_t>((v->hash_cap + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_tsdf_clear, dim3(blocks), dim3(256), 0, stream, v->dev, (int64_t)v->hash_cap);
+    OT_LAUNCH_CHECK();
     v->batch_pc = C_BATCH_PAIRS;
     v->frame_id = 0;
     v->imported = false;

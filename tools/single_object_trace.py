@@ -81,6 +81,15 @@ def main():
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t) * 1e3)
     print("single object ms (median of last 5):", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
+    # the volume's size against configs[1]'s (integrate occupancy): units, voxel updates, unit integrations
+    vol.reset()
+    for k in range(ext.shape[0]):
+        lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128, 1000.0, 3.0, s_)
+    nu, vu, ui = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+    lib.ot_tsdf_num_units(vol._h, C.byref(nu), s_)
+    lib.ot_tsdf_counters(vol._h, C.byref(vu), C.byref(ui), s_)
+    print(f"units {nu.value}, voxel updates {vu.value} ({vu.value / 64:.0f} per frame), unit integrations {ui.value} "
+          f"({ui.value / max(nu.value, 1):.1f} frames per unit)")
 
 
 if __name__ == "__main__":
