@@ -271,6 +271,14 @@ ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* ve
 ot_status ot_tsdf_extract_triangle_mesh_count(ot_tsdf* vol, int64_t* n_vertices, int64_t* n_triangles, void* stream);
 ot_status ot_tsdf_emit_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors, int32_t* triangles,
                                      void* stream);
+/* Count and emit in one call, for callers that can guess the size (e.g. the last extraction of this volume): the
+ * emission into the given arrays (capacity_vertices / capacity_triangles rows) is queued before the totals are read
+ * back, so the GPU does not wait for the host.  Returns OT_OK with the totals when they fit; otherwise
+ * OT_ERR_CAPACITY with the totals set (rows past the capacities were not written): emit with
+ * ot_tsdf_emit_triangle_mesh into arrays of that size. */
+ot_status ot_tsdf_extract_triangle_mesh_into(ot_tsdf* vol, double* vertices, double* vertex_colors,
+                                             int32_t* triangles, int64_t capacity_vertices, int64_t capacity_triangles,
+                                             int64_t* n_vertices, int64_t* n_triangles, void* stream);
 /* Serial of the last extraction (ot_tsdf_extract_triangle_mesh), or -1 once the volume has changed since (frames
  * integrated, reset, units imported). */
 ot_status ot_tsdf_mesh_serial(const ot_tsdf* vol, int64_t* serial_host);

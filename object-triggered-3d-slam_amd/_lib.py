@@ -89,6 +89,7 @@ SIGNATURES = {
     "ot_tsdf_fetch_triangle_mesh": [_p, _p, _p, _p, _p],
     "ot_tsdf_extract_triangle_mesh_count": [_p, _pi64, _pi64, _p],
     "ot_tsdf_emit_triangle_mesh": [_p, _p, _p, _p, _p],
+    "ot_tsdf_extract_triangle_mesh_into": [_p, _p, _p, _p, _i64, _i64, _pi64, _pi64, _p],
     "ot_mesh_compute_vertex_normals": [_p, _i64, _p, _i64, _p, _p],
     "ot_mesh_sample_points_uniformly": [_p, _p, _p, _i64, _p, _i64, _i64, C.c_uint64, _p, _p, _p, _p],
     "ot_mesh_sample_points_uniformly_batch": [_p, _i32, _i64, C.c_uint64, _p],

@@ -15,6 +15,7 @@
 //   k_mc_triangles : per-lane triangle offsets by block scan; vertex ids by popcount lookups
 #include <atomic>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include "../../include/otslam_mc_tables.h"
 #include "compact.h"
@@ -47,6 +48,8 @@ struct McDev {
     unsigned short* ctri;        // [id][4096] (cube byte order): first triangle of the cube inside its unit
     int4* vk;                    // per vertex: owner unit key + edge bit (the merge key of a sharded extraction)
     int32_t* tk;                 // per triangle: its cube's unit key
+    long long cap_v = 0x7FFFFFFFFFFFFFFFll;  // emission: rows the destination arrays hold (writes beyond are dropped:
+    long long cap_t = 0x7FFFFFFFFFFFFFFFll;  // a capacity guess made before the counts are known, then redone)
 };
 
 // the marching-cubes workspace of U units, carved from one allocation (kept with the volume: MeshBuffers::ws)
@@ -271,14 +274,16 @@ __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, doub
         for (int a = 0; a < 3; ++a) pt[a] = half + vl * (double)g[a];
         const double f0 = fabs((double)f0f), f1 = fabs((double)f1f);
         pt[axis] += f0 * vl / (f0 + f1);
+        if (vid < m.cap_v) {
 #pragma unroll
-        for (int a = 0; a < 3; ++a) V[vid * 3 + a] = pt[a];
-        if (m.vk) m.vk[vid] = make_int4(kx, ky, kz, gbit);
-        if (VC) {
+            for (int a = 0; a < 3; ++a) V[vid * 3 + a] = pt[a];
+            if (m.vk) m.vk[vid] = make_int4(kx, ky, kz, gbit);
+            if (VC) {
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const double a0 = c0[a] / 255.0, a1 = c1[a] / 255.0;
-                VC[vid * 3 + a] = (f1 * a0 + f0 * a1) / (f0 + f1);
+                for (int a = 0; a < 3; ++a) {
+                    const double a0 = c0[a] / 255.0, a1 = c1[a] / 255.0;
+                    VC[vid * 3 + a] = (f1 * a0 + f0 * a1) / (f0 + f1);
+                }
             }
         }
         ++vid;
@@ -334,13 +339,15 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
             const int a = edge_vid(m, snbr, x, y, z, c_tri[cube][k]);
             const int b = edge_vid(m, snbr, x, y, z, c_tri[cube][k + 1]);
             const int c = edge_vid(m, snbr, x, y, z, c_tri[cube][k + 2]);
-            T[out * 3 + 0] = a;
-            T[out * 3 + 1] = c;
-            T[out * 3 + 2] = b;
-            if (m.tk) {
-                m.tk[out * 3 + 0] = ukey[0];
-                m.tk[out * 3 + 1] = ukey[1];
-                m.tk[out * 3 + 2] = ukey[2];
+            if (out < m.cap_t) {
+                T[out * 3 + 0] = a;
+                T[out * 3 + 1] = c;
+                T[out * 3 + 2] = b;
+                if (m.tk) {
+                    m.tk[out * 3 + 0] = ukey[0];
+                    m.tk[out * 3 + 1] = ukey[1];
+                    m.tk[out * 3 + 2] = ukey[2];
+                }
             }
             ++out;
         }
@@ -501,7 +508,10 @@ namespace ot {
 // Marching cubes, phase 1: classify, count and scan (one read-back for the vertex / triangle totals); the structure
 // (cube bytes, bases, merge-key buffers) is kept with the volume.  Phase 2 (mc_emit) writes the mesh to any
 // destination while the structure is valid.
-static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices, int64_t* n_triangles) {
+// spec (nullable): launches work that needs the structure but not the totals (a speculative emission) between the
+// count kernels and the totals' read-back, so the GPU runs it while the host waits
+static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices, int64_t* n_triangles,
+                          const std::function<ot_status(McDev&)>& spec = nullptr) {
     ot_status st = upload_tables();
     if (st != OT_OK) return st;
     int64_t U = 0;
@@ -550,8 +560,18 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
         ms.p[2 * i] = (const unsigned*)tp[i];
         ms.p[2 * i + 1] = (const unsigned*)tp[i] + 1;
     }
-    st = mail_words(vol, ms, stream);
+    mb.ws_units = U;
+    st = mail_words_launch(vol, ms, stream);
     if (st != OT_OK) return st;
+    if (spec) {  // the host waits for the read-back only, the speculative work runs behind it
+        if (!vol->ev_mail) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_mail, hipEventDisableTiming));
+        OT_HIP_TRY(hipEventRecord(vol->ev_mail, stream));
+        st = spec(m);
+        if (st != OT_OK) return st;
+        OT_HIP_TRY(hipEventSynchronize(vol->ev_mail));
+    } else {
+        OT_HIP_TRY(hipStreamSynchronize(stream));
+    }
     std::memcpy(tails, vol->hmail, sizeof(tails));
     const int64_t nt = tails[0] + tails[1], nv = tails[2] + tails[3];
     if (nv > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] more than 2^31 vertices");
@@ -561,7 +581,6 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
     if (st != OT_OK) return st;
     mb.nv = nv;
     mb.nt = nt;
-    mb.ws_units = U;
     mb.serial += 1;
     mb.valid = true;
     *n_vertices = nv;
@@ -572,6 +591,8 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
 // Phase 2: vertex positions / colours and triangle indices (and the merge keys) into the given device arrays.  They
 // depend on the same edge bitmasks and bases but not on each other: the vertices run on the volume's side stream
 // beside the triangles (fork / join by events); the mesh is complete in stream order on return.
+static ot_status mc_emit_launch(ot_tsdf* vol, McDev m, int64_t nv, double* V, double* VC, int32_t* T,
+                                hipStream_t stream);
 static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStream_t stream) {
     MeshBuffers& mb = vol->mesh;
     if (mb.nv == 0 && mb.nt == 0) return OT_OK;
@@ -580,7 +601,14 @@ static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStr
     mc_layout((char*)mb.ws, mb.ws_units, m);
     m.vk = mb.vk;
     m.tk = mb.tk;
-    const unsigned g = (unsigned)mb.ws_units;
+    ot_status st = mc_emit_launch(vol, m, mb.nv, V, VC, T, stream);
+    if (st == OT_OK) mb.emitted = true;
+    return st;
+}
+// the emission kernels of structure m (U = vol->mesh.ws_units) into V / VC / T (nv: vertex rows for the NoColor zeros)
+static ot_status mc_emit_launch(ot_tsdf* vol, McDev m, int64_t nv, double* V, double* VC, int32_t* T,
+                                hipStream_t stream) {
+    const unsigned g = (unsigned)vol->mesh.ws_units;
     if (!vol->side) {
         OT_HIP_TRY(hipStreamCreateWithFlags(&vol->side, hipStreamNonBlocking));
         OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_fork, hipEventDisableTiming));
@@ -595,8 +623,7 @@ static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStr
     OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_join, 0));
     OT_LAUNCH_CHECK();
     if (VC && vol->color_type != OT_COLOR_RGB8)
-        OT_HIP_TRY(hipMemsetAsync(VC, 0, sizeof(double) * 3 * mb.nv, stream));
-    mb.emitted = true;
+        OT_HIP_TRY(hipMemsetAsync(VC, 0, sizeof(double) * 3 * (size_t)std::min<int64_t>(nv, m.cap_v), stream));
     return OT_OK;
 }
 }  // namespace ot
@@ -626,6 +653,35 @@ ot_status ot_tsdf_extract_triangle_mesh_count(ot_tsdf* vol, int64_t* n_vertices,
                                               void* stream_) {
     if (!vol || !n_vertices || !n_triangles) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
     return mc_count(vol, S(stream_), n_vertices, n_triangles);
+}
+
+ot_status ot_tsdf_extract_triangle_mesh_into(ot_tsdf* vol, double* vertices, double* vertex_colors,
+                                             int32_t* triangles, int64_t capacity_vertices, int64_t capacity_triangles,
+                                             int64_t* n_vertices, int64_t* n_triangles, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!vol || !n_vertices || !n_triangles || capacity_vertices < 0 || capacity_triangles < 0 ||
+        (capacity_vertices > 0 && !vertices) || (capacity_triangles > 0 && !triangles))
+        return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    MeshBuffers& mb = vol->mesh;
+    auto spec = [&](McDev& m) -> ot_status {  // the emission into the caller's arrays, before the totals are known
+        ot_status gs = grow(mb.vk, mb.cap_vk, std::max<int64_t>(capacity_vertices, 1));
+        if (gs != OT_OK) return gs;
+        gs = grow(mb.tk, mb.cap_tk, std::max<int64_t>(capacity_triangles, 1) * 3);
+        if (gs != OT_OK) return gs;
+        m.vk = mb.vk;
+        m.tk = mb.tk;
+        m.cap_v = capacity_vertices;
+        m.cap_t = capacity_triangles;
+        return mc_emit_launch(vol, m, capacity_vertices, vertices, vertex_colors, triangles, stream);
+    };
+    ot_status st = mc_count(vol, stream, n_vertices, n_triangles, spec);
+    if (st != OT_OK) return st;
+    if (*n_vertices <= capacity_vertices && *n_triangles <= capacity_triangles) {
+        mb.emitted = true;
+        return OT_OK;
+    }
+    return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] the mesh exceeds the given capacity: emit it with "
+                                 "ot_tsdf_emit_triangle_mesh into arrays of *n_vertices / *n_triangles rows");
 }
 
 ot_status ot_tsdf_emit_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors, int32_t* triangles,

@@ -32,6 +32,7 @@ constexpr int C_HASHERR = 3;   // hash full or key out of range
 constexpr int C_BATCH_PAIRS = 4;  // (frame, unit) pairs of a batch: counters[4 + parity] (batches alternate, see k_batch_units)
 constexpr int C_KMAX = 8;   // [8, 11): max over allocated units of key_a + KEY_BIAS + 1 (0: no unit yet)
 constexpr int C_KNEG = 11;  // [11, 14): max over allocated units of KEY_BIAS - key_a + 1 (so min key_a = KEY_BIAS + 1 - it)
+constexpr int C_UNITS_DONE = 14;  // k_batch_units: workgroups finished (the last one mails the counters, then zeroes it)
 constexpr int N_COUNTERS = 16;
 
 // stats[] slots (u64)
@@ -182,6 +183,12 @@ struct ot_tsdf {
                                            // by a one-wave kernel (mail_words) instead of staged D2H copies
     hipEvent_t hb_event[2] = {nullptr, nullptr};
     int hb_next = 0;
+    // the counters as the last batch's units kernel left them (the integrate does not change them), mailed by its last
+    // workgroup to hmail + OT_MAIL_WORDS: an extraction reads the unit count behind `ev_early` instead of waiting for
+    // the integrate (valid while early_frame == frame_id, no reset or import since)
+    hipEvent_t ev_early = nullptr;
+    int early_frame = -1;
+    hipEvent_t ev_mail = nullptr;  // behind a mailbox read-back that work queued after it must not delay
     int batch_pc = ot::C_BATCH_PAIRS;      // pair counter of the next batch (alternates 4, 5)
     float2* bdm = nullptr;                 // device [batch][h][w] packed (depth, multiplier)
     uint32_t* brgba = nullptr;             // device [batch][h][w] packed colour
@@ -214,6 +221,7 @@ struct MailSrc {
     const unsigned* p[ot::OT_MAIL_WORDS];
     int n;
 };
+ot_status mail_words_launch(ot_tsdf* vol, const MailSrc& s, hipStream_t stream);  // no synchronisation
 ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream);
 ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream);
 }  // namespace ot

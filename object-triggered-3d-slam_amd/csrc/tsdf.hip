@@ -543,7 +543,8 @@ struct UnitWork {
 };
 
 // Unit headers of the batch: allocate new units, move and clear the frame masks (ready for the next batch).
-__global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __restrict__ work, int pc) {
+__global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __restrict__ work, int pc,
+                                                     unsigned* __restrict__ early_mail) {
     __shared__ unsigned long long red[4];
     const int n = d.counters[pc];
     // the other counter belongs to the next batch; the previous batch's integrate (its last reader) has finished
@@ -583,9 +584,18 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
     pairs = wave_sum(pairs);
     if (lane_id() == 0) red[threadIdx.x >> 6] = pairs;
     __syncthreads();
+    __shared__ int s_last;
     if (threadIdx.x == 0) {
         const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
         if (tot) atomicAdd(&d.stats[S_UNIT_INTEGRATIONS], tot);
+        __threadfence();
+        s_last = atomicAdd(&d.counters[C_UNITS_DONE], 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < N_COUNTERS) {  // every workgroup's counter atomics are done: mail the final values
+        const int v = __hip_atomic_load(&d.counters[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        early_mail[threadIdx.x] = threadIdx.x == C_UNITS_DONE ? 0u : (unsigned)v;
+        if (threadIdx.x == C_UNITS_DONE) d.counters[C_UNITS_DONE] = 0;
     }
 }
 
@@ -1297,7 +1307,10 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     }
     hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, tp, vol->dev, n);
-    hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc);
+    hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc,
+                       vol->hmail + OT_MAIL_WORDS);
+    if (!vol->ev_early) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_early, hipEventDisableTiming));
+    OT_HIP_TRY(hipEventRecord(vol->ev_early, stream));
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
     const bool fast = !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
@@ -1323,6 +1336,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     }
     vol->frame_id += n;
     vol->sorted_frame = -1;
+    vol->early_frame = vol->frame_id;  // the mailed counters are final for this frame count (see ev_early)
     return OT_OK;
 }
 
@@ -1376,10 +1390,16 @@ __global__ void k_mail_words(MailSrc s, unsigned* __restrict__ out) {
     if (i < s.n) out[i] = *s.p[i];
 }
 
-ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
+ot_status mail_words_launch(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
     if (s.n > OT_MAIL_WORDS) return fail(OT_ERR_INVALID_ARGUMENT, "mailbox overflow");
     hipLaunchKernelGGL(k_mail_words, dim3(1), dim3(64), 0, stream, s, vol->hmail);
     OT_LAUNCH_CHECK();
+    return OT_OK;
+}
+
+ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
+    ot_status st = mail_words_launch(vol, s, stream);
+    if (st != OT_OK) return st;
     OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
 }
@@ -1398,12 +1418,18 @@ ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) 
     ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
     int c[N_COUNTERS];  // error flags and the unit count in one read-back (the pinned mailbox)
-    MailSrc ms;
-    ms.n = N_COUNTERS;
-    for (int i = 0; i < N_COUNTERS; ++i) ms.p[i] = (const unsigned*)vol->dev.counters + i;
-    st = mail_words(vol, ms, stream);
-    if (st != OT_OK) return st;
-    std::memcpy(c, vol->hmail, sizeof(c));
+    if (vol->early_frame == vol->frame_id && !vol->imported && vol->ev_early) {
+        // mailed by the last batch's units kernel: wait for that kernel only, not for the integrate behind it
+        OT_HIP_TRY(hipEventSynchronize(vol->ev_early));
+        std::memcpy(c, vol->hmail + OT_MAIL_WORDS, sizeof(c));
+    } else {
+        MailSrc ms;
+        ms.n = N_COUNTERS;
+        for (int i = 0; i < N_COUNTERS; ++i) ms.p[i] = (const unsigned*)vol->dev.counters + i;
+        st = mail_words(vol, ms, stream);
+        if (st != OT_OK) return st;
+        std::memcpy(c, vol->hmail, sizeof(c));
+    }
     st = counter_errors(c);
     if (st != OT_OK) return st;
     int nu = (int)std::min<int64_t>(c[C_UNITS], vol->max_units);
@@ -1511,7 +1537,7 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
     if ((e = hipMalloc(&v->bframes, sizeof(BatchFrame) * MAX_BATCH)) != hipSuccess) return cleanup(e);
     if ((e = hipHostMalloc(&v->hbframes, sizeof(BatchFrame) * MAX_BATCH * 2, hipHostMallocDefault)) != hipSuccess)
         return cleanup(e);
-    if ((e = hipHostMalloc(&v->hmail, sizeof(unsigned) * OT_MAIL_WORDS, hipHostMallocCoherent)) != hipSuccess)
+    if ((e = hipHostMalloc(&v->hmail, sizeof(unsigned) * 2 * OT_MAIL_WORDS, hipHostMallocCoherent)) != hipSuccess)
         return cleanup(e);
     ot_status st = ot_tsdf_reset(v);
     if (st != OT_OK) {
@@ -1535,6 +1561,8 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     if (v->hbframes) (void)hipHostFree(v->hbframes);
     if (v->hmail) (void)hipHostFree(v->hmail);
     if (v->ev_fork) (void)hipEventDestroy(v->ev_fork);
+    if (v->ev_early) (void)hipEventDestroy(v->ev_early);
+    if (v->ev_mail) (void)hipEventDestroy(v->ev_mail);
     if (v->ev_join) (void)hipEventDestroy(v->ev_join);
     if (v->side) (void)hipStreamDestroy(v->side);
     for (hipEvent_t ev : v->hb_event)
@@ -1556,6 +1584,7 @@ ot_status ot_tsdf_reset(ot_tsdf* v) {
     v->batch_pc = C_BATCH_PAIRS;
     v->frame_id = 0;
     v->imported = false;
+    v->early_frame = -1;
     v->pending.clear();
     v->sorted_frame = -1;
     v->sorted_units = -1;
@@ -1577,6 +1606,7 @@ ot_status ot_tsdf_reset_async(ot_tsdf* v, void* stream_) {
     v->batch_pc = C_BATCH_PAIRS;
     v->frame_id = 0;
     v->imported = false;
+    v->early_frame = -1;
     v->sorted_frame = -1;
     v->sorted_units = -1;
     v->mesh.nv = v->mesh.nt = 0;

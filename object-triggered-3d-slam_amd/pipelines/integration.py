@@ -226,13 +226,36 @@ class ScalableTSDFVolume:
         keys (vertex (U,4) int32 = owner unit key + edge bit, triangle (T,3) int32 = its cube's unit key) that
         distributed.merge_shard_meshes uses."""
         nv, nt = C.c_int64(0), C.c_int64(0)
-        # count, then emit straight into the mesh's own arrays (no copy out of the volume's buffers)
-        L.call("ot_tsdf_extract_triangle_mesh_count", self._h, C.byref(nv), C.byref(nt), D.stream_ptr())
+        rgb = self.color_type == TSDFVolumeColorType.RGB8
+        cv, ct = getattr(self, "_mesh_cap", (0, 0))
+        if cv and ct:
+            # sized from this volume's last extraction: the emission straight into the mesh arrays is queued before
+            # the totals come back (the GPU does not wait for the host); too small -> emitted again below
+            V = D.empty((cv, 3), "float64")
+            VC = D.empty((cv, 3), "float64") if rgb else None
+            T = D.empty((ct, 3), "int32")
+            try:
+                L.call("ot_tsdf_extract_triangle_mesh_into", self._h, D.ptr(V), D.ptr(VC), D.ptr(T), cv, ct,
+                       C.byref(nv), C.byref(nt), D.stream_ptr())
+                fits = True
+            except L.OTError:
+                if nv.value == 0 and nt.value == 0:  # not a capacity miss: the extraction itself failed
+                    raise
+                fits = False
+        else:
+            # count, then emit straight into the mesh's own arrays (no copy out of the volume's buffers)
+            L.call("ot_tsdf_extract_triangle_mesh_count", self._h, C.byref(nv), C.byref(nt), D.stream_ptr())
+            fits = False
         self._keep.clear()
-        V = D.empty((nv.value, 3), "float64")
-        VC = D.empty((nv.value, 3), "float64") if self.color_type == TSDFVolumeColorType.RGB8 else None
-        T = D.empty((nt.value, 3), "int32")
-        L.call("ot_tsdf_emit_triangle_mesh", self._h, D.ptr(V), D.ptr(VC), D.ptr(T), D.stream_ptr())
+        if fits:
+            V, T = V[:nv.value], T[:nt.value]
+            VC = VC[:nv.value] if VC is not None else None
+        else:
+            V = D.empty((nv.value, 3), "float64")
+            VC = D.empty((nv.value, 3), "float64") if rgb else None
+            T = D.empty((nt.value, 3), "int32")
+            L.call("ot_tsdf_emit_triangle_mesh", self._h, D.ptr(V), D.ptr(VC), D.ptr(T), D.stream_ptr())
+        self._mesh_cap = (nv.value + nv.value // 8 + 1024, nt.value + nt.value // 8 + 1024)
         mesh = TriangleMesh()
         mesh._v = _Arr(dev=V)
         mesh._t = _Arr(dev=T)

@@ -110,6 +110,55 @@ def test_extraction_phases_c_abi(pkg, O, synth, seq16):
     assert "changed" in lib.ot_last_error().decode()
 
 
+def test_extraction_into_guessed_capacity(pkg, O, synth, seq16):
+    """ot_tsdf_extract_triangle_mesh_into (the facade's path from a volume's second extraction on: emission queued
+    before the totals are read back): a capacity that fits gives the oracle's mesh; one that does not reports
+    OT_ERR_CAPACITY with the totals and the facade emits again -- both through the facade (same volume extracted, then
+    grown by more frames and extracted again) and through the C ABI directly."""
+    import ctypes as C
+
+    import torch
+
+    L = pkg._lib
+    lib = L.load()
+    depth, color, ext = seq16
+    integ = pkg.pipelines.integration
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    vol = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
+    ref = O.TSDF(0.01, 0.04, 1, 4)
+    for k in range(8):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+            convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
+        if k in (0, 1, 7):  # 0: count + emit; 1: a guess from frame 0's mesh (too small: grown); 7: guess fits
+            mesh = vol.extract_triangle_mesh()
+            V, VC, T = ref.extract_triangle_mesh()
+            assert_bitwise(np.asarray(mesh.vertices), V, f"vertices after {k + 1} frames")
+            assert_bitwise(np.asarray(mesh.triangles), T, f"triangles after {k + 1} frames")
+            assert_bitwise(np.asarray(mesh.vertex_colors), VC, f"colours after {k + 1} frames")
+            mesh.compute_vertex_normals()
+            assert_bitwise(np.asarray(mesh.vertex_normals), O.vertex_normals(V, T), f"normals after {k + 1} frames")
+    mesh = vol.extract_triangle_mesh()  # unchanged volume: the guess fits
+    assert_bitwise(np.asarray(mesh.vertices), V, "second extraction of an unchanged volume")
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    nv, nt = C.c_int64(0), C.c_int64(0)
+    small_v, small_t = V.shape[0] // 2, T.shape[0] // 2
+    dv = torch.empty((small_v, 3), dtype=torch.float64, device="cuda")
+    dt = torch.empty((small_t, 3), dtype=torch.int32, device="cuda")
+    st = lib.ot_tsdf_extract_triangle_mesh_into(vol._h, C.c_void_p(dv.data_ptr()), None, C.c_void_p(dt.data_ptr()),
+                                                small_v, small_t, C.byref(nv), C.byref(nt), s)
+    assert st == L.OT_ERR_CAPACITY and (nv.value, nt.value) == (V.shape[0], T.shape[0])
+    dv = torch.empty((nv.value, 3), dtype=torch.float64, device="cuda")
+    dt = torch.empty((nt.value, 3), dtype=torch.int32, device="cuda")
+    assert lib.ot_tsdf_emit_triangle_mesh(vol._h, C.c_void_p(dv.data_ptr()), None, C.c_void_p(dt.data_ptr()), s) == 0
+    torch.cuda.synchronize()
+    assert_bitwise(dv.cpu().numpy(), V, "emitted after a capacity miss")
+    assert_bitwise(dt.cpu().numpy(), T, "triangles emitted after a capacity miss")
+
+
 def test_empty_volume_mesh(pkg, gpu):
     integ = pkg.pipelines.integration
     vol = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)

@@ -26,8 +26,10 @@ def report(path):
         for r in csv.DictReader(fh):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], int(r.get("Stream_Id", 0) or 0)))
     rows.sort()
-    # every repetition launches the same kernels: the last REPS-th of the trace is the last repetition
-    last = rows[len(rows) - len(rows) // REPS:]
+    # every repetition starts with the volume reset (k_tsdf_clear); the statistics pass after the timed repetitions
+    # starts with one too: the last timed repetition lies between the last two
+    clears = [i for i, r in enumerate(rows) if "k_tsdf_clear" in r[2]]
+    last = rows[clears[-2]:clears[-1]] if len(clears) >= 2 else rows[len(rows) - len(rows) // REPS:]
     t0 = last[0][0]
     busy = {}
     prev_end = t0
