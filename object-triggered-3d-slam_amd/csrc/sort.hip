@@ -99,14 +99,16 @@ __global__ __launch_bounds__(Rs<D>::THREADS) void k_rs_upsweep(const KeyT* __res
     const int s = rs_segment(sg, blockIdx.x);
     const int base = sg.start[s] + (blockIdx.x - sg.tile[s]) * RS_TILE;
     const int end = rs_seg_end(sg, s);
-    // per lane and pass a run of equal digits, flushed into the LDS histogram when the digit changes: a tile's keys
-    // are spatially coherent (its high digits rarely change), and same-bin LDS atomics from a whole wave serialise
+    // per lane and pass a run of equal digits, flushed into the LDS histogram when the digit changes: a lane takes
+    // RS_ITEMS CONSECUTIVE keys (a histogram does not care about order), and neighbouring keys of the spatially coherent
+    // inputs share their higher digits, so most passes add one run per lane instead of one LDS atomic per key (same-bin
+    // LDS atomics from a whole wave serialise)
     unsigned cur[RS_MAXP], cnt[RS_MAXP];
 #pragma unroll
     for (int p = 0; p < RS_MAXP; ++p) cur[p] = cnt[p] = 0u;
 #pragma unroll
     for (int r = 0; r < RS_ITEMS; ++r) {
-        const int i = base + r * RS_THREADS + tid;
+        const int i = base + tid * RS_ITEMS + r;
         if (i < end) {
             const KeyT k = keys[i];
 #pragma unroll

@@ -127,13 +127,14 @@ def test_extraction_into_guessed_capacity(pkg, O, synth, seq16):
     intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
     vol = integ.ScalableTSDFVolume(voxel_length=0.01, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
     ref = O.TSDF(0.01, 0.04, 1, 4)
-    for k in range(8):
+    nf = depth.shape[0]
+    for k in range(nf):
         rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
             pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
             convert_rgb_to_intensity=False)
         vol.integrate(rgbd, intr, ext[k])
         ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
-        if k in (0, 1, 7):  # 0: count + emit; 1: a guess from frame 0's mesh (too small: grown); 7: guess fits
+        if k in (0, 1, nf - 1):  # 0: count + emit; then guesses from the previous mesh (too small: emitted again)
             mesh = vol.extract_triangle_mesh()
             V, VC, T = ref.extract_triangle_mesh()
             assert_bitwise(np.asarray(mesh.vertices), V, f"vertices after {k + 1} frames")
