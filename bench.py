@@ -620,11 +620,9 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
                 vol, (d16, col, ext) = vols[j], dev[j]
                 vol.reset()
                 dp, cp, ep = d16.data_ptr(), col.data_ptr(), ext.ctypes.data  # plain int addresses per call
-                for k in range(ext.shape[0]):
-                    st = lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128,
-                                                   1000.0, 3.0, stream)
-                    if st:
-                        raise RuntimeError(lib.ot_last_error().decode())
+                # the object's 64 frames in one host call (ot_tsdf_integrate_u16_frames = 64 ot_tsdf_integrate_u16)
+                if lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, stream):
+                    raise RuntimeError(lib.ot_last_error().decode())
                 mesh = vol.extract_triangle_mesh()
                 mesh.compute_vertex_normals()
                 out[j] = mesh
@@ -658,10 +656,8 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
 
         def one():
             vol.reset()
-            for k in range(ext.shape[0]):
-                if lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128,
-                                             1000.0, 3.0, s_):
-                    raise RuntimeError(lib.ot_last_error().decode())
+            if lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_):
+                raise RuntimeError(lib.ot_last_error().decode())
             mesh = vol.extract_triangle_mesh()
             mesh.compute_vertex_normals()
             return mesh.sample_points_min_z(100000, 0.03)

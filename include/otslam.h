@@ -174,6 +174,12 @@ ot_status ot_tsdf_integrate(ot_tsdf* vol, const float* depth, const uint8_t* col
 ot_status ot_tsdf_integrate_u16(ot_tsdf* vol, const uint16_t* depth, const uint8_t* color,
                                 const ot_intrinsics* intrinsic, const double extrinsic[16],
                                 double depth_scale, double depth_trunc, void* stream);
+/* n frames of a scan already resident in device memory in one call: frame k's u16 depth at depth + k*W*H, its RGB8 at
+ * color + 3*k*W*H (color may be NULL), its extrinsic at extrinsics + 16*k (host).  The same queueing, batching and
+ * bits as n calls of ot_tsdf_integrate_u16, without n host round trips (the front of one object's latency). */
+ot_status ot_tsdf_integrate_u16_frames(ot_tsdf* vol, int32_t n, const uint16_t* depth, const uint8_t* color,
+                                       const ot_intrinsics* in, const double* extrinsics, double depth_scale,
+                                       double depth_trunc, void* stream);
 ot_status ot_tsdf_flush(ot_tsdf* vol, void* stream);
 /* Frames queued on the host for the next batch (their input buffers are still referenced; every frame queued before
  * them has been enqueued on its stream).  Host-only, no synchronisation. */

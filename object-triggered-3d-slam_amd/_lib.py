@@ -63,6 +63,7 @@ SIGNATURES = {
     "ot_tsdf_reset_async": [_p, _p],
     "ot_tsdf_integrate": [_p, _p, _p, _pint, _p, _p],
     "ot_tsdf_integrate_u16": [_p, _p, _p, _pint, _p, _d, _d, _p],
+    "ot_tsdf_integrate_u16_frames": [_p, _i32, _p, _p, _pint, _p, _d, _d, _p],
     "ot_tsdf_flush": [_p, _p],
     "ot_tsdf_set_batch": [_p, _i32],
     "ot_tsdf_pending_frames": [_p, _p],

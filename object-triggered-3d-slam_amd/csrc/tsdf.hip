@@ -1648,6 +1648,20 @@ ot_status ot_tsdf_integrate_u16(ot_tsdf* vol, const uint16_t* depth, const uint8
     return OT_OK;
 }
 
+ot_status ot_tsdf_integrate_u16_frames(ot_tsdf* vol, int32_t n, const uint16_t* depth, const uint8_t* color,
+                                       const ot_intrinsics* in, const double* extrinsics, double depth_scale,
+                                       double depth_trunc, void* stream) {
+    if (!vol || n < 0 || !in || (n > 0 && (!depth || !extrinsics)))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume::Integrate] invalid arguments");
+    const int64_t npx = (int64_t)in->width * in->height;
+    for (int32_t k = 0; k < n; ++k) {  // exactly n calls of ot_tsdf_integrate_u16, without n host round trips
+        ot_status st = ot_tsdf_integrate_u16(vol, depth + (size_t)k * npx, color ? color + (size_t)k * npx * 3 : nullptr,
+                                             in, extrinsics + 16 * (size_t)k, depth_scale, depth_trunc, stream);
+        if (st != OT_OK) return st;
+    }
+    return OT_OK;
+}
+
 ot_status ot_tsdf_flush(ot_tsdf* vol, void* stream) {
     if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "volume is NULL");
     return tsdf_flush(vol, S(stream));

@@ -31,7 +31,9 @@ _side: dict = {}
 
 def side_stream():
     """A second stream paired with the current one (created once per stream): independent work of the same caller
-    -- a fresh mesh's vertex normals beside its sampling's area chains -- runs there, joined by an event."""
+    -- a fresh mesh's vertex normals beside its sampling's area chains -- runs there, joined by an event.  It takes the
+    least stream priority the device offers, so the caller's critical-path kernels (the chains' wide passes) are
+    dispatched first and the side work fills the gaps of the chains' single-wave walks."""
     import torch
 
     cur = torch.cuda.current_stream()
@@ -39,5 +41,6 @@ def side_stream():
     with _lock:
         st = _side.get(key)
         if st is None:
-            st = _side[key] = torch.cuda.Stream(device=cur.device_index)
+            least, _greatest = torch.cuda.Stream.priority_range()
+            st = _side[key] = torch.cuda.Stream(device=cur.device_index, priority=least)
         return st

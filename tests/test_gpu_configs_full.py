@@ -3,8 +3,9 @@
 
 configs[3] (reconstruct_rgbd_filter.py:81-132,154-155): 8 object scans x 64 640x480 frames, per object integrate at
 5 mm (colour precision 64, the facade and C-ABI default) -> extract_triangle_mesh -> compute_vertex_normals ->
-sample_points_uniformly(100000) (the batched sampler bench.py uses) -> z >= 0.03 mask, then the merge in sorted
-object order (distributed.merge_object_clouds; one process: local concatenation).  Every object's mesh (vertices,
+sample_points_uniformly(100000) -> z >= 0.03 mask (fused and batched over the objects, as bench.py runs it, and the
+two-step form beside it), then the merge in sorted object order (distributed.merge_object_clouds; one process: local
+concatenation).  Every object's mesh (vertices,
 triangles, colours, normals), its filtered cloud (points and colours) and the merged cloud are bit-exact against the
 CPU oracle, and the batched sampler equals the oracle's single-mesh sampler per object.
 
@@ -73,18 +74,22 @@ def test_configs3_objects_full_size_bitexact(pkg, synth, obj_scans, obj_oracle, 
         vol = integ.ScalableTSDFVolume(voxel_length=VOXEL, sdf_trunc=TRUNC,
                                        color_type=integ.TSDFVolumeColorType.RGB8)
         assert vol.color_precision == 64
-        for k in range(ext.shape[0]):
-            st = lib.ot_tsdf_integrate_u16(vol._h, C.c_void_p(d16.data_ptr() + k * npx * 2),
-                                           C.c_void_p(col.data_ptr() + k * npx * 3), C.byref(intr),
-                                           ext[k].ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
-            assert st == 0, lib.ot_last_error()
+        st = lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], C.c_void_p(d16.data_ptr()),
+                                              C.c_void_p(col.data_ptr()), C.byref(intr),
+                                              ext.ctypes.data_as(C.c_void_p), 1000.0, 3.0, stream)
+        assert st == 0, lib.ot_last_error()
         mesh = vol.extract_triangle_mesh()
         mesh.compute_vertex_normals()
         meshes.append(mesh)
         del vol
-    pcds = pkg.geometry.TriangleMesh.sample_points_uniformly_batch(meshes, number_of_points=N_SAMPLES)
-    filtered = [p.filter_min_z(Z_MIN) for p in pcds]
-    merged = D.merge_object_clouds([f._xyz.dev() for f in filtered])
+    # the bench's tail: sampling and Z mask fused, all objects in one call, then one collective merge (capacity in-band)
+    filtered = pkg.geometry.TriangleMesh.sample_points_min_z_batch(meshes, N_SAMPLES, Z_MIN)
+    merged = D.merge_object_clouds([f._xyz.dev() for f in filtered], capacity=N_OBJECTS * N_SAMPLES)
+    # and the reference's two steps (sample, then mask) on the batched sampler: the same clouds
+    two = [p.filter_min_z(Z_MIN) for p in
+           pkg.geometry.TriangleMesh.sample_points_uniformly_batch(meshes, number_of_points=N_SAMPLES)]
+    for f, t in zip(filtered, two):
+        assert_bitwise(np.asarray(f.points), np.asarray(t.points), "fused vs two-step z-masked samples")
     for j, (m, f, ref) in enumerate(zip(meshes, filtered, obj_oracle)):
         assert len(ref["T"]) > 10000, f"object {j}: degenerate oracle mesh"
         assert_bitwise(np.asarray(m.vertices), ref["V"], f"object {j} mesh vertices")

@@ -44,8 +44,7 @@ def mark(name, t0):
 def one(record):
     t = time.perf_counter()
     vol.reset()
-    for k in range(ext.shape[0]):
-        lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128, 1000.0, 3.0, s_)
+    lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
     t_calls = time.perf_counter()
     lib.ot_tsdf_flush(vol._h, s_)
     t = mark("integrate (64 calls + flush)", t)

@@ -68,9 +68,7 @@ def main():
 
     def one():
         vol.reset()
-        for k in range(ext.shape[0]):
-            lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128, 1000.0,
-                                      3.0, s_)
+        lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
         mesh = vol.extract_triangle_mesh()
         mesh.compute_vertex_normals()
         return mesh.sample_points_min_z(100000, 0.03)
@@ -82,11 +80,11 @@ def main():
         one()
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t) * 1e3)
+    print("stream priority range (least, greatest):", torch.cuda.Stream.priority_range())
     print("single object ms (median of last 5):", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
     # the volume's size against configs[1]'s (integrate occupancy): units, voxel updates, unit integrations
     vol.reset()
-    for k in range(ext.shape[0]):
-        lib.ot_tsdf_integrate_u16(vol._h, dp + k * npx * 2, cp + k * npx * 3, intr_ref, ep + k * 128, 1000.0, 3.0, s_)
+    lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
     nu, vu, ui = C.c_int64(0), C.c_int64(0), C.c_int64(0)
     lib.ot_tsdf_num_units(vol._h, C.byref(nu), s_)
     lib.ot_tsdf_counters(vol._h, C.byref(vu), C.byref(ui), s_)
