@@ -26,6 +26,6 @@ cat gpurun_out/${T}_obj_phases.log
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T}_obj_trace -o run -- python3 -u tools/single_object_trace.py > gpurun_out/${T}_obj_trace.log 2>&1 || { echo TRACE_FAILED; tail -20 gpurun_out/${T}_obj_trace.log; exit 1; }
 python3 tools/single_object_trace.py --report gpurun_out/${T}_obj_trace/run_kernel_trace.csv > gpurun_out/${T}_obj_timeline.txt 2>&1
-grep -E "single object|units" gpurun_out/${T}_obj_trace.log || true
+grep -E "single object|units|priority" gpurun_out/${T}_obj_trace.log || true
 tail -30 gpurun_out/${T}_obj_timeline.txt
 echo DONE
