@@ -856,6 +856,33 @@ ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, 
 }  // extern "C"
 
 namespace ot {
+// The sampler's kernels run on a per-thread stream of the device's greatest priority, forked from and synchronised
+// before returning to the caller's stream: its latency chain (the chains' wide passes and single-wave walks) is
+// dispatched ahead of independent work the caller queued elsewhere (a fresh mesh's vertex normals on a side stream),
+// which fills the walks' idle CUs instead.  The entry points synchronise on return, so nothing later on the caller's
+// stream can overtake them.
+struct HiStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr;
+    int dev = -1;
+};
+static thread_local HiStream g_hi;
+static ot_status hi_stream_fork(hipStream_t caller, hipStream_t* out) {
+    int dev = 0;
+    OT_HIP_TRY(hipGetDevice(&dev));
+    if (!g_hi.s || g_hi.dev != dev) {  // one per thread (and device: a thread that switches devices re-creates it)
+        int least = 0, greatest = 0;
+        OT_HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        OT_HIP_TRY(hipStreamCreateWithPriority(&g_hi.s, hipStreamNonBlocking, greatest));
+        OT_HIP_TRY(hipEventCreateWithFlags(&g_hi.fork, hipEventDisableTiming));
+        g_hi.dev = dev;
+    }
+    OT_HIP_TRY(hipEventRecord(g_hi.fork, caller));
+    OT_HIP_TRY(hipStreamWaitEvent(g_hi.s, g_hi.fork, 0));
+    *out = g_hi.s;
+    return OT_OK;
+}
+
 // The area sums and CDFs of every job (SamplePointsUniformly's two serial float64 chains, run side by side) into
 // scratch slot 17, followed by `extra` bytes for the caller, whose leading `upload` bytes travel to the device with the
 // chain table in one copy: fill(host, dev) writes them once the layout is known.  cdf[j]: the job's CDF (device);
@@ -952,11 +979,13 @@ ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs, 
 
 ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
                                       double z_min, int64_t* n_kept_host, void* stream_) {
-    hipStream_t stream = S(stream_);
     if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
     if (n_jobs < 0 || (n_jobs > 0 && (!jobs || !n_kept_host)))
         return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
     if (n_jobs == 0) return OT_OK;
+    hipStream_t stream = nullptr;
+    ot_status fst = hi_stream_fork(S(stream_), &stream);
+    if (fst != OT_OK) return fst;
     if (n_points > ((int64_t)1 << 40)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many points");
     const int64_t tiles64 = (n_points + MZ_TILE - 1) / MZ_TILE;
     if (tiles64 > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many points");

@@ -204,11 +204,19 @@ __device__ inline double dmax(double a, double b) {
     return r;
 }
 
+// Issue order: the min of entry i - 1 goes between the min and the max of entry i, so no max reads the result of the
+// instruction right before it (a dependent float64 pair needs a wait state: one s_nop per entry otherwise); entry i - 1
+// is still the old value when entry i's max reads it.
 template <int KMAX>
 __device__ inline void topk_insert(double (&best)[KMAX], double d) {
+    double m = dmin(best[KMAX - 1], d);
 #pragma unroll
-    for (int i = KMAX - 1; i > 0; --i) best[i] = dmax(best[i - 1], dmin(best[i], d));
-    best[0] = dmin(best[0], d);
+    for (int i = KMAX - 1; i > 0; --i) {
+        const double mi = m;
+        m = dmin(best[i - 1], d);
+        best[i] = dmax(best[i - 1], mi);
+    }
+    best[0] = m;
 }
 
 // candidates [beg, end) of the sorted points, two per step with both rows loaded before either is tested
