@@ -290,25 +290,33 @@ __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, doub
     }
 }
 
-__device__ inline int edge_vid(const McDev& m, const int* snbr, int x, int y, int z, int e) {
+// sbase: the 8 owner units' first vertex (vert_base of their rank), read once per workgroup, so a triangle corner costs
+// two independent loads (the owner's edge word and its prefix) instead of a rank -> base chain behind them
+__device__ inline int edge_vid(const McDev& m, const int* snbr, const long long* sbase, int x, int y, int z, int e) {
     const int ox = x + c_eshift[e][0], oy = y + c_eshift[e][1], oz = z + c_eshift[e][2];
-    const int owner = snbr[((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4)];
+    const int o = ((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4);
+    const int owner = snbr[o];
     const int local = (ox & 15) * 256 + (oy & 15) * 16 + (oz & 15);
     const int bit = local * 3 + c_eshift[e][3];
     const int word = bit >> 5;
     if (owner < 0) return 0;
     const unsigned wbits = m.eflags[(size_t)owner * EWORDS + word];
     const unsigned below = wbits & ((1u << (bit & 31)) - 1u);
-    return (int)(m.vert_base[m.rank_of[owner]] + m.wprefix[(size_t)owner * EWORDS + word] + __popc(below));
+    return (int)(sbase[o] + m.wprefix[(size_t)owner * EWORDS + word] + __popc(below));
 }
 
 __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_t* T) {
     __shared__ int snbr[8];
+    __shared__ long long sbase[8];
     const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
     const int ukey[3] = {d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]};
-    if (t < 8) snbr[t] = m.nbr[id * 16 + t];
+    if (t < 8) {
+        const int o = m.nbr[id * 16 + t];
+        snbr[t] = o;
+        sbase[t] = o >= 0 ? m.vert_base[m.rank_of[o]] : 0;
+    }
     const uint4 q = *reinterpret_cast<const uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16);
     const unsigned cw[4] = {q.x, q.y, q.z, q.w};
     int cnt = 0;
@@ -336,9 +344,9 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
         const int cube = (int)((cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu);
         if (cube == 0) continue;
         for (int k = 0; k < 15 && c_tri[cube][k] != -1; k += 3) {
-            const int a = edge_vid(m, snbr, x, y, z, c_tri[cube][k]);
-            const int b = edge_vid(m, snbr, x, y, z, c_tri[cube][k + 1]);
-            const int c = edge_vid(m, snbr, x, y, z, c_tri[cube][k + 2]);
+            const int a = edge_vid(m, snbr, sbase, x, y, z, c_tri[cube][k]);
+            const int b = edge_vid(m, snbr, sbase, x, y, z, c_tri[cube][k + 1]);
+            const int c = edge_vid(m, snbr, sbase, x, y, z, c_tri[cube][k + 2]);
             if (out < m.cap_t) {
                 T[out * 3 + 0] = a;
                 T[out * 3 + 1] = c;

@@ -514,9 +514,16 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
     double s = 0.0;  // sum: 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0
     int nseg = 0;
     int64_t b = 0;
-    double pv[4] = {0.0, 0.0, 0.0, 0.0};  // prefetched values of chunk pf
-    int64_t pf = -1;
+    // the values of chunk vb, loaded ahead: every step issues the load of its chunk before reading the metadata, and a
+    // serial chunk issues its successor's, so a chunk walked serially rarely waits for memory (a crossing chunk
+    // follows a fast step; serial chunks cluster where the running value is small)
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    int64_t vb = -1;
     while (b < nb) {  // wave-uniform control flow: every lane holds the same s and b
+        if (vb != b) {
+            chunk_load4(j.x, j.n, b * CH, lane, v);
+            vb = b;
+        }
         const int k_b = M.kind(b), e_b = M.ex(b), re = M.rend(b);
         const bool head = b == 0 || M.rend(b - 1) < b;
         const long long base = head ? 0 : M.pre(b - 1);
@@ -553,18 +560,15 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
                 continue;
             }
         }
-        // not provable from s: walk this chunk serially (its values prefetched by the previous serial chunk when that
-        // was chunk b - 1 -- serial chunks cluster where the running value is small -- and chunk b + 1's fetched now)
-        double v[4];
-        if (pf == b) {
+        // not provable from s: walk this chunk serially (its values already in flight), chunk b + 1's load issued first
+        double w[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = pv[q];
-        } else {
-            chunk_load4(j.x, j.n, b * CH, lane, v);
+        for (int q = 0; q < 4; ++q) w[q] = v[q];
+        if (b + 1 < nb) {
+            chunk_load4(j.x, j.n, (b + 1) * CH, lane, v);
+            vb = b + 1;
         }
-        if (b + 1 < nb) chunk_load4(j.x, j.n, (b + 1) * CH, lane, pv);
-        pf = b + 1;
-        s = chain_serial_chunk<CDF>(j, b, s, v, lane);
+        s = chain_serial_chunk<CDF>(j, b, s, w, lane);
         if (lane == 0) j.kind[b] = 2;
         ++b;
     }
