@@ -58,7 +58,17 @@ __device__ inline int2 grid_column(const GridDev& g, int f, int x, int y) {
 __device__ inline int2 column_range(const GridDev& g, int2 col, int zlo, int zhi) {
     int b = 0, e = 0;
     bool any = false;
-    for (int i = 0; i < col.y; ++i) {
+    int i0 = 0;
+    if (col.y > 8) {  // tall column (a wall seen edge-on): bisect for the first cell with z >= zlo
+        int lo = -1, hi = col.y;  // cz[lo] < zlo <= cz[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (g.cz[col.x + mid] < zlo) lo = mid;
+            else hi = mid;
+        }
+        i0 = hi;
+    }
+    for (int i = i0; i < col.y; ++i) {
         const int z = g.cz[col.x + i];
         if (z > zhi) break;
         if (z >= zlo) {
@@ -120,8 +130,25 @@ __global__ __launch_bounds__(256) void k_grid_insert(const unsigned long long* _
     g.cz[c] = (int)(key & ((1ull << g.sy) - 1));
     const unsigned long long col = key >> g.sy;
     if (c > 0 && (skeys[heads[c - 1]] >> g.sy) == col) return;
-    int cnt = 1;
-    while (c + cnt < ncells && (skeys[heads[c + cnt]] >> g.sy) == col) ++cnt;
+    // the column's cells are contiguous (cell-major keys): its end by galloping, then bisection -- a wall's column
+    // holds dozens of cells, and a probe is two dependent loads
+    int64_t lo = c, hi = ncells, step = 1;
+    while (true) {
+        const int64_t p = c + step;
+        if (p >= ncells) break;
+        if ((skeys[heads[p]] >> g.sy) != col) {
+            hi = p;
+            break;
+        }
+        lo = p;
+        step <<= 1;
+    }
+    while (hi - lo > 1) {  // colkey(lo) == col; hi == ncells or colkey(hi) != col
+        const int64_t mid = (lo + hi) >> 1;
+        if ((skeys[heads[mid]] >> g.sy) == col) lo = mid;
+        else hi = mid;
+    }
+    const int cnt = (int)(hi - c);
     unsigned slot = (unsigned)mix64(col) & (unsigned)g.hash_mask;
     while (true) {  // capacity >= 2 * ncells >= 2 * columns: always terminates
         const unsigned long long old = atomicCAS(&g.hkeys[slot], KEY_EMPTY, col);
