@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-4 records on the final build (part A): every -m gpu test, smoke(), the default bench line, the rocprofv3
+# headline kernel stats (the roofline's kernel time cross-check), the configs[2] kernel breakdown and one object's
+# kernel timeline.  Part B is tools/pmc.sh (same-hash PMC traffic for the bench's roofline objects).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+T=${TAG:-r04z}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${T}_gpu_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_gpu_tests.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${T}_smoke.log 2>&1 \
+    || { echo SMOKE_FAILED; tail -20 gpurun_out/${T}_smoke.log; exit 1; }
+tail -1 gpurun_out/${T}_smoke.log
+timeout -k 10 400 python3 bench.py > gpurun_out/${T}_bench.log 2>&1 || { echo BENCH_FAILED; tail -30 gpurun_out/${T}_bench.log; exit 1; }
+tail -1 gpurun_out/${T}_bench.log > gpurun_out/${T}_bench.json
+python3 -c "
+import json; d=json.load(open('gpurun_out/${T}_bench.json'))
+print('value', d['value'], 'ms/step', d['ms_per_step'], 'roofline', d['roofline'].get('frac'), d['roofline'].get('kernel_ms'))
+print('filtered', d['filtered']['ms_per_frame'], 'objects', d['objects']['ms'], d['objects']['single_object_ms'], d['objects']['objects_over_single'])"
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_h -o bench -- python3 bench.py \
+    --objects 0 --hybrid-objects 0 --filter-frames 0 --cpu-frames 0 > gpurun_out/${T}_bench_prof_h.log 2>&1 \
+    || { echo PROF_FAILED; tail -30 gpurun_out/${T}_bench_prof_h.log; exit 1; }
+tail -1 gpurun_out/${T}_bench_prof_h.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_fb_prof -o run -- python3 -u \
+    tools/filter_batch_time.py --frames 64 --batches 32 --reps 3 > gpurun_out/${T}_fb_prof.log 2>&1 \
+    || { echo FBPROF_FAILED; tail -20 gpurun_out/${T}_fb_prof.log; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T}_obj_trace -o run -- python3 -u \
+    tools/single_object_trace.py > gpurun_out/${T}_obj_trace.log 2>&1 || { echo TRACE_FAILED; tail -20 gpurun_out/${T}_obj_trace.log; exit 1; }
+python3 tools/single_object_trace.py --report gpurun_out/${T}_obj_trace/run_kernel_trace.csv > gpurun_out/${T}_obj_timeline.txt 2>&1
+grep -E "single object|units" gpurun_out/${T}_obj_trace.log || true
+echo DONE
