@@ -162,29 +162,6 @@ __device__ inline T wave_sum(T v) {
     return v;
 }
 
-// wave-wide min / max of a u64 without LDS permutes: DPP inside each row of 16 (quad xor 1, xor 2, half-row mirror,
-// row mirror: every lane ends with its row's result), then the four rows' results by readlane.  Result wave-uniform.
-template <int CTRL>
-__device__ inline unsigned long long dpp_perm_u64(unsigned long long v) {
-    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)v, CTRL, 0xF, 0xF, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xF, 0xF, false);
-    return ((unsigned long long)hi << 32) | lo;
-}
-__device__ inline unsigned long long readlane_u64(unsigned long long v, int l) {
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
-    return ((unsigned long long)hi << 32) | lo;
-}
-template <bool MAX>
-__device__ inline unsigned long long wave_minmax_u64(unsigned long long v) {
-    auto pick = [](unsigned long long a, unsigned long long b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
-    v = pick(v, dpp_perm_u64<0xB1>(v));   // quad_perm [1,0,3,2]
-    v = pick(v, dpp_perm_u64<0x4E>(v));   // quad_perm [2,3,0,1]
-    v = pick(v, dpp_perm_u64<0x141>(v));  // row_half_mirror
-    v = pick(v, dpp_perm_u64<0x140>(v));  // row_mirror
-    return pick(pick(readlane_u64(v, 0), readlane_u64(v, 16)), pick(readlane_u64(v, 32), readlane_u64(v, 48)));
-}
-
 // Decoupled look-back (single-pass prefix over the tiles of one chain), run by ONE whole wave of the tile's
 // workgroup: publishes the tile's aggregate, reads its predecessors' status words 64 at a time (lane i: tile - 1 - i),
 // folds every aggregate up to the nearest inclusive prefix, publishes its own inclusive prefix and returns the

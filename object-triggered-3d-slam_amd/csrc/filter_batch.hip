@@ -182,9 +182,14 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_pixels(FbParams p, int* __res
         }
     }
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {  // wave-uniform results (DPP + readlane: no LDS permutes)
-        mn[a] = wave_minmax_u64<false>(mn[a]);
-        mx[a] = wave_minmax_u64<true>(mx[a]);
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            unsigned long long t = __shfl_xor(mn[a], off, 64);
+            mn[a] = t < mn[a] ? t : mn[a];
+            t = __shfl_xor(mx[a], off, 64);
+            mx[a] = t > mx[a] ? t : mx[a];
+        }
     }
     c = wave_sum(c);
     __shared__ unsigned long long s[4][6];
@@ -719,6 +724,28 @@ __global__ void k_fb_kept_offsets(const int64_t* __restrict__ kept, int64_t nk, 
     koff[f] = lo;
 }
 
+// kept rows: xyz / rgb of the kept voxels and their index inside their frame's voxel cloud
+__global__ __launch_bounds__(256) void k_fb_gather(const int64_t* __restrict__ kept, int64_t nk,
+                                                   const int* __restrict__ voff, int F, const double* __restrict__ vx,
+                                                   const double* __restrict__ vc, double* __restrict__ ox,
+                                                   double* __restrict__ oc, int64_t* __restrict__ oidx) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nk) return;
+    const int64_t i = kept[t];
+    int lo = 0, hi = F;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (voff[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        ox[t * 3 + a] = vx[i * 3 + a];
+        oc[t * 3 + a] = vc[i * 3 + a];
+    }
+    oidx[t] = i - voff[lo];
+}
+
 // voxel heads of the segmented (u32-key, unpacked) sort: a new key, or the first point of a frame.  With the frame tags
 // in the keys (FbKeys::tag) adjacent frames' keys always differ; otherwise the frame starts are found from the values'
 // global pixel indices
@@ -738,33 +765,6 @@ struct SegHeadPredPix {
 struct KeptEmit {
     int64_t* out;
     __device__ void operator()(int64_t i, int64_t pos) const { out[pos] = i; }
-};
-// the compaction's emit writes the kept rows themselves (xyz, rgb, index inside the frame's voxel cloud) beside the
-// kept index: no separate gather pass re-reading the index list
-struct KeptRowsEmit {
-    int64_t* kept;
-    const int* voff;
-    int F;
-    const double* vx;
-    const double* vc;
-    double* ox;
-    double* oc;
-    int64_t* oidx;
-    __device__ void operator()(int64_t i, int64_t pos) const {
-        kept[pos] = i;
-        int lo = 0, hi = F;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (voff[mid] <= i) lo = mid;
-            else hi = mid;
-        }
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            ox[pos * 3 + a] = vx[i * 3 + a];
-            oc[pos * 3 + a] = vc[i * 3 + a];
-        }
-        oidx[pos] = i - voff[lo];
-    }
 };
 
 }  // namespace ot
@@ -1071,17 +1071,19 @@ ot_status ot_rgbd_filter_run(ot_rgbd_filter* fl, int32_t n_frames, const uint16_
     int64_t* kept = (int64_t*)fl->b_out.get((size_t)K * (8 + 8 + 48) + (size_t)(F + 1) * 8 + 512);
     if (!kept) return fail(OT_ERR_HIP, "[rgbd_filter] allocation failed");
     int64_t nk = 0;
+    st = compact(K, SorKeep{avg, stats, d_voff, F}, KeptEmit{kept}, stream, &nk, 13);  // synchronises
+    if (st != OT_OK) return st;
+    fl->kept = nk;
     int64_t* d_koff = kept + K;
     fl->kidx = d_koff + (F + 1);
     fl->kx = (double*)(fl->kidx + K);
     fl->kc = fl->kx + K * 3;
-    st = compact(K, SorKeep{avg, stats, d_voff, F},
-                 KeptRowsEmit{kept, d_voff, F, fl->vx, fl->vc, fl->kx, fl->kc, fl->kidx}, stream, &nk,
-                 13);  // synchronises
-    if (st != OT_OK) return st;
-    fl->kept = nk;
     hipLaunchKernelGGL(k_fb_kept_offsets, dim3((F + 64) / 64), dim3(64), 0, stream, (const int64_t*)kept, nk,
                        (const int*)d_voff, F, d_koff);
+    if (nk > 0)
+        hipLaunchKernelGGL(k_fb_gather, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, stream, (const int64_t*)kept,
+                           nk, (const int*)d_voff, F, (const double*)fl->vx, (const double*)fl->vc, fl->kx, fl->kc,
+                           fl->kidx);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipMemcpyAsync(fl->koff.data(), d_koff, sizeof(int64_t) * (F + 1), hipMemcpyDeviceToHost, stream));
     OT_HIP_TRY(hipStreamSynchronize(stream));
