@@ -131,6 +131,7 @@ class OTError(RuntimeError):
 # test hooks exported by the library but outside the drop-in boundary (not declared in include/otslam.h)
 TEST_SIGNATURES = {
     "otx_serial_chain_f64": [_p, _i64, _i32, _p, _pi64, _p],
+    "otx_chain_walk_trace": [_p, _i64, _i32, _p, _p, _i32, _p],
     "otx_tsdf_stats": [_p, _p],
     "otx_sort_pairs_u64_u32": [_p, _p, _p, _p, _i64, _i32, _p],
     "otx_sort_segments_u32_u32": [_p, _p, _p, _p, _p, _i32, _i32, _p],

@@ -26,6 +26,8 @@ struct ChainJob {
     long long* seg_n;
     long long* seg_base;
     int32_t* nseg;
+    unsigned long long* trace = nullptr;  // test hook (otx_chain_walk_trace): per walk event {clock64, kind | chunk << 8}
+    int trace_cap = 0;
 };
 
 // per-chain auxiliary arrays

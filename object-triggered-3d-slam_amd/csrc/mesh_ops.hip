@@ -519,7 +519,18 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
     // follows a fast step; serial chunks cluster where the running value is small)
     double v[4] = {0.0, 0.0, 0.0, 0.0};
     int64_t vb = -1;
+    int ti = 0;  // trace events written (test hook only: j.trace is null in every product call)
+    auto mark = [&](int kind, int64_t chunk) {
+        if (j.trace) {
+            if (lane == 0 && ti < j.trace_cap) {
+                j.trace[2 * ti] = (unsigned long long)clock64();
+                j.trace[2 * ti + 1] = (unsigned long long)kind | ((unsigned long long)chunk << 8);
+            }
+            ++ti;
+        }
+    };
     while (b < nb) {  // wave-uniform control flow: every lane holds the same s and b
+        mark(0, b);
         if (vb != b) {
             chunk_load4(j.x, j.n, b * CH, lane, v);
             vb = b;
@@ -549,6 +560,7 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
                 k = lo;
             }
             if (k >= b) {
+                mark(p_re > lim ? 2 : 1, k);
                 if (CDF && lane == 0) {
                     j.seg_b[nseg] = (int)b;
                     j.seg_n[nseg] = N;
@@ -569,9 +581,11 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
             vb = b + 1;
         }
         s = chain_serial_chunk<CDF>(j, b, s, w, lane);
+        mark(3, b);
         if (lane == 0) j.kind[b] = 2;
         ++b;
     }
+    mark(4, nb);
     if (lane == 0) {
         if (!CDF) j.out[0] = s;
         j.nseg[0] = nseg;
@@ -1061,6 +1075,29 @@ ot_status ot_mesh_get_surface_area(const double* V, int64_t nv, const int32_t* T
     launch_chains<false>(djob, 1, nt, stream);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipMemcpyAsync(area_host, sum, sizeof(double), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    return OT_OK;
+}
+
+// test hook (not part of the drop-in boundary): the chain walk of otx_serial_chain_f64 with its events traced into
+// trace (device, 2 * cap u64: {clock64, kind | chunk << 8}; kind 0 step start, 1 run accepted, 2 accepted after the
+// 64-way search, 3 serial chunk done, 4 end); *events_host: events recorded (may exceed cap)
+ot_status otx_chain_walk_trace(const double* x, int64_t n, int32_t cdf, double* out, unsigned long long* trace,
+                               int32_t cap, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (n <= 0 || !x || !out || !trace || cap <= 0 || ((uintptr_t)x & 15))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[chain] invalid arguments");
+    char* ws = (char*)scratch(chain_aux_bytes(n) + sizeof(ChainJob) + 256, 17);
+    if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+    ChainJob jb{};
+    jb.x = x, jb.n = n, jb.out = out;
+    ChainJob* djob = (ChainJob*)chain_aux(ws, n, jb);
+    jb.trace = trace;
+    jb.trace_cap = cap;
+    OT_HIP_TRY(hipMemcpyAsync(djob, &jb, sizeof(ChainJob), hipMemcpyHostToDevice, stream));
+    if (cdf) launch_chains<true>(djob, 1, n, stream);
+    else launch_chains<false>(djob, 1, n, stream);
+    OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
 }
