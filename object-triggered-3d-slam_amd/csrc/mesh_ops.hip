@@ -287,6 +287,27 @@ __device__ inline int wave_first_idx(int idx) {
     return m ? __builtin_amdgcn_readlane(idx, __ffsll((long long)m) - 1) : CH;
 }
 
+// The segment arithmetic stays in float64: every grid count r = rint(a / u) and every prefix the walk keeps is an integer
+// below 2^53, so float64 adds of them are exact; a prefix past the binade's limit may round, but rounding is monotone
+// and the limit T = 2^53 - 1 - N is representable, so "prefix > T" is decided exactly.  No int64 conversions on the
+// single wave's latency chain.
+template <int CTRL>
+__device__ inline double dpp_row_shr_f64(double v) {  // lanes without a source in their row of 16 read +0.0
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ inline double wave_incl_scan_f64(double v, int lane) {
+    v += dpp_row_shr_f64<0x111>(v);
+    v += dpp_row_shr_f64<0x112>(v);
+    v += dpp_row_shr_f64<0x114>(v);
+    v += dpp_row_shr_f64<0x118>(v);  // inclusive inside each row of 16
+    const double r0 = readlane_f64(v, 15), r1 = readlane_f64(v, 31), r2 = readlane_f64(v, 47);
+    const int row = lane >> 4;
+    return v + ((row >= 1 ? r0 : 0.0) + ((row >= 2 ? r1 : 0.0) + (row >= 3 ? r2 : 0.0)));
+}
+
 template <bool CDF>
 __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, const double v[4], int lane) {
     const int64_t base = b * CH;
@@ -297,32 +318,30 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
         int stop = pos;
         if (e != EX_NONE) {
             const double scale = pow2(52 - e), u = pow2(e - 52);
-            const long long N = (long long)(s * scale);  // exact integer in [2^52, 2^53)
-            long long r[4], incl[4], loc = 0;
+            const double N = s * scale;                    // exact integer in [2^52, 2^53)
+            const double T = (double)(R_MAX - 1) - N;      // exact: the largest prefix that stays in the binade
+            double incl[4], loc = 0.0;
             int bad = CH;  // first element of this lane the integer step cannot take
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int idx = 4 * lane + k;
                 const double m = v[k] * scale;  // exact: power-of-two scaling
-                const bool ok = m >= 0.0 && m < (double)R_MAX && m - floor(m) != 0.5;
+                const double r = rint(m);
+                const bool ok = m >= 0.0 && m < (double)R_MAX && fabs(m - r) != 0.5;
                 const bool act = idx >= pos && idx < cnt;
-                r[k] = (act && ok) ? (long long)rint(m) : 0;
+                loc += (act && ok) ? r : 0.0;
+                incl[k] = loc;
                 if (act && !ok && bad == CH) bad = idx;
                 if (idx >= cnt && bad == CH) bad = idx;
             }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                loc += r[k];
-                incl[k] = loc;
-            }
-            const long long excl = wave_incl_scan_i64(loc, lane) - loc;
+            const double excl = wave_incl_scan_f64(loc, lane) - loc;  // exact where it matters (see above)
             const int first_bad = wave_first_idx(bad);
             int cross = CH;  // first element whose running integer leaves the binade
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 incl[k] += excl;
                 const int idx = 4 * lane + k;
-                if (idx >= pos && idx < first_bad && N + incl[k] > R_MAX - 1 && cross == CH) cross = idx;
+                if (idx >= pos && idx < first_bad && incl[k] > T && cross == CH) cross = idx;
             }
             const int first_cross = wave_first_idx(cross);
             stop = first_bad < first_cross ? first_bad : first_cross;
@@ -331,11 +350,11 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int idx = 4 * lane + k;
-                    if (CDF && idx >= pos && idx < stop) j.out[base + idx] = (double)(N + incl[k]) * u;
+                    if (CDF && idx >= pos && idx < stop) j.out[base + idx] = (N + incl[k]) * u;
                 }
                 const int last = stop - 1;
-                const long long mine = (last & 3) == 0 ? incl[0] : (last & 3) == 1 ? incl[1] : (last & 3) == 2 ? incl[2] : incl[3];
-                s = (double)(N + readlane64(mine, last >> 2)) * u;
+                const double mine = (last & 3) == 0 ? incl[0] : (last & 3) == 1 ? incl[1] : (last & 3) == 2 ? incl[2] : incl[3];
+                s = (N + readlane_f64(mine, last >> 2)) * u;
             }
         }
         if (stop < cnt) {  // one exact float64 add, in Open3D's order
