@@ -390,20 +390,6 @@ struct FbCellKeys {
 // found by a decoupled look-back inside the frame (tiles take tickets in start order, so a tile only waits on running
 // ones); rlen[f] = the frame's run count (its segment of the sort holds that many, the rest is capacity).
 
-// key of pixel pix of frame f (false: no point), as the tiles compute it
-__device__ inline bool fb_pixel_key(const FbParams& p, const FbKeys& kb, const double* m, const double vmin[3],
-                                    const uint16_t* __restrict__ dep, int pix, unsigned& key) {
-    float d = div_rn((float)dep[pix], p.scale_f, p.rscale_f);
-    if ((double)d >= p.trunc) d = 0.0f;
-    double xyz[3];
-    if (!fb_point(p, m, d, pix, xyz)) return false;
-    long long kk[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) kk[a] = (long long)(int)floor_div(xyz[a] - vmin[a], p.vs, p.inv_vs);
-    key = (unsigned)fb_voxel_key(kb, (unsigned long long)kk[0], (unsigned long long)kk[1], (unsigned long long)kk[2]);
-    return true;
-}
-
 __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, const int* __restrict__ toff,
                                                         const int* __restrict__ poff, unsigned* __restrict__ rkeys,
                                                         unsigned* __restrict__ rvals,
@@ -414,8 +400,6 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
     __shared__ int wsum[4];
     __shared__ unsigned s_lastkey[4];
     __shared__ int s_lastval[4];
-    __shared__ unsigned s_prevkey;
-    __shared__ int s_prevval;
     __shared__ int s_excl;
     __shared__ unsigned long long s_rec[FB_TILE];
     __shared__ unsigned s_rkey[FB_TILE];
@@ -430,12 +414,6 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
 #pragma unroll
     for (int k = 0; k < 16; ++k) m[k] = p.frames[f].pose[k];
     const double vmin[3] = {p.frames[f].vmin[0], p.frames[f].vmin[1], p.frames[f].vmin[2]};
-    if (threadIdx.x == 0) {  // the pixel before the tile (the previous tile's last one)
-        unsigned pk = 0u;
-        const int pp = tile * FB_TILE - 1;
-        s_prevval = (pp >= 0 && fb_pixel_key(p, kb, m, vmin, dep, pp, pk)) ? 1 : 0;
-        s_prevkey = pk;
-    }
     float d[FB_PIX];
     unsigned raw[FB_PIX], rgb[FB_PIX], key[FB_PIX];
     bool val[FB_PIX];
@@ -454,8 +432,7 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
                                             (unsigned long long)kk[2]);
         }
     }
-    // the previous pixel of the lane's first: the previous lane's last (a shuffle), the previous wave's last (LDS) or
-    // the previous tile's last (thread 0 above)
+    // the previous pixel of the lane's first: the previous lane's last (a shuffle) or the previous wave's last (LDS)
     const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
     unsigned pk = __shfl_up(key[FB_PIX - 1], 1, 64);
     int pv = __shfl_up(val[FB_PIX - 1] ? 1 : 0, 1, 64);
@@ -465,8 +442,10 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_runs(FbParams p, FbKeys kb, c
     }
     __syncthreads();
     if (lane == 0) {
-        pk = wid == 0 ? s_prevkey : s_lastkey[wid - 1];
-        pv = wid == 0 ? s_prevval : s_lastval[wid - 1];
+        // a tile's first pixel always starts a run (splitting a run at a tile border changes no sum: the pieces
+        // stay consecutive in the stable sort), so no tile recomputes its predecessor's last key
+        pk = wid == 0 ? 0u : s_lastkey[wid - 1];
+        pv = wid == 0 ? 0 : s_lastval[wid - 1];
     }
     int c = 0, nr = 0;
     bool head[FB_PIX];
