@@ -372,6 +372,11 @@ constexpr int SEGSORT_ITEMS = 16;  // items per thread of the segmented sort's t
 ot_status sort_segments_u32_u32(const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout,
                                 const int64_t* seg, int nseg, int end_bit, hipStream_t stream, int scratch_slot,
                                 const int* dlen) {
+    // 10-bit digits (1024-thread tiles of 4096 items) for 28..30-bit keys: 3 passes instead of 4 (the configs[2]
+    // cell-major voxel keys of 1280x720 frames are 28..30 bits)
+    if (end_bit > 27 && end_bit <= 30)
+        return rs_sort<unsigned, SEGSORT_ITEMS / 4, 10>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot,
+                                                        dlen);
     // 9-bit digits (512-thread tiles of the same 4096 items) when they save a pass: 25..27-bit keys in 3 passes
     if ((end_bit + 8) / 9 < (end_bit + 7) / 8)
         return rs_sort<unsigned, SEGSORT_ITEMS / 2, 9>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot,
