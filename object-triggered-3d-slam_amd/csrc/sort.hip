@@ -372,11 +372,8 @@ constexpr int SEGSORT_ITEMS = 16;  // items per thread of the segmented sort's t
 ot_status sort_segments_u32_u32(const unsigned* kin, unsigned* kout, const unsigned* vin, unsigned* vout,
                                 const int64_t* seg, int nseg, int end_bit, hipStream_t stream, int scratch_slot,
                                 const int* dlen) {
-    // 10-bit digits (1024-thread tiles of 4096 items) for 28..30-bit keys: 3 passes instead of 4 (the configs[2]
-    // cell-major voxel keys of 1280x720 frames are 28..30 bits)
-    if (end_bit > 27 && end_bit <= 30)
-        return rs_sort<unsigned, SEGSORT_ITEMS / 4, 10>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot,
-                                                        dlen);
+    // (10-bit digits, 1024-thread tiles, 3 passes for the 28..30-bit configs[2] keys: measured slower, 624 + 85 us vs
+    // 516 + 52 us per 32-frame batch for 4 passes of 8 bits)
     // 9-bit digits (512-thread tiles of the same 4096 items) when they save a pass: 25..27-bit keys in 3 passes
     if ((end_bit + 8) / 9 < (end_bit + 7) / 8)
         return rs_sort<unsigned, SEGSORT_ITEMS / 2, 9>(kin, kout, vin, vout, seg, nseg, end_bit, stream, scratch_slot,

@@ -61,7 +61,7 @@ def test_sort_presorted_and_reversed(pkg, gpu):
     ([0, 1, 2047, 2048, 2049, 0, 5], 12), ([812746, 810001, 0, 799999], 28), ([100000] * 33, 32), ([3] * 64, 2),
     # 9-bit digits (3 passes for 25..27 bits, 2 for 17..18): the configs[2] voxel keys
     ([812746, 810001, 0, 799999], 27), ([0, 1, 4095, 4096, 4097, 0, 5], 25), ([100000] * 33, 18),
-    # 10-bit digits (3 passes for 28..30 bits: the cell-major configs[2] keys of 1280x720 frames)
+    # 28..30-bit keys (the cell-major configs[2] keys of 1280x720 frames)
     ([0, 1, 4095, 4096, 4097, 0, 5], 29), ([480000] * 32, 30), ([3] * 64, 28),
 ])
 def test_segmented_sort_bitexact(pkg, gpu, sizes, end_bit):
