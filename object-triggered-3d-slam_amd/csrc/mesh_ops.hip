@@ -309,11 +309,22 @@ __device__ inline double wave_incl_scan_f64(double v, int lane) {
 }
 
 template <bool CDF>
-__device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, const double v[4], int lane) {
+__device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, const double v[4], int lane,
+                                            int& ti) {
     const int64_t base = b * CH;
     const int cnt = j.n - base < CH ? (int)(j.n - base) : CH;
     int pos = 0;
+    auto mark = [&](int kind, int at) {  // test hook only (j.trace is null in every product call)
+        if (j.trace) {
+            if (lane == 0 && ti < j.trace_cap) {
+                j.trace[2 * ti] = (unsigned long long)clock64();
+                j.trace[2 * ti + 1] = (unsigned long long)kind | ((unsigned long long)at << 8);
+            }
+            ++ti;
+        }
+    };
     while (pos < cnt) {  // wave-uniform
+        mark(5, pos);
         const int e = binade(s);
         int stop = pos;
         if (e != EX_NONE) {
@@ -344,6 +355,7 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
                 if (idx >= pos && idx < first_bad && incl[k] > T && cross == CH) cross = idx;
             }
             const int first_cross = wave_first_idx(cross);
+            mark(6, pos);
             stop = first_bad < first_cross ? first_bad : first_cross;
             stop = stop < cnt ? stop : cnt;
             if (stop > pos) {
@@ -599,7 +611,7 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
             chunk_load4(j.x, j.n, (b + 1) * CH, lane, v);
             vb = b + 1;
         }
-        s = chain_serial_chunk<CDF>(j, b, s, w, lane);
+        s = chain_serial_chunk<CDF>(j, b, s, w, lane, ti);
         mark(3, b);
         if (lane == 0) j.kind[b] = 2;
         ++b;

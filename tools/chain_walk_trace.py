@@ -49,10 +49,28 @@ def main():
         # each step: from its start event (kind 0) to the next start (or the end event)
         starts = np.nonzero(kind == 0)[0]
         per = {}
+        pre = []
         for i, si in enumerate(starts):
             nxt = starts[i + 1] if i + 1 < len(starts) else len(kind) - 1
-            k = int(kind[si + 1]) if si + 1 < len(kind) else 4
+            ks = [int(x) for x in kind[si + 1:nxt + 1] if x in (1, 2, 3)]
+            k = ks[0] if ks else 4
             per.setdefault(k, []).append(int(clk[nxt] - clk[si]))
+            if k == 3:  # serial: step start -> first segment (metadata, the failed fast check, the values' wait)
+                f5 = [j for j in range(si + 1, nxt) if kind[j] == 5]
+                if f5:
+                    pre.append(int(clk[f5[0]] - clk[si]))
+        if pre:
+            print(f"   serial steps: start -> first segment mean {np.mean(pre):.0f} cycles")
+        # inside serial chunks: kind 5 = segment start, 6 = after the segment's scans (before its stores / float add)
+        seg_a, seg_b = [], []
+        for i in range(len(kind) - 1):
+            if kind[i] == 5:
+                seg_a.append(int(clk[i + 1] - clk[i]))  # start -> scans done
+            if kind[i] == 6:
+                seg_b.append(int(clk[i + 1] - clk[i]))  # scans done -> next event
+        if seg_a:
+            print(f"   segments {len(seg_a)}: start->scans mean {np.mean(seg_a):.0f} cycles, scans->next mean "
+                  f"{np.mean(seg_b):.0f}")
         total = int(clk[-1] - clk[0])
         print(f"{name}: {len(starts)} steps, {total} cycles in the walk loop")
         for k, v in sorted(per.items()):
