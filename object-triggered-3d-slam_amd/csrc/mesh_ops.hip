@@ -10,6 +10,7 @@
 // then generated in parallel, one lane per output point: binary search of its triangle in the n_t array,
 // r1/r2 from a counter-based RNG (splitmix64 of seed + counter; Open3D's mt19937 is unseeded), barycentric
 // a = 1 - sqrt(r1), b = sqrt(r1)(1 - r2), c = sqrt(r1) r2.
+#include <atomic>
 #include <functional>
 #include <vector>
 
@@ -512,35 +513,50 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
 // single wave's latency chain: one object's sampling waits on it, round 4: sum / CDF walks 86 / 118 us per configs[3]
 // mesh).  Chains with more chunks than WALK_LDS_CHUNKS read global memory as before.
 constexpr int WALK_LDS_CHUNKS = 7168;  // 16 B + 1 B per chunk: 119 KiB of LDS (1.8 M values)
+// STAGED: the accessors index the dynamic LDS array itself, so the compiler emits LDS reads (through a generic
+// pointer it had to emit flat loads, whose latency sat on every walk step: ~1.5-2.3k cycles per step, r04n trace)
+extern __shared__ int4 s_walk_meta[];
+template <bool STAGED>
 struct WalkMeta {
     const ChainJob* j;
-    const int4* m;        // LDS: {ex, rend, pre lo, pre hi} per chunk, or nullptr
-    const signed char* k; // LDS: kind per chunk
-    __device__ int ex(int64_t b) const { return m ? m[b].x : j->ex[b]; }
-    __device__ int rend(int64_t b) const { return m ? m[b].y : j->rend[b]; }
-    __device__ long long pre(int64_t b) const {
-        return m ? (long long)(((unsigned long long)(unsigned)m[b].w << 32) | (unsigned)m[b].z) : j->pre[b];
+    int64_t nb;
+    __device__ int ex(int64_t b) const {
+        if constexpr (STAGED) return s_walk_meta[b].x;
+        else return j->ex[b];
     }
-    __device__ int kind(int64_t b) const { return m ? (int)k[b] : j->kind[b]; }
-};
-
-template <bool CDF>
-__global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict__ jobs, int lds_chunks) {
-    extern __shared__ int4 s_meta[];
-    const ChainJob j = jobs[blockIdx.x];
-    const int64_t nb = (j.n + CH - 1) / CH;
-    const bool staged = nb <= lds_chunks;
-    signed char* s_kind = reinterpret_cast<signed char*>(s_meta + (staged ? nb : 0));
-    if (staged) {  // the whole workgroup stages the metadata, then one wave walks
-        for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
-            const unsigned long long pv = (unsigned long long)j.pre[b];
-            s_meta[b] = make_int4(j.ex[b], j.rend[b], (int)(unsigned)pv, (int)(unsigned)(pv >> 32));
-            s_kind[b] = (signed char)j.kind[b];
+    __device__ int rend(int64_t b) const {
+        if constexpr (STAGED) return s_walk_meta[b].y;
+        else return j->rend[b];
+    }
+    __device__ long long pre(int64_t b) const {
+        if constexpr (STAGED) {
+            const int4 q = s_walk_meta[b];
+            return (long long)(((unsigned long long)(unsigned)q.w << 32) | (unsigned)q.z);
+        } else {
+            return j->pre[b];
         }
     }
-    __syncthreads();
+    __device__ int kind(int64_t b) const {
+        if constexpr (STAGED) return (int)reinterpret_cast<const signed char*>(s_walk_meta + nb)[b];
+        else return j->kind[b];
+    }
+};
+
+template <bool CDF, bool STAGED>
+__global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict__ jobs) {
+    const ChainJob j = jobs[blockIdx.x];
+    const int64_t nb = (j.n + CH - 1) / CH;
+    if constexpr (STAGED) {  // the whole workgroup stages the metadata, then one wave walks
+        signed char* s_kind = reinterpret_cast<signed char*>(s_walk_meta + nb);
+        for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
+            const unsigned long long pv = (unsigned long long)j.pre[b];
+            s_walk_meta[b] = make_int4(j.ex[b], j.rend[b], (int)(unsigned)pv, (int)(unsigned)(pv >> 32));
+            s_kind[b] = (signed char)j.kind[b];
+        }
+        __syncthreads();
+    }
     if (threadIdx.x >= 64) return;
-    const WalkMeta M{&j, staged ? s_meta : nullptr, staged ? s_kind : nullptr};
+    const WalkMeta<STAGED> M{&j, nb};
     const int lane = threadIdx.x;
     double s = 0.0;  // sum: 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0
     int nseg = 0;
@@ -681,15 +697,18 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
     }
     hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
     // metadata staged in LDS when every job's chunks fit (max_n bounds them all)
-    const int lds_chunks = nb <= WALK_LDS_CHUNKS ? (int)nb : 0;
-    const size_t lds_bytes = (size_t)lds_chunks * 17 + 16;
-    static bool attr_set[2] = {false, false};
-    if (!attr_set[CDF]) {  // above 64 KiB of dynamic LDS the kernel must opt in (once per process)
-        (void)hipFuncSetAttribute((const void*)k_chain_walk<CDF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)((size_t)WALK_LDS_CHUNKS * 17 + 16));
-        attr_set[CDF] = true;
+    if (nb <= WALK_LDS_CHUNKS) {
+        const size_t lds_bytes = (size_t)nb * 17 + 16;
+        static std::atomic<bool> attr_set[2] = {false, false};
+        if (!attr_set[CDF].load()) {  // above 64 KiB of dynamic LDS the kernel must opt in (once per process)
+            (void)hipFuncSetAttribute((const void*)k_chain_walk<CDF, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)((size_t)WALK_LDS_CHUNKS * 17 + 16));
+            attr_set[CDF].store(true);
+        }
+        hipLaunchKernelGGL((k_chain_walk<CDF, true>), dim3(n_jobs), dim3(1024), lds_bytes, stream, djobs);
+    } else {
+        hipLaunchKernelGGL((k_chain_walk<CDF, false>), dim3(n_jobs), dim3(64), 0, stream, djobs);
     }
-    hipLaunchKernelGGL(k_chain_walk<CDF>, dim3(n_jobs), dim3(1024), lds_bytes, stream, djobs, lds_chunks);
     if (CDF) hipLaunchKernelGGL(k_chain_emit, grid, dim3(256), 0, stream, djobs);
 }
 
