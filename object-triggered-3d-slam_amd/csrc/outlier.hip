@@ -232,29 +232,18 @@ __device__ inline double dmax(double a, double b) {
 }
 
 // Issue order: the min of entry i - 1 goes between the min and the max of entry i, so no max reads the result of the
-// instruction right before it; entry i - 1 is still the old value when entry i's max reads it.  Entries [LO, KMAX)
-// only: the caller guarantees d >= best[LO - 1] on every lane, so the entries below LO keep their values (their
-// max(best[i-1], min(best[i], d)) is best[i]).
-template <int KMAX, int LO>
-__device__ inline void topk_insert_from(double (&best)[KMAX], double d) {
+// instruction right before it (a dependent float64 pair needs a wait state: one s_nop per entry otherwise); entry i - 1
+// is still the old value when entry i's max reads it.
+template <int KMAX>
+__device__ inline void topk_insert(double (&best)[KMAX], double d) {
     double m = dmin(best[KMAX - 1], d);
 #pragma unroll
-    for (int i = KMAX - 1; i > LO; --i) {
+    for (int i = KMAX - 1; i > 0; --i) {
         const double mi = m;
         m = dmin(best[i - 1], d);
         best[i] = dmax(best[i - 1], mi);
     }
-    best[LO] = LO > 0 ? dmax(best[LO > 0 ? LO - 1 : 0], m) : m;
-}
-// The whole wave takes one insertion when any lane accepts, and a lane that does not accept (or lands high) leaves the
-// low entries as they are: candidates come nearest-first, so after the first columns nearly every accepted d lands
-// in the top quarter of the list, and the wave moves only that quarter (or half) when its ballot says so.
-template <int KMAX>
-__device__ inline void topk_insert(double (&best)[KMAX], double d) {
-    constexpr int Q = KMAX - KMAX / 4, H = KMAX / 2;
-    if (KMAX >= 8 && __ballot(d < best[Q - 1]) == 0) topk_insert_from<KMAX, Q>(best, d);
-    else if (KMAX >= 4 && __ballot(d < best[H - 1]) == 0) topk_insert_from<KMAX, H>(best, d);
-    else topk_insert_from<KMAX, 0>(best, d);
+    best[0] = m;
 }
 
 // candidates [beg, end) of the sorted points, two per step with both rows loaded before either is tested
