@@ -14,6 +14,7 @@ import numpy as np
 
 from . import _device as D
 from . import _lib as L
+from . import streams as _streams
 from .utility import DoubleVector, Vector3dVector, Vector3iVector
 
 
@@ -544,7 +545,7 @@ class TriangleMesh:
             # waits for them (_Arr ready event; the sampler passes it to ot_mesh_sample_points_uniformly_after)
             torch = D.torch
             cur = torch.cuda.current_stream()
-            side = importlib.import_module(__package__ + ".streams").side_stream()
+            side = _streams.side_stream()
             side.wait_stream(cur)
             st = L.load().ot_tsdf_mesh_vertex_normals(vol._h, mc[1], D.ptr(V), nv, D.ptr(T), nt, D.ptr(out),
                                                        C.c_void_p(side.cuda_stream))
