@@ -62,7 +62,7 @@ void* scratch(size_t bytes, int slot) {
 
 static thread_local std::vector<Arena> g_pinned;
 
-void* pinned_scratch(size_t bytes, int slot) {
+void* pinned_scratch(size_t bytes, int slot, bool coherent) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     if ((int)g_pinned.size() <= dev) g_pinned.resize(dev + 1);
@@ -75,7 +75,7 @@ void* pinned_scratch(size_t bytes, int slot) {
         if (a.ptr[slot]) (void)hipHostFree(a.ptr[slot]);  // synchronises the device
         const size_t nb = bytes + bytes / 4 + 256;
         void* p = nullptr;
-        if (hipHostMalloc(&p, nb, hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc(&p, nb, coherent ? hipHostMallocCoherent : hipHostMallocDefault) != hipSuccess) {
             a.ptr[slot] = nullptr;
             a.size[slot] = 0;
             return nullptr;
@@ -87,9 +87,6 @@ void* pinned_scratch(size_t bytes, int slot) {
     return a.ptr[slot];
 }
 
-struct ArgBlob {
-    unsigned long long w[UPLOAD_ARG_BYTES / 8];
-};
 __global__ __launch_bounds__(64) void k_store_blob(ArgBlob b, unsigned long long* dst, int words) {
     for (int i = threadIdx.x; i < words; i += 64) dst[i] = b.w[i];
 }

@@ -33,12 +33,18 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 void* scratch(size_t bytes, int slot);
 // pinned host counterpart (per thread and device, grow-only): small tables uploaded with hipMemcpyAsync without the
 // pageable staging copy; the caller must have synchronised on its previous upload from the slot before rewriting it
-void* pinned_scratch(size_t bytes, int slot);
+// coherent: fine-grained memory a kernel writes results into directly (a slot keeps the kind it was first made with)
+void* pinned_scratch(size_t bytes, int slot, bool coherent = false);
 // a small host table (<= UPLOAD_ARG_BYTES) to device memory in stream order, carried by the kernel arguments of one
 // tiny launch instead of a copy command (measured: a ~1 KB hipMemcpyAsync from pinned memory took ~35 us on one
 // object's critical path beside a running kernel); larger tables take hipMemcpyAsync.  src is consumed on return.
 constexpr size_t UPLOAD_ARG_BYTES = 3072;
 ot_status upload_small(void* dst, const void* src, size_t bytes, hipStream_t stream);
+// the kernel-argument carrier of upload_small (also passed to a caller's own first kernel, which then stores it: one
+// launch fewer on a latency chain)
+struct ArgBlob {
+    unsigned long long w[UPLOAD_ARG_BYTES / 8];
+};
 // device allocations made by the library's grow-only buffers so far (scratch arenas, filter handles): a timed
 // region that allocates shows up as a change (bench.py reports it; test hook otx_alloc_count)
 void note_alloc();

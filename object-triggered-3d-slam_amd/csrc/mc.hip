@@ -427,10 +427,11 @@ __global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t
 
 // the extraction's two exclusive scans (triangle and vertex counts per unit, U of each) in one launch: block 0 scans
 // the triangle counts, block 1 the vertex counts, 4096 per round (4 consecutive per thread) with a carried total --
-// one ~5 us launch instead of a library scan's two launches per array (U is a few thousand units)
+// one ~5 us launch instead of a library scan's two launches per array (U is a few thousand units).  Each block mails
+// its array's total (triangles, vertices) to the volume's pinned mailbox: the host's read-back needs no launch of its own
 __global__ __launch_bounds__(1024) void k_mc_scan2(const long long* __restrict__ c0, long long* __restrict__ b0,
                                                   const long long* __restrict__ c1, long long* __restrict__ b1,
-                                                  int n) {
+                                                  int n, long long* __restrict__ totals) {
     const long long* in = blockIdx.x ? c1 : c0;
     long long* out = blockIdx.x ? b1 : b0;
     __shared__ long long wsum[16];
@@ -469,6 +470,7 @@ __global__ __launch_bounds__(1024) void k_mc_scan2(const long long* __restrict__
         if (t == 0) s_carry += tot;
         __syncthreads();
     }
+    if (t == 0) totals[blockIdx.x] = s_carry;
 }
 
 static std::atomic<bool> g_tables_uploaded{false};
@@ -557,20 +559,11 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
     hipLaunchKernelGGL(k_mc_count, dim3(g), dim3(EWORDS), 0, stream, m);
     OT_LAUNCH_CHECK();
     if (U > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] too many units");
+    // the scans mail the triangle and vertex totals (hmail words 0..3)
     hipLaunchKernelGGL(k_mc_scan2, dim3(2), dim3(1024), 0, stream, (const long long*)m.tri_cnt, m.tri_base,
-                       (const long long*)m.vert_cnt, m.vert_base, (int)U);
+                       (const long long*)m.vert_cnt, m.vert_base, (int)U, (long long*)vol->hmail);
     OT_LAUNCH_CHECK();
-    long long tails[4];  // the scans' last bases and counts: one mailbox read-back
-    MailSrc ms;
-    ms.n = 8;
-    const long long* tp[4] = {m.tri_base + U - 1, m.tri_cnt + U - 1, m.vert_base + U - 1, m.vert_cnt + U - 1};
-    for (int i = 0; i < 4; ++i) {
-        ms.p[2 * i] = (const unsigned*)tp[i];
-        ms.p[2 * i + 1] = (const unsigned*)tp[i] + 1;
-    }
     mb.ws_units = U;
-    st = mail_words_launch(vol, ms, stream);
-    if (st != OT_OK) return st;
     if (spec) {  // the host waits for the read-back only, the speculative work runs behind it
         if (!vol->ev_mail) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_mail, hipEventDisableTiming));
         OT_HIP_TRY(hipEventRecord(vol->ev_mail, stream));
@@ -580,8 +573,9 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
     } else {
         OT_HIP_TRY(hipStreamSynchronize(stream));
     }
-    std::memcpy(tails, vol->hmail, sizeof(tails));
-    const int64_t nt = tails[0] + tails[1], nv = tails[2] + tails[3];
+    long long totals[2];
+    std::memcpy(totals, vol->hmail, sizeof(totals));
+    const int64_t nt = totals[0], nv = totals[1];
     if (nv > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] more than 2^31 vertices");
     st = grow(mb.vk, mb.cap_vk, nv);  // merge keys: 16 B per vertex, 12 B per triangle
     if (st != OT_OK) return st;

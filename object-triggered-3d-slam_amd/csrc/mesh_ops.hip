@@ -11,6 +11,7 @@
 // r1/r2 from a counter-based RNG (splitmix64 of seed + counter; Open3D's mt19937 is unseeded), barycentric
 // a = 1 - sqrt(r1), b = sqrt(r1)(1 - r2), c = sqrt(r1) r2.
 #include <atomic>
+#include <cstring>
 #include <functional>
 #include <vector>
 
@@ -70,10 +71,8 @@ __global__ __launch_bounds__(256) void k_vertex_normals(const unsigned long long
 }
 
 // ------------------------------------------------------------------------------------------- sampling
-__global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V, const int32_t* __restrict__ T,
-                                                   int64_t nt, double* __restrict__ area) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= nt) return;
+// TriangleMesh::GetTriangleArea: 0.5 * |(p0 - p1) x (p0 - p2)|, Open3D's expression order
+__device__ inline double tri_area(const double* __restrict__ V, const int32_t* __restrict__ T, int64_t t) {
     const double* p0 = V + (int64_t)T[t * 3] * 3;
     const double* p1 = V + (int64_t)T[t * 3 + 1] * 3;
     const double* p2 = V + (int64_t)T[t * 3 + 2] * 3;
@@ -86,7 +85,28 @@ __global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V,
     const double c0 = x[1] * y[2] - x[2] * y[1];
     const double c1 = x[2] * y[0] - x[0] * y[2];
     const double c2 = x[0] * y[1] - x[1] * y[0];
-    area[t] = 0.5 * sqrt((c0 * c0 + c1 * c1) + c2 * c2);
+    return 0.5 * sqrt((c0 * c0 + c1 * c1) + c2 * c2);
+}
+__global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V, const int32_t* __restrict__ T,
+                                                   int64_t nt, double* __restrict__ area) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nt) return;
+    area[t] = tri_area(V, T, t);
+}
+// k_tri_areas that also lands the sampler's uploaded tables (blob words -> dst) and zeroes its look-back words
+// (zwords at zero) from block 0: the chains' table upload and the status memset ride on the first kernel of the chain
+// instead of two launches of their own (~5 us each on one object's latency chain)
+__global__ __launch_bounds__(256) void k_tri_areas_blob(const double* __restrict__ V, const int32_t* __restrict__ T,
+                                                        int64_t nt, double* __restrict__ area, ArgBlob b,
+                                                        unsigned long long* __restrict__ dst, int words,
+                                                        unsigned long long* __restrict__ zero, int zwords) {
+    if (blockIdx.x == 0) {
+        for (int i = threadIdx.x; i < words; i += 256) dst[i] = b.w[i];
+        for (int i = threadIdx.x; i < zwords; i += 256) zero[i] = 0ull;
+    }
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nt) return;
+    area[t] = tri_area(V, T, t);
 }
 
 // Open3D's sequential recurrences (GetSurfaceArea: s = (((a0 + a1) + a2) + ...), then the CDF loop
@@ -254,33 +274,18 @@ __global__ __launch_bounds__(256) void k_chain_cdf_prep(const ChainJob* __restri
     }
 }
 
-// One chunk from the exact s in Open3D's order, by integer segments: inside the binade of s every element that is
+// One chunk from the exact s in Open3D's order, by integer stretches: inside the binade of s every element that is
 // not a tie, stays below 2^53 grid steps and keeps the running integer below 2^53 is one step of an integer prefix
 // sum (the whole wave at once); the first element that breaks this is added by one exact float64 add (s + a) and the
-// next segment starts after it.  A chunk costs one wave prefix per binade crossing / tie / special value instead of
-// 256 dependent adds.  CDF values are stored as they are produced.  The segment is a single wave's latency chain, so
-// its cross-lane steps avoid LDS: the prefix is a DPP scan inside rows of 16 plus the row totals read by readlane,
-// the first bad / crossing element is found by a ballot and one readlane, and broadcasts are readlanes.
+// next stretch starts after it.  A chunk costs a few wave prefixes instead of 256 dependent adds.  CDF values are
+// stored as they are produced.  The walk is a single wave's latency chain, so its cross-lane steps avoid LDS: the
+// prefix is a DPP scan inside rows of 16 plus the row totals read by readlane, the first bad / crossing element is
+// found by a ballot and one readlane, and broadcasts are readlanes.
 __device__ inline long long readlane64(long long v, int l) {
     const int lo = __builtin_amdgcn_readlane((int)v, l), hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
     return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 __device__ inline double readlane_f64(double v, int l) { return __longlong_as_double(readlane64(__double_as_longlong(v), l)); }
-template <int CTRL>
-__device__ inline long long dpp_row_shr64(long long v) {  // lanes without a source in their row of 16 read 0
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, true);
-    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-__device__ inline long long wave_incl_scan_i64(long long v, int lane) {
-    v += dpp_row_shr64<0x111>(v);  // row_shr:1
-    v += dpp_row_shr64<0x112>(v);  // row_shr:2
-    v += dpp_row_shr64<0x114>(v);  // row_shr:4
-    v += dpp_row_shr64<0x118>(v);  // row_shr:8 -> inclusive scan inside each row of 16
-    const long long r0 = readlane64(v, 15), r1 = readlane64(v, 31), r2 = readlane64(v, 47);
-    const int row = lane >> 4;
-    return v + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
-}
 // the smallest per-lane index (CH when no lane has one): lanes hold ascending index ranges, so it is the value of the
 // first lane that has one
 __device__ inline int wave_first_idx(int idx) {
@@ -309,6 +314,22 @@ __device__ inline double wave_incl_scan_f64(double v, int lane) {
     return v + ((row >= 1 ? r0 : 0.0) + ((row >= 2 ? r1 : 0.0) + (row >= 3 ? r2 : 0.0)));
 }
 
+// the value a[idx & 3] of lane idx >> 2 (wave-uniform idx), broadcast
+__device__ inline double lane_elem(const double* a, int idx) {
+    const double mine = (idx & 3) == 0 ? a[0] : (idx & 3) == 1 ? a[1] : (idx & 3) == 2 ? a[2] : a[3];
+    return readlane_f64(mine, idx >> 2);
+}
+
+// One pass computes the grid counts and their wave prefixes in TWO grids at once, the binade e of s and the next one
+// (independent scans: they overlap on the latency chain), then resolves the chunk from them: a stretch of integer steps
+// in the current grid, the one exact float64 add that ends it (a binade crossing, a tie, a special value), and the next
+// stretch in the same grid or, after a crossing, in grid e + 1 -- from the prefixes already computed (the limit moves by
+// the prefix before the stretch instead of the prefix restarting).  A chunk's usual crossing thus costs one ballot
+// pair instead of a second pass; a new pass starts only when s leaves binades e and e + 1.
+// Exactness: every prefix compared is against a limit lim = 2^53 - 1 - N + Pq < 2^53 (N >= 2^52, and a stretch starts
+// from a prefix Pq < 2^52 only, else a new pass), so "prefix > lim" is decided exactly even where a prefix past the
+// binade's end rounds (a tree sum of non-negative integers is exact up to 2^53 and >= 2^53 beyond); accepted prefixes
+// are <= lim, so N + (P - Pq) and the stored values are exact.
 template <bool CDF>
 __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, const double v[4], int lane,
                                             int& ti) {
@@ -326,57 +347,94 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
     };
     while (pos < cnt) {  // wave-uniform
         mark(5, pos);
-        const int e = binade(s);
-        int stop = pos;
-        if (e != EX_NONE) {
-            const double scale = pow2(52 - e), u = pow2(e - 52);
-            const double N = s * scale;                    // exact integer in [2^52, 2^53)
-            const double T = (double)(R_MAX - 1) - N;      // exact: the largest prefix that stays in the binade
-            double incl[4], loc = 0.0;
-            int bad = CH;  // first element of this lane the integer step cannot take
+        const int e0 = binade(s);
+        if (e0 == EX_NONE) {  // s == 0 (the chain's start), special or out of range: one exact add in Open3D's order
+            s = lane_elem(v, pos) + s;
+            if (CDF && lane == 0) j.out[base + pos] = s;
+            ++pos;
+            continue;
+        }
+        // grid counts from pos on: P0 in binade e0 (grid u0 = 2^(e0-52)), P1 in binade e0 + 1; okm: per-lane bits of the
+        // elements the integer step can take in each grid
+        double P0[4], P1[4];
+        unsigned ok0 = 0u, ok1 = 0u;
+        {
+            const double sc0 = pow2(52 - e0), sc1 = pow2(51 - e0);
+            double l0 = 0.0, l1 = 0.0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int idx = 4 * lane + k;
-                const double m = v[k] * scale;  // exact: power-of-two scaling
-                const double r = rint(m);
-                const bool ok = m >= 0.0 && m < (double)R_MAX && fabs(m - r) != 0.5;
                 const bool act = idx >= pos && idx < cnt;
-                loc += (act && ok) ? r : 0.0;
-                incl[k] = loc;
-                if (act && !ok && bad == CH) bad = idx;
-                if (idx >= cnt && bad == CH) bad = idx;
+                const double m0 = v[k] * sc0, m1 = v[k] * sc1;  // exact: power-of-two scalings
+                const double r0 = rint(m0), r1 = rint(m1);
+                const bool g0 = m0 >= 0.0 && m0 < (double)R_MAX && fabs(m0 - r0) != 0.5;
+                const bool g1 = m1 >= 0.0 && m1 < (double)R_MAX && fabs(m1 - r1) != 0.5;
+                l0 += (act && g0) ? r0 : 0.0;
+                l1 += (act && g1) ? r1 : 0.0;
+                P0[k] = l0;
+                P1[k] = l1;
+                ok0 |= g0 ? 1u << k : 0u;
+                ok1 |= g1 ? 1u << k : 0u;
             }
-            const double excl = wave_incl_scan_f64(loc, lane) - loc;  // exact where it matters (see above)
+            const double x0 = wave_incl_scan_f64(l0, lane) - l0, x1 = wave_incl_scan_f64(l1, lane) - l1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                P0[k] += x0;
+                P1[k] += x1;
+            }
+        }
+        mark(6, pos);
+        int g = 0, q = pos;
+        double Pq = 0.0;  // grid g's prefix before q
+        while (true) {    // wave-uniform: stretches from the prefixes above
+            const double N = s * pow2(52 - e0 - g), u = pow2(e0 + g - 52);  // N: exact integer in [2^52, 2^53)
+            const double lim = ((double)(R_MAX - 1) - N) + Pq;              // exact, < 2^53
+            const unsigned okm = g ? ok1 : ok0;
+            double P[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) P[k] = g ? P1[k] : P0[k];
+            int bad = CH;  // first element from q on that the integer step cannot take (cnt: the chunk's end)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int idx = 4 * lane + k;
+                if (idx >= q && (idx >= cnt || !((okm >> k) & 1u)) && bad == CH) bad = idx;
+            }
             const int first_bad = wave_first_idx(bad);
             int cross = CH;  // first element whose running integer leaves the binade
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                incl[k] += excl;
                 const int idx = 4 * lane + k;
-                if (idx >= pos && idx < first_bad && incl[k] > T && cross == CH) cross = idx;
+                if (idx >= q && idx < first_bad && P[k] > lim && cross == CH) cross = idx;
             }
             const int first_cross = wave_first_idx(cross);
-            mark(6, pos);
-            stop = first_bad < first_cross ? first_bad : first_cross;
+            mark(7, q);
+            int stop = first_bad < first_cross ? first_bad : first_cross;
             stop = stop < cnt ? stop : cnt;
-            if (stop > pos) {
+            if (stop > q) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int idx = 4 * lane + k;
-                    if (CDF && idx >= pos && idx < stop) j.out[base + idx] = (N + incl[k]) * u;
+                    if (CDF && idx >= q && idx < stop) j.out[base + idx] = (N + (P[k] - Pq)) * u;
                 }
-                const int last = stop - 1;
-                const double mine = (last & 3) == 0 ? incl[0] : (last & 3) == 1 ? incl[1] : (last & 3) == 2 ? incl[2] : incl[3];
-                s = (N + readlane_f64(mine, last >> 2)) * u;
+                s = (N + (lane_elem(P, stop - 1) - Pq)) * u;
             }
+            if (stop < cnt) {  // one exact float64 add, in Open3D's order
+                s = lane_elem(v, stop) + s;
+                if (CDF && lane == 0) j.out[base + stop] = s;
+                ++stop;
+            }
+            q = stop;
+            if (q >= cnt) break;
+            const int e1 = binade(s);
+            if (e1 == e0 + 1 && g == 0) g = 1;
+            else if (e1 != e0 + g) break;  // s left binades e0 and e0 + 1 (or is special): a new pass from q
+            double Q[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Q[k] = g ? P1[k] : P0[k];
+            Pq = lane_elem(Q, q - 1);
+            if (!(Pq < (double)(R_MAX >> 1))) break;  // (a huge crossing element) the limit would pass 2^53: new pass
         }
-        if (stop < cnt) {  // one exact float64 add, in Open3D's order
-            const double mine = (stop & 3) == 0 ? v[0] : (stop & 3) == 1 ? v[1] : (stop & 3) == 2 ? v[2] : v[3];
-            s = readlane_f64(mine, stop >> 2) + s;
-            if (CDF && lane == 0) j.out[base + stop] = s;
-            ++stop;
-        }
-        pos = stop;
+        pos = q;
     }
     return s;
 }
@@ -956,8 +1014,9 @@ static ot_status hi_stream_fork(hipStream_t caller, hipStream_t* out) {
 // chain table in one copy: fill(host, dev) writes them once the layout is known.  cdf[j]: the job's CDF (device);
 // ncum[j]: room for its rounded counts; *extra_dev: the caller's device region.
 static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, size_t extra, size_t upload,
-                             const std::function<void(char*, char*)>& fill, hipStream_t stream,
-                             std::vector<double*>& cdf, std::vector<long long*>& ncum, char** extra_dev) {
+                             const std::function<void(char*, char*)>& fill, size_t zero_off, size_t zero_bytes,
+                             hipStream_t stream, std::vector<double*>& cdf, std::vector<long long*>& ncum,
+                             char** extra_dev) {
     size_t bytes = 256;
     int64_t max_nt = 0;
     for (int j = 0; j < n_jobs; ++j) {
@@ -996,14 +1055,32 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
         cc.x = qs[j], cc.out = cdf[j];  // the CDF overwrites the areas once q = a / s is formed
         chain[j] = cs;
         chain[n_jobs + j] = cc;
-        hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, jobs[j].vertices,
-                           jobs[j].triangles, nt, cdf[j]);
     }
     ChainJob* djobs = (ChainJob*)(((uintptr_t)cur + 63) & ~(uintptr_t)63);
     *extra_dev = (char*)djobs + table;
     if (upload) fill(up + table, *extra_dev);
-    ot_status ust = upload_small(djobs, up, table + upload, stream);
-    if (ust != OT_OK) return ust;
+    // the tables (and the caller's zeroed words) land from the first areas launch when they fit its arguments
+    const size_t blob_bytes = table + upload;
+    const bool blob = blob_bytes <= UPLOAD_ARG_BYTES && (zero_off & 7) == 0 && (zero_bytes & 7) == 0;
+    if (!blob) {
+        ot_status ust = upload_small(djobs, up, blob_bytes, stream);
+        if (ust != OT_OK) return ust;
+        if (zero_bytes) OT_HIP_TRY(hipMemsetAsync(*extra_dev + zero_off, 0, zero_bytes, stream));
+    }
+    for (int j = 0; j < n_jobs; ++j) {
+        const int64_t nt = jobs[j].n_triangles;
+        const dim3 grid((unsigned)((nt + 255) / 256));
+        if (blob && j == 0) {
+            ArgBlob b;
+            std::memcpy(b.w, up, blob_bytes);
+            hipLaunchKernelGGL(k_tri_areas_blob, grid, dim3(256), 0, stream, jobs[j].vertices, jobs[j].triangles, nt,
+                               cdf[j], b, (unsigned long long*)djobs, (int)((blob_bytes + 7) / 8),
+                               (unsigned long long*)(*extra_dev + zero_off), (int)(zero_bytes / 8));
+        } else {
+            hipLaunchKernelGGL(k_tri_areas, grid, dim3(256), 0, stream, jobs[j].vertices, jobs[j].triangles, nt,
+                               cdf[j]);
+        }
+    }
     launch_chains<false>(djobs, n_jobs, max_nt, stream);
     const int64_t max_nb = (max_nt + CH - 1) / CH;
     hipLaunchKernelGGL(k_chain_cdf_prep, dim3((unsigned)((max_nb + 3) / 4), (unsigned)n_jobs), dim3(256), 0, stream,
@@ -1025,7 +1102,7 @@ ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs, 
     std::vector<double*> cdf;
     std::vector<long long*> ncum;
     char* extra = nullptr;
-    ot_status st = sample_cdfs(jobs, n_jobs, 0, 0, nullptr, stream, cdf, ncum, &extra);
+    ot_status st = sample_cdfs(jobs, n_jobs, 0, 0, nullptr, 0, 0, stream, cdf, ncum, &extra);
     if (st != OT_OK) return st;
     // the vertex normals / colours the emission interpolates may still be in flight on another stream (the facade
     // computes the normals of a fresh mesh beside the area chains above, which read only V and T)
@@ -1058,7 +1135,7 @@ ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_
     const int64_t tiles64 = (n_points + MZ_TILE - 1) / MZ_TILE;
     if (tiles64 > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many points");
     const int tiles = (int)tiles64;
-    // caller region: [MinZJob x n | cdf ptrs | ncum ptrs] (uploaded) | align 64 | kept i64 [n] | ticket i32 [n] |
+    // caller region: [MinZJob x n | cdf ptrs | ncum ptrs] (uploaded) | align 64 | i64 [n] (spare) | ticket i32 [n] |
     // align 64 | status u64 [n][tiles] (zeroed)
     const size_t up_bytes = (sizeof(MinZJob) + 16) * (size_t)n_jobs;
     const size_t zero_off = (up_bytes + 63) & ~(size_t)63;
@@ -1079,15 +1156,17 @@ ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_
             np[j] = ncum[j];
         }
     };
-    ot_status st = sample_cdfs(jobs, n_jobs, total, up_bytes, fill, stream, cdf, ncum, &extra);
+    // the kept counts land in pinned host memory, written by each job's last tile (no read-back copy)
+    long long* kept = (long long*)pinned_scratch(sizeof(long long) * (size_t)n_jobs, 1, true);
+    if (!kept) return fail(OT_ERR_HIP, "pinned allocation failed");
+    ot_status st = sample_cdfs(jobs, n_jobs, total, up_bytes, fill, zero_off, total - zero_off, stream, cdf, ncum,
+                               &extra);
     if (st != OT_OK) return st;
     const MinZJob* djobs = (const MinZJob*)extra;
     const double* const* dcdf = (const double* const*)(djobs + n_jobs);
     long long* const* dncum = (long long* const*)(dcdf + n_jobs);
-    long long* kept = (long long*)(extra + zero_off);
-    int* ticket = (int*)(kept + n_jobs);
+    int* ticket = (int*)(extra + zero_off + 8 * (size_t)n_jobs);
     unsigned long long* status = (unsigned long long*)(extra + status_off);
-    OT_HIP_TRY(hipMemsetAsync(extra + zero_off, 0, total - zero_off, stream));
     int64_t max_nt = 0;
     for (int j = 0; j < n_jobs; ++j) max_nt = jobs[j].n_triangles > max_nt ? jobs[j].n_triangles : max_nt;
     hipLaunchKernelGGL(k_round_counts_jobs, dim3((unsigned)((max_nt + 255) / 256), n_jobs), dim3(256), 0, stream, djobs,
@@ -1095,10 +1174,8 @@ ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_
     hipLaunchKernelGGL(k_sample_min_z, dim3(tiles, n_jobs), dim3(256), 0, stream, djobs, n_points,
                        (unsigned long long)seed, z_min, tiles, status, ticket, kept);
     OT_LAUNCH_CHECK();
-    std::vector<long long> hk(n_jobs);
-    OT_HIP_TRY(hipMemcpyAsync(hk.data(), kept, sizeof(long long) * n_jobs, hipMemcpyDeviceToHost, stream));
     OT_HIP_TRY(hipStreamSynchronize(stream));  // the kept counts, and the host job table is released on return
-    for (int j = 0; j < n_jobs; ++j) n_kept_host[j] = hk[j];
+    for (int j = 0; j < n_jobs; ++j) n_kept_host[j] = kept[j];
     return OT_OK;
 }
 

@@ -221,7 +221,6 @@ struct MailSrc {
     const unsigned* p[ot::OT_MAIL_WORDS];
     int n;
 };
-ot_status mail_words_launch(ot_tsdf* vol, const MailSrc& s, hipStream_t stream);  // no synchronisation
 ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream);
 ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream);
 }  // namespace ot

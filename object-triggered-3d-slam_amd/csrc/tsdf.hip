@@ -1102,6 +1102,62 @@ __global__ void k_pack_unit_keys(TsdfDev d, int n, UnitKeyPack pk, unsigned long
     ids[i] = (unsigned)i;
 }
 
+// Unit order in ONE launch when the packed keys need <= USORT_BITS bits (a volume a few metres across): unit keys are
+// distinct (one id per hash slot), so a unit's place in key order is the number of smaller keys -- a presence bitmap
+// of the key space in LDS, a block scan of its popcounts per 8-word group, then per unit the group prefix plus the
+// popcounts before its bit.  The same ids as the radix sort (k_pack_unit_keys + 4 launches of sort_pairs_u64_u32),
+// whose launches dominated the unit sort of a single object (38 us for 5.6k units, profiles/r04z_obj_timeline.txt).
+constexpr int USORT_BITS = 20;                   // 2^20-bit bitmap: 128 KiB of LDS
+constexpr int USORT_WORDS = 1 << (USORT_BITS - 5);
+constexpr int USORT_GROUPS = USORT_WORDS / 8;    // 4096 group prefixes: 16 KiB
+__device__ inline unsigned unit_key_bits(const TsdfDev& d, const UnitKeyPack& pk, int i) {
+    return ((unsigned)(d.unit_keys[i * 3 + 0] - pk.x0) << pk.sx) | ((unsigned)(d.unit_keys[i * 3 + 1] - pk.y0) << pk.sy) |
+           (unsigned)(d.unit_keys[i * 3 + 2] - pk.z0);
+}
+__global__ __launch_bounds__(1024) void k_unit_rank_sort(TsdfDev d, int n, UnitKeyPack pk, int kb,
+                                                         unsigned* __restrict__ sorted_ids) {
+    __shared__ unsigned s_bits[USORT_WORDS];
+    __shared__ unsigned s_gp[USORT_GROUPS];
+    __shared__ unsigned s_w[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int words = kb > 5 ? 1 << (kb - 5) : 1, groups = (words + 7) >> 3;
+    for (int q = t; q < words; q += 1024) s_bits[q] = 0u;
+    __syncthreads();
+    for (int i = t; i < n; i += 1024) {
+        const unsigned k = unit_key_bits(d, pk, i);
+        atomicOr(&s_bits[k >> 5], 1u << (k & 31));
+    }
+    __syncthreads();
+    // thread t: groups [g0, g1), a contiguous stretch (4 groups = 32 words at 20 bits)
+    const int per = (groups + 1023) >> 10, g0 = t * per, g1 = g0 + per < groups ? g0 + per : groups;
+    unsigned loc = 0u;
+    for (int g = g0; g < g1; ++g)
+        for (int q = g * 8; q < g * 8 + 8 && q < words; ++q) loc += __popc(s_bits[q]);
+    unsigned inc = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned v = __shfl_up(inc, o);
+        if (lane >= o) inc += v;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    unsigned run = inc - loc;
+    for (int q = 0; q < w; ++q) run += s_w[q];
+    for (int g = g0; g < g1; ++g) {
+        s_gp[g] = run;
+        for (int q = g * 8; q < g * 8 + 8 && q < words; ++q) run += __popc(s_bits[q]);
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += 1024) {
+        const unsigned k = unit_key_bits(d, pk, i);
+        const int q = (int)(k >> 5);
+        unsigned r = s_gp[q >> 3] + __popc(s_bits[q] & ((1u << (k & 31)) - 1u));
+        for (int p = q & ~7; p < q; ++p) r += __popc(s_bits[p]);
+        sorted_ids[r] = (unsigned)i;
+    }
+}
+static bool g_unit_sort_radix = false;  // test hook otx_unit_sort_radix: force the radix path (parity of the two)
+
 // ------------------------------------------------------------------------------------ host helpers
 static IntegrateParams make_integrate_params(const ot_tsdf* vol, const float* depth, const uint8_t* color,
                                              const float* mult, const ot_intrinsics* in, const double* ext) {
@@ -1390,16 +1446,10 @@ __global__ void k_mail_words(MailSrc s, unsigned* __restrict__ out) {
     if (i < s.n) out[i] = *s.p[i];
 }
 
-ot_status mail_words_launch(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
+ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
     if (s.n > OT_MAIL_WORDS) return fail(OT_ERR_INVALID_ARGUMENT, "mailbox overflow");
     hipLaunchKernelGGL(k_mail_words, dim3(1), dim3(64), 0, stream, s, vol->hmail);
     OT_LAUNCH_CHECK();
-    return OT_OK;
-}
-
-ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
-    ot_status st = mail_words_launch(vol, s, stream);
-    if (st != OT_OK) return st;
     OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
 }
@@ -1436,11 +1486,6 @@ ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) 
     *n_units = nu;
     if (vol->sorted_frame == vol->frame_id && vol->sorted_units == nu) return OT_OK;
     if (nu > 0) {
-        char* ws = (char*)scratch((size_t)nu * 24 + 256, 5);
-        if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
-        unsigned long long* kin = (unsigned long long*)(ws + 256);
-        unsigned long long* kout = kin + nu;
-        unsigned* vin = (unsigned*)(kout + nu);
         int hb[6];  // per-axis key bounds, kept by the allocating kernels (note_unit_key)
         for (int a = 0; a < 3; ++a) {
             hb[a] = KEY_BIAS + 1 - c[C_KNEG + a];
@@ -1453,6 +1498,19 @@ ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) 
             while (bits[a] < 31 && (span >> bits[a]) != 0) ++bits[a];
         }
         const UnitKeyPack pk{hb[0], hb[1], hb[2], bits[2], bits[1] + bits[2]};
+        const int kb = bits[0] + bits[1] + bits[2];
+        if (kb <= USORT_BITS && !g_unit_sort_radix) {
+            hipLaunchKernelGGL(k_unit_rank_sort, dim3(1), dim3(1024), 0, stream, vol->dev, nu, pk, kb, vol->sorted_ids);
+            OT_LAUNCH_CHECK();
+            vol->sorted_units = nu;
+            vol->sorted_frame = vol->frame_id;
+            return OT_OK;
+        }
+        char* ws = (char*)scratch((size_t)nu * 24 + 256, 5);
+        if (!ws) return fail(OT_ERR_HIP, "scratch allocation failed");
+        unsigned long long* kin = (unsigned long long*)(ws + 256);
+        unsigned long long* kout = kin + nu;
+        unsigned* vin = (unsigned*)(kout + nu);
         hipLaunchKernelGGL(k_pack_unit_keys, dim3((nu + 255) / 256), dim3(256), 0, stream, vol->dev, nu, pk, kin, vin);
         OT_LAUNCH_CHECK();
         st = sort_pairs_u64_u32(kin, kout, vin, vol->sorted_ids, (size_t)nu, std::min(63, bits[0] + bits[1] + bits[2]),
@@ -1834,6 +1892,12 @@ ot_status otx_tsdf_stats(ot_tsdf* vol, uint64_t* out4) {
     ot_status st = tsdf_flush(vol, nullptr);
     if (st != OT_OK) return st;
     OT_HIP_TRY(hipMemcpy(out4, vol->dev.stats, sizeof(uint64_t) * 4, hipMemcpyDeviceToHost));
+    return OT_OK;
+}
+
+// test hook: 1 = sort units with the radix sort at every key width (the rank sort's parity test), 0 = default
+ot_status otx_unit_sort_radix(int32_t on) {
+    g_unit_sort_radix = on != 0;
     return OT_OK;
 }
 

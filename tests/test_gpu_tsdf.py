@@ -130,6 +130,27 @@ def _compare_volumes(vol, ref):
     return keys.shape[0]
 
 
+def test_unit_order_rank_sort_matches_radix(pkg, O, gpu, synth, seq16):
+    """Unit order: the one-launch rank sort (unit keys packed in <= 20 bits, every volume here) and the radix sort it
+    replaces give the same order -- both volumes export the oracle's sorted unit keys and the same mesh, bit for bit."""
+    L = pkg._lib
+    depth, color, ext = seq16
+    out = []
+    for radix in (1, 0):
+        L.call("otx_unit_sort_radix", radix)
+        try:
+            vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005)
+            assert _compare_volumes(vol, ref) > 300
+            m = vol.extract_triangle_mesh()
+            out.append((np.asarray(m.vertices).copy(), np.asarray(m.vertex_colors).copy(),
+                        np.asarray(m.triangles).copy()))
+        finally:
+            L.call("otx_unit_sort_radix", 0)
+    for a, b, what in zip(out[0], out[1], ("vertices", "vertex colours", "triangles")):
+        assert a.shape[0] > 1000
+        assert_bitwise(b, a, what + " (rank sort vs radix sort)")
+
+
 @pytest.mark.parametrize("voxel", [0.01, 0.005])
 @pytest.mark.parametrize("batch", [1, 3, None])
 def test_tsdf_integrate_bitexact(pkg, O, gpu, synth, seq16, voxel, batch):

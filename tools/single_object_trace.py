@@ -4,6 +4,8 @@ the last repetition (durations and the idle gaps between kernels).  Tool only.
 
   rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 tools/single_object_trace.py
   python3 tools/single_object_trace.py --report DIR/run_kernel_trace.csv
+  python3 tools/single_object_trace.py --no-normals   (diagnostic: the same object without compute_vertex_normals, i.e.
+                                                       what the normals' side-stream kernel costs the critical path)
 """
 import csv
 import ctypes as C
@@ -46,7 +48,7 @@ def report(path):
         print(f"{v:9.1f} us  {k}")
 
 
-def main():
+def main(normals=True):
     synth = importlib.import_module(PKG + ".synth")
     depth, color, ext = synth.make_sequence(synth.object_scene(0), n_frames=64)
     import torch
@@ -70,7 +72,8 @@ def main():
         vol.reset()
         lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
         mesh = vol.extract_triangle_mesh()
-        mesh.compute_vertex_normals()
+        if normals:
+            mesh.compute_vertex_normals()
         return mesh.sample_points_min_z(100000, 0.03)
 
     ts = []
@@ -81,7 +84,7 @@ def main():
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t) * 1e3)
     print("stream priority range (least, greatest):", torch.cuda.Stream.priority_range())
-    print("single object ms (median of last 5):", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
+    print("single object ms (median of last 5)" + ("" if normals else ", WITHOUT normals") + ":", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
     # the volume's size against configs[1]'s (integrate occupancy): units, voxel updates, unit integrations
     vol.reset()
     lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
@@ -96,4 +99,4 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--report":
         report(sys.argv[2])
     else:
-        main()
+        main(normals="--no-normals" not in sys.argv)
