@@ -83,6 +83,26 @@ def main(normals=True):
         one()
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t) * 1e3)
+    # host side of the same call sequence: when each call returns (no synchronisation in between), medians over 5
+    marks = []
+    for _ in range(6):
+        torch.cuda.synchronize()
+        t = [time.perf_counter()]
+        vol.reset()
+        lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
+        t.append(time.perf_counter())
+        mesh = vol.extract_triangle_mesh()
+        t.append(time.perf_counter())
+        if normals:
+            mesh.compute_vertex_normals()
+        t.append(time.perf_counter())
+        mesh.sample_points_min_z(100000, 0.03)
+        t.append(time.perf_counter())
+        torch.cuda.synchronize()
+        t.append(time.perf_counter())
+        marks.append(np.diff(np.array(t)) * 1e6)
+    med = np.median(np.array(marks[1:]), axis=0)
+    print("host us per call (integrate, extract, normals, sample, final sync):", [round(float(x), 1) for x in med])
     print("stream priority range (least, greatest):", torch.cuda.Stream.priority_range())
     print("single object ms (median of last 5)" + ("" if normals else ", WITHOUT normals") + ":", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
     # the volume's size against configs[1]'s (integrate occupancy): units, voxel updates, unit integrations
