@@ -355,6 +355,12 @@ ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs_h
  * [n_jobs], the kept row count of each job.  Synchronises the stream. */
 ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs_host, int32_t n_jobs, int64_t n_points,
                                       uint64_t seed, double z_min, int64_t* n_kept_host, void* stream);
+/* The same in two calls: _async queues the sampling and returns without synchronising (the output arrays must stay
+ * allocated), _wait synchronises it and fills n_kept_host.  Between them the calling thread may queue other work (the
+ * facade queues a fresh mesh's deferred vertex normals there, beside the sampling's walks) but no other sampling. */
+ot_status ot_mesh_sample_points_min_z_async(const ot_mesh_sample_job* jobs_host, int32_t n_jobs, int64_t n_points,
+                                            uint64_t seed, double z_min, void* stream);
+ot_status ot_mesh_sample_points_min_z_wait(int32_t n_jobs, int64_t* n_kept_host);
 
 /* ---------------------------------------------------------------------------------------------------
  * Hybrid map — fusion/hybrid_map.py

@@ -274,13 +274,16 @@ __global__ __launch_bounds__(256) void k_chain_cdf_prep(const ChainJob* __restri
     }
 }
 
-// One chunk from the exact s in Open3D's order, by integer stretches: inside the binade of s every element that is
+// One chunk from the exact s in Open3D's order, by integer segments: inside the binade of s every element that is
 // not a tie, stays below 2^53 grid steps and keeps the running integer below 2^53 is one step of an integer prefix
 // sum (the whole wave at once); the first element that breaks this is added by one exact float64 add (s + a) and the
-// next stretch starts after it.  A chunk costs a few wave prefixes instead of 256 dependent adds.  CDF values are
-// stored as they are produced.  The walk is a single wave's latency chain, so its cross-lane steps avoid LDS: the
-// prefix is a DPP scan inside rows of 16 plus the row totals read by readlane, the first bad / crossing element is
-// found by a ballot and one readlane, and broadcasts are readlanes.
+// next segment starts after it.  A chunk costs one wave prefix per binade crossing / tie / special value instead of
+// 256 dependent adds.  CDF values are stored as they are produced.  The segment is a single wave's latency chain, so
+// its cross-lane steps avoid LDS: the prefix is a DPP scan inside rows of 16 plus the row totals read by readlane,
+// the first bad / crossing element is found by a ballot and one readlane, and broadcasts are readlanes.
+// (Round 4, measured and reverted: scanning the binade of s and the next one in one pass and resolving a crossing's
+// second segment from the precomputed prefixes made the walks 57.6 / 77.6 -> 70.7 / 96.4 us per configs[3] mesh: a
+// segment's cost is its dependent ballot / readlane chain, which the second grid does not remove, not its scan.)
 __device__ inline long long readlane64(long long v, int l) {
     const int lo = __builtin_amdgcn_readlane((int)v, l), hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
     return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
@@ -314,22 +317,6 @@ __device__ inline double wave_incl_scan_f64(double v, int lane) {
     return v + ((row >= 1 ? r0 : 0.0) + ((row >= 2 ? r1 : 0.0) + (row >= 3 ? r2 : 0.0)));
 }
 
-// the value a[idx & 3] of lane idx >> 2 (wave-uniform idx), broadcast
-__device__ inline double lane_elem(const double* a, int idx) {
-    const double mine = (idx & 3) == 0 ? a[0] : (idx & 3) == 1 ? a[1] : (idx & 3) == 2 ? a[2] : a[3];
-    return readlane_f64(mine, idx >> 2);
-}
-
-// One pass computes the grid counts and their wave prefixes in TWO grids at once, the binade e of s and the next one
-// (independent scans: they overlap on the latency chain), then resolves the chunk from them: a stretch of integer steps
-// in the current grid, the one exact float64 add that ends it (a binade crossing, a tie, a special value), and the next
-// stretch in the same grid or, after a crossing, in grid e + 1 -- from the prefixes already computed (the limit moves by
-// the prefix before the stretch instead of the prefix restarting).  A chunk's usual crossing thus costs one ballot
-// pair instead of a second pass; a new pass starts only when s leaves binades e and e + 1.
-// Exactness: every prefix compared is against a limit lim = 2^53 - 1 - N + Pq < 2^53 (N >= 2^52, and a stretch starts
-// from a prefix Pq < 2^52 only, else a new pass), so "prefix > lim" is decided exactly even where a prefix past the
-// binade's end rounds (a tree sum of non-negative integers is exact up to 2^53 and >= 2^53 beyond); accepted prefixes
-// are <= lim, so N + (P - Pq) and the stored values are exact.
 template <bool CDF>
 __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double s, const double v[4], int lane,
                                             int& ti) {
@@ -347,94 +334,57 @@ __device__ inline double chain_serial_chunk(const ChainJob& j, int64_t b, double
     };
     while (pos < cnt) {  // wave-uniform
         mark(5, pos);
-        const int e0 = binade(s);
-        if (e0 == EX_NONE) {  // s == 0 (the chain's start), special or out of range: one exact add in Open3D's order
-            s = lane_elem(v, pos) + s;
-            if (CDF && lane == 0) j.out[base + pos] = s;
-            ++pos;
-            continue;
-        }
-        // grid counts from pos on: P0 in binade e0 (grid u0 = 2^(e0-52)), P1 in binade e0 + 1; okm: per-lane bits of the
-        // elements the integer step can take in each grid
-        double P0[4], P1[4];
-        unsigned ok0 = 0u, ok1 = 0u;
-        {
-            const double sc0 = pow2(52 - e0), sc1 = pow2(51 - e0);
-            double l0 = 0.0, l1 = 0.0;
+        const int e = binade(s);
+        int stop = pos;
+        if (e != EX_NONE) {
+            const double scale = pow2(52 - e), u = pow2(e - 52);
+            const double N = s * scale;                    // exact integer in [2^52, 2^53)
+            const double T = (double)(R_MAX - 1) - N;      // exact: the largest prefix that stays in the binade
+            double incl[4], loc = 0.0;
+            int bad = CH;  // first element of this lane the integer step cannot take
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int idx = 4 * lane + k;
+                const double m = v[k] * scale;  // exact: power-of-two scaling
+                const double r = rint(m);
+                const bool ok = m >= 0.0 && m < (double)R_MAX && fabs(m - r) != 0.5;
                 const bool act = idx >= pos && idx < cnt;
-                const double m0 = v[k] * sc0, m1 = v[k] * sc1;  // exact: power-of-two scalings
-                const double r0 = rint(m0), r1 = rint(m1);
-                const bool g0 = m0 >= 0.0 && m0 < (double)R_MAX && fabs(m0 - r0) != 0.5;
-                const bool g1 = m1 >= 0.0 && m1 < (double)R_MAX && fabs(m1 - r1) != 0.5;
-                l0 += (act && g0) ? r0 : 0.0;
-                l1 += (act && g1) ? r1 : 0.0;
-                P0[k] = l0;
-                P1[k] = l1;
-                ok0 |= g0 ? 1u << k : 0u;
-                ok1 |= g1 ? 1u << k : 0u;
+                loc += (act && ok) ? r : 0.0;
+                incl[k] = loc;
+                if (act && !ok && bad == CH) bad = idx;
+                if (idx >= cnt && bad == CH) bad = idx;
             }
-            const double x0 = wave_incl_scan_f64(l0, lane) - l0, x1 = wave_incl_scan_f64(l1, lane) - l1;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                P0[k] += x0;
-                P1[k] += x1;
-            }
-        }
-        mark(6, pos);
-        int g = 0, q = pos;
-        double Pq = 0.0;  // grid g's prefix before q
-        while (true) {    // wave-uniform: stretches from the prefixes above
-            const double N = s * pow2(52 - e0 - g), u = pow2(e0 + g - 52);  // N: exact integer in [2^52, 2^53)
-            const double lim = ((double)(R_MAX - 1) - N) + Pq;              // exact, < 2^53
-            const unsigned okm = g ? ok1 : ok0;
-            double P[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) P[k] = g ? P1[k] : P0[k];
-            int bad = CH;  // first element from q on that the integer step cannot take (cnt: the chunk's end)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int idx = 4 * lane + k;
-                if (idx >= q && (idx >= cnt || !((okm >> k) & 1u)) && bad == CH) bad = idx;
-            }
+            const double excl = wave_incl_scan_f64(loc, lane) - loc;  // exact where it matters (see above)
             const int first_bad = wave_first_idx(bad);
             int cross = CH;  // first element whose running integer leaves the binade
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
+                incl[k] += excl;
                 const int idx = 4 * lane + k;
-                if (idx >= q && idx < first_bad && P[k] > lim && cross == CH) cross = idx;
+                if (idx >= pos && idx < first_bad && incl[k] > T && cross == CH) cross = idx;
             }
             const int first_cross = wave_first_idx(cross);
-            mark(7, q);
-            int stop = first_bad < first_cross ? first_bad : first_cross;
+            mark(6, pos);
+            stop = first_bad < first_cross ? first_bad : first_cross;
             stop = stop < cnt ? stop : cnt;
-            if (stop > q) {
+            if (stop > pos) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int idx = 4 * lane + k;
-                    if (CDF && idx >= q && idx < stop) j.out[base + idx] = (N + (P[k] - Pq)) * u;
+                    if (CDF && idx >= pos && idx < stop) j.out[base + idx] = (N + incl[k]) * u;
                 }
-                s = (N + (lane_elem(P, stop - 1) - Pq)) * u;
+                const int last = stop - 1;
+                const double mine = (last & 3) == 0 ? incl[0] : (last & 3) == 1 ? incl[1] : (last & 3) == 2 ? incl[2] : incl[3];
+                s = (N + readlane_f64(mine, last >> 2)) * u;
             }
-            if (stop < cnt) {  // one exact float64 add, in Open3D's order
-                s = lane_elem(v, stop) + s;
-                if (CDF && lane == 0) j.out[base + stop] = s;
-                ++stop;
-            }
-            q = stop;
-            if (q >= cnt) break;
-            const int e1 = binade(s);
-            if (e1 == e0 + 1 && g == 0) g = 1;
-            else if (e1 != e0 + g) break;  // s left binades e0 and e0 + 1 (or is special): a new pass from q
-            double Q[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) Q[k] = g ? P1[k] : P0[k];
-            Pq = lane_elem(Q, q - 1);
-            if (!(Pq < (double)(R_MAX >> 1))) break;  // (a huge crossing element) the limit would pass 2^53: new pass
         }
-        pos = q;
+        if (stop < cnt) {  // one exact float64 add, in Open3D's order
+            const double mine = (stop & 3) == 0 ? v[0] : (stop & 3) == 1 ? v[1] : (stop & 3) == 2 ? v[2] : v[3];
+            s = readlane_f64(mine, stop >> 2) + s;
+            if (CDF && lane == 0) j.out[base + stop] = s;
+            ++stop;
+        }
+        pos = stop;
     }
     return s;
 }
@@ -614,6 +564,9 @@ __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict_
         __syncthreads();
     }
     if (threadIdx.x >= 64) return;
+    // the walking wave is one object's latency chain: it takes the issue arbiter's first pick over co-resident waves of
+    // other work (another object's integrate, a mesh's vertex normals)
+    __builtin_amdgcn_s_setprio(3);
     const WalkMeta<STAGED> M{&j, nb};
     const int lane = threadIdx.x;
     double s = 0.0;  // sum: 0 + a_0 + ...;  cdf: cdf_0 = q_0 + 0.0 = q_0
@@ -993,6 +946,13 @@ struct HiStream {
     int dev = -1;
 };
 static thread_local HiStream g_hi;
+// ot_mesh_sample_points_min_z_async's pending call on this thread: its tables live in this thread's scratch slot 17 and
+// pinned slots 0 / 1 until ot_mesh_sample_points_min_z_wait, so no other sampling may start on the thread before
+struct MinZPending {
+    hipStream_t s = nullptr;
+    int32_t n_jobs = 0;
+};
+static thread_local MinZPending g_minz;
 static ot_status hi_stream_fork(hipStream_t caller, hipStream_t* out) {
     int dev = 0;
     OT_HIP_TRY(hipGetDevice(&dev));
@@ -1017,6 +977,7 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
                              const std::function<void(char*, char*)>& fill, size_t zero_off, size_t zero_bytes,
                              hipStream_t stream, std::vector<double*>& cdf, std::vector<long long*>& ncum,
                              char** extra_dev) {
+    if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     size_t bytes = 256;
     int64_t max_nt = 0;
     for (int j = 0; j < n_jobs; ++j) {
@@ -1122,12 +1083,13 @@ ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs, 
     return OT_OK;
 }
 
-ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
-                                      double z_min, int64_t* n_kept_host, void* stream_) {
-    if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
-    if (n_jobs < 0 || (n_jobs > 0 && (!jobs || !n_kept_host)))
-        return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
-    if (n_jobs == 0) return OT_OK;
+}  // extern "C"
+
+namespace ot {
+// The fused sampler's launches on this thread's greatest-priority stream; the kept counts land in pinned slot 1 once it
+// drains.  *hs: that stream.
+static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
+                               double z_min, void* stream_, hipStream_t* hs) {
     hipStream_t stream = nullptr;
     ot_status fst = hi_stream_fork(S(stream_), &stream);
     if (fst != OT_OK) return fst;
@@ -1174,9 +1136,59 @@ ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_
     hipLaunchKernelGGL(k_sample_min_z, dim3(tiles, n_jobs), dim3(256), 0, stream, djobs, n_points,
                        (unsigned long long)seed, z_min, tiles, status, ticket, kept);
     OT_LAUNCH_CHECK();
-    OT_HIP_TRY(hipStreamSynchronize(stream));  // the kept counts, and the host job table is released on return
+    *hs = stream;
+    return OT_OK;
+}
+static ot_status min_z_wait(hipStream_t hs, int32_t n_jobs, int64_t* n_kept_host) {
+    OT_HIP_TRY(hipStreamSynchronize(hs));  // the kept counts (written by each job's last tile)
+    const long long* kept = (const long long*)pinned_scratch(sizeof(long long) * (size_t)n_jobs, 1, true);
     for (int j = 0; j < n_jobs; ++j) n_kept_host[j] = kept[j];
     return OT_OK;
+}
+}  // namespace ot
+
+extern "C" {
+
+static ot_status min_z_args(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points) {
+    if (n_points <= 0) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] number_of_points <= 0");
+    if (n_jobs < 0 || (n_jobs > 0 && !jobs)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
+    return OT_OK;
+}
+
+ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
+                                      double z_min, int64_t* n_kept_host, void* stream) {
+    ot_status st = min_z_args(jobs, n_jobs, n_points);
+    if (st != OT_OK) return st;
+    if (n_jobs > 0 && !n_kept_host) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
+    if (n_jobs == 0) return OT_OK;
+    if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
+    hipStream_t hs = nullptr;
+    st = min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, stream, &hs);
+    if (st != OT_OK) return st;
+    return min_z_wait(hs, n_jobs, n_kept_host);
+}
+
+ot_status ot_mesh_sample_points_min_z_async(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points,
+                                            uint64_t seed, double z_min, void* stream) {
+    ot_status st = min_z_args(jobs, n_jobs, n_points);
+    if (st != OT_OK) return st;
+    if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
+    if (n_jobs == 0) return OT_OK;
+    hipStream_t hs = nullptr;
+    st = min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, stream, &hs);
+    if (st != OT_OK) return st;
+    g_minz.s = hs;
+    g_minz.n_jobs = n_jobs;
+    return OT_OK;
+}
+
+ot_status ot_mesh_sample_points_min_z_wait(int32_t n_jobs, int64_t* n_kept_host) {
+    if (n_jobs == 0 && !g_minz.s) return OT_OK;
+    if (!g_minz.s || n_jobs != g_minz.n_jobs || !n_kept_host)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] no pending async sampling of n_jobs jobs");
+    const hipStream_t hs = g_minz.s;
+    g_minz = MinZPending{};
+    return min_z_wait(hs, n_jobs, n_kept_host);
 }
 
 ot_status ot_mesh_get_surface_area(const double* V, int64_t nv, const int32_t* T, int64_t nt, double* area_host,

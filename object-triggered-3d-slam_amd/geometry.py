@@ -21,15 +21,28 @@ from .utility import DoubleVector, Vector3dVector, Vector3iVector
 class _Arr:
     """An (N, k) array living on the host (numpy) and/or the device (torch)."""
 
-    __slots__ = ("_h", "_d", "_viewed", "_ready")
+    __slots__ = ("_h", "_d", "_viewed", "_ready", "_launch")
 
-    def __init__(self, host=None, dev=None, ready=None):
+    def __init__(self, host=None, dev=None, ready=None, launch=None):
         self._h, self._d = host, dev
         self._viewed = False  # a writable host view was handed out: the host copy is authoritative
         self._ready = ready   # torch.cuda.Event: the device data is complete once it fires (written on another stream)
+        self._launch = launch  # deferred producer: queues the kernels that write _d, returns their completion event
+
+    def _start(self):
+        """Queue a deferred producer (once); from then on _ready is its completion event."""
+        if self._launch is not None:
+            fn, self._launch = self._launch, None
+            self._ready = fn()
+
+    def ready_event(self):
+        """The event the device data waits on (None: complete in stream order), the deferred producer queued first."""
+        self._start()
+        return self._ready
 
     def _join(self):
         """Make the current stream wait for the producer of the device data (once)."""
+        self._start()
         if self._ready is not None:
             D.torch.cuda.current_stream().wait_event(self._ready)
             self._ready = None
@@ -472,6 +485,7 @@ class TriangleMesh:
         self._mc = None  # (volume handle, extraction serial) of a mesh fresh out of extract_triangle_mesh
     @property
     def vertices(self):
+        self._settle()
         return Vector3dVector._view(self._v.host_view())
 
     @vertices.setter
@@ -481,6 +495,7 @@ class TriangleMesh:
 
     @property
     def triangles(self):
+        self._settle()
         return Vector3iVector._view(self._t.host_view())
 
     @triangles.setter
@@ -524,6 +539,12 @@ class TriangleMesh:
     def __repr__(self):
         return f"TriangleMesh with {len(self._v)} points and {len(self._t)} triangles."
 
+    def _settle(self):
+        """Deferred vertex normals read V and T on the device: queue them, and order the current stream after them,
+        before a writable view of either array is handed out (its edits reach the device copy in place)."""
+        if self._vn is not None and self._vn._launch is not None:
+            self._vn._join()
+
     def compute_vertex_normals(self, normalized=True):
         """TriangleMesh::ComputeVertexNormals (reconstruct_rgbd_filter.py:113).  A mesh fresh out of
         extract_triangle_mesh (arrays not reassigned or viewed for writing since) takes the marching-cubes walk of its
@@ -540,23 +561,34 @@ class TriangleMesh:
             V, T = self._v.dev(), self._t.dev()
             fresh = (V.data_ptr(), V._version, T.data_ptr(), T._version) == tuple(mc[2:6])
         if fresh and getattr(vol, "_h", None) is not None:
-            # the marching-cubes walk runs on a side stream: the caller's next step (sample_points_uniformly) starts
-            # its area chains, which read only V and T, while the normals are computed; any reader of the normals
-            # waits for them (_Arr ready event; the sampler passes it to ot_mesh_sample_points_uniformly_after)
+            # Deferred: the marching-cubes walk is queued on a side stream at the latest when the normals are read, or
+            # by the next sampling once its area chains are queued (sample_points_min_z: the walk then runs beside the
+            # chains' single-wave walks instead of contending with their wide first passes).  Any reader of the
+            # normals waits for them (_Arr ready event; sample_points_uniformly passes it to
+            # ot_mesh_sample_points_uniformly_after).
             torch = D.torch
             cur = torch.cuda.current_stream()
-            side = _streams.side_stream()
-            side.wait_stream(cur)
-            st = L.load().ot_tsdf_mesh_vertex_normals(vol._h, mc[1], D.ptr(V), nv, D.ptr(T), nt, D.ptr(out),
-                                                       C.c_void_p(side.cuda_stream))
-            if st == L.OT_OK:
+            vref, serial = mc[0], mc[1]
+
+            def launch():
+                v = vref()
+                side = _streams.side_stream(cur)
+                side.wait_stream(cur)
+                st = L.OT_ERR_INVALID_ARGUMENT
+                if v is not None and getattr(v, "_h", None) is not None:
+                    st = L.load().ot_tsdf_mesh_vertex_normals(v._h, serial, D.ptr(V), nv, D.ptr(T), nt, D.ptr(out),
+                                                              C.c_void_p(side.cuda_stream))
+                if st != L.OT_OK:  # the volume changed or went away since the extraction: the generic corner sort
+                    L.call("ot_mesh_compute_vertex_normals", D.ptr(V), nv, D.ptr(T), nt, D.ptr(out),
+                           C.c_void_p(side.cuda_stream))
                 for t in (V, T, out):  # allocated on the caller's stream, used on the side stream
                     t.record_stream(side)
                 done = torch.cuda.Event()
                 done.record(side)
-                self._vn = _Arr(dev=out, ready=done)
-                return self
-            cur.wait_stream(side)
+                return done
+
+            self._vn = _Arr(dev=out, launch=launch)
+            return self
         L.call("ot_mesh_compute_vertex_normals", D.ptr(self._v.dev()), nv, D.ptr(self._t.dev()), nt, D.ptr(out),
                D.stream_ptr())
         self._vn = _Arr(dev=out)
@@ -586,7 +618,7 @@ class TriangleMesh:
         PC = D.empty((n, 3), "float64") if self.has_vertex_colors() else None
         # normals still in flight on the side stream (compute_vertex_normals of a fresh mesh): the C side waits for
         # them after the area chains, right before the emission that interpolates them
-        ready = self._vn._ready if (PN is not None and not self._vn._viewed and self._vn._d is not None) else None
+        ready = self._vn.ready_event() if (PN is not None and not self._vn._viewed and self._vn._d is not None) else None
         VN = (self._vn._d if ready is not None else self._vn.dev()) if PN is not None else None
         job = (L.ot_mesh_sample_job * 1)(L.ot_mesh_sample_job(
             D.ptr(self._v.dev()), D.ptr(VN), D.ptr(self._vc.dev()) if PC is not None else None, len(self._v),
@@ -628,8 +660,19 @@ class TriangleMesh:
             outs.append((P, PC))
         kept = (C.c_int64 * max(len(meshes), 1))()
         if meshes:
-            L.call("ot_mesh_sample_points_min_z", C.cast(jobs, C.c_void_p), len(meshes), n,
-                   C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), float(z_min), kept, D.stream_ptr())
+            # deferred vertex normals of these meshes are queued once the sampling is (their walk does not read the
+            # normals): they run beside the sampling's walks
+            pend = [m._vn for m in meshes if m._vn is not None and m._vn._launch is not None]
+            args = (C.cast(jobs, C.c_void_p), len(meshes), n, C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), float(z_min))
+            if pend:
+                L.call("ot_mesh_sample_points_min_z_async", *args, D.stream_ptr())
+                try:
+                    for a in pend:
+                        a._start()
+                finally:
+                    L.call("ot_mesh_sample_points_min_z_wait", len(meshes), kept)
+            else:
+                L.call("ot_mesh_sample_points_min_z", *args, kept, D.stream_ptr())
         clouds = []
         for j, (P, PC) in enumerate(outs):
             pcd = PointCloud()

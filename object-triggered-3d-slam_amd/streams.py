@@ -29,14 +29,14 @@ def worker_streams(n: int) -> list:
 _side: dict = {}
 
 
-def side_stream():
+def side_stream(of=None):
     """A second stream paired with the current one (created once per stream): independent work of the same caller
     -- a fresh mesh's vertex normals beside its sampling's area chains -- runs there, joined by an event.  It takes the
     least stream priority the device offers, so the caller's critical-path kernels (the chains' wide passes) are
     dispatched first and the side work fills the gaps of the chains' single-wave walks."""
     import torch
 
-    cur = torch.cuda.current_stream()
+    cur = of if of is not None else torch.cuda.current_stream()  # of: pair with this stream instead of the current one
     key = (cur.device_index, cur.cuda_stream)
     with _lock:
         st = _side.get(key)

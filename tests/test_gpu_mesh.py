@@ -241,6 +241,39 @@ def test_sample_min_z_with_normals_in_flight(pkg, O, synth, seq16):
     assert_bitwise(np.asarray(mesh.vertex_normals), O.vertex_normals(V, T), "normals after the fused sampler")
 
 
+def test_deferred_normals_queued_by_the_sampler(pkg, O, synth, seq16):
+    """compute_vertex_normals of a fresh mesh is deferred: the fused sampler queues it once its own chains are queued
+    (ot_mesh_sample_points_min_z_async / _wait) and the normals equal the oracle's.  A mesh whose volume changes
+    between compute_vertex_normals and the launch takes the generic corner sort on its own arrays (same bits)."""
+    depth, color, ext = seq16
+    vol, ref = _volumes(pkg, O, synth, depth[:3], color[:3], ext[:3], 0.01)
+    V, VC, T = ref.extract_triangle_mesh()
+    rN = O.vertex_normals(V, T)
+    mesh = vol.extract_triangle_mesh()
+    mesh.compute_vertex_normals()
+    assert mesh._vn._launch is not None  # deferred
+    out = mesh.sample_points_min_z(100000, 0.03, seed=2)
+    assert mesh._vn._launch is None  # queued by the sampler
+    P, _, PC = O.sample_points_uniformly(V, T, 100000, 2, VC=VC)
+    rx, _ = O.filter_min_z(P, PC, 0.03)
+    assert_bitwise(np.asarray(out.points), rx, "fused points (normals deferred)")
+    assert_bitwise(np.asarray(mesh.vertex_normals), rN, "deferred normals queued by the sampler")
+    mesh2 = vol.extract_triangle_mesh()
+    mesh2.compute_vertex_normals()
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[3]), pkg.geometry.Image(depth[3]), convert_rgb_to_intensity=False)
+    vol.integrate(rgbd, pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth)), ext[3])
+    vol.flush()
+    assert_bitwise(np.asarray(mesh2.vertex_normals), rN, "deferred normals after the volume changed")
+    # a writable view of the vertices queues the deferred normals first (they read V on the device)
+    mesh3 = vol.extract_triangle_mesh()
+    mesh3.compute_vertex_normals()
+    Vv = np.asarray(mesh3.vertices)
+    assert mesh3._vn._launch is None
+    assert_bitwise(np.asarray(mesh3.vertex_normals), O.vertex_normals(Vv, np.asarray(mesh3.triangles)),
+                   "deferred normals queued by a vertices view")
+
+
 def test_sampling_batch_matches_single(pkg, O, synth, seq16, meshes):
     """TriangleMesh.sample_points_uniformly_batch: the per-mesh clouds equal the single-mesh calls (and the oracle)
     for meshes of different sizes sampled together."""

@@ -61,19 +61,16 @@ def main():
                     pre.append(int(clk[f5[0]] - clk[si]))
         if pre:
             print(f"   serial steps: start -> first segment mean {np.mean(pre):.0f} cycles")
-        # inside serial chunks: kind 5 = pass start, 6 = after the pass's two-grid scans, 7 = a stretch's ballots done
-        # (before its stores / float add)
-        seg_a, seg_b, st = [], [], []
+        # inside serial chunks: kind 5 = segment start, 6 = after the segment's scans (before its stores / float add)
+        seg_a, seg_b = [], []
         for i in range(len(kind) - 1):
             if kind[i] == 5:
                 seg_a.append(int(clk[i + 1] - clk[i]))  # start -> scans done
             if kind[i] == 6:
-                seg_b.append(int(clk[i + 1] - clk[i]))  # scans done -> first stretch resolved
-            if kind[i] == 7:
-                st.append(int(clk[i + 1] - clk[i]))  # stretch resolved -> next event
+                seg_b.append(int(clk[i + 1] - clk[i]))  # scans done -> next event
         if seg_a:
-            print(f"   passes {len(seg_a)}: start->scans mean {np.mean(seg_a):.0f} cycles, scans->first stretch mean "
-                  f"{np.mean(seg_b):.0f}; stretches {len(st)}: mean {np.mean(st) if st else 0:.0f} cycles to the next event")
+            print(f"   segments {len(seg_a)}: start->scans mean {np.mean(seg_a):.0f} cycles, scans->next mean "
+                  f"{np.mean(seg_b):.0f}")
         total = int(clk[-1] - clk[0])
         print(f"{name}: {len(starts)} steps, {total} cycles in the walk loop")
         for k, v in sorted(per.items()):
