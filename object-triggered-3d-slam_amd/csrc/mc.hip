@@ -10,9 +10,9 @@
 //                    owner unit's edge bitmask (atomicOr); per-unit triangle count
 //   k_mc_count     : per-unit popcount prefix over the 384 bitmask words => vertex ids without a hash map
 //   (device scans of the per-unit counts give vertex / triangle bases)
-//   k_mc_vertices  : one lane per bitmask word, vertex = half + vl*key, += f0*vl/(f0+f1) on the edge axis,
-//                    colour (f1*c0 + f0*c1)/(f0+f1) with c = colour/255 — Open3D's float64 expressions
-//   k_mc_triangles : per-lane triangle offsets by block scan; vertex ids by popcount lookups
+//   k_mc_emit      : odd workgroups, vertices: one lane per bitmask word, vertex = half + vl*key, += f0*vl/(f0+f1) on
+//                    the edge axis, colour (f1*c0 + f0*c1)/(f0+f1) with c = colour/255 — Open3D's float64 expressions
+//                    even workgroups, triangles: per-lane triangle offsets by block scan; vertex ids by popcount lookups
 #include <atomic>
 #include <cstring>
 #include <functional>
@@ -242,10 +242,9 @@ __device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z
     }
 }
 
-__global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, double vl, double* V, double* VC) {
-    const int r = blockIdx.x;
-    const int id = (int)m.sorted_ids[r];
-    const int w = threadIdx.x;
+// the vertices of edge-bitmask word w of the unit of rank r
+__device__ inline void mc_vertices_word(const TsdfDev& d, const McDev& m, double vl, double* V, double* VC, int r,
+                                        int id, int w) {
     unsigned bits = m.eflags[(size_t)id * EWORDS + w];
     if (!bits) return;
     long long vid = m.vert_base[r] + m.wprefix[(size_t)id * EWORDS + w];
@@ -305,10 +304,10 @@ __device__ inline int edge_vid(const McDev& m, const int* snbr, const long long*
     return (int)(sbase[o] + m.wprefix[(size_t)owner * EWORDS + word] + __popc(below));
 }
 
-__global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_t* T) {
+// the triangles of the unit of rank r (a whole 256-lane workgroup: it scans and synchronises)
+__device__ inline void mc_triangles_unit(const TsdfDev& d, const McDev& m, int32_t* T, int r) {
     __shared__ int snbr[8];
     __shared__ long long sbase[8];
-    const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
     const int ukey[3] = {d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]};
@@ -359,6 +358,19 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
             }
             ++out;
         }
+    }
+}
+
+// Phase 2 in ONE launch: even workgroups emit the triangles of unit rank b / 2, odd ones its vertices (384 bitmask
+// words over 256 lanes).  Both read only the counted structure; one launch replaces a side-stream fork / join whose
+// event records sat between the count scans and the emission (r04ab: 13 us gap on one object's chain).
+__global__ __launch_bounds__(256) void k_mc_emit(TsdfDev d, McDev m, double vl, double* V, double* VC, int32_t* T) {
+    const int r = blockIdx.x >> 1;
+    if (blockIdx.x & 1) {  // block-uniform
+        const int id = (int)m.sorted_ids[r];
+        for (int w = threadIdx.x; w < EWORDS; w += 256) mc_vertices_word(d, m, vl, V, VC, r, id, w);
+    } else {
+        mc_triangles_unit(d, m, T, r);
     }
 }
 
@@ -591,8 +603,8 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
 }
 
 // Phase 2: vertex positions / colours and triangle indices (and the merge keys) into the given device arrays.  They
-// depend on the same edge bitmasks and bases but not on each other: the vertices run on the volume's side stream
-// beside the triangles (fork / join by events); the mesh is complete in stream order on return.
+// depend on the same edge bitmasks and bases but not on each other: one launch interleaves their workgroups; the mesh is
+// complete in stream order on return.
 static ot_status mc_emit_launch(ot_tsdf* vol, McDev m, int64_t nv, double* V, double* VC, int32_t* T,
                                 hipStream_t stream);
 static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStream_t stream) {
@@ -610,19 +622,10 @@ static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStr
 // the emission kernels of structure m (U = vol->mesh.ws_units) into V / VC / T (nv: vertex rows for the NoColor zeros)
 static ot_status mc_emit_launch(ot_tsdf* vol, McDev m, int64_t nv, double* V, double* VC, int32_t* T,
                                 hipStream_t stream) {
-    const unsigned g = (unsigned)vol->mesh.ws_units;
-    if (!vol->side) {
-        OT_HIP_TRY(hipStreamCreateWithFlags(&vol->side, hipStreamNonBlocking));
-        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_fork, hipEventDisableTiming));
-        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_join, hipEventDisableTiming));
-    }
-    OT_HIP_TRY(hipEventRecord(vol->ev_fork, stream));
-    OT_HIP_TRY(hipStreamWaitEvent(vol->side, vol->ev_fork, 0));
-    hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, vol->side, vol->dev, m, vol->voxel_length, V,
-                       vol->color_type == OT_COLOR_RGB8 ? VC : nullptr);
-    OT_HIP_TRY(hipEventRecord(vol->ev_join, vol->side));
-    hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, T);
-    OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_join, 0));
+    const int64_t U = vol->mesh.ws_units;
+    if (U > 0x3FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] too many units");
+    hipLaunchKernelGGL(k_mc_emit, dim3((unsigned)(2 * U)), dim3(256), 0, stream, vol->dev, m, vol->voxel_length, V,
+                       vol->color_type == OT_COLOR_RGB8 ? VC : nullptr, T);
     OT_LAUNCH_CHECK();
     if (VC && vol->color_type != OT_COLOR_RGB8)
         OT_HIP_TRY(hipMemsetAsync(VC, 0, sizeof(double) * 3 * (size_t)std::min<int64_t>(nv, m.cap_v), stream));
