@@ -853,39 +853,58 @@ __global__ __launch_bounds__(256) void k_sample_min_z(const MinZJob* __restrict_
     if (staged)
         for (int i = threadIdx.x; i < cnt; i += 256) s_nc[i] = (int)jb.ncum[t_lo + i];
     __syncthreads();
+    // the items' searches in lockstep (one power-of-two descent shared by the MZ_ITEMS points of a lane: the block's
+    // cnt fixes its steps), then every item's triangle corners, then their vertex rows -- each phase's loads issued
+    // together instead of one point's dependent chain after another's
     double x[MZ_ITEMS][3], col[MZ_ITEMS][3];
-    bool keep[MZ_ITEMS];
+    bool keep[MZ_ITEMS], found[MZ_ITEMS];
     int pre[MZ_ITEMS];
+    int64_t tt[MZ_ITEMS];
+    if (staged) {
+        int pos[MZ_ITEMS];
+#pragma unroll
+        for (int i = 0; i < MZ_ITEMS; ++i) pos[i] = -1;  // largest index with count <= k
+        int step = 1;
+        while (step * 2 <= cnt) step *= 2;
+        for (; step > 0; step >>= 1) {
+#pragma unroll
+            for (int i = 0; i < MZ_ITEMS; ++i) {
+                const long long k = (long long)tile * MZ_TILE + i * 256 + threadIdx.x;
+                const int q = pos[i] + step;
+                if (q < cnt && (long long)s_nc[q] <= k) pos[i] = q;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < MZ_ITEMS; ++i) {
+            const int64_t k = (int64_t)tile * MZ_TILE + i * 256 + threadIdx.x;
+            tt[i] = (int64_t)t_lo + pos[i] + 1;
+            found[i] = k < N && tt[i] < jb.nt;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < MZ_ITEMS; ++i) {
+            const int64_t k = (int64_t)tile * MZ_TILE + i * 256 + threadIdx.x;
+            double a, b, c;
+            found[i] = k < N && cnt > 0 && sample_triangle(jb.ncum, jb.nt, k, seed, tt[i], a, b, c);
+        }
+    }
+    int64_t corner[MZ_ITEMS][3];
+#pragma unroll
+    for (int i = 0; i < MZ_ITEMS; ++i)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) corner[i][d] = found[i] ? jb.T[tt[i] * 3 + d] : 0;
 #pragma unroll
     for (int i = 0; i < MZ_ITEMS; ++i) {
         const int64_t k = (int64_t)tile * MZ_TILE + i * 256 + threadIdx.x;
-        int64_t t;
-        double a, b, c;
 #pragma unroll
         for (int d = 0; d < 3; ++d) x[i][d] = col[i][d] = 0.0;
-        keep[i] = false;
-        if (k < N) {
-            bool found;
-            if (staged) {
-                int lo = 0, hi = cnt;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if ((long long)s_nc[mid] > k) hi = mid;
-                    else lo = mid + 1;
-                }
-                t = (int64_t)t_lo + lo;
-                found = t < jb.nt;
-                if (found) sample_bary(seed, k, a, b, c);
-            } else {
-                found = cnt > 0 && sample_triangle(jb.ncum, jb.nt, k, seed, t, a, b, c);
-            }
-            if (found) {
-                const int64_t i0 = jb.T[t * 3], i1 = jb.T[t * 3 + 1], i2 = jb.T[t * 3 + 2];
-                interp3(jb.V, i0, i1, i2, a, b, c, x[i]);
-                if (jb.PC) interp3(jb.VC, i0, i1, i2, a, b, c, col[i]);
-            }
-            keep[i] = x[i][2] >= z_min;
+        if (found[i]) {
+            double a, b, c;
+            sample_bary(seed, k, a, b, c);
+            interp3(jb.V, corner[i][0], corner[i][1], corner[i][2], a, b, c, x[i]);
+            if (jb.PC) interp3(jb.VC, corner[i][0], corner[i][1], corner[i][2], a, b, c, col[i]);
         }
+        keep[i] = k < N && x[i][2] >= z_min;
         int tot;
         pre[i] = wave_excl_count(keep[i], tot);
         if (lane == 0) wsum[i][wid] = tot;
@@ -986,6 +1005,7 @@ namespace ot {
 struct HiStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr;
+    hipEvent_t sums = nullptr;  // an async sampling's area sums done (its wide first passes behind it)
     int dev = -1;
 };
 static thread_local HiStream g_hi;
@@ -1004,6 +1024,7 @@ static ot_status hi_stream_fork(hipStream_t caller, hipStream_t* out) {
         OT_HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
         OT_HIP_TRY(hipStreamCreateWithPriority(&g_hi.s, hipStreamNonBlocking, greatest));
         OT_HIP_TRY(hipEventCreateWithFlags(&g_hi.fork, hipEventDisableTiming));
+        OT_HIP_TRY(hipEventCreateWithFlags(&g_hi.sums, hipEventDisableTiming));
         g_hi.dev = dev;
     }
     OT_HIP_TRY(hipEventRecord(g_hi.fork, caller));
@@ -1019,7 +1040,7 @@ static ot_status hi_stream_fork(hipStream_t caller, hipStream_t* out) {
 static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, size_t extra, size_t upload,
                              const std::function<void(char*, char*)>& fill, size_t zero_off, size_t zero_bytes,
                              hipStream_t stream, std::vector<double*>& cdf, std::vector<long long*>& ncum,
-                             char** extra_dev) {
+                             char** extra_dev, hipEvent_t after_sums = nullptr) {
     if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     size_t bytes = 256;
     int64_t max_nt = 0;
@@ -1086,6 +1107,7 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
         }
     }
     launch_chains<false>(djobs, n_jobs, max_nt, stream);
+    if (after_sums) OT_HIP_TRY(hipEventRecord(after_sums, stream));
     const int64_t max_nb = (max_nt + CH - 1) / CH;
     hipLaunchKernelGGL(k_chain_cdf_prep, dim3((unsigned)((max_nb + 3) / 4), (unsigned)n_jobs), dim3(256), 0, stream,
                        (const ChainJob*)djobs, (const ChainJob*)(djobs + n_jobs));
@@ -1132,7 +1154,7 @@ namespace ot {
 // The fused sampler's launches on this thread's greatest-priority stream; the kept counts land in pinned slot 1 once it
 // drains.  *hs: that stream.
 static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
-                               double z_min, void* stream_, hipStream_t* hs) {
+                               double z_min, void* stream_, hipStream_t* hs, bool mark_sums = false) {
     hipStream_t stream = nullptr;
     ot_status fst = hi_stream_fork(S(stream_), &stream);
     if (fst != OT_OK) return fst;
@@ -1169,7 +1191,7 @@ static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, i
     for (int j = 0; j < n_jobs; ++j)
         if (jobs[j].n_triangles > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many triangles");
     ot_status st = sample_cdfs(jobs, n_jobs, total, up_bytes, fill, zero_off, zero_end - zero_off, stream, cdf, ncum,
-                               &extra);
+                               &extra, mark_sums ? g_hi.sums : nullptr);
     if (st != OT_OK) return st;
     const MinZJob* djobs = (const MinZJob*)extra;
     const double* const* dcdf = (const double* const*)(djobs + n_jobs);
@@ -1223,10 +1245,16 @@ ot_status ot_mesh_sample_points_min_z_async(const ot_mesh_sample_job* jobs, int3
     if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     if (n_jobs == 0) return OT_OK;
     hipStream_t hs = nullptr;
-    st = min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, stream, &hs);
+    st = min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, stream, &hs, true);
     if (st != OT_OK) return st;
     g_minz.s = hs;
     g_minz.n_jobs = n_jobs;
+    return OT_OK;
+}
+
+ot_status ot_mesh_sample_points_min_z_after_sums(void* stream) {
+    if (!g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] no pending async sampling");
+    OT_HIP_TRY(hipStreamWaitEvent(S(stream), g_hi.sums, 0));
     return OT_OK;
 }
 

@@ -29,11 +29,12 @@ class _Arr:
         self._ready = ready   # torch.cuda.Event: the device data is complete once it fires (written on another stream)
         self._launch = launch  # deferred producer: queues the kernels that write _d, returns their completion event
 
-    def _start(self):
-        """Queue a deferred producer (once); from then on _ready is its completion event."""
+    def _start(self, after=None):
+        """Queue a deferred producer (once); from then on _ready is its completion event.  after(stream): called with
+        the producer's stream before its kernels are queued (an extra dependency)."""
         if self._launch is not None:
             fn, self._launch = self._launch, None
-            self._ready = fn()
+            self._ready = fn(after)
 
     def ready_event(self):
         """The event the device data waits on (None: complete in stream order), the deferred producer queued first."""
@@ -570,10 +571,12 @@ class TriangleMesh:
             cur = torch.cuda.current_stream()
             vref, serial = mc[0], mc[1]
 
-            def launch():
+            def launch(after=None):
                 v = vref()
                 side = _streams.side_stream(cur)
                 side.wait_stream(cur)
+                if after is not None:
+                    after(side)
                 st = L.OT_ERR_INVALID_ARGUMENT
                 if v is not None and getattr(v, "_h", None) is not None:
                     st = L.load().ot_tsdf_mesh_vertex_normals(v._h, serial, D.ptr(V), nv, D.ptr(T), nt, D.ptr(out),
@@ -660,15 +663,17 @@ class TriangleMesh:
             outs.append((P, PC))
         kept = (C.c_int64 * max(len(meshes), 1))()
         if meshes:
-            # deferred vertex normals of these meshes are queued once the sampling is (their walk does not read the
-            # normals): they run beside the sampling's walks
+            # deferred vertex normals of these meshes are queued once the sampling is, behind its area sums (the
+            # sampling does not read the normals): they run beside its CDF walk instead of contending with its wide
+            # first passes
             pend = [m._vn for m in meshes if m._vn is not None and m._vn._launch is not None]
             args = (C.cast(jobs, C.c_void_p), len(meshes), n, C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), float(z_min))
             if pend:
                 L.call("ot_mesh_sample_points_min_z_async", *args, D.stream_ptr())
                 try:
+                    after = lambda side: L.call("ot_mesh_sample_points_min_z_after_sums", C.c_void_p(side.cuda_stream))
                     for a in pend:
-                        a._start()
+                        a._start(after)
                 finally:
                     L.call("ot_mesh_sample_points_min_z_wait", len(meshes), kept)
             else:
