@@ -361,9 +361,6 @@ ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs_host, int32
 ot_status ot_mesh_sample_points_min_z_async(const ot_mesh_sample_job* jobs_host, int32_t n_jobs, int64_t n_points,
                                             uint64_t seed, double z_min, void* stream);
 ot_status ot_mesh_sample_points_min_z_wait(int32_t n_jobs, int64_t* n_kept_host);
-/* Between _async and _wait: `stream` waits until the pending sampling's area sums are done (the chains' wide first
- * passes are behind it; work queued there then overlaps the CDF walk instead of contending with them). */
-ot_status ot_mesh_sample_points_min_z_after_sums(void* stream);
 
 /* ---------------------------------------------------------------------------------------------------
  * Hybrid map — fusion/hybrid_map.py

@@ -97,7 +97,6 @@ SIGNATURES = {
     "ot_mesh_sample_points_min_z": [_p, _i32, _i64, C.c_uint64, _d, _pi64, _p],
     "ot_mesh_sample_points_min_z_async": [_p, _i32, _i64, C.c_uint64, _d, _p],
     "ot_mesh_sample_points_min_z_wait": [_i32, _pi64],
-    "ot_mesh_sample_points_min_z_after_sums": [_p],
     "ot_mesh_sample_points_uniformly_after": [_p, _i32, _i64, C.c_uint64, _p, _p],
     "ot_mesh_get_surface_area": [_p, _i64, _p, _i64, C.POINTER(C.c_double), _p],
     "ot_occupancy_to_points": [_p, _i32, _i32, _i32, _d, _d, _d, _p, _pi64, _p],

@@ -10,9 +10,9 @@
 //                    owner unit's edge bitmask (atomicOr); per-unit triangle count
 //   k_mc_count     : per-unit popcount prefix over the 384 bitmask words => vertex ids without a hash map
 //   (device scans of the per-unit counts give vertex / triangle bases)
-//   k_mc_emit      : odd workgroups, vertices: one lane per bitmask word, vertex = half + vl*key, += f0*vl/(f0+f1) on
-//                    the edge axis, colour (f1*c0 + f0*c1)/(f0+f1) with c = colour/255 — Open3D's float64 expressions
-//                    even workgroups, triangles: per-lane triangle offsets by block scan; vertex ids by popcount lookups
+//   k_mc_vertices  : one lane per bitmask word, vertex = half + vl*key, += f0*vl/(f0+f1) on the edge axis,
+//                    colour (f1*c0 + f0*c1)/(f0+f1) with c = colour/255 — Open3D's float64 expressions
+//   k_mc_triangles : per-lane triangle offsets by block scan; vertex ids by popcount lookups
 #include <atomic>
 #include <cstring>
 #include <functional>
@@ -41,9 +41,8 @@ struct McDev {
     unsigned char* cubes;        // [id][4096]
     unsigned* eflags;            // [id][384]
     int* wprefix;                // [id][384]
-    long long* tri_cnt;          // [rank] look-back status words of the triangle bases (k_mc_count)
-    long long* vert_cnt;         // [rank] look-back status words of the vertex bases
-    int* ticket;                 // k_mc_count's rank tickets
+    long long* tri_cnt;          // [rank]
+    long long* vert_cnt;         // [rank]
     long long* tri_base;         // [rank]
     long long* vert_base;        // [rank]
     unsigned short* ctri;        // [id][4096] (cube byte order): first triangle of the cube inside its unit
@@ -55,7 +54,7 @@ struct McDev {
 
 // the marching-cubes workspace of U units, carved from one allocation (kept with the volume: MeshBuffers::ws)
 static size_t mc_ws_bytes(int64_t U) {
-    return (size_t)U * (4 * 8 + 4 + 16 * 4 + EWORDS * 4 * 2 + UNIT_VOX + UNIT_VOX * 2) + 17 * 256;
+    return (size_t)U * (4 * 8 + 4 + 16 * 4 + EWORDS * 4 * 2 + UNIT_VOX + UNIT_VOX * 2) + 16 * 256;
 }
 static void mc_layout(char* ws, int64_t U, McDev& m) {
     char* p = ws;
@@ -74,7 +73,6 @@ static void mc_layout(char* ws, int64_t U, McDev& m) {
     m.wprefix = (int*)take(sizeof(int) * EWORDS * U);
     m.cubes = (unsigned char*)take((size_t)UNIT_VOX * U);
     m.ctri = (unsigned short*)take(sizeof(unsigned short) * UNIT_VOX * U);
-    m.ticket = (int*)take(sizeof(int));
 }
 
 __device__ inline int find_unit(const TsdfDev& d, int x, int y, int z) {
@@ -104,11 +102,7 @@ __global__ __launch_bounds__(256) void k_mc_prepare(TsdfDev d, McDev m) {
                                     : find_unit(d, d.unit_keys[id * 3] + dx, d.unit_keys[id * 3 + 1] + dy,
                                                 d.unit_keys[id * 3 + 2] + dz);
     }
-    if (t == 0) {
-        m.rank_of[id] = r;
-        m.tri_cnt[r] = m.vert_cnt[r] = 0;  // k_mc_count's look-back status words
-        if (r == 0) *m.ticket = 0;
-    }
+    if (t == 0) m.rank_of[id] = r;
     for (int w = t; w < EWORDS; w += 256) m.eflags[(size_t)id * EWORDS + w] = 0u;
 }
 
@@ -127,7 +121,7 @@ __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
     if (d.shard_world > 1 &&
         !unit_owned(d, pack_key(d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]))) {
         *reinterpret_cast<uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16) = make_uint4(0u, 0u, 0u, 0u);
-        if (t == 0) m.tri_base[r] = 0;  // the unit's triangle count until k_mc_count turns it into its base
+        if (t == 0) m.tri_cnt[r] = 0;
         return;
     }
     if (t < 8) snbr[t] = m.nbr[id * 16 + t];
@@ -201,7 +195,7 @@ __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
     ntri = wave_sum(ntri);
     if (lane_id() == 0) wsum[t >> 6] = ntri;
     __syncthreads();
-    if (t == 0) m.tri_base[r] = wsum[0] + wsum[1] + wsum[2] + wsum[3];  // the count, until k_mc_count's base
+    if (t == 0) m.tri_cnt[r] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     // neighbours' classify blocks may set bits of this unit's words too: merge, do not overwrite
     for (int w = t; w < EWORDS; w += 256) {
         const unsigned b = sflags[w];
@@ -209,18 +203,12 @@ __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
     }
 }
 
-// per-unit exclusive popcount prefix of the 384 bitmask words (6 waves, one word per lane), and the unit's triangle
-// and vertex bases by decoupled look-back (wave 0 over the triangle counts classify left in tri_base, wave 1 over the
-// vertex counts, side by side; ranks start in ticket order, so a look-back waits only on running workgroups); the
-// last rank mails both totals to the volume's pinned mailbox -- the bases without a scan launch of their own
-__global__ __launch_bounds__(EWORDS) void k_mc_count(McDev m, long long* __restrict__ mail) {
+// per-unit exclusive popcount prefix of the 384 bitmask words (6 waves, one word per lane)
+__global__ __launch_bounds__(EWORDS) void k_mc_count(McDev m) {
     __shared__ int wsum[EWORDS / 64];
-    __shared__ int s_r;
-    const int t = threadIdx.x;
-    if (t == 0) s_r = atomicAdd(m.ticket, 1);
-    __syncthreads();
-    const int r = s_r;
+    const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
+    const int t = threadIdx.x;
     const int pc = __popc(m.eflags[(size_t)id * EWORDS + t]);
     int inc = wave_incl_scan(pc);
     if (lane_id() == 63) wsum[t >> 6] = inc;
@@ -232,16 +220,7 @@ __global__ __launch_bounds__(EWORDS) void k_mc_count(McDev m, long long* __restr
         tot += wsum[w];
     }
     m.wprefix[(size_t)id * EWORDS + t] = off + inc - pc;
-    const int wv = t >> 6;
-    if (wv < 2) {  // wave-uniform
-        const long long cnt = wv == 0 ? m.tri_base[r] : (long long)tot;
-        unsigned long long* st = reinterpret_cast<unsigned long long*>(wv == 0 ? m.tri_cnt : m.vert_cnt);
-        const long long excl = lookback_wave(st, r, (unsigned long long)cnt);
-        if (lane_id() == 0) {
-            (wv == 0 ? m.tri_base : m.vert_base)[r] = excl;
-            if (r == (int)gridDim.x - 1) mail[wv] = excl + cnt;  // totals: [0] triangles, [1] vertices
-        }
-    }
+    if (t == 0) m.vert_cnt[r] = tot;
 }
 
 // tsdf and colour of one voxel; colour from the float64 pool when the volume keeps it (exact: a float colour widens
@@ -263,9 +242,10 @@ __device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z
     }
 }
 
-// the vertices of edge-bitmask word w of the unit of rank r
-__device__ inline void mc_vertices_word(const TsdfDev& d, const McDev& m, double vl, double* V, double* VC, int r,
-                                        int id, int w) {
+__global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, double vl, double* V, double* VC) {
+    const int r = blockIdx.x;
+    const int id = (int)m.sorted_ids[r];
+    const int w = threadIdx.x;
     unsigned bits = m.eflags[(size_t)id * EWORDS + w];
     if (!bits) return;
     long long vid = m.vert_base[r] + m.wprefix[(size_t)id * EWORDS + w];
@@ -325,10 +305,10 @@ __device__ inline int edge_vid(const McDev& m, const int* snbr, const long long*
     return (int)(sbase[o] + m.wprefix[(size_t)owner * EWORDS + word] + __popc(below));
 }
 
-// the triangles of the unit of rank r (a whole 256-lane workgroup: it scans and synchronises)
-__device__ inline void mc_triangles_unit(const TsdfDev& d, const McDev& m, int32_t* T, int r) {
+__global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_t* T) {
     __shared__ int snbr[8];
     __shared__ long long sbase[8];
+    const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
     const int t = threadIdx.x;
     const int ukey[3] = {d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]};
@@ -379,21 +359,6 @@ __device__ inline void mc_triangles_unit(const TsdfDev& d, const McDev& m, int32
             }
             ++out;
         }
-    }
-}
-
-// Phase 2 in ONE launch: workgroups [0, U) emit the triangles of unit rank b (dispatched first: the longer half),
-// [U, 2U) the vertices of rank b - U (384 bitmask words over 256 lanes).  Both read only the counted structure; one
-// launch replaces a side-stream fork / join whose event records sat between the count scans and the emission (r04ab:
-// 13 us gap on one object's chain).  (Even / odd interleaving of the two halves: 138 us vs 120 for fork / join.)
-__global__ __launch_bounds__(256) void k_mc_emit(TsdfDev d, McDev m, double vl, double* V, double* VC, int32_t* T) {
-    const int U = (int)(gridDim.x >> 1);
-    if ((int)blockIdx.x >= U) {  // block-uniform
-        const int r = (int)blockIdx.x - U;
-        const int id = (int)m.sorted_ids[r];
-        for (int w = threadIdx.x; w < EWORDS; w += 256) mc_vertices_word(d, m, vl, V, VC, r, id, w);
-    } else {
-        mc_triangles_unit(d, m, T, (int)blockIdx.x);
     }
 }
 
@@ -458,6 +423,54 @@ __global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t
     N[v * 3 + 0] = n[0];
     N[v * 3 + 1] = n[1];
     N[v * 3 + 2] = n[2];
+}
+
+// the extraction's two exclusive scans (triangle and vertex counts per unit, U of each) in one launch: block 0 scans
+// the triangle counts, block 1 the vertex counts, 4096 per round (4 consecutive per thread) with a carried total --
+// one ~5 us launch instead of a library scan's two launches per array (U is a few thousand units).  Each block mails
+// its array's total (triangles, vertices) to the volume's pinned mailbox: the host's read-back needs no launch of its own
+__global__ __launch_bounds__(1024) void k_mc_scan2(const long long* __restrict__ c0, long long* __restrict__ b0,
+                                                  const long long* __restrict__ c1, long long* __restrict__ b1,
+                                                  int n, long long* __restrict__ totals) {
+    const long long* in = blockIdx.x ? c1 : c0;
+    long long* out = blockIdx.x ? b1 : b0;
+    __shared__ long long wsum[16];
+    __shared__ long long s_carry;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) s_carry = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += 4096) {
+        const int i0 = base + 4 * t;
+        long long v[4], loc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = i0 + k < n ? in[i0 + k] : 0;
+            loc += v[k];
+        }
+        long long inc = loc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const long long o = __shfl_up(inc, d);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        long long off = s_carry, tot = 0;
+        for (int q = 0; q < 16; ++q) {
+            off += q < w ? wsum[q] : 0;
+            tot += wsum[q];
+        }
+        long long run = off + inc - loc;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (i0 + k < n) out[i0 + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        if (t == 0) s_carry += tot;
+        __syncthreads();
+    }
+    if (t == 0) totals[blockIdx.x] = s_carry;
 }
 
 static std::atomic<bool> g_tables_uploaded{false};
@@ -540,12 +553,15 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
     m.vk = nullptr;
     m.tk = nullptr;
     mc_layout((char*)mb.ws, U, m);
-    if (U > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] too many units");
     const unsigned g = (unsigned)U;
     hipLaunchKernelGGL(k_mc_prepare, dim3(g), dim3(256), 0, stream, vol->dev, m);
     hipLaunchKernelGGL(k_mc_classify, dim3(g), dim3(256), 0, stream, vol->dev, m);
-    // the count kernel's last rank mails the triangle and vertex totals (hmail words 0..3)
-    hipLaunchKernelGGL(k_mc_count, dim3(g), dim3(EWORDS), 0, stream, m, (long long*)vol->hmail);
+    hipLaunchKernelGGL(k_mc_count, dim3(g), dim3(EWORDS), 0, stream, m);
+    OT_LAUNCH_CHECK();
+    if (U > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] too many units");
+    // the scans mail the triangle and vertex totals (hmail words 0..3)
+    hipLaunchKernelGGL(k_mc_scan2, dim3(2), dim3(1024), 0, stream, (const long long*)m.tri_cnt, m.tri_base,
+                       (const long long*)m.vert_cnt, m.vert_base, (int)U, (long long*)vol->hmail);
     OT_LAUNCH_CHECK();
     mb.ws_units = U;
     if (spec) {  // the host waits for the read-back only, the speculative work runs behind it
@@ -575,8 +591,8 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
 }
 
 // Phase 2: vertex positions / colours and triangle indices (and the merge keys) into the given device arrays.  They
-// depend on the same edge bitmasks and bases but not on each other: one launch interleaves their workgroups; the mesh is
-// complete in stream order on return.
+// depend on the same edge bitmasks and bases but not on each other: the vertices run on the volume's side stream
+// beside the triangles (fork / join by events); the mesh is complete in stream order on return.
 static ot_status mc_emit_launch(ot_tsdf* vol, McDev m, int64_t nv, double* V, double* VC, int32_t* T,
                                 hipStream_t stream);
 static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStream_t stream) {
@@ -594,10 +610,19 @@ static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStr
 // the emission kernels of structure m (U = vol->mesh.ws_units) into V / VC / T (nv: vertex rows for the NoColor zeros)
 static ot_status mc_emit_launch(ot_tsdf* vol, McDev m, int64_t nv, double* V, double* VC, int32_t* T,
                                 hipStream_t stream) {
-    const int64_t U = vol->mesh.ws_units;
-    if (U > 0x3FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] too many units");
-    hipLaunchKernelGGL(k_mc_emit, dim3((unsigned)(2 * U)), dim3(256), 0, stream, vol->dev, m, vol->voxel_length, V,
-                       vol->color_type == OT_COLOR_RGB8 ? VC : nullptr, T);
+    const unsigned g = (unsigned)vol->mesh.ws_units;
+    if (!vol->side) {
+        OT_HIP_TRY(hipStreamCreateWithFlags(&vol->side, hipStreamNonBlocking));
+        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_fork, hipEventDisableTiming));
+        OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_join, hipEventDisableTiming));
+    }
+    OT_HIP_TRY(hipEventRecord(vol->ev_fork, stream));
+    OT_HIP_TRY(hipStreamWaitEvent(vol->side, vol->ev_fork, 0));
+    hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, vol->side, vol->dev, m, vol->voxel_length, V,
+                       vol->color_type == OT_COLOR_RGB8 ? VC : nullptr);
+    OT_HIP_TRY(hipEventRecord(vol->ev_join, vol->side));
+    hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, T);
+    OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_join, 0));
     OT_LAUNCH_CHECK();
     if (VC && vol->color_type != OT_COLOR_RGB8)
         OT_HIP_TRY(hipMemsetAsync(VC, 0, sizeof(double) * 3 * (size_t)std::min<int64_t>(nv, m.cap_v), stream));

@@ -798,7 +798,9 @@ __global__ __launch_bounds__(256) void k_sample(const double* __restrict__ V, co
 // fails, as numpy's mask) in sampling order, xyz and colours only (the reference rebuilds its cloud from those two, so
 // normals are not interpolated).  A workgroup takes MZ_TILE consecutive points in a ticket order, counts the kept
 // ones and finds its output offset by a decoupled look-back over the job's earlier workgroups; grid (tiles, jobs).
-constexpr int MZ_ITEMS = 4, MZ_TILE = 256 * MZ_ITEMS;
+// one point per lane: 4 per lane (98 workgroups for 100k points, 1.5 waves per CU) left the kernel latency-bound at
+// 34 us whatever its search did (r04ab-r04ad)
+constexpr int MZ_ITEMS = 1, MZ_TILE = 256 * MZ_ITEMS;
 struct MinZJob {
     const double* V;
     const double* VC;
@@ -1005,7 +1007,6 @@ namespace ot {
 struct HiStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr;
-    hipEvent_t sums = nullptr;  // an async sampling's area sums done (its wide first passes behind it)
     int dev = -1;
 };
 static thread_local HiStream g_hi;
@@ -1024,7 +1025,6 @@ static ot_status hi_stream_fork(hipStream_t caller, hipStream_t* out) {
         OT_HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
         OT_HIP_TRY(hipStreamCreateWithPriority(&g_hi.s, hipStreamNonBlocking, greatest));
         OT_HIP_TRY(hipEventCreateWithFlags(&g_hi.fork, hipEventDisableTiming));
-        OT_HIP_TRY(hipEventCreateWithFlags(&g_hi.sums, hipEventDisableTiming));
         g_hi.dev = dev;
     }
     OT_HIP_TRY(hipEventRecord(g_hi.fork, caller));
@@ -1040,7 +1040,7 @@ static ot_status hi_stream_fork(hipStream_t caller, hipStream_t* out) {
 static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, size_t extra, size_t upload,
                              const std::function<void(char*, char*)>& fill, size_t zero_off, size_t zero_bytes,
                              hipStream_t stream, std::vector<double*>& cdf, std::vector<long long*>& ncum,
-                             char** extra_dev, hipEvent_t after_sums = nullptr) {
+                             char** extra_dev) {
     if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     size_t bytes = 256;
     int64_t max_nt = 0;
@@ -1107,7 +1107,6 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
         }
     }
     launch_chains<false>(djobs, n_jobs, max_nt, stream);
-    if (after_sums) OT_HIP_TRY(hipEventRecord(after_sums, stream));
     const int64_t max_nb = (max_nt + CH - 1) / CH;
     hipLaunchKernelGGL(k_chain_cdf_prep, dim3((unsigned)((max_nb + 3) / 4), (unsigned)n_jobs), dim3(256), 0, stream,
                        (const ChainJob*)djobs, (const ChainJob*)(djobs + n_jobs));
@@ -1154,7 +1153,7 @@ namespace ot {
 // The fused sampler's launches on this thread's greatest-priority stream; the kept counts land in pinned slot 1 once it
 // drains.  *hs: that stream.
 static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
-                               double z_min, void* stream_, hipStream_t* hs, bool mark_sums = false) {
+                               double z_min, void* stream_, hipStream_t* hs) {
     hipStream_t stream = nullptr;
     ot_status fst = hi_stream_fork(S(stream_), &stream);
     if (fst != OT_OK) return fst;
@@ -1191,7 +1190,7 @@ static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, i
     for (int j = 0; j < n_jobs; ++j)
         if (jobs[j].n_triangles > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many triangles");
     ot_status st = sample_cdfs(jobs, n_jobs, total, up_bytes, fill, zero_off, zero_end - zero_off, stream, cdf, ncum,
-                               &extra, mark_sums ? g_hi.sums : nullptr);
+                               &extra);
     if (st != OT_OK) return st;
     const MinZJob* djobs = (const MinZJob*)extra;
     const double* const* dcdf = (const double* const*)(djobs + n_jobs);
@@ -1245,16 +1244,10 @@ ot_status ot_mesh_sample_points_min_z_async(const ot_mesh_sample_job* jobs, int3
     if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     if (n_jobs == 0) return OT_OK;
     hipStream_t hs = nullptr;
-    st = min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, stream, &hs, true);
+    st = min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, stream, &hs);
     if (st != OT_OK) return st;
     g_minz.s = hs;
     g_minz.n_jobs = n_jobs;
-    return OT_OK;
-}
-
-ot_status ot_mesh_sample_points_min_z_after_sums(void* stream) {
-    if (!g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] no pending async sampling");
-    OT_HIP_TRY(hipStreamWaitEvent(S(stream), g_hi.sums, 0));
     return OT_OK;
 }
 

@@ -199,6 +199,9 @@ struct ot_tsdf {
     int sorted_frame = -1;
     // extracted mesh
     ot::MeshBuffers mesh;
+    // a second stream for independent extraction stages (vertex positions beside triangle indices), fork / join
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // kernel timing (events around the dominant integration kernel)
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;

@@ -1618,8 +1618,11 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
         if (p) (void)hipFree(p);
     if (v->hbframes) (void)hipHostFree(v->hbframes);
     if (v->hmail) (void)hipHostFree(v->hmail);
+    if (v->ev_fork) (void)hipEventDestroy(v->ev_fork);
     if (v->ev_early) (void)hipEventDestroy(v->ev_early);
     if (v->ev_mail) (void)hipEventDestroy(v->ev_mail);
+    if (v->ev_join) (void)hipEventDestroy(v->ev_join);
+    if (v->side) (void)hipStreamDestroy(v->side);
     for (hipEvent_t ev : v->hb_event)
         if (ev) (void)hipEventDestroy(ev);
     delete v;

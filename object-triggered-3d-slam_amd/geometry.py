@@ -663,17 +663,15 @@ class TriangleMesh:
             outs.append((P, PC))
         kept = (C.c_int64 * max(len(meshes), 1))()
         if meshes:
-            # deferred vertex normals of these meshes are queued once the sampling is, behind its area sums (the
-            # sampling does not read the normals): they run beside its CDF walk instead of contending with its wide
-            # first passes
+            # deferred vertex normals of these meshes are queued once the sampling is (the sampling does not read the
+            # normals): its chains' first passes are then dispatched ahead of them
             pend = [m._vn for m in meshes if m._vn is not None and m._vn._launch is not None]
             args = (C.cast(jobs, C.c_void_p), len(meshes), n, C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), float(z_min))
             if pend:
                 L.call("ot_mesh_sample_points_min_z_async", *args, D.stream_ptr())
                 try:
-                    after = lambda side: L.call("ot_mesh_sample_points_min_z_after_sums", C.c_void_p(side.cuda_stream))
                     for a in pend:
-                        a._start(after)
+                        a._start()
                 finally:
                     L.call("ot_mesh_sample_points_min_z_wait", len(meshes), kept)
             else:
