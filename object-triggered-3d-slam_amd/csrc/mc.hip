@@ -367,8 +367,10 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
 // Their triangles are the vertex's triangles; walking the cubes in ascending triangle index (unit rank, then the cube's
 // offset inside the unit) and each cube's triangles in table order adds the triangle normals in triangle order --
 // Open3D's loop over the triangles -- with no sort of the 3T corners.  One lane per vertex.
-__device__ inline void mc_vertex_normal(const TsdfDev& d, const McDev& m, int64_t units, const double* __restrict__ V,
-                                        const int32_t* __restrict__ T, int64_t v, double* __restrict__ N) {
+__global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t units, const double* __restrict__ V,
+                                                     const int32_t* __restrict__ T, int64_t nv, double* __restrict__ N) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v >= nv) return;
     const int4 key = m.vk[v];
     const int local = key.w / 3, axis = key.w % 3;
     const int g[3] = {key.x * UNIT_RES + (local >> 8), key.y * UNIT_RES + ((local >> 4) & 15),
@@ -421,15 +423,6 @@ __device__ inline void mc_vertex_normal(const TsdfDev& d, const McDev& m, int64_
     N[v * 3 + 0] = n[0];
     N[v * 3 + 1] = n[1];
     N[v * 3 + 2] = n[2];
-}
-// Grid-stride over the vertices on at most VN_BLOCKS workgroups: the normals of a fresh mesh run beside the sampling
-// of the same object (its chains' wide first passes and single-wave walks), and a quarter of the CUs keeps them from
-// crowding those passes off the chip (r04ae: a full-width launch made the passes' 23 us take 62)
-constexpr int VN_BLOCKS = 64;
-__global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t units, const double* __restrict__ V,
-                                                     const int32_t* __restrict__ T, int64_t nv, double* __restrict__ N) {
-    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nv; v += (int64_t)gridDim.x * 256)
-        mc_vertex_normal(d, m, units, V, T, v, N);
 }
 
 // the extraction's two exclusive scans (triangle and vertex counts per unit, U of each) in one launch: block 0 scans
@@ -725,9 +718,8 @@ ot_status ot_tsdf_mesh_vertex_normals(ot_tsdf* vol, int64_t serial, const double
     mc_layout((char*)mb.ws, mb.ws_units, m);
     m.vk = mb.vk;
     m.tk = mb.tk;
-    const int64_t blocks = (n_vertices + 255) / 256;
-    hipLaunchKernelGGL(k_mc_vnormals, dim3((unsigned)(blocks < VN_BLOCKS ? blocks : VN_BLOCKS)), dim3(256), 0, stream,
-                       vol->dev, m, mb.ws_units, vertices, triangles, n_vertices, out);
+    hipLaunchKernelGGL(k_mc_vnormals, dim3((unsigned)((n_vertices + 255) / 256)), dim3(256), 0, stream, vol->dev, m,
+                       mb.ws_units, vertices, triangles, n_vertices, out);
     OT_LAUNCH_CHECK();
     return OT_OK;
 }
