@@ -148,9 +148,10 @@ struct MeshBuffers {
     double* c = nullptr;
     int32_t* t = nullptr;
     int4* vk = nullptr;     // per vertex: owner unit key (x, y, z) and edge bit (local voxel * 3 + axis)
+    int* vown = nullptr;    // per vertex: owner unit id (the vertex-normal walk starts from it: no hash probe)
     int32_t* tk = nullptr;  // per triangle: its cube's unit key (x, y, z)
     int64_t nv = 0, nt = 0;
-    int64_t cap_v = 0, cap_t = 0, cap_vk = 0, cap_tk = 0;
+    int64_t cap_v = 0, cap_t = 0, cap_vk = 0, cap_tk = 0, cap_vown = 0;
 };
 
 }  // namespace ot

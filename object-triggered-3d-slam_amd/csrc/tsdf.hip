@@ -1612,7 +1612,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
     void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, v->mult,
-                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, d.fmask, d.bslots, d.work,
+                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, v->mesh.vown, d.fmask, d.bslots, d.work,
                     v->bframes, v->bdm, v->brgba};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
