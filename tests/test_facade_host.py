@@ -38,3 +38,42 @@ def test_add_never_aliases_operands():
     both = pkg.geometry.PointCloud() + pcd
     np.asarray(both.points)[1, 1] = 99.0
     assert np.asarray(pcd.points)[1, 1] == 4.0
+
+
+def test_deferred_producer_runs_once_before_any_read():
+    """A deferred device producer (compute_vertex_normals of a fresh mesh): queued exactly once, by the first reader
+    (or by ready_event, as sample_points_uniformly does), never again; the `after` hook the sampler passes is called
+    with the producer's stream argument."""
+    import torch
+
+    calls = []
+
+    def launch(after=None):
+        calls.append(after)
+        return None  # no completion event: complete in stream order (CPU tensors here)
+
+    a = pkg.geometry._Arr(dev=torch.arange(6, dtype=torch.float64).reshape(2, 3), launch=launch)
+    assert len(a) == 2 and calls == []  # the length needs no launch
+    assert a.ready_event() is None and len(calls) == 1
+    assert np.asarray(a.host())[1, 2] == 5.0 and len(calls) == 1  # read: no second launch
+    b = pkg.geometry._Arr(dev=torch.zeros((1, 3), dtype=torch.float64), launch=launch)
+    marker = object()
+    b._start(marker)
+    b._start(marker)
+    assert calls[1:] == [marker]
+
+
+def test_mesh_views_settle_deferred_normals_first():
+    """TriangleMesh.vertices / .triangles views are writable and their edits reach the device copy in place, which the
+    deferred normals read: taking a view queues the normals first (and the current stream waits for them)."""
+    import torch
+
+    order = []
+    m = pkg.geometry.TriangleMesh(np.zeros((3, 3)), np.array([[0, 1, 2]], np.int32))
+    m._vn = pkg.geometry._Arr(dev=torch.zeros((3, 3), dtype=torch.float64),
+                              launch=lambda after=None: order.append("normals"))
+    np.asarray(m.vertices)
+    order.append("view")
+    assert order == ["normals", "view"]
+    np.asarray(m.triangles)
+    assert order == ["normals", "view"]  # once
