@@ -369,12 +369,6 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
 // Their triangles are the vertex's triangles; walking the cubes in ascending triangle index (unit rank, then the cube's
 // offset inside the unit) and each cube's triangles in table order adds the triangle normals in triangle order --
 // Open3D's loop over the triangles -- with no sort of the 3T corners.  One lane per vertex.
-// The walk is one lane's chain of dependent loads (round 4: ~45 us per vertex at low occupancy, r04af), so its loads
-// issue in phases: the owner id (stored by the emission, no hash probe) -> the 4 cubes' neighbour ids -> their cube
-// bytes, ranks and in-unit triangle offsets -> their triangle bases; then per cube (in triangle order) the rows of its
-// triangles that contain the edge, then their corners.  The 4 edges along each axis are a fixed table (no register
-// array indexed at run time).
-__constant__ unsigned char c_axis_edges[3][4] = {{0, 2, 4, 6}, {1, 3, 5, 7}, {8, 9, 10, 11}};
 __global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t units, const double* __restrict__ V,
                                                      const int32_t* __restrict__ T, int64_t nv, double* __restrict__ N) {
     const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -383,71 +377,48 @@ __global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t
     const int local = key.w / 3, axis = key.w % 3;
     const int g[3] = {key.x * UNIT_RES + (local >> 8), key.y * UNIT_RES + ((local >> 4) & 15),
                       key.z * UNIT_RES + (local & 15)};
+    long long start[4];
+    int cubev[4], edge[4];
+    int nc = 0;
     const int owner = m.vown ? m.vown[v] : find_unit(d, key.x, key.y, key.z);  // the emission's owner id: no probe
     if (owner < 0 || owner >= units) return;  // cannot happen for a vertex of this extraction
-    int edge[4], id[4], ci[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int e = c_axis_edges[axis][k];
+    for (int e = 0; e < 12; ++e) {
+        if (c_eshift[e][3] != axis) continue;
         const int c[3] = {g[0] - c_eshift[e][0], g[1] - c_eshift[e][1], g[2] - c_eshift[e][2]};
         // the cube's unit is the owner or one of its -x/-y/-z neighbours (arithmetic shift: floor for negatives)
         const int ox = key.x - (c[0] >> 4), oy = key.y - (c[1] >> 4), oz = key.z - (c[2] >> 4);
-        edge[k] = e;
-        ci[k] = ((c[0] & 15) * 16 + (c[1] & 15)) * 16 + (c[2] & 15);
-        id[k] = m.nbr[owner * 16 + 8 + (ox << 2 | oy << 1 | oz)];
+        const int id = m.nbr[owner * 16 + 8 + (ox << 2 | oy << 1 | oz)];
+        if (id < 0 || id >= units) continue;
+        const int ci = ((c[0] & 15) * 16 + (c[1] & 15)) * 16 + (c[2] & 15);
+        const int cube = m.cubes[(size_t)id * UNIT_VOX + ci];
+        if (cube == 0) continue;
+        start[nc] = m.tri_base[m.rank_of[id]] + m.ctri[(size_t)id * UNIT_VOX + ci];
+        cubev[nc] = cube;
+        edge[nc] = e;
+        ++nc;
     }
-    int cubev[4], rk[4], ct[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const bool ok = id[k] >= 0 && id[k] < units;
-        cubev[k] = ok ? (int)m.cubes[(size_t)id[k] * UNIT_VOX + ci[k]] : 0;
-        rk[k] = ok ? m.rank_of[id[k]] : 0;
-        ct[k] = ok ? (int)m.ctri[(size_t)id[k] * UNIT_VOX + ci[k]] : 0;
-    }
-    long long start[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) start[k] = cubev[k] ? m.tri_base[rk[k]] + ct[k] : 0x7FFFFFFFFFFFFFFFll;
-    // ascending triangle index (a 4-input sorting network; empty cubes sort last)
-#define OT_VN_SWAP(a, b)                                       \
-    if (start[b] < start[a]) {                                 \
-        const long long ts = start[a];                         \
-        start[a] = start[b], start[b] = ts;                    \
-        const int tc = cubev[a];                               \
-        cubev[a] = cubev[b], cubev[b] = tc;                    \
-        const int te = edge[a];                                \
-        edge[a] = edge[b], edge[b] = te;                       \
-    }
-    OT_VN_SWAP(0, 1)
-    OT_VN_SWAP(2, 3)
-    OT_VN_SWAP(0, 2)
-    OT_VN_SWAP(1, 3)
-    OT_VN_SWAP(1, 2)
-#undef OT_VN_SWAP
+    // ascending triangle index (<= 4 cubes: insertion sort)
+    for (int i = 1; i < nc; ++i)
+        for (int j = i; j > 0 && start[j] < start[j - 1]; --j) {
+            const long long ts = start[j];
+            start[j] = start[j - 1], start[j - 1] = ts;
+            const int tc = cubev[j];
+            cubev[j] = cubev[j - 1], cubev[j - 1] = tc;
+            const int te = edge[j];
+            edge[j] = edge[j - 1], edge[j - 1] = te;
+        }
     double n[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (cubev[i]) {  // empty cubes sorted last
-            const int cube = cubev[i], e = edge[i];
-            // the cube's table triangles (<= 5, in order) that contain the edge: rows, then corners, then the sum
-            bool has[5];
-            int row[5][3];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const int t0 = c_tri[cube][3 * k], t1 = c_tri[cube][3 * k + 1], t2 = c_tri[cube][3 * k + 2];
-                has[k] = t0 != -1 && (t0 == e || t1 == e || t2 == e);
-                const long long tri = start[i] + k;
-#pragma unroll
-                for (int r = 0; r < 3; ++r) row[k][r] = has[k] ? T[tri * 3 + r] : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < 5; ++k)
-                if (has[k]) {
-                    double tn[3];
-                    triangle_normal(V, row[k][0], row[k][1], row[k][2], tn);
-                    n[0] += tn[0];
-                    n[1] += tn[1];
-                    n[2] += tn[2];
-                }
+    for (int i = 0; i < nc; ++i) {
+        long long tri = start[i];
+        for (int k = 0; k < 15 && c_tri[cubev[i]][k] != -1; k += 3, ++tri) {
+            const int e = edge[i];
+            if (c_tri[cubev[i]][k] != e && c_tri[cubev[i]][k + 1] != e && c_tri[cubev[i]][k + 2] != e) continue;
+            double tn[3];
+            triangle_normal(V, T[tri * 3], T[tri * 3 + 1], T[tri * 3 + 2], tn);
+            n[0] += tn[0];
+            n[1] += tn[1];
+            n[2] += tn[2];
         }
     }
     finish_vertex_normal(n);
