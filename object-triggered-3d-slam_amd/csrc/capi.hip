@@ -91,24 +91,6 @@ __global__ __launch_bounds__(64) void k_store_blob(ArgBlob b, unsigned long long
     for (int i = threadIdx.x; i < words; i += 64) dst[i] = b.w[i];
 }
 
-ot_status spin_event(hipEvent_t e) {
-    while (true) {
-        const hipError_t st = hipEventQuery(e);
-        if (st == hipSuccess) return OT_OK;
-        if (st != hipErrorNotReady) OT_HIP_TRY(st);
-        __builtin_ia32_pause();
-    }
-}
-
-ot_status spin_stream(hipStream_t s) {
-    while (true) {
-        const hipError_t st = hipStreamQuery(s);
-        if (st == hipSuccess) return OT_OK;
-        if (st != hipErrorNotReady) OT_HIP_TRY(st);
-        __builtin_ia32_pause();
-    }
-}
-
 ot_status upload_small(void* dst, const void* src, size_t bytes, hipStream_t stream) {
     if (bytes == 0) return OT_OK;
     if (bytes > UPLOAD_ARG_BYTES || ((uintptr_t)dst & 7)) {

@@ -45,10 +45,6 @@ ot_status upload_small(void* dst, const void* src, size_t bytes, hipStream_t str
 struct ArgBlob {
     unsigned long long w[UPLOAD_ARG_BYTES / 8];
 };
-// host waits on the single-object chain's read-backs by polling (hipEventQuery / hipStreamQuery) instead of the
-// runtime's blocking wait, whose wake-up after a millisecond-long wait lands tens of microseconds late
-ot_status spin_event(hipEvent_t e);
-ot_status spin_stream(hipStream_t s);
 // device allocations made by the library's grow-only buffers so far (scratch arenas, filter handles): a timed
 // region that allocates shows up as a change (bench.py reports it; test hook otx_alloc_count)
 void note_alloc();

@@ -571,8 +571,7 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
         OT_HIP_TRY(hipEventRecord(vol->ev_mail, stream));
         st = spec(m);
         if (st != OT_OK) return st;
-        st = spin_event(vol->ev_mail);
-        if (st != OT_OK) return st;
+        OT_HIP_TRY(hipEventSynchronize(vol->ev_mail));
     } else {
         OT_HIP_TRY(hipStreamSynchronize(stream));
     }

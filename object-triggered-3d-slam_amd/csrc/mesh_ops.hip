@@ -1209,8 +1209,7 @@ static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, i
     return OT_OK;
 }
 static ot_status min_z_wait(hipStream_t hs, int32_t n_jobs, int64_t* n_kept_host) {
-    const ot_status st = spin_stream(hs);  // the kept counts (written by each job's last tile)
-    if (st != OT_OK) return st;
+    OT_HIP_TRY(hipStreamSynchronize(hs));  // the kept counts (written by each job's last tile)
     const long long* kept = (const long long*)pinned_scratch(sizeof(long long) * (size_t)n_jobs, 1, true);
     for (int j = 0; j < n_jobs; ++j) n_kept_host[j] = kept[j];
     return OT_OK;

@@ -1470,8 +1470,7 @@ ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) 
     int c[N_COUNTERS];  // error flags and the unit count in one read-back (the pinned mailbox)
     if (vol->early_frame == vol->frame_id && !vol->imported && vol->ev_early) {
         // mailed by the last batch's units kernel: wait for that kernel only, not for the integrate behind it
-        st = spin_event(vol->ev_early);
-        if (st != OT_OK) return st;
+        OT_HIP_TRY(hipEventSynchronize(vol->ev_early));
         std::memcpy(c, vol->hmail + OT_MAIL_WORDS, sizeof(c));
     } else {
         MailSrc ms;
