@@ -103,6 +103,38 @@ def main(normals=True):
         marks.append(np.diff(np.array(t)) * 1e6)
     med = np.median(np.array(marks[1:]), axis=0)
     print("host us per call (integrate, extract, normals, sample, final sync):", [round(float(x), 1) for x in med])
+    # the host's work between the extraction's return and the sampling's first launch, piece by piece (the sampler call
+    # of TriangleMesh.sample_points_min_z_batch unrolled here)
+    D = importlib.import_module(PKG + "._device")
+    parts = []
+    for _ in range(6):
+        torch.cuda.synchronize()
+        vol.reset()
+        lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
+        mesh = vol.extract_triangle_mesh()
+        t = [time.perf_counter()]
+        mesh.compute_vertex_normals()
+        t.append(time.perf_counter())
+        P = D.empty((100000, 3), "float64")
+        PC = D.empty((100000, 3), "float64")
+        t.append(time.perf_counter())
+        jobs = (L.ot_mesh_sample_job * 1)()
+        jobs[0] = L.ot_mesh_sample_job(D.ptr(mesh._v.dev()), None, D.ptr(mesh._vc.dev()), len(mesh._v),
+                                       D.ptr(mesh._t.dev()), len(mesh._t), D.ptr(P), None, D.ptr(PC))
+        kept = (C.c_int64 * 1)()
+        t.append(time.perf_counter())
+        L.call("ot_mesh_sample_points_min_z_async", C.cast(jobs, C.c_void_p), 1, 100000, C.c_uint64(0), 0.03,
+               D.stream_ptr())
+        t.append(time.perf_counter())
+        if normals:
+            mesh._vn._start()
+        t.append(time.perf_counter())
+        L.call("ot_mesh_sample_points_min_z_wait", 1, kept)
+        torch.cuda.synchronize()
+        parts.append(np.diff(np.array(t)) * 1e6)
+    med = np.median(np.array(parts[1:]), axis=0)
+    print("host us after the extraction (normals call, output allocs, job table, sampler enqueue, normals launch):",
+          [round(float(x), 1) for x in med])
     print("stream priority range (least, greatest):", torch.cuda.Stream.priority_range())
     print("single object ms (median of last 5)" + ("" if normals else ", WITHOUT normals") + ":", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
     # the volume's size against configs[1]'s (integrate occupancy): units, voxel updates, unit integrations
