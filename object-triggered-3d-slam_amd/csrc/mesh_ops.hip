@@ -999,11 +999,11 @@ ot_status ot_mesh_sample_points_uniformly_batch(const ot_mesh_sample_job* jobs, 
 }  // extern "C"
 
 namespace ot {
-// The sampler's kernels run on a per-thread stream of the device's greatest priority, forked from and synchronised
-// before returning to the caller's stream: its latency chain (the chains' wide passes and single-wave walks) is
-// dispatched ahead of independent work the caller queued elsewhere (a fresh mesh's vertex normals on a side stream),
-// which fills the walks' idle CUs instead.  The entry points synchronise on return, so nothing later on the caller's
-// stream can overtake them.
+// The fused sampler runs on the caller's stream.  (Until late round 4 it ran on a per-thread stream of the device's
+// greatest priority, forked from the caller's, so that a fresh mesh's vertex normals queued elsewhere were dispatched
+// behind its chain; with the normals deferred until the sampling is queued, the fork's cross-queue latency is all that
+// remained of it.  Test hook otx_sampler_hi_stream(1) restores it for A/B timing.)
+static bool g_sampler_hi = false;
 struct HiStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr;
@@ -1150,13 +1150,15 @@ ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs, 
 }  // extern "C"
 
 namespace ot {
-// The fused sampler's launches on this thread's greatest-priority stream; the kept counts land in pinned slot 1 once it
-// drains.  *hs: that stream.
+// The fused sampler's launches (on the caller's stream); the kept counts land in pinned slot 1 once it drains.  *hs:
+// the stream to wait on.
 static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
                                double z_min, void* stream_, hipStream_t* hs) {
-    hipStream_t stream = nullptr;
-    ot_status fst = hi_stream_fork(S(stream_), &stream);
-    if (fst != OT_OK) return fst;
+    hipStream_t stream = S(stream_);
+    if (g_sampler_hi) {
+        ot_status fst = hi_stream_fork(S(stream_), &stream);
+        if (fst != OT_OK) return fst;
+    }
     if (n_points > ((int64_t)1 << 40)) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many points");
     const int64_t tiles64 = (n_points + MZ_TILE - 1) / MZ_TILE;
     if (tiles64 > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many points");
@@ -1248,6 +1250,12 @@ ot_status ot_mesh_sample_points_min_z_async(const ot_mesh_sample_job* jobs, int3
     if (st != OT_OK) return st;
     g_minz.s = hs;
     g_minz.n_jobs = n_jobs;
+    return OT_OK;
+}
+
+// test hook (not part of the drop-in boundary): 1 = the fused sampler on a greatest-priority stream (A/B timing)
+ot_status otx_sampler_hi_stream(int32_t on) {
+    g_sampler_hi = on != 0;
     return OT_OK;
 }
 

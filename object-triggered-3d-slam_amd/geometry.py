@@ -570,11 +570,13 @@ class TriangleMesh:
             torch = D.torch
             cur = torch.cuda.current_stream()
             vref, serial = mc[0], mc[1]
+            made = torch.cuda.Event()  # the arrays are complete here: the launch waits for this point of `cur` only,
+            made.record(cur)           # not for the sampling queued on `cur` after it
 
             def launch(after=None):
                 v = vref()
                 side = _streams.side_stream(cur)
-                side.wait_stream(cur)
+                side.wait_event(made)
                 if after is not None:
                     after(side)
                 st = L.OT_ERR_INVALID_ARGUMENT

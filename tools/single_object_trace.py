@@ -56,6 +56,8 @@ def main(normals=True):
     pkg = importlib.import_module(PKG)
     L = importlib.import_module(PKG + "._lib")
     lib = L.load()
+    if "--hi" in sys.argv:  # A/B: the fused sampler on a greatest-priority stream, as before late round 4
+        L.call("otx_sampler_hi_stream", 1)
     intr_t = synth.REF_INTRINSICS_640
     W, H = intr_t[0], intr_t[1]
     intr = L.ot_intrinsics(W, H, *intr_t[2:])
@@ -136,7 +138,8 @@ def main(normals=True):
     print("host us after the extraction (normals call, output allocs, job table, sampler enqueue, normals launch):",
           [round(float(x), 1) for x in med])
     print("stream priority range (least, greatest):", torch.cuda.Stream.priority_range())
-    print("single object ms (median of last 5)" + ("" if normals else ", WITHOUT normals") + ":", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
+    print("single object ms (median of last 5)" + ("" if normals else ", WITHOUT normals") +
+          (", sampler on the greatest-priority stream" if "--hi" in sys.argv else "") + ":", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
     # the volume's size against configs[1]'s (integrate occupancy): units, voxel updates, unit integrations
     vol.reset()
     lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
