@@ -1013,7 +1013,8 @@ static thread_local HiStream g_hi;
 // ot_mesh_sample_points_min_z_async's pending call on this thread: its tables live in this thread's scratch slot 17 and
 // pinned slots 0 / 1 until ot_mesh_sample_points_min_z_wait, so no other sampling may start on the thread before
 struct MinZPending {
-    hipStream_t s = nullptr;
+    bool active = false;
+    hipStream_t s = nullptr;  // may be the null (default) stream
     int32_t n_jobs = 0;
 };
 static thread_local MinZPending g_minz;
@@ -1041,7 +1042,7 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
                              const std::function<void(char*, char*)>& fill, size_t zero_off, size_t zero_bytes,
                              hipStream_t stream, std::vector<double*>& cdf, std::vector<long long*>& ncum,
                              char** extra_dev) {
-    if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
+    if (g_minz.active) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     size_t bytes = 256;
     int64_t max_nt = 0;
     for (int j = 0; j < n_jobs; ++j) {
@@ -1232,7 +1233,7 @@ ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs, int32_t n_
     if (st != OT_OK) return st;
     if (n_jobs > 0 && !n_kept_host) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] invalid jobs");
     if (n_jobs == 0) return OT_OK;
-    if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
+    if (g_minz.active) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     hipStream_t hs = nullptr;
     st = min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, stream, &hs);
     if (st != OT_OK) return st;
@@ -1243,11 +1244,12 @@ ot_status ot_mesh_sample_points_min_z_async(const ot_mesh_sample_job* jobs, int3
                                             uint64_t seed, double z_min, void* stream) {
     ot_status st = min_z_args(jobs, n_jobs, n_points);
     if (st != OT_OK) return st;
-    if (g_minz.s) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
+    if (g_minz.active) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     if (n_jobs == 0) return OT_OK;
     hipStream_t hs = nullptr;
     st = min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, stream, &hs);
     if (st != OT_OK) return st;
+    g_minz.active = true;
     g_minz.s = hs;
     g_minz.n_jobs = n_jobs;
     return OT_OK;
@@ -1260,8 +1262,8 @@ ot_status otx_sampler_hi_stream(int32_t on) {
 }
 
 ot_status ot_mesh_sample_points_min_z_wait(int32_t n_jobs, int64_t* n_kept_host) {
-    if (n_jobs == 0 && !g_minz.s) return OT_OK;
-    if (!g_minz.s || n_jobs != g_minz.n_jobs || !n_kept_host)
+    if (n_jobs == 0 && !g_minz.active) return OT_OK;
+    if (!g_minz.active || n_jobs != g_minz.n_jobs || !n_kept_host)
         return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] no pending async sampling of n_jobs jobs");
     const hipStream_t hs = g_minz.s;
     g_minz = MinZPending{};
