@@ -120,7 +120,6 @@ __global__ __launch_bounds__(256) void k_tri_areas_blob(const double* __restrict
 //   k_chain_chunk  M_b = sum r_t at u_b = 2^(e_b-52), flag ties / negative / non-finite / r >= 2^53
 //   k_chain_runs   runs = maximal stretches of unflagged chunks with one guessed binade (a flagged chunk is a run
 //                  of its own): the inclusive prefix of M_b inside each run and every chunk's run end, in parallel
-//                  (the first phase of the staged walk's own workgroup whenever the metadata fits LDS)
 //   k_chain_walk   one wave per chain, one step per RUN instead of per 64 chunks: from the exact s (N = s / u) it
 //                  accepts the longest stretch [b, k] of the run with e(s) == e_b and N + prefix <= 2^53 - 1
 //                  (every intermediate sum stays inside the binade: the prefix is monotone, so the run end decides
@@ -404,8 +403,7 @@ __device__ inline long long sat_add(long long a, long long b) {
 }
 
 constexpr int RUN_ITEMS = 4;  // consecutive chunks per thread: a 1024-thread tile covers 4096 chunks
-// one 1024-thread workgroup per chain (k_chain_runs, or the staged walk's own first phase)
-__device__ inline void chain_runs_block(const ChainJob& j) {
+__global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict__ jobs) {
     __shared__ long long s_wv[16];
     __shared__ int s_wh[16];
     __shared__ long long s_cin[16];
@@ -413,6 +411,7 @@ __device__ inline void chain_runs_block(const ChainJob& j) {
     __shared__ int s_nin[16];
     __shared__ long long s_carry;
     __shared__ int s_next;
+    const ChainJob j = jobs[blockIdx.x];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int64_t nb = (j.n + CH - 1) / CH;
     constexpr int TILE = 1024 * RUN_ITEMS;
@@ -516,10 +515,6 @@ __device__ inline void chain_runs_block(const ChainJob& j) {
         __syncthreads();
     }
 }
-__global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict__ jobs) {
-    const ChainJob j = jobs[blockIdx.x];
-    chain_runs_block(j);
-}
 
 // The walk's per-chunk metadata (ex, run end, run prefix, kind), staged in LDS by the whole workgroup before the one
 // walking wave starts: every walk step then reads LDS instead of making dependent global round trips (the walk is a
@@ -559,11 +554,7 @@ template <bool CDF, bool STAGED>
 __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict__ jobs) {
     const ChainJob j = jobs[blockIdx.x];
     const int64_t nb = (j.n + CH - 1) / CH;
-    if constexpr (STAGED) {  // the whole workgroup finds the runs, stages the metadata, then one wave walks
-        // the runs (k_chain_runs' pass) in this launch: one launch fewer on the chain; the emit reads pre from HBM
-        chain_runs_block(j);
-        __threadfence_block();
-        __syncthreads();
+    if constexpr (STAGED) {  // the whole workgroup stages the metadata, then one wave walks
         signed char* s_kind = reinterpret_cast<signed char*>(s_walk_meta + nb);
         for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
             const unsigned long long pv = (unsigned long long)j.pre[b];
@@ -715,8 +706,8 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
         hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(1024), 0, stream, djobs);
         hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
     }
-    // metadata staged in LDS when every job's chunks fit (max_n bounds them all); that walk finds the runs itself
-    if (nb > WALK_LDS_CHUNKS) hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
+    hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
+    // metadata staged in LDS when every job's chunks fit (max_n bounds them all)
     if (nb <= WALK_LDS_CHUNKS) {
         const size_t lds_bytes = (size_t)nb * 17 + 16;
         static std::atomic<bool> attr_set[2] = {false, false};
