@@ -8,14 +8,15 @@ reconstruct_rgbd_filter.py:154-155) => weak scaling, no data-path collective; ba
 timing.  Prints ONE JSON line on rank 0.
 
 Also reported:
-  roofline     — dominant kernel (k_batch_integrate<true>, float64 colour): algorithmic bytes per launch (5*W*H + 40*U_f)
-                 over its mean device time measured with HIP events on the launch stream (`frac` = `frac_effective`:
-                 temporal blocking keeps voxel state on chip across a batch, so it may exceed 1), and the measured HBM
-                 bytes per launch from rocprofv3 PMC counters (profiles/pmc_traffic.json, used only when its source
-                 hash and workload match this build) over the same time (`hbm_frac`);
+  roofline     — dominant kernel (k_batch_integrate<true>, float64 colour): the measured HBM bytes per launch from
+                 rocprofv3 PMC counters (profiles/pmc_traffic.json, used only when its source hash and workload match
+                 this build) over its mean device time measured with HIP events on the launch stream (`frac`, physical,
+                 <= 1); beside it `frac_effective` = algorithmic bytes per launch (5*W*H + 40*U_f) over
+                 the same time (temporal blocking keeps voxel state on chip across a batch, so it may exceed 1) and the
+                 VALU / TA / TD busy fractions that bind the kernel;
   cpu_baseline — the CPU oracle (strict-IEEE restatement of Open3D's ScalableTSDFVolume, OpenMP where Open3D
-                 places it) on a bounded sample of the same frames, rank 0 only: 1 warm-up, median of 5 passes;
-  sustained    — the headline step repeated for >= 1.5 s after the timed steps (corroborates `value`);
+                 places it) on all 256 frames of the same scan, rank 0 only: 1 warm-up, median of 3 passes;
+  sustained    — the headline step repeated for >= 12 s after the timed steps (corroborates `value`);
   filtered     — configs[2]: 512 distinct 1280x720 frames through the batched device-resident chain
                  (ot_rgbd_filter_run), Mpoints/s;
   objects / hybrid_map / single_frame / spatial — configs[3], [4], [0] and single-object sharding (N > 1).
@@ -51,7 +52,9 @@ def parse():
     ap.add_argument("--sdf-trunc", type=float, default=0.04)
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
     ap.add_argument("--cpu-frames", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--sustain", type=float, default=1.5, help="seconds of sustained headline steps (0 = skip)")
+    ap.add_argument("--sustain", type=float, default=12.0,
+                    help="seconds of sustained headline steps after the timed ones (0 = skip): >= 12 s so a 5-s busy "
+                         "sampler lands in it at least twice")
     ap.add_argument("--color-bits", type=int, default=64, choices=(32, 64),
                     help="headline colour precision: 64 = Open3D's float64 TSDFVoxel::color_ (the C ABI and facade "
                          "default, bit-exact colours); 32 = float32 colour state")
@@ -260,25 +263,36 @@ def main():
     kname = "k_batch_integrate<true>" if args.color_bits == 64 else "k_batch_integrate<false>"
     pmc_cfg = {"voxel": args.voxel, "frames": args.frames, "batch": args.batch, "color_bits": args.color_bits}
     traffic, traffic_note = _traffic(args, L, kname, pmc_cfg)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "frac_effective": round(achieved / HBM_PEAK_GBS, 4),
-                "effective": args.batch != 1,  # voxel state reused on chip across a batch
+    # `frac` is PHYSICAL: HBM bytes the kernel moved per launch (rocprofv3 PMC FETCH_SIZE x measured
+    # correction + WRITE_SIZE, same build and workload) over its launch time.  The algorithmic figure of SURVEY 8(d)
+    # counts a voxel's 40-B read + write once per FRAME, but temporal blocking keeps the state on chip across the
+    # batch, so it is reported apart as `frac_effective` (it may exceed 1: it counts bytes never moved).
+    hbm_achieved = traffic / (kernel_ms_avg * 1e-3) / 1e9 if (traffic and kernel_ms_avg > 0) else None
+    roofline = {"bound": "hbm", "achieved": round(hbm_achieved, 1) if hbm_achieved else None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(hbm_achieved / HBM_PEAK_GBS, 4) if hbm_achieved else None,
                 "traffic": traffic, "traffic_source": traffic_note,
+                "achieved_basis": "PMC HBM bytes per launch (traffic) / kernel_ms_avg" if hbm_achieved else
+                                  "no same-build PMC entry: physical fraction unmeasured",
+                "algorithmic_achieved": round(achieved, 1), "frac_effective": round(achieved / HBM_PEAK_GBS, 4),
+                "effective_note": "algorithmic bytes (5*W*H + 40*U_f per frame, SURVEY 8(d)) / kernel time: voxel state "
+                                  "stays in registers across the batch, so this counts bytes the kernel never moves",
                 "kernel": ("k_integrate" if args.batch == 1 else "k_batch_integrate") +
                           ("<true>" if args.color_bits == 64 else "<false>"),
                 "color_bits": args.color_bits,
                 "kernel_ms_avg": round(kernel_ms_avg, 5), "launches_per_step": klaunch.value,
                 "algorithmic_bytes_per_launch": round(per_launch_bytes),
                 "voxel_updates_per_frame": round(upd.value / args.frames)}
-    if traffic and kernel_ms_avg > 0:  # measured HBM bytes per launch over the same launch time
-        roofline["hbm_achieved"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9, 1)
-        roofline["hbm_frac"] = round(traffic / (kernel_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    if hbm_achieved:  # kept under the old names too (round-3/4 records)
+        roofline["hbm_achieved"] = roofline["achieved"]
+        roofline["hbm_frac"] = roofline["frac"]
     ient, _ = _pmc_entry(args, L, kname, pmc_cfg)
-    if ient and ient.get("valu_busy_frac") is not None:  # the other ceilings: vector-ALU issue and the vector-memory
-        roofline["valu_busy_frac"] = round(ient["valu_busy_frac"], 4)  # address / data path (PMC, same build)
-    for key in ("ta_busy_frac", "td_busy_frac"):
+    # the ceilings that actually bind this kernel: vector-ALU issue and the vector-memory data path (PMC, same build)
+    for key in ("valu_busy_frac", "ta_busy_frac", "td_busy_frac"):
         if ient and ient.get(key) is not None:
             roofline[key] = round(ient[key], 4)
+    if ient and ient.get("valu_busy_frac") is not None:
+        roofline["binding"] = "VALU issue {:.2f} + TD {:.2f} busy (HBM {:.2f})".format(
+            ient["valu_busy_frac"], ient.get("td_busy_frac") or 0.0, roofline["frac"] or 0.0)
     roofline["frontend_ms_per_batch"] = round(fms.value / max(fbatches.value, 1), 5)
     if ient:  # raw counters and the correction applied to them (calibrated on 8-B gathers, tools/fetch_calib.hip)
         roofline["traffic_raw"] = {k: ient.get(k) for k in ("raw_fetch_kib", "raw_write_kib", "fetch_correction",
@@ -892,16 +906,24 @@ def filter_stream(fs):
 
 def _sor_roofline(args, L):
     """The chain's dominant kernel, k_sor_knn (SOR stage 1), against the ceiling that binds it: vector-ALU issue
-    (PMC SQ_ACTIVE_INST_VALU x 4 per SIMD-cycle of the dispatch, same build; tools/pmc.sh runs it on 32-frame
-    batches of the same stream).  Its HBM traffic is reported beside it."""
-    ent, note = _pmc_entry(args, L, "k_sor_knn", {})
+    (PMC SQ_ACTIVE_INST_VALU x 4 per SIMD-cycle of the dispatch, same build; tools/pmc.sh runs it on batches of
+    --filter-batch frames of the same stream -- the entry's workload must say the batch this bench times).  Its HBM
+    traffic per launch is reported beside it, with the algorithmic bytes (12 B per point read + 12 B per kept point,
+    SURVEY 8(d)) when the entry records them."""
+    ent, note = _pmc_entry(args, L, "k_sor_knn", {"batch": args.filter_batch})
     if not ent or ent.get("valu_busy_frac") is None:
         return {"kernel": "k_sor_knn", "bound": "valu", "frac": None, "source": note}
     cyc = ent.get("dispatch_cycles")
-    return {"kernel": "k_sor_knn", "bound": "valu", "frac": round(ent["valu_busy_frac"], 4),
-            "valu_insts_per_launch": ent.get("valu_insts_per_launch"), "frames_per_launch": 32,
-            "dispatch_cycles": round(cyc) if cyc else None,
-            "hbm_bytes_per_launch": ent.get("bytes_per_launch"), "source": note}
+    out = {"kernel": "k_sor_knn", "bound": "valu", "frac": round(ent["valu_busy_frac"], 4),
+           "valu_insts_per_launch": ent.get("valu_insts_per_launch"),
+           "frames_per_launch": ent.get("config", {}).get("batch"),
+           "dispatch_cycles": round(cyc) if cyc else None, "td_busy_frac": ent.get("td_busy_frac"),
+           "hbm_bytes_per_launch": ent.get("bytes_per_launch"), "source": note}
+    if ent.get("config", {}).get("algorithmic_bytes_per_launch"):
+        alg = ent["config"]["algorithmic_bytes_per_launch"]
+        out["algorithmic_bytes_per_launch"] = alg
+        out["traffic_over_algorithmic"] = round(ent["bytes_per_launch"] / alg, 3)
+    return out
 
 
 def _pmc_entry(args, L, kernel, config):

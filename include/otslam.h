@@ -151,7 +151,10 @@ ot_status ot_rgbd_filter_copy(const ot_rgbd_filter* filter, int32_t frame, doubl
 typedef struct ot_tsdf ot_tsdf;
 
 /* ScalableTSDFVolume(voxel_length, sdf_trunc, color_type, volume_unit_resolution=16,
- * depth_sampling_stride=4).  max_units bounds the block pool in HBM (0 = default 32768 units). */
+ * depth_sampling_stride=4).  max_units is the INITIAL block-pool capacity in HBM (0 = default 32768 units): like
+ * Open3D's volume the pool is unbounded -- a batch that needs more units grows the pool and the hash (records copied,
+ * keys rehashed) and its dropped units are integrated again from the staged frames, bit-identical to a large pool;
+ * only a failed device allocation is an error (OT_ERR_HIP, from the integrate / flush call whose batch needed it). */
 ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_type,
                          int32_t volume_unit_resolution, int32_t depth_sampling_stride, int64_t max_units,
                          ot_tsdf** out);

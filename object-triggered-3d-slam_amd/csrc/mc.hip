@@ -526,6 +526,8 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
                           const std::function<ot_status(McDev&)>& spec = nullptr) {
     ot_status st = upload_tables();
     if (st != OT_OK) return st;
+    st = wait_normals(vol, stream);  // the last mesh's deferred normals still read the structure rewritten below
+    if (st != OT_OK) return st;
     int64_t U = 0;
     st = tsdf_sorted_units(vol, stream, &U);
     if (st != OT_OK) return st;
@@ -579,6 +581,9 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
     std::memcpy(totals, vol->hmail, sizeof(totals));
     const int64_t nt = totals[0], nv = totals[1];
     if (nv > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] more than 2^31 vertices");
+    // a speculative emission may still be writing the merge-key buffers that grow() below would free: wait for it
+    // (the stream already waits on the side stream's ev_join) instead of relying on hipFree's implicit synchronisation
+    if (spec && (nv > mb.cap_vk || nv > mb.cap_vown || nt * 3 > mb.cap_tk)) OT_HIP_TRY(hipStreamSynchronize(stream));
     st = grow(mb.vk, mb.cap_vk, nv);  // merge keys: 16 B per vertex, 12 B per triangle
     if (st != OT_OK) return st;
     st = grow(mb.vown, mb.cap_vown, nv);
@@ -616,6 +621,8 @@ static ot_status mc_emit(ot_tsdf* vol, double* V, double* VC, int32_t* T, hipStr
 static ot_status mc_emit_launch(ot_tsdf* vol, McDev m, int64_t nv, double* V, double* VC, int32_t* T,
                                 hipStream_t stream) {
     const unsigned g = (unsigned)vol->mesh.ws_units;
+    ot_status st = wait_normals(vol, stream);  // the emission rewrites vk / vown, which deferred normals read
+    if (st != OT_OK) return st;
     if (!vol->side) {
         OT_HIP_TRY(hipStreamCreateWithFlags(&vol->side, hipStreamNonBlocking));
         OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_fork, hipEventDisableTiming));
@@ -730,6 +737,12 @@ ot_status ot_tsdf_mesh_vertex_normals(ot_tsdf* vol, int64_t serial, const double
     hipLaunchKernelGGL(k_mc_vnormals, dim3((unsigned)((n_vertices + 255) / 256)), dim3(256), 0, stream, vol->dev, m,
                        mb.ws_units, vertices, triangles, n_vertices, out);
     OT_LAUNCH_CHECK();
+    // the walk reads the structure on `stream` (often a side stream of the caller's): later work on the volume that
+    // rewrites the structure or the units waits for this point first (wait_normals in mc_count, the emission,
+    // integrate, reset, growth)
+    if (!vol->ev_normals) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_normals, hipEventDisableTiming));
+    OT_HIP_TRY(hipEventRecord(vol->ev_normals, stream));
+    vol->normals_pending = true;
     return OT_OK;
 }
 

@@ -3,13 +3,13 @@
 // HBM layout (one allocation per field group, sized at create time):
 //   hash table  : open addressing, linear probing, capacity = pow2 >= 4 * max_units
 //                 hkeys u64 (packed int3 unit key, KEY_EMPTY = ~0), hvals i32 (unit id, -1 = not allocated),
-//                 stamp i32 (last frame that touched the slot)
+//                 fmask u64 (frames of the current batch touching the unit)
 //   unit pool   : max_units blocks of 16^3 voxels, field-planar inside a block:
 //                 vox[id][field][z][x*16 + y], field = {tsdf, weight, r, g, b} (f32).  One 256-lane
 //                 workgroup owns a block; lane (x, y) walks z, so every z step is one coalesced 1-KiB row
 //                 per field (the per-column z walk is what reproduces Open3D's incremental float math).
 //   unit_keys   : int32 [max_units][3]
-//   touched     : per-frame list of unit ids (bit 31 = freshly allocated this frame => state starts at 0)
+// max_units and the hash capacity grow on demand (tsdf.hip grow_pool): Open3D's volume is unbounded.
 #pragma once
 
 #include <vector>
@@ -25,7 +25,7 @@ constexpr int UNIT_FLOATS = UNIT_FIELDS * UNIT_VOX;  // float32 colour record: 2
 constexpr int UNIT_FLOATS_C64 = 8 * UNIT_VOX;        // float64 colour record: tsdf, weight (f32) + r, g, b (f64) = 128 KiB
 
 // counters[] slots
-constexpr int C_TOUCHED = 0;   // units touched by the current frame
+constexpr int C_UNUSED0 = 0;  // (was the per-frame path's touched count)
 constexpr int C_UNITS = 1;     // units allocated
 constexpr int C_OVERFLOW = 2;  // pool exhausted (units dropped)
 constexpr int C_HASHERR = 3;   // hash full or key out of range
@@ -42,8 +42,6 @@ constexpr int S_UNIT_INTEGRATIONS = 1;
 struct TsdfDev {
     unsigned long long* hkeys;
     int* hvals;
-    int* stamp;
-    int* touched;
     int* counters;
     unsigned long long* stats;
     int* unit_keys;
@@ -161,7 +159,7 @@ struct ot_tsdf {
     double voxel_length = 0.0, sdf_trunc = 0.0, unit_length = 0.0;
     int color_type = 1, stride = 4;
     bool color64 = false;  // colour state in float64 (Open3D's Vector3d) instead of float32
-    int64_t max_units = 0;
+    int64_t max_units = 0;  // current pool capacity (grows: grow_pool)
     int64_t hash_cap = 0;
     ot::TsdfDev dev{};
     int frame_id = 0;
@@ -170,9 +168,6 @@ struct ot_tsdf {
     float* mult = nullptr;
     ot_intrinsics mult_intr{};
     bool mult_valid = false;
-    // float depth staging for the u16 path
-    float* depth_f = nullptr;
-    int64_t depth_f_cap = 0;
     // batching of integrate_u16: frames per fused launch (ot_tsdf_set_batch; 64 = MAX_BATCH, measured best, §4)
     int batch_max = ot::MAX_BATCH;
     std::vector<ot::PendingFrame> pending;
@@ -203,6 +198,10 @@ struct ot_tsdf {
     // a second stream for independent extraction stages (vertex positions beside triangle indices), fork / join
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // deferred vertex normals (ot_tsdf_mesh_vertex_normals on the caller's side stream) read the marching-cubes
+    // structure (mesh.ws, vk, vown): work that rewrites it or the units waits for this event first (wait_normals)
+    hipEvent_t ev_normals = nullptr;
+    bool normals_pending = false;
     // kernel timing (events around the dominant integration kernel)
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
@@ -224,4 +223,6 @@ struct MailSrc {
 };
 ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream);
 ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream);
+// order `stream` after the volume's deferred vertex normals, if any are still in flight
+ot_status wait_normals(ot_tsdf* vol, hipStream_t stream);
 }  // namespace ot

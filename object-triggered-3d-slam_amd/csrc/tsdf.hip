@@ -1,5 +1,5 @@
-// tsdf.hip — ScalableTSDFVolume on MI355X: GPU block hash + block pool in HBM, per-frame touched-unit
-// detection and block-parallel integration.
+// tsdf.hip — ScalableTSDFVolume on MI355X: GPU block hash + block pool in HBM, batched touched-unit detection and
+// temporally blocked integration.
 //
 // Reference semantics (Open3D ScalableTSDFVolume::Integrate and
 // UniformTSDFVolume::IntegrateWithDepthToCameraDistanceMultiplier), called from
@@ -9,12 +9,10 @@
 //   (ii)  stride-4 unprojection with camera_pose = inverse(extrinsic) in float64
 //   (iii) touched units = union over samples of [floor((p - trunc)/L), floor((p + trunc)/L)]^3
 //   (iv)  per touched unit, per voxel: project, sample depth, sdf update — all f32, z walked incrementally.
-// Kernels
-//   k_touch     : one lane per stride sample; hash find-or-insert (CAS), per-slot frame stamp (atomicExch)
-//                 so each unit is listed once per frame; new units take a pool id (atomicAdd).
-//   k_integrate : one 256-lane workgroup per touched unit (persistent grid-stride over the touched list),
-//                 lane = (x, y) column, z loop in order.  Fresh units start from zero in registers and are
-//                 written whole (no pool memset); old units read/write only the voxels that update.
+// Every flush is a batch of 1..64 frames (a single frame is a batch of one): k_batch_touch -> k_batch_units ->
+// k_batch_integrate, below.  The unit pool is unbounded like Open3D's: when a batch needs more units than the pool
+// holds, the pool and the hash grow (records copied, keys rehashed) and the batch's dropped units are integrated
+// again from its staged frames (settle_batch), so the result is the one an unbounded pool gives.
 #include <algorithm>
 #include <cstring>
 #include <type_traits>
@@ -24,15 +22,6 @@
 #include "tsdf.h"
 
 namespace ot {
-
-struct TouchParams {
-    const float* depth;
-    int W, H, stride, ws, hs;
-    double fx, fy, cx, cy;
-    Mat4d pose;
-    double trunc, unit_len;
-    int frame;
-};
 
 struct IntegrateParams {
     const float* depth;
@@ -91,179 +80,6 @@ __device__ inline int hash_find(const TsdfDev& d, unsigned long long key) {
         slot = (slot + 1) & (unsigned)d.hash_mask;
     }
     return -1;
-}
-
-// Mark unit `key` touched by frame p.frame; append it to the touched list the first time.
-__device__ inline void touch_unit(const TsdfDev& d, int frame, int x, int y, int z) {
-    if (!key_in_range(x, y, z)) {
-        atomicOr(&d.counters[C_HASHERR], 2);
-        return;
-    }
-    const unsigned long long key = pack_key(x, y, z);
-    if (!unit_owned(d, key)) return;
-    const int slot = hash_insert(d, key);
-    if (slot < 0) {
-        atomicOr(&d.counters[C_HASHERR], 1);
-        return;
-    }
-    if (d.stamp[slot] == frame) return;  // fast path; a stale read only costs the atomic below
-    if (atomicExch(&d.stamp[slot], frame) == frame) return;
-    int id = d.hvals[slot];
-    int fresh = 0;
-    if (id < 0) {
-        id = atomicAdd(&d.counters[C_UNITS], 1);
-        if (id >= d.max_units) {
-            atomicOr(&d.counters[C_OVERFLOW], 1);
-            return;
-        }
-        d.hvals[slot] = id;
-        d.unit_keys[id * 3 + 0] = x;
-        d.unit_keys[id * 3 + 1] = y;
-        d.unit_keys[id * 3 + 2] = z;
-        fresh = 1;
-        note_unit_key(d, x, y, z);
-    }
-    const int pos = atomicAdd(&d.counters[C_TOUCHED], 1);
-    d.touched[pos] = fresh ? (int)((unsigned)id | 0x80000000u) : id;
-}
-
-__global__ __launch_bounds__(256) void k_touch(TouchParams p, TsdfDev d) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
-    if (s >= p.ws * p.hs) return;
-    const int r = (s / p.ws) * p.stride, c = (s % p.ws) * p.stride;
-    const float df = p.depth[(int64_t)r * p.W + c];
-    if (!(df > 0.0f)) return;
-    const double z = (double)df;
-    const double x = ((double)c - p.cx) * z / p.fx;
-    const double y = ((double)r - p.cy) * z / p.fy;
-    double q[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const double a = p.pose.m[k * 4 + 0] * x;
-        const double b = p.pose.m[k * 4 + 1] * y;
-        const double cc = p.pose.m[k * 4 + 2] * z;
-        q[k] = ((a + b) + cc) + p.pose.m[k * 4 + 3];
-    }
-    int lo[3], hi[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        lo[k] = (int)floor((q[k] - p.trunc) / p.unit_len);
-        hi[k] = (int)floor((q[k] + p.trunc) / p.unit_len);
-    }
-    for (int ux = lo[0]; ux <= hi[0]; ++ux)
-        for (int uy = lo[1]; uy <= hi[1]; ++uy)
-            for (int uz = lo[2]; uz <= hi[2]; ++uz) touch_unit(d, p.frame, ux, uy, uz);
-}
-
-// One voxel column (x, y) of one unit against one frame.  Shared by the per-frame and batched kernels.
-// Returns the number of voxel updates.  `st` holds the column state when REG (registers), else the
-// function reads/writes HBM directly.
-__device__ inline void column_origin(const IntegrateParams& p, int kx, int ky, int kz, int x, int y, float pc[3]) {
-    const float ox = (float)((double)kx * p.unit_len);
-    const float oy = (float)((double)ky * p.unit_len);
-    const float oz = (float)((double)kz * p.unit_len);
-    const float px = (p.half + p.vl * (float)x) + ox;
-    const float py = (p.half + p.vl * (float)y) + oy;
-    const float pz = p.half + oz;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const float a = p.E[r * 4 + 0] * px;
-        const float b = p.E[r * 4 + 1] * py;
-        const float c = p.E[r * 4 + 2] * pz;
-        pc[r] = ((a + b) + c) + p.E[r * 4 + 3];
-    }
-}
-
-// Projection + depth test of one voxel.  On success returns true with the truncated sdf and the pixel.
-__device__ inline bool voxel_sample(const IntegrateParams& p, const float pc[3], float& tsdf_new, int& pix) {
-    if (!(pc[2] > 0.0f)) return false;
-    const float u_f = ((pc[0] * p.fx) / pc[2] + p.cx) + 0.5f;
-    const float v_f = ((pc[1] * p.fy) / pc[2] + p.cy) + 0.5f;
-    if (!(u_f >= 0.0001f && u_f < p.safe_w && v_f >= 0.0001f && v_f < p.safe_h)) return false;
-    const int u = (int)u_f, v = (int)v_f;
-    pix = v * p.W + u;
-    const float d = p.depth[pix];
-    if (!(d > 0.0f)) return false;
-    const float sdf = (d - pc[2]) * p.mult[pix];
-    if (!(sdf > -p.trunc)) return false;
-    const float s = sdf * p.trunc_inv;
-    tsdf_new = (s < 1.0f) ? s : 1.0f;
-    return true;
-}
-
-template <bool C64>
-__global__ __launch_bounds__(256) void k_integrate(IntegrateParams p, TsdfDev d) {
-    using CT = typename std::conditional<C64, double, float>::type;
-    const int n = d.counters[C_TOUCHED];
-    const int tid = threadIdx.x;
-    const int x = tid >> 4, y = tid & 15;
-    unsigned long long upd = 0, units = 0;
-    const bool use_color = p.color != nullptr;
-    for (int t = blockIdx.x; t < n; t += gridDim.x) {
-        const int ent = d.touched[t];
-        const int id = ent & 0x7FFFFFFF;
-        const bool fresh = ent < 0;
-        const int kx = d.unit_keys[id * 3 + 0], ky = d.unit_keys[id * 3 + 1], kz = d.unit_keys[id * 3 + 2];
-        float* base = unit_base(d, id);
-        CT* cbase = color_base<CT>(d, id);
-        float pc[3];
-        column_origin(p, kx, ky, kz, x, y, pc);
-        ++units;
-        for (int z = 0; z < UNIT_RES; ++z) {
-            const int vi = z * 256 + tid;
-            float tn;
-            int pix = 0;
-            const bool hit = voxel_sample(p, pc, tn, pix);
-            if (fresh) {
-                float ts = 0.0f, w = 0.0f;
-                CT cr = 0, cg = 0, cb = 0;
-                if (hit) {
-                    ts = tn;  // (0*0 + t) / (0 + 1)
-                    w = 1.0f;
-                    if (use_color) {  // (0 * 0 + c) / (0 + 1) = c exactly
-                        const uint8_t* c = p.color + (int64_t)pix * 3;
-                        cr = (CT)c[0];
-                        cg = (CT)c[1];
-                        cb = (CT)c[2];
-                    }
-                    ++upd;
-                }
-                base[vi] = ts;
-                base[UNIT_VOX + vi] = w;
-                cbase[vi] = cr;
-                cbase[UNIT_VOX + vi] = cg;
-                cbase[2 * UNIT_VOX + vi] = cb;
-            } else if (hit) {
-                const float w = base[UNIT_VOX + vi];
-                const float ts = base[vi];
-                const float w1 = w + 1.0f;
-                base[vi] = (ts * w + tn) / w1;
-                if (use_color) {  // C64: Open3D's float64 expression; else its float32 rounding
-                    const uint8_t* c = p.color + (int64_t)pix * 3;
-                    const CT wc = (CT)w, w1c = (CT)w1;
-                    const CT cr = cbase[vi], cg = cbase[UNIT_VOX + vi], cb = cbase[2 * UNIT_VOX + vi];
-                    cbase[vi] = (cr * wc + (CT)c[0]) / w1c;
-                    cbase[UNIT_VOX + vi] = (cg * wc + (CT)c[1]) / w1c;
-                    cbase[2 * UNIT_VOX + vi] = (cb * wc + (CT)c[2]) / w1c;
-                }
-                base[UNIT_VOX + vi] = w1;
-                ++upd;
-            }
-            pc[0] += p.es0;
-            pc[1] += p.es1;
-            pc[2] += p.es2;
-        }
-    }
-    // block reduction of the update counter
-    upd = wave_sum(upd);
-    __shared__ unsigned long long red[4];
-    if (lane_id() == 0) red[tid >> 6] = upd;
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
-        if (tot) atomicAdd(&d.stats[S_UPDATES], tot);
-        if (units) atomicAdd(&d.stats[S_UNIT_INTEGRATIONS], units);
-    }
 }
 
 // ============================================================================ batched (temporal blocking)
@@ -433,6 +249,9 @@ __device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* m
     return false;
 }
 
+// REPLAY (settle_batch, after the pool grew): the batch's touch again from its STAGED depths (the caller's frames may be
+// gone by then; the staged depth is exactly the value the first pass computed from them), no staging.
+template <bool REPLAY>
 __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restrict__ frames, BatchTouchParams p,
                                                      TsdfDev d, int nframes) {
     __shared__ unsigned long long s_keys[LTAB];
@@ -450,7 +269,7 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
     // measured 7 us slower per 64 frames).  Every rank of a spatially sharded volume stages every pixel:
     // integrating from the raw frames instead (a u16 depth + a multiplier-table gather per voxel visit) made the
     // integrate 1.9x slower per unit (round 4, tools/shard_frontend.py), more than the staging it saves
-    {
+    if constexpr (!REPLAY) {
         const int64_t quads = (p.npx + 3) >> 2;
         const int64_t per = (quads + gridDim.x - 1) / gridDim.x;
         const int64_t q0 = (int64_t)blockIdx.x * per, q1 = q0 + per < quads ? q0 + per : quads;
@@ -467,7 +286,7 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
         for (int f = f0; f < f0 + TF && f < nframes; ++f) {
             const BatchFrame& fr = frames[f];
             const int64_t pix = (int64_t)r * p.W + c;  // the staged depth, computed as the staging does
-            const float df = fr.depth16 ? prep_depth(fr, fr.depth16[pix]) : fr.depthf[pix];
+            const float df = REPLAY ? fr.dm[pix].x : fr.depth16 ? prep_depth(fr, fr.depth16[pix]) : fr.depthf[pix];
             if (!(df > 0.0f)) continue;
             const double z = (double)df;
             const double x = ((double)c - p.cx) * z / p.fx;
@@ -542,7 +361,10 @@ struct UnitWork {
     unsigned long long pad;
 };
 
-// Unit headers of the batch: allocate new units, move and clear the frame masks (ready for the next batch).
+// Unit headers of the batch: allocate new units, move and clear the frame masks (ready for the next batch).  A unit the
+// pool cannot hold is dropped (id -1, C_OVERFLOW; not counted) and integrated by the replay once the pool has grown.
+// REPLAY: units that already have an id were integrated by the batch's first pass: skipped (id -1, not counted).
+template <bool REPLAY>
 __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __restrict__ work, int pc,
                                                      unsigned* __restrict__ early_mail) {
     __shared__ unsigned long long red[4];
@@ -570,6 +392,8 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
                 note_unit_key(d, kx, ky, kz);
                 id |= (int)0x80000000u;
             }
+        } else if (REPLAY) {
+            id = -1;
         }
         UnitWork w;
         w.id = id;
@@ -579,7 +403,7 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
         w.mask = mask;
         w.pad = 0ull;
         work[t] = w;
-        pairs += (unsigned long long)__popcll(mask);
+        if (id != -1) pairs += (unsigned long long)__popcll(mask);
     }
     pairs = wave_sum(pairs);
     if (lane_id() == 0) red[threadIdx.x >> 6] = pairs;
@@ -1217,48 +1041,6 @@ static ot_status check_frame(const ot_tsdf* vol, const void* depth, const uint8_
     return OT_OK;
 }
 
-static ot_status integrate_float(ot_tsdf* vol, const float* depth, const uint8_t* color, const ot_intrinsics* in,
-                                 const double* ext, hipStream_t stream) {
-    ot_status st = ensure_mult(vol, in, stream);
-    if (st != OT_OK) return st;
-    const int frame = ++vol->frame_id;
-    TouchParams tp;
-    tp.depth = depth;
-    tp.W = in->width;
-    tp.H = in->height;
-    tp.stride = vol->stride;
-    tp.ws = (in->width + vol->stride - 1) / vol->stride;
-    tp.hs = (in->height + vol->stride - 1) / vol->stride;
-    tp.fx = in->fx;
-    tp.fy = in->fy;
-    tp.cx = in->cx;
-    tp.cy = in->cy;
-    inverse4(ext, tp.pose.m);
-    tp.trunc = vol->sdf_trunc;
-    tp.unit_len = vol->unit_length;
-    tp.frame = frame;
-    OT_HIP_TRY(hipMemsetAsync(vol->dev.counters + C_TOUCHED, 0, sizeof(int), stream));
-    const int ns = tp.ws * tp.hs;
-    hipLaunchKernelGGL(k_touch, dim3((ns + 255) / 256), dim3(256), 0, stream, tp, vol->dev);
-    IntegrateParams ip = make_integrate_params(vol, depth, color, vol->mult, in, ext);
-    const int grid = (int)std::min<int64_t>(vol->max_units, 2048);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (vol->profiling) {
-        OT_HIP_TRY(hipEventCreate(&e0));
-        OT_HIP_TRY(hipEventCreate(&e1));
-        OT_HIP_TRY(hipEventRecord(e0, stream));
-    }
-    if (vol->color64) hipLaunchKernelGGL(k_integrate<true>, dim3(grid), dim3(256), 0, stream, ip, vol->dev);
-    else hipLaunchKernelGGL(k_integrate<false>, dim3(grid), dim3(256), 0, stream, ip, vol->dev);
-    OT_LAUNCH_CHECK();
-    if (vol->profiling) {
-        OT_HIP_TRY(hipEventRecord(e1, stream));
-        vol->prof_events.emplace_back(e0, e1);
-    }
-    vol->sorted_frame = -1;
-    return OT_OK;
-}
-
 // Grid of k_batch_integrate: INT_GRID_MULT x the co-resident workgroups (cached per device and kernel; a benign race at
 // worst computes the same value twice).  A 64-frame batch of the configs[1] scan has ~12k (unit, quarter) items: at 8x
 // (16k workgroups) nearly every workgroup takes one item and the dispatcher balances them; at 4x some take two in a
@@ -1289,9 +1071,14 @@ static int integrate_grid(int variant) {
     return cache_c[dev];
 }
 
+static ot_status settle_batch(ot_tsdf* vol, const BatchTouchParams& tp, const IntegrateParams& ip0, unsigned tiles,
+                              int n, int pc, int variant, hipStream_t stream);
+
 static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n, hipStream_t stream) {
     const ot_intrinsics& in = frames[0].intr;
-    ot_status st = ensure_mult(vol, &in, stream);
+    ot_status st = wait_normals(vol, stream);  // deferred vertex normals of the last mesh still read the volume
+    if (st != OT_OK) return st;
+    st = ensure_mult(vol, &in, stream);
     if (st != OT_OK) return st;
     const int64_t npx = (int64_t)in.width * in.height;
     if (vol->bdepth_cap < npx * n) {
@@ -1361,9 +1148,9 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         OT_HIP_TRY(hipEventCreate(&f1));
         OT_HIP_TRY(hipEventRecord(f0, stream));
     }
-    hipLaunchKernelGGL(k_batch_touch, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
+    hipLaunchKernelGGL(k_batch_touch<false>, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)vol->bframes, tp, vol->dev, n);
-    hipLaunchKernelGGL(k_batch_units, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc,
+    hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc,
                        vol->hmail + OT_MAIL_WORDS);
     if (!vol->ev_early) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_early, hipEventDisableTiming));
     OT_HIP_TRY(hipEventRecord(vol->ev_early, stream));
@@ -1393,23 +1180,155 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     vol->frame_id += n;
     vol->sorted_frame = -1;
     vol->early_frame = vol->frame_id;  // the mailed counters are final for this frame count (see ev_early)
+    return settle_batch(vol, tp, ip0, tiles, n, pc, variant, stream);
+}
+
+// ------------------------------------------------------------------------------------------ unbounded unit pool
+// Open3D's ScalableTSDFVolume allocates blocks without bound (a fixed pool dropped units and failed at the
+// next read, outside the reference caller's per-frame try/except).  Here the pool grows: records, keys and the sorted
+// order are copied into pools twice as large (or more), and the hash is rebuilt from the unit keys at >= 4x the pool.
+
+__global__ __launch_bounds__(256) void k_rehash(TsdfDev d, int n) {
+    const int id = blockIdx.x * 256 + threadIdx.x;
+    if (id >= n) return;
+    const int slot = hash_insert(d, pack_key(d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]));
+    if (slot < 0) atomicOr(&d.counters[C_HASHERR], 1);  // cannot happen: capacity >= 4x the units
+    else d.hvals[slot] = id;
+}
+
+// Grow to hold at least `need` units (stream-ordered copies; the stream is synchronised first: the kernels queued on
+// the volume may still read the old buffers).  Every allocation is made before any old buffer is freed, so a failed
+// allocation leaves the volume as it was and is reported as the error of the call that needed the room.
+static ot_status grow_pool(ot_tsdf* vol, int64_t need, int n_used, hipStream_t stream) {
+    constexpr int64_t MAX_UNITS = 1 << 24;
+    if (need > MAX_UNITS) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] more than 2^24 units");
+    int64_t nmax = std::max<int64_t>(2 * vol->max_units, need + need / 2);
+    nmax = std::min<int64_t>(nmax, MAX_UNITS);
+    int64_t cap = 1;
+    while (cap < 4 * nmax) cap <<= 1;
+    ot_status st = wait_normals(vol, stream);
+    if (st != OT_OK) return st;
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    TsdfDev& d = vol->dev;
+    TsdfDev nd = d;
+    unsigned* nsorted = nullptr;
+    void* fresh[8] = {nullptr};
+    auto alloc = [&](void** p, size_t bytes, int k) {
+        const hipError_t e = hipMalloc(p, bytes);
+        fresh[k] = *p;
+        return e;
+    };
+    hipError_t e = hipSuccess;
+    if ((e = alloc((void**)&nd.vox, sizeof(float) * (size_t)d.unit_floats * nmax, 0)) == hipSuccess &&
+        (e = alloc((void**)&nd.unit_keys, sizeof(int) * 3 * nmax, 1)) == hipSuccess &&
+        (e = alloc((void**)&nsorted, sizeof(unsigned) * nmax, 2)) == hipSuccess &&
+        (e = alloc((void**)&nd.hkeys, sizeof(unsigned long long) * cap, 3)) == hipSuccess &&
+        (e = alloc((void**)&nd.hvals, sizeof(int) * cap, 4)) == hipSuccess &&
+        (e = alloc((void**)&nd.fmask, sizeof(unsigned long long) * cap, 5)) == hipSuccess &&
+        (e = alloc((void**)&nd.bslots, sizeof(int) * cap, 6)) == hipSuccess &&
+        (e = alloc((void**)&nd.work, 32 * cap, 7)) == hipSuccess) {
+    }
+    if (e != hipSuccess) {
+        for (void* p : fresh)
+            if (p) (void)hipFree(p);
+        (void)hipGetLastError();
+        return fail(OT_ERR_HIP, std::string("[ScalableTSDFVolume] allocation failed while growing the unit pool to ") +
+                                    std::to_string(nmax) + " units: " + hipGetErrorString(e));
+    }
+    note_alloc();
+    const size_t rec = sizeof(float) * (size_t)d.unit_floats;
+    if (n_used > 0) {
+        OT_HIP_TRY(hipMemcpyAsync(nd.vox, d.vox, rec * n_used, hipMemcpyDeviceToDevice, stream));
+        OT_HIP_TRY(hipMemcpyAsync(nd.unit_keys, d.unit_keys, sizeof(int) * 3 * n_used, hipMemcpyDeviceToDevice, stream));
+        OT_HIP_TRY(hipMemcpyAsync(nsorted, vol->sorted_ids, sizeof(unsigned) * n_used, hipMemcpyDeviceToDevice, stream));
+    }
+    OT_HIP_TRY(hipMemsetAsync(nd.hkeys, 0xFF, sizeof(unsigned long long) * cap, stream));
+    OT_HIP_TRY(hipMemsetAsync(nd.hvals, 0xFF, sizeof(int) * cap, stream));
+    OT_HIP_TRY(hipMemsetAsync(nd.fmask, 0, sizeof(unsigned long long) * cap, stream));
+    nd.hash_mask = (int)(cap - 1);
+    nd.max_units = (int)nmax;
+    if (n_used > 0) hipLaunchKernelGGL(k_rehash, dim3((unsigned)((n_used + 255) / 256)), dim3(256), 0, stream, nd, n_used);
+    OT_LAUNCH_CHECK();
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    for (void* p : {(void*)d.vox, (void*)d.unit_keys, (void*)vol->sorted_ids, (void*)d.hkeys, (void*)d.hvals,
+                    (void*)d.fmask, (void*)d.bslots, d.work})
+        if (p) (void)hipFree(p);
+    d = nd;
+    vol->sorted_ids = nsorted;
+    vol->max_units = nmax;
+    vol->hash_cap = cap;
     return OT_OK;
 }
 
-static ot_status integrate_single(ot_tsdf* vol, const PendingFrame& f, hipStream_t stream) {
-    if (!f.depth) return integrate_float(vol, f.depthf, f.color, &f.intr, f.extrinsic, stream);
-    const int64_t npx = (int64_t)f.intr.width * f.intr.height;
-    if (vol->depth_f_cap < npx) {
-        if (vol->depth_f) {
-            OT_HIP_TRY(hipStreamSynchronize(stream));
-            OT_HIP_TRY(hipFree(vol->depth_f));
+// After each batch: the counters its units kernel mailed (behind ev_early: the host waits for the units kernel, not for
+// the integrate queued behind it, so the GPU keeps its queue).  Units the pool could not hold (C_OVERFLOW), or keys the
+// hash could not hold (C_HASHERR bit 0), were skipped by the batch's integrate: grow, then replay the batch for exactly
+// those units -- touch again from the staged depths (still resident: the next batch has not been staged yet), allocate
+// the missing units (units that have an id were integrated and are skipped), integrate them with the batch's frames.
+// Units are independent and each sees the batch's frames in call order, so the volume equals an unbounded pool's.
+// A pool more than 3/4 full also grows here, ahead of need.
+static ot_status settle_batch(ot_tsdf* vol, const BatchTouchParams& tp0, const IntegrateParams& ip0, unsigned tiles,
+                              int n, int pc, int variant, hipStream_t stream) {
+    for (int round = 0;; ++round) {
+        OT_HIP_TRY(hipEventSynchronize(vol->ev_early));
+        int c[N_COUNTERS];
+        std::memcpy(c, vol->hmail + OT_MAIL_WORDS, sizeof(c));
+        const bool short_of_room = c[C_OVERFLOW] != 0 || (c[C_HASHERR] & 1) != 0;
+        if (!short_of_room) {
+            if ((int64_t)c[C_UNITS] * 4 > vol->max_units * 3)
+                return grow_pool(vol, (int64_t)c[C_UNITS] * 2, c[C_UNITS], stream);
+            return OT_OK;
         }
-        OT_HIP_TRY(hipMalloc(&vol->depth_f, sizeof(float) * npx));
-        vol->depth_f_cap = npx;
+        if (round >= 8) return fail(OT_ERR_CAPACITY, "[ScalableTSDFVolume] unit pool: growth did not converge");
+        // ids below the old capacity were all handed out; the allocations past it were dropped (C_UNITS overshoots)
+        const int used = (int)std::min<int64_t>(c[C_UNITS], vol->max_units);
+        const int64_t need = std::max<int64_t>((int64_t)c[C_UNITS], vol->max_units) + 1;
+        ot_status st = grow_pool(vol, need, used, stream);
+        if (st != OT_OK) return st;
+        int h[N_COUNTERS];
+        OT_HIP_TRY(hipMemcpy(h, vol->dev.counters, sizeof(h), hipMemcpyDeviceToHost));
+        h[C_UNITS] = used;
+        h[C_OVERFLOW] = 0;
+        h[C_HASHERR] &= ~1;
+        h[pc] = 0;  // the replay's touched-slot count (the batch's own pair counter; the next batch's stays zero)
+        OT_HIP_TRY(hipMemcpy(vol->dev.counters, h, sizeof(h), hipMemcpyHostToDevice));
+        BatchTouchParams tp = tp0;
+        tp.slot_cap = (int)vol->hash_cap;
+        hipLaunchKernelGGL(k_batch_touch<true>, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
+                           (const BatchFrame*)vol->bframes, tp, vol->dev, n);
+        hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc,
+                           vol->hmail + OT_MAIL_WORDS);
+        OT_HIP_TRY(hipEventRecord(vol->ev_early, stream));
+        const BatchFrame* bf = vol->bframes;
+        const UnitWork* uw = (const UnitWork*)vol->dev.work;
+        void* args[] = {(void*)&bf, (void*)&ip0, (void*)&vol->dev, (void*)&uw, (void*)&pc};
+        OT_HIP_TRY(hipLaunchKernel(integrate_kernel(variant), dim3(integrate_grid(variant)), dim3(64 * INT_WG), args, 0,
+                                   stream));
+        OT_LAUNCH_CHECK();
+        vol->sorted_frame = -1;
     }
-    ot_status st = ot_depth_to_float(f.depth, vol->depth_f, npx, f.depth_scale, f.depth_trunc, stream);
-    if (st != OT_OK) return st;
-    return integrate_float(vol, vol->depth_f, f.color, &f.intr, f.extrinsic, stream);
+}
+
+// room for `extra` more units before a kernel that allocates up to that many (imports): grow now if needed
+static ot_status reserve_units(ot_tsdf* vol, int64_t extra, hipStream_t stream) {
+    int nu = 0;
+    OT_HIP_TRY(hipMemcpyAsync(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost, stream));
+    OT_HIP_TRY(hipStreamSynchronize(stream));
+    const int used = (int)std::min<int64_t>(nu, vol->max_units);
+    if (used + extra <= vol->max_units) return OT_OK;
+    return grow_pool(vol, used + extra, used, stream);
+}
+
+ot_status wait_normals(ot_tsdf* vol, hipStream_t stream) {
+    if (!vol->normals_pending) return OT_OK;
+    const hipError_t q = hipEventQuery(vol->ev_normals);
+    if (q == hipSuccess) {
+        vol->normals_pending = false;
+        return OT_OK;
+    }
+    if (q != hipErrorNotReady) OT_HIP_TRY(q);
+    OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_normals, 0));
+    return OT_OK;
 }
 
 ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream) {
@@ -1424,8 +1343,7 @@ ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream) {
         while (i + n < frames.size() && (int)n < cap &&
                std::memcmp(&frames[i + n].intr, &frames[i].intr, sizeof(ot_intrinsics)) == 0)
             ++n;
-        ot_status st = (n == 1) ? integrate_single(vol, frames[i], stream)
-                                : integrate_batch(vol, frames.data() + i, (int)n, stream);
+        ot_status st = integrate_batch(vol, frames.data() + i, (int)n, stream);
         if (st != OT_OK) return st;
         i += n;
     }
@@ -1531,7 +1449,6 @@ __global__ __launch_bounds__(256) void k_tsdf_clear(TsdfDev d, int64_t cap) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cap; i += (int64_t)gridDim.x * 256) {
         d.hkeys[i] = ~0ull;
         d.hvals[i] = -1;
-        d.stamp[i] = -1;
         d.fmask[i] = 0ull;
     }
     if (blockIdx.x == 0) {
@@ -1578,8 +1495,6 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
     hipError_t e;
     if ((e = hipMalloc(&d.hkeys, sizeof(unsigned long long) * cap)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.hvals, sizeof(int) * cap)) != hipSuccess) return cleanup(e);
-    if ((e = hipMalloc(&d.stamp, sizeof(int) * cap)) != hipSuccess) return cleanup(e);
-    if ((e = hipMalloc(&d.touched, sizeof(int) * max_units)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.counters, sizeof(int) * N_COUNTERS)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.stats, sizeof(unsigned long long) * 4)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.unit_keys, sizeof(int) * 3 * max_units)) != hipSuccess) return cleanup(e);
@@ -1611,8 +1526,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     (void)hipDeviceSynchronize();
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
-    void* ptrs[] = {d.hkeys, d.hvals, d.stamp, d.touched, d.counters, d.stats, d.unit_keys, d.vox, v->mult,
-                    v->depth_f, v->sorted_ids, v->batch_ws, v->mesh.ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, v->mesh.vown, d.fmask, d.bslots, d.work,
+    void* ptrs[] = {d.hkeys, d.hvals, d.counters, d.stats, d.unit_keys, d.vox, v->mult, v->sorted_ids, v->batch_ws, v->mesh.ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, v->mesh.vown, d.fmask, d.bslots, d.work,
                     v->bframes, v->bdm, v->brgba};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1622,6 +1536,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     if (v->ev_early) (void)hipEventDestroy(v->ev_early);
     if (v->ev_mail) (void)hipEventDestroy(v->ev_mail);
     if (v->ev_join) (void)hipEventDestroy(v->ev_join);
+    if (v->ev_normals) (void)hipEventDestroy(v->ev_normals);
     if (v->side) (void)hipStreamDestroy(v->side);
     for (hipEvent_t ev : v->hb_event)
         if (ev) (void)hipEventDestroy(ev);
@@ -1632,9 +1547,10 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
 ot_status ot_tsdf_reset(ot_tsdf* v) {
     if (!v) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume::Reset] volume is NULL");
     TsdfDev& d = v->dev;
+    OT_HIP_TRY(hipDeviceSynchronize());  // queued work on the volume (deferred normals included) first
+    v->normals_pending = false;
     OT_HIP_TRY(hipMemset(d.hkeys, 0xFF, sizeof(unsigned long long) * v->hash_cap));
     OT_HIP_TRY(hipMemset(d.hvals, 0xFF, sizeof(int) * v->hash_cap));
-    OT_HIP_TRY(hipMemset(d.stamp, 0xFF, sizeof(int) * v->hash_cap));
     OT_HIP_TRY(hipMemset(d.fmask, 0, sizeof(unsigned long long) * v->hash_cap));
     OT_HIP_TRY(hipMemset(d.counters, 0, sizeof(int) * N_COUNTERS));
     OT_HIP_TRY(hipMemset(d.stats, 0, sizeof(unsigned long long) * 4));
@@ -1655,6 +1571,8 @@ ot_status ot_tsdf_reset_async(ot_tsdf* v, void* stream_) {
     if (!v) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume::Reset] volume is NULL");
     hipStream_t stream = S(stream_);
     ot_status st = tsdf_flush(v, stream);  // queued frames belong to the old contents: apply, then clear
+    if (st != OT_OK) return st;
+    st = wait_normals(v, stream);  // the last mesh's deferred normals may still read the volume
     if (st != OT_OK) return st;
     // the hash table, frame masks, counters and statistics in one launch (six fill commands cost ~5 us of host time
     // each, on one object's critical path)
@@ -1945,7 +1863,6 @@ static ot_status import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, cons
                               const CT* color, hipStream_t stream) {
     if (!vol || n < 0 || (n > 0 && (!keys || !tsdf || !weight)))
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: invalid arguments");
-    if (n > vol->max_units) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: more units than max_units");
     const bool rgb8 = vol->color_type == OT_COLOR_RGB8;
     if (rgb8 && vol->color64 != (sizeof(CT) == 8))
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] import: colour dtype does not match the volume's "
@@ -1953,6 +1870,8 @@ static ot_status import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, cons
     ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
     if (n == 0) return OT_OK;
+    st = reserve_units(vol, n, stream);  // the pool grows instead of dropping imported units
+    if (st != OT_OK) return st;
     if (rgb8)
         hipLaunchKernelGGL(k_import<CT>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf, weight, color);
     else  // NoColor: float32 record, zero colour planes
@@ -2015,6 +1934,8 @@ ot_status ot_tsdf_import_border(ot_tsdf* vol, int64_t n, const int32_t* keys, co
     ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
     if (n == 0) return OT_OK;
+    st = reserve_units(vol, n, stream);  // halo units: room for every row (a superset of those kept)
+    if (st != OT_OK) return st;
     const void* c = vol->color_type == OT_COLOR_RGB8 ? color : nullptr;
     if (vol->color64)  // (only RGB8 volumes store float64 colour)
         hipLaunchKernelGGL(k_import_border<double>, dim3((unsigned)n), dim3(256), 0, stream, vol->dev, keys, tsdf,

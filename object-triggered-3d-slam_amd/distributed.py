@@ -4,11 +4,15 @@ The reference reconstructs objects one after another in a Python loop (reconstru
 later concatenates their clouds behind the occupancy-grid cloud (hybrid_map.py:62-96, :115).  Objects share no
 state, so here each rank (one process per GPU, torch.distributed over RCCL/xGMI) takes a CONTIGUOUS chunk of
 the sorted object list; concatenating the per-rank results in rank order therefore reproduces the reference's
-sorted-file order exactly.  The only collective is the final all-gather of the filtered clouds:
-  1. all_gather of per-rank point counts (int64[world])
-  2. all_gather_into_tensor of count-padded float64 [max_n, 3] buffers (float64 keeps the merge bit-exact;
-     <= 32 objects x 100k points x 24 B ~ 77 MB over xGMI, a few ms)
-then every rank trims the padding; rank 0 prepends the map cloud and writes the PLY.
+sorted-file order exactly.  The only data-path collective is the final all-gather of the filtered clouds
+(merge_object_clouds), float64 rows so the merge is bit-exact, in one of two forms chosen by the padded size:
+  * all_gather_rows_capped: ONE all_gather_into_tensor of [capacity + 1, 3] rows per rank with the row count
+    in-band (no count exchange, no host read between collectives) -- while world * (capacity + 1) * 24 B stays
+    under CAPPED_MAX_BYTES;
+  * all_gather_rows: an all_gather of the int64 counts, one host read, then an all_gather of [max count, 3] rows --
+    when padding to the common bound would move more (configs[3] at 8 ranks: 100k-row bound per object against
+    ~6.7k real rows, DESIGN.md §6 models both over xGMI).
+Every rank trims the padding; rank 0 prepends the map cloud and writes the PLY.
 Works unchanged on gloo (CPU tensors) for the world-size-2 CPU tests.
 """
 from __future__ import annotations
@@ -258,9 +262,23 @@ def merge_object_clouds(local_clouds, group=None, capacity=None):
                                                                    dist.get_backend(group) == "nccl") else \
             torch.device("cpu")
     local = torch.cat(local_clouds, 0) if local_clouds else torch.zeros((0, 3), dtype=torch.float64, device=dev)
-    if capacity is not None:
+    if capacity is not None and capped_fits(capacity, 3, group):
         return all_gather_rows_capped(local.to(torch.float64), capacity, group)
     return all_gather_rows(local.to(torch.float64), group)
+
+
+# ONE padded collective only while the padded gather stays small: every rank receives world x (capacity + 1)
+# rows, so at 8 ranks x 100k-row bounds (19 MB) the padding costs ~0.17 ms over xGMI against ~0.05 ms for a count
+# exchange + host read + a tight gather of the real ~6.7k rows per object
+CAPPED_MAX_BYTES = 4 << 20
+
+
+def capped_fits(capacity, k, group=None):
+    """whether all_gather_rows_capped's padded gather (world x (capacity + 1) x k float64) is under CAPPED_MAX_BYTES"""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    return world * (int(capacity) + 1) * int(k) * 8 <= CAPPED_MAX_BYTES
 
 
 def reconstruct_and_merge(cfg, yaml_file=None, pgm_file=None, save_path=None, objects=None, o3d=None, streams=2):
@@ -340,7 +358,7 @@ def _reconstruct_points(R, cfg, label, o3d):
             pass
     mesh = volume.extract_triangle_mesh()
     mesh.compute_vertex_normals()
-    if len(mesh.vertices) == 0:
+    if R._mesh_empty(mesh):  # reference: len(mesh.vertices) == 0, without a writable host view
         return None
     # sample_points_uniformly + the Z mask (reconstruct_rgbd_filter.py:123-132) in one pass
     return mesh.sample_points_min_z(cfg.n_samples, cfg.z_filter)._xyz.dev()

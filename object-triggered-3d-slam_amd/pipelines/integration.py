@@ -25,7 +25,9 @@ class ScalableTSDFVolume:
     """pipelines.integration.ScalableTSDFVolume(voxel_length, sdf_trunc, color_type=NoColor,
     volume_unit_resolution=16, depth_sampling_stride=4).
 
-    Extra keyword arguments (not in Open3D): `max_units` (block-pool capacity in HBM), `batch_frames`
+    Like Open3D's, the volume is unbounded: its block pool grows when a batch needs more units (records copied,
+    keys rehashed, the batch's dropped units integrated again from its staged frames: the same volume bit for bit).
+    Extra keyword arguments (not in Open3D): `max_units` (initial block-pool capacity in HBM), `batch_frames`
     (frames queued per fused integration launch, default and max 64; 1 = integrate immediately; results are
     bit-identical for any value: a batch applies its frames to each voxel in call order) and `color_precision`
     (64, the default: the running colour mean in float64 with exact division, Open3D's TSDFVoxel::color_ --

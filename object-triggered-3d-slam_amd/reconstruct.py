@@ -11,6 +11,7 @@ package) so the same code runs on the MI355X facade, or on a recording stub in t
   reconstruct_range        <- multi_reconstruct_rgbd_filter.py:51-137
   reconstruct_gt           <- reconstruct_rgbd_gt.py:28-98
   run_all                  <- reconstruct_rgbd_filter.py:143-157 / reconstruct_rgbd.py:121-135
+  check_one_frame          <- check_one_frame.py:1-31
 """
 from __future__ import annotations
 
@@ -109,6 +110,14 @@ def _integrate_frame(o3d, cfg, volume, intrinsic, colors, depths, poses, i):
     volume.integrate(rgbd, intrinsic, extrinsic)
 
 
+def _mesh_empty(mesh):
+    """The reference's `len(mesh.vertices) == 0` (reconstruct_rgbd_filter.py:115-117).  On this package's mesh it reads
+    the row count only (TriangleMesh.has_vertices, also Open3D API): `mesh.vertices` would hand out a writable host view,
+    which settles the deferred vertex normals and copies V to the host and back."""
+    has = getattr(mesh, "has_vertices", None)
+    return (not has()) if callable(has) else len(mesh.vertices) == 0
+
+
 def _filtered_cloud(o3d, cfg, mesh):
     """sample_points_uniformly(N) then keep z >= threshold, points and colours only (:123-132).  This package's
     facade does both in one pass (TriangleMesh.sample_points_min_z: the same cloud); Open3D takes the reference's
@@ -154,7 +163,7 @@ def reconstruct_object(label: str, cfg: ScanConfig, o3d=None, output: str = "poi
     if output == "mesh":
         o3d.io.write_triangle_mesh(path, mesh)
         return path
-    if len(mesh.vertices) == 0:
+    if _mesh_empty(mesh):
         _log("Mesh is empty", log)
         return None
     o3d.io.write_point_cloud(path, _filtered_cloud(o3d, cfg, mesh))
@@ -186,7 +195,7 @@ def reconstruct_range(name: str, start: int, end: int, cfg: ScanConfig, file_pre
         return None
     mesh = volume.extract_triangle_mesh()
     mesh.compute_vertex_normals()
-    if len(mesh.vertices) == 0:
+    if _mesh_empty(mesh):
         return None
     path = os.path.join(cfg.save_dir, f"{name}.ply")
     o3d.io.write_point_cloud(path, _filtered_cloud(o3d, cfg, mesh))
@@ -220,3 +229,23 @@ def run_all(cfg: ScanConfig, o3d=None, output: str = "points", objects=None, log
     the multi-GPU driver shards this list, see distributed.py)."""
     labels = get_unique_object_names(cfg) if objects is None else objects
     return {label: reconstruct_object(label, cfg, o3d=o3d, output=output, log=log) for label in labels}
+
+
+def check_one_frame(base_dir: str, o3d=None, cfg: ScanConfig = None, show: bool = True):
+    """check_one_frame.py:1-31: one RGB-D frame of the object scan (color/color_0000.png, depth/depth_0000.png) ->
+    create_from_color_and_depth(depth_scale 1000, depth_trunc 5.0) -> create_from_rgbd_image (identity extrinsic)
+    -> voxel_down_sample(0.01) -> draw_geometries (headless here: visualization.draw_geometries).  Returns the cloud."""
+    o3d = o3d or _default_o3d()
+    cfg = cfg or ScanConfig(base_dir=base_dir)
+    color_path = os.path.join(base_dir, "color/color_0000.png")
+    depth_path = os.path.join(base_dir, "depth/depth_0000.png")
+    intrinsics = _intrinsic(o3d, cfg)
+    color_raw = o3d.io.read_image(color_path)
+    depth_raw = o3d.io.read_image(depth_path)
+    rgbd = o3d.geometry.RGBDImage.create_from_color_and_depth(color_raw, depth_raw, depth_scale=cfg.depth_scale,
+                                                              depth_trunc=5.0, convert_rgb_to_intensity=False)
+    pcd = o3d.geometry.PointCloud.create_from_rgbd_image(rgbd, intrinsics)
+    pcd = pcd.voxel_down_sample(0.01)
+    if show:
+        o3d.visualization.draw_geometries([pcd])
+    return pcd

@@ -22,7 +22,8 @@ def _pmc(path, source_hash):
            "kernels_traffic": {
                "k_batch_integrate": {"bytes_per_launch": 1600000000, "valu_busy_frac": 0.65},
                "k_sor_knn": {"bytes_per_launch": 450000000, "valu_busy_frac": 0.86, "valu_insts_per_launch": 1.0e9,
-                             "dispatch_cycles": 4.7e6}},
+                             "dispatch_cycles": 4.7e6,
+                             "config": {"batch": 64, "frames": 128, "algorithmic_bytes_per_launch": 300000000}}},
            "kernels": {}}
     with open(path, "w") as f:
         json.dump(doc, f)
@@ -32,18 +33,22 @@ def test_same_build_pmc_is_used(tmp_path):
     bench, L = _bench_and_lib()
     p = tmp_path / "pmc.json"
     _pmc(p, L.source_hash())
-    args = types.SimpleNamespace(traffic=str(p))
+    args = types.SimpleNamespace(traffic=str(p), filter_batch=64)
     traffic, note = bench._traffic(args, L, "k_batch_integrate", {"voxel": 0.005, "frames": 256, "batch": 0})
     assert traffic == 1600000000 and "source hash" in note
     roof = bench._sor_roofline(args, L)
     assert roof["bound"] == "valu" and roof["frac"] == 0.86 and roof["kernel"] == "k_sor_knn"
+    # the entry's workload is the bench's batch: frames per launch and the traffic / algorithmic ratio come from it
+    assert roof["frames_per_launch"] == 64 and roof["traffic_over_algorithmic"] == 1.5
+    # a PMC entry taken at another batch size than the one timed is refused
+    assert bench._sor_roofline(types.SimpleNamespace(traffic=str(p), filter_batch=32), L)["frac"] is None
 
 
 def test_stale_or_other_workload_pmc_is_refused(tmp_path):
     bench, L = _bench_and_lib()
     p = tmp_path / "pmc.json"
     _pmc(p, "0000000000000000")
-    args = types.SimpleNamespace(traffic=str(p))
+    args = types.SimpleNamespace(traffic=str(p), filter_batch=64)
     traffic, note = bench._traffic(args, L, "k_batch_integrate", {"voxel": 0.005, "frames": 256, "batch": 0})
     assert traffic is None and "stale" in note
     assert bench._sor_roofline(args, L)["frac"] is None

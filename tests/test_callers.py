@@ -81,6 +81,15 @@ def test_reconstruct_gt(R, tmp_path):
     _check(calls, "reconstruct_rgbd_gt")
 
 
+def test_check_one_frame(R, tmp_path):
+    """check_one_frame.py's recorded sequence (intrinsic, two image reads, depth_trunc 5.0 RGBD,
+    create_from_rgbd_image, voxel_down_sample(0.01), draw_geometries) made by the restated caller, call for call and
+    argument for argument."""
+    calls = _run(tmp_path, lambda root, o3d: R.check_one_frame(root, o3d=o3d))
+    _check(calls, "check_one_frame")
+    assert [c["call"] for c in calls][-2:] == ["voxel_down_sample", "draw_geometries"]
+
+
 def test_extrinsics_are_inverse_of_pose_times_tfix(R, tmp_path):
     calls = _run(tmp_path, lambda root, o3d: R.run_all(R.ScanConfig(base_dir=root), o3d=o3d))
     first = next(c for c in calls if c["call"] == "integrate")

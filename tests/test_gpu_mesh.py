@@ -274,6 +274,29 @@ def test_deferred_normals_queued_by_the_sampler(pkg, O, synth, seq16):
                    "deferred normals queued by a vertices view")
 
 
+def test_deferred_normals_vs_later_volume_work(pkg, O, synth, seq16):
+    """the deferred vertex normals run on a side stream and read the volume's marching-cubes structure
+    (cubes, neighbour tables, triangle bases, vertex keys / owners).  The sampler starts them; the same volume then
+    integrates another frame, is extracted again (its structure rewritten) and reset, all on the caller's stream
+    before anyone reads the first mesh's normals.  That work waits for the normals (the volume's normals event), so
+    the first mesh's normals still equal the oracle's for ITS vertices and triangles."""
+    depth, color, ext = seq16
+    vol, ref = _volumes(pkg, O, synth, depth[:3], color[:3], ext[:3], 0.005)
+    V, VC, T = ref.extract_triangle_mesh()
+    rN = O.vertex_normals(V, T)
+    mesh = vol.extract_triangle_mesh()
+    mesh.compute_vertex_normals()
+    mesh.sample_points_min_z(100000, 0.03, seed=3)  # queues the normals on the side stream
+    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+        pkg.geometry.Image(color[3]), pkg.geometry.Image(depth[3]), convert_rgb_to_intensity=False)
+    vol.integrate(rgbd, pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth)), ext[3])
+    mesh2 = vol.extract_triangle_mesh()  # rewrites the structure the first mesh's normals walk
+    mesh2.compute_vertex_normals()
+    mesh2.sample_points_min_z(1000, 0.03)
+    vol.reset()
+    assert_bitwise(np.asarray(mesh.vertex_normals), rN, "first mesh's normals after later work on the volume")
+
+
 def test_sampling_batch_matches_single(pkg, O, synth, seq16, meshes):
     """TriangleMesh.sample_points_uniformly_batch: the per-mesh clouds equal the single-mesh calls (and the oracle)
     for meshes of different sizes sampled together."""

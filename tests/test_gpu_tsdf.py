@@ -318,17 +318,48 @@ def test_tsdf_unsupported_format(pkg, gpu, synth, seq16):
         vol.integrate(rgbd, small, ext[0])
 
 
-def test_tsdf_capacity_error(pkg, gpu, synth, seq16):
-    depth, color, ext = seq16
+@pytest.mark.parametrize("batch", [1, None])
+def test_tsdf_pool_grows(pkg, O, gpu, synth, batch):
+    """Open3D's ScalableTSDFVolume is unbounded.  A volume created with room for 64 units integrates the
+    configs[1] scan's first 16 frames at 5 mm (hundreds of units: the first batch alone overflows the pool and the
+    hash) -- frame by frame (every flush a 1-frame batch) and as one 16-frame batch.  The pool grows and the dropped
+    units are integrated again from the staged frames: keys, tsdf, weight, float64 colour and the update counters
+    bitwise equal to the oracle's, and no error at any call."""
+    integ = _integration(pkg)
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=0), n_frames=256, frames=range(16), intr=intr_t)
+    vol = integ.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                   max_units=64, batch_frames=batch)
+    ref = O.TSDF(0.005, 0.04, 1, 4)
+    for k in range(depth.shape[0]):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+            convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
+    assert _compare_volumes(vol, ref) > 600
+    m, (V, VC, T) = vol.extract_triangle_mesh(), ref.extract_triangle_mesh()
+    assert_bitwise(np.asarray(m.vertices), V, "mesh vertices after pool growth")
+    assert_bitwise(np.asarray(m.triangles), T, "mesh triangles after pool growth")
+
+
+def test_tsdf_pool_grows_on_import(pkg, gpu, synth, seq16):
+    """import_units into a 64-unit volume makes room first (the rows are counted before the import kernel)."""
     integ = _integration(pkg)
     intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth))
-    vol = integ.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
-                                   max_units=64)
-    rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
-        pkg.geometry.Image(color[0]), pkg.geometry.Image(depth[0]), convert_rgb_to_intensity=False)
-    vol.integrate(rgbd, intr, ext[0])
-    with pytest.raises(RuntimeError, match="pool exhausted"):
-        vol.export_units()
+    depth, color, ext = seq16
+    a = integ.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
+    for k in range(depth.shape[0]):
+        a.integrate(pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), convert_rgb_to_intensity=False), intr, ext[k])
+    rows = [t.cpu().numpy() for t in a.export_units()]
+    assert rows[0].shape[0] > 300
+    b = integ.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                 max_units=64)
+    b.import_units(*a.export_units())
+    for x, y, what in zip((t.cpu().numpy() for t in b.export_units()), rows, ("keys", "tsdf", "weight", "colour")):
+        assert_bitwise(x, y, f"imported {what} after pool growth")
 
 
 @pytest.mark.parametrize("batch", [1, 32])

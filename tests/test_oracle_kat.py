@@ -19,8 +19,9 @@ def test_depth_to_float_kat(O):
 
 
 def test_inverse4_kat(O, synth):
-    assert_bitwise(O.inverse4(np.eye(4)), np.eye(4), "inverse(I)")
-    assert_bitwise(O.inverse4(synth.T_FIX), synth.T_FIX.T, "inverse(T_fix) = T_fix^T (permutation)")
+    # analytic expectations carry no sign of zero (the cofactors give -0.0): value-exact here, not bitwise
+    np.testing.assert_array_equal(O.inverse4(np.eye(4)), np.eye(4), "inverse(I)")
+    np.testing.assert_array_equal(O.inverse4(synth.T_FIX), synth.T_FIX.T, "inverse(T_fix) = T_fix^T (permutation)")
     rng = np.random.default_rng(0)
     for _ in range(20):
         A = rng.standard_normal((4, 4)) + 4 * np.eye(4)

@@ -3,6 +3,7 @@ batch sizes (and the kernel breakdown when run under rocprofv3 --kernel-trace --
 import argparse
 import ctypes as C
 import importlib
+import json
 import os
 import sys
 import time
@@ -45,7 +46,7 @@ for B in [int(x) for x in a.batches.split(",")]:
     h = C.c_void_p()
     L.call("ot_rgbd_filter_create", C.byref(intr), B, 1000.0, 5.0, 0.005, 20, 2.0, C.byref(h))
     def run_all():
-        pts = kept = 0
+        pts = kept = vox = 0
         for f0 in range(0, a.frames, B):
             n = min(B, a.frames - f0)
             e = np.ascontiguousarray(ext[f0:f0 + n])
@@ -54,7 +55,9 @@ for B in [int(x) for x in a.batches.split(",")]:
             P, K, KK = C.c_int64(), C.c_int64(), C.c_int64()
             L.call("ot_rgbd_filter_sizes", h, C.byref(P), C.byref(K), C.byref(KK), None, None, None)
             pts += P.value
+            vox += K.value
             kept += KK.value
+        run_all.vox = vox
         return pts, kept
     run_all()
     torch.cuda.synchronize()
@@ -65,4 +68,10 @@ for B in [int(x) for x in a.batches.split(",")]:
     dt = (time.perf_counter() - t1) / a.reps
     print(f"batch {B}: {dt * 1e3 / a.frames:.4f} ms/frame, {pts / dt / 1e6:.1f} Mpoints/s, kept/frame {kept / a.frames:.0f}",
           flush=True)
+    nb = (a.frames + B - 1) // B
+    # per launch of the batch's kernels (one k_sor_knn per batch): SURVEY 8(d) algorithmic bytes of the SOR kNN =
+    # 12 B per input point (the voxel centroids) + 12 B per kept point; read by tools/parse_pmc.py
+    print(json.dumps({"filter_batch": B, "frames": a.frames, "voxels_per_launch": run_all.vox / nb,
+                      "kept_per_launch": kept / nb,
+                      "sor_algorithmic_bytes_per_launch": 12.0 * (run_all.vox + kept) / nb}), flush=True)
     L.call("ot_rgbd_filter_destroy", h)

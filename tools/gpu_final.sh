@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 records on the final build (part A): every -m gpu test, smoke(), the default bench line, the rocprofv3
+# Round records on the final build (part A): every -m gpu test, smoke(), the default bench line, the rocprofv3
 # headline kernel stats (the roofline's kernel time cross-check), the configs[2] kernel breakdown and one object's
 # kernel timeline.  Part B is tools/pmc.sh (same-hash PMC traffic for the bench's roofline objects).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-T=${TAG:-r04z}
+T=${TAG:?set TAG, e.g. r05z}
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
     > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${T}_gpu_tests.log; exit 1; }
 tail -1 gpurun_out/${T}_gpu_tests.log
@@ -24,7 +24,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
     || { echo PROF_FAILED; tail -30 gpurun_out/${T}_bench_prof_h.log; exit 1; }
 tail -1 gpurun_out/${T}_bench_prof_h.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_fb_prof -o run -- python3 -u \
-    tools/filter_batch_time.py --frames 64 --batches 32 --reps 3 > gpurun_out/${T}_fb_prof.log 2>&1 \
+    tools/filter_batch_time.py --frames 128 --batches 64 --reps 3 > gpurun_out/${T}_fb_prof.log 2>&1 \
     || { echo FBPROF_FAILED; tail -20 gpurun_out/${T}_fb_prof.log; exit 1; }
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T}_obj_trace -o run -- python3 -u \
     tools/single_object_trace.py > gpurun_out/${T}_obj_trace.log 2>&1 || { echo TRACE_FAILED; tail -20 gpurun_out/${T}_obj_trace.log; exit 1; }

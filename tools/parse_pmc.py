@@ -44,6 +44,20 @@ def load(dirs):
     return per
 
 
+def filter_config(dirs):
+    """workload of the configs[2] PMC runs: tools/filter_batch_time.py prints one JSON line per batch size with the
+    frames per launch and the SOR kNN's algorithmic bytes per launch (12 B per input point + 12 B per kept point)"""
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "*.log")) + [d + ".log"]:
+            if os.path.exists(f):
+                for line in open(f):
+                    if line.startswith("{") and "filter_batch" in line:
+                        j = json.loads(line)
+                        return {"batch": j["filter_batch"], "frames": j["frames"],
+                                "algorithmic_bytes_per_launch": round(j["sor_algorithmic_bytes_per_launch"])}
+    return {}
+
+
 def calibration(dirs):
     """Factors known bytes / counter bytes per fetch_calib pattern (None when the calibration run is missing)."""
     per = load(dirs)
@@ -96,8 +110,8 @@ def main():
         cfg = dict(BASE_CFG)
         if kern.startswith("k_batch_integrate"):
             cfg["color_bits"] = 64 if kern.endswith("<true>") else 32
-        else:
-            cfg = {}
+        else:  # k_sor_knn: the configs[2] chain at the batch size the filter runs used (their logs say it)
+            cfg = filter_config(dirs)
         ent = {"config": cfg, "bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch),
                "write_bytes": round(write), "fetch_correction": fcorr, "write_correction": wcorr,
                "fetch_correction_source": "tools/fetch_calib.hip k_cal_gather8 (8-B buffer gathers, measured)" if f8

@@ -4,12 +4,12 @@
 #   c  : tools/fetch_calib (known-byte reads / writes per access pattern: the FETCH / WRITE corrections)
 #   h64: the headline bench leg at colour precision 64 (k_batch_integrate<true>)
 #   h32: the same at colour precision 32 (k_batch_integrate<false>), FETCH / WRITE only
-#   f  : the configs[2] batched chain (k_sor_knn)
+#   f  : the configs[2] batched chain (k_sor_knn), 64-frame batches as bench.py times them
 # Output: gpurun_out/pmc_<w>_<i>/ and profiles/pmc_traffic.json (tagged with the source hash of this build).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 HEAD_ARGS="--steps 2 --warmup 1 --sustain 0 --cpu-frames 0 --filter-frames 0 --objects 0 --hybrid-objects 0 --color32 0"
-FILT_ARGS="--frames 64 --batches 32 --reps 1"
+FILT_ARGS="--frames 128 --batches 64 --reps 1"  # the bench times 64-frame batches (--filter-batch 64)
 TRAFFIC=("FETCH_SIZE" "WRITE_SIZE")
 DIAG=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES"
       "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE TA_TA_BUSY_sum TD_TD_BUSY_sum")
