@@ -70,10 +70,16 @@ def parse():
     ap.add_argument("--object-frames", type=int, default=64, help="configs[3]: frames per object scan")
     ap.add_argument("--filter-streams", type=int, default=3,
                     help="configs[2]: batches filtered concurrently (host threads x HIP streams)")
+    ap.add_argument("--objects-sampling", default="fused", choices=("fused", "batch"),
+                    help="configs[3]: per object one host call from the marching-cubes totals to the sampler "
+                         "(extract_mesh_and_sample_min_z), or every object's mesh first and one batched sampling call")
     ap.add_argument("--object-streams", type=int, default=2,
                     help="configs[3]: objects reconstructed concurrently per GPU (host threads x HIP streams)")
     ap.add_argument("--spatial", type=int, default=1,
                     help="N > 1: also time one object spatially sharded over the N GPUs (SURVEY 8(e))")
+    ap.add_argument("--shard-steps", type=int, default=20,
+                    help="N = 1: per-rank step of the headline scan spatially sharded over 2 / 4 / 8 ranks, every rank's "
+                         "shard timed on this GPU (0 = skip)")
     ap.add_argument("--hybrid-objects", type=int, default=32,
                     help="configs[4]: object clouds in the hybrid-map fusion + change detection; 0 = skip")
     return ap.parse_args()
@@ -328,6 +334,8 @@ def main():
 
     spatial = spatial_shard(args, L, lib, synth, torch, dist, rank, world, n_units.value) \
         if (world > 1 and args.spatial) else None
+    shard_steps = shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, ms_per_step) \
+        if (world == 1 and args.shard_steps > 0) else None
 
     cpu = None
     if rank == 0 and args.cpu_frames > 0:
@@ -350,7 +358,7 @@ def main():
                       "sdf_trunc": args.sdf_trunc, "volume_units": n_units.value,
                       "unit_integrations_per_step": unit_int.value, "parallelism": f"objects{world}"},
            "roofline": roofline, "cpu_baseline": cpu, "sustained": sustained, "color32": color32,
-           "spatial_amdahl": spatial_amdahl(fms.value / max(fbatches.value, 1), kernel_ms_avg),
+           "spatial_amdahl": spatial_amdahl(fms.value / max(fbatches.value, 1), kernel_ms_avg, shard_steps),
            "filtered": filt, "objects": objects,
            "hybrid_map": hybrid, "single_frame": single, "spatial": spatial, "source_hash": L.source_hash()}
     if rank == 0:
@@ -502,7 +510,61 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
             "frontend_note": "every rank stages and unprojects every frame (undivided); the integrate divides by units"}
 
 
-def spatial_amdahl(frontend_ms, integrate_ms):
+def shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, headline_ms, worlds=(2, 4, 8)):
+    """SURVEY 8(e) measured on one GPU: the headline step (reset + the 256-frame scan + flush) of a volume that keeps
+    only rank r's units (ot_tsdf_set_shard(r, N)), for every rank r of N = 2, 4, 8, with the double-buffered front end
+    (the sharded default: batch k+1's staging / touch beside batch k's integrate) and, for comparison, without it.  A
+    rank's step on an N-GPU node is this time (its shard, its front end, nothing shared with the other ranks), so
+    headline_ms / max over r is the strong-scaling speed-up of one object before the halo extraction."""
+    W, H = intr.width, intr.height
+    npx = W * H
+    dptrs = [C.c_void_p(d_depth.data_ptr() + k * npx * 2) for k in range(args.frames)]
+    cptrs = [C.c_void_p(d_color.data_ptr() + k * npx * 3) for k in range(args.frames)]
+    eptrs = [ext[k].ctypes.data_as(C.c_void_p) for k in range(args.frames)]
+    integrate, pintr = lib.ot_tsdf_integrate_u16, C.byref(intr)
+    out = {}
+    for N in worlds:
+        per_mode = {}
+        for mode in (1, 0):
+            worst, units = 0.0, []
+            for r in range(N):
+                vol = C.c_void_p()
+                L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
+                try:
+                    L.call("ot_tsdf_set_color_precision", vol, args.color_bits)
+                    L.call("ot_tsdf_set_shard", vol, r, N)
+                    L.call("ot_tsdf_set_frontend_overlap", vol, mode)
+
+                    def step():
+                        L.call("ot_tsdf_reset_async", vol, stream)
+                        for k in range(args.frames):
+                            if integrate(vol, dptrs[k], cptrs[k], pintr, eptrs[k], 1000.0, 3.0, stream):
+                                raise RuntimeError(lib.ot_last_error().decode())
+                        L.call("ot_tsdf_flush", vol, stream)
+
+                    for _ in range(3):
+                        step()
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for _ in range(args.shard_steps):
+                        step()
+                    torch.cuda.synchronize()
+                    worst = max(worst, (time.perf_counter() - t0) * 1e3 / args.shard_steps)
+                    nu = C.c_int64(0)
+                    L.call("ot_tsdf_num_units", vol, C.byref(nu), stream)
+                    units.append(nu.value)
+                finally:
+                    L.call("ot_tsdf_destroy", vol)
+            per_mode["overlap" if mode else "serial"] = {"rank_step_ms_max": round(worst, 4),
+                                                         "speedup": round(headline_ms / worst, 2) if worst else None}
+        per_mode["units_per_rank_min_max"] = [min(units), max(units)]
+        out[str(N)] = per_mode
+    return {"method": "every rank's shard of the headline scan timed on this GPU (reset + 256 frames + flush, "
+                      f"{args.shard_steps} steps after 3 warm-up), max over ranks; speedup = headline ms_per_step / that",
+            "headline_ms_per_step": round(headline_ms, 4), "worlds": out}
+
+
+def spatial_amdahl(frontend_ms, integrate_ms, measured=None):
     """Amdahl bound of ONE object spatially sharded over N GPUs, from this run's per-batch device times:
     every rank stages every pixel of every frame and unprojects every stride sample (the front end: staging + touch +
     unit headers; only the touch's hash inserts divide), while the integrate divides by the units each rank owns.
@@ -514,8 +576,12 @@ def spatial_amdahl(frontend_ms, integrate_ms):
         return None
     return {"frontend_ms_per_batch": round(F, 5), "integrate_ms_per_batch": round(I, 5),
             "undivided_fraction": round(F / (F + I), 4),
-            "speedup_cap": {str(n): round((F + I) / (F + I / n), 2) for n in (2, 4, 8)},
-            "note": "one object over N GPUs; the weak-scaling headline (one object per GPU) is not bounded by this"}
+            "speedup_cap_serial": {str(n): round((F + I) / (F + I / n), 2) for n in (2, 4, 8)},
+            "speedup_cap_overlap": {str(n): round((F + I) / max(F, I / n), 2) for n in (2, 4, 8)},
+            "measured": measured,
+            "note": "one object over N GPUs; caps model a step as F + I/N per batch (front end then integrate) or "
+                    "max(F, I/N) (double-buffered front end beside the previous batch's integrate); `measured` times "
+                    "every rank's shard; the weak-scaling headline (one object per GPU) is not bounded by this"}
 
 
 def single_frame(L, synth, torch, depth, color, ext, intr_t, reps=50):
@@ -638,19 +704,26 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
                 # the object's 64 frames in one host call (ot_tsdf_integrate_u16_frames = 64 ot_tsdf_integrate_u16)
                 if lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, stream):
                     raise RuntimeError(lib.ot_last_error().decode())
+                if fused:  # extract -> normals -> 100k samples + Z mask, one host call
+                    out[j] = vol.extract_mesh_and_sample_min_z(100000, 0.03)[1]
+                    continue
                 mesh = vol.extract_triangle_mesh()
                 mesh.compute_vertex_normals()
                 out[j] = mesh
             streams[t].synchronize()
         return out
 
+    fused = args.objects_sampling == "fused"
+
     def run():
         parts = {}
         for r in pool.map(reconstruct, range(T)):
             parts.update(r)
-        meshes = [parts[j] for j in range(len(dev))]
-        # the objects' 100k-point samplings and Z masks in one call: their serial area-CDF chains run side by side
-        pcds = pkg.geometry.TriangleMesh.sample_points_min_z_batch(meshes, 100000, 0.03)
+        if fused:
+            pcds = [parts[j] for j in range(len(dev))]
+        else:  # the objects' 100k-point samplings and Z masks in one call: their area-CDF chains side by side
+            pcds = pkg.geometry.TriangleMesh.sample_points_min_z_batch([parts[j] for j in range(len(dev))], 100000,
+                                                                      0.03)
         clouds = [p._xyz.dev() for p in pcds]
         # one collective, counts in-band: every rank holds <= ceil(objects / N) objects of <= 100k points
         merged = D.merge_object_clouds(clouds, capacity=((args.objects + world - 1) // world) * 100000)
@@ -673,6 +746,8 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
             vol.reset()
             if lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_):
                 raise RuntimeError(lib.ot_last_error().decode())
+            if fused:
+                return vol.extract_mesh_and_sample_min_z(100000, 0.03)[1]
             mesh = vol.extract_triangle_mesh()
             mesh.compute_vertex_normals()
             return mesh.sample_points_min_z(100000, 0.03)
@@ -688,7 +763,8 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
         single = round(float(np.median(ts)) * 1e3, 3)
     merge = _merge_label(world)
     return {"workload": f"configs[3]: {args.objects} object scans x {args.object_frames} 640x480 frames, "
-                        f"{args.voxel * 1000:g} mm TSDF -> mesh -> normals -> 100k samples + z mask (one pass) per object, "
+                        f"{args.voxel * 1000:g} mm TSDF -> mesh -> normals -> 100k samples + z mask (one pass) per object "
+                        f"({'one host call from the mesh totals to the sampler' if fused else 'batched sampling'}), "
                         f"contiguous object shards over {world} GPU(s) ({T} concurrent streams per GPU), merge: {merge}",
             "frames_per_s": round(args.objects * args.object_frames / dt, 1), "ms": round(dt * 1e3, 3),
             "objects_per_rank": len(ids), "merged_points": int(merged.shape[0]), "merge": merge,

@@ -189,6 +189,13 @@ ot_status ot_tsdf_flush(ot_tsdf* vol, void* stream);
 ot_status ot_tsdf_pending_frames(const ot_tsdf* vol, int32_t* n_host);
 /* Batch size used by ot_tsdf_integrate_u16 (1 = integrate immediately, default and maximum 64). */
 ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames);
+/* Double-buffered batch front end (spatial sharding of one object: reconstruct_rgbd_filter.py:88-109):
+ * with mode 1 batch k+1's staging, touch and unit headers run on the caller's stream while batch k's integrate runs on
+ * a second stream of the volume (two staging sets); readers (num_units, export, extraction, flush, reset) order the
+ * caller's stream after the last integrate.  -1 (default): on for a spatially sharded volume (ot_tsdf_set_shard with
+ * world > 1, whose integrate is 1/world of the work and would otherwise wait behind the undivided front end), off
+ * otherwise; 0: off.  Results are identical in every mode. */
+ot_status ot_tsdf_set_frontend_overlap(ot_tsdf* vol, int32_t mode);
 
 /* Number of allocated volume units.  Queued frames are integrated first, on `stream`; synchronises `stream`. */
 ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n_units_host, void* stream);
@@ -358,6 +365,21 @@ ot_status ot_mesh_sample_points_uniformly_after(const ot_mesh_sample_job* jobs_h
  * [n_jobs], the kept row count of each job.  Synchronises the stream. */
 ot_status ot_mesh_sample_points_min_z(const ot_mesh_sample_job* jobs_host, int32_t n_jobs, int64_t n_points,
                                       uint64_t seed, double z_min, int64_t* n_kept_host, void* stream);
+/* reconstruct_rgbd_filter.py:112-132 of one volume in ONE host call (replaces the facade's extract_triangle_mesh ->
+ * compute_vertex_normals -> sample_points_uniformly + Z-mask sequence at :112-132; no host work between the
+ * marching-cubes totals and the sampler's first launch): the mesh into vertices / vertex_colors / triangles with the
+ * given capacities exactly as ot_tsdf_extract_triangle_mesh_into, then ot_mesh_sample_points_min_z of it (n_points,
+ * seed, z_min; kept rows into out_xyz / out_rgb, each with room for n_points rows; out_rgb may be NULL), and its vertex
+ * normals (ot_tsdf_mesh_vertex_normals, bit-identical to ot_mesh_compute_vertex_normals) into vertex_normals (NULL:
+ * none) on normals_stream beside the sampling -- a reader of the normals orders itself after normals_stream.
+ * OT_ERR_CAPACITY: the mesh did not fit; *n_vertices / *n_triangles are its size, nothing was sampled (emit it with
+ * ot_tsdf_emit_triangle_mesh and sample it separately).  An empty mesh samples nothing (*n_kept_host = 0).
+ * Synchronises `stream`. */
+ot_status ot_tsdf_extract_sample_min_z(ot_tsdf* vol, double* vertices, double* vertex_colors, int32_t* triangles,
+                                       int64_t capacity_vertices, int64_t capacity_triangles, double* vertex_normals,
+                                       void* normals_stream, int64_t n_points, uint64_t seed, double z_min,
+                                       double* out_xyz, double* out_rgb, int64_t* n_vertices_host,
+                                       int64_t* n_triangles_host, int64_t* n_kept_host, void* stream);
 /* The same in two calls: _async queues the sampling and returns without synchronising (the output arrays must stay
  * allocated), _wait synchronises it and fills n_kept_host.  Between them the calling thread may queue other work (the
  * facade queues a fresh mesh's deferred vertex normals there, beside the sampling's walks) but no other sampling. */

@@ -66,6 +66,7 @@ SIGNATURES = {
     "ot_tsdf_integrate_u16_frames": [_p, _i32, _p, _p, _pint, _p, _d, _d, _p],
     "ot_tsdf_flush": [_p, _p],
     "ot_tsdf_set_batch": [_p, _i32],
+    "ot_tsdf_set_frontend_overlap": [_p, _i32],
     "ot_tsdf_pending_frames": [_p, _p],
     "ot_tsdf_num_units": [_p, _pi64, _p],
     "ot_tsdf_counters": [_p, _pi64, _pi64, _p],
@@ -91,6 +92,8 @@ SIGNATURES = {
     "ot_tsdf_extract_triangle_mesh_count": [_p, _pi64, _pi64, _p],
     "ot_tsdf_emit_triangle_mesh": [_p, _p, _p, _p, _p],
     "ot_tsdf_extract_triangle_mesh_into": [_p, _p, _p, _p, _i64, _i64, _pi64, _pi64, _p],
+    "ot_tsdf_extract_sample_min_z": [_p, _p, _p, _p, _i64, _i64, _p, _p, _i64, C.c_uint64, _d, _p, _p, _pi64, _pi64,
+                                     _pi64, _p],
     "ot_mesh_compute_vertex_normals": [_p, _i64, _p, _i64, _p, _p],
     "ot_mesh_sample_points_uniformly": [_p, _p, _p, _i64, _p, _i64, _i64, C.c_uint64, _p, _p, _p, _p],
     "ot_mesh_sample_points_uniformly_batch": [_p, _i32, _i64, C.c_uint64, _p],

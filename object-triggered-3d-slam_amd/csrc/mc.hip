@@ -369,6 +369,13 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
 // Their triangles are the vertex's triangles; walking the cubes in ascending triangle index (unit rank, then the cube's
 // offset inside the unit) and each cube's triangles in table order adds the triangle normals in triangle order --
 // Open3D's loop over the triangles -- with no sort of the 3T corners.  One lane per vertex.
+// The walk is one lane's chain of dependent loads, so its loads issue in phases: the owner id (stored by the emission,
+// no hash probe) -> the 4 cubes' neighbour ids -> their cube bytes, ranks and in-unit triangle offsets -> their triangle
+// bases; then per cube (in triangle order) the rows of its triangles that contain the edge, then their corners.  The 4
+// edges along each axis are a fixed table (no register array indexed at run time).  A cube's triangles are its first
+// c_ntri[cube] table rows: the rows after the -1 terminator are ZERO-filled, and testing them for the edge would count
+// phantom triangles of edge 0 (round 4's mismatch).
+__constant__ unsigned char c_axis_edges[3][4] = {{0, 2, 4, 6}, {1, 3, 5, 7}, {8, 9, 10, 11}};
 __global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t units, const double* __restrict__ V,
                                                      const int32_t* __restrict__ T, int64_t nv, double* __restrict__ N) {
     const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -377,48 +384,71 @@ __global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t
     const int local = key.w / 3, axis = key.w % 3;
     const int g[3] = {key.x * UNIT_RES + (local >> 8), key.y * UNIT_RES + ((local >> 4) & 15),
                       key.z * UNIT_RES + (local & 15)};
-    long long start[4];
-    int cubev[4], edge[4];
-    int nc = 0;
     const int owner = m.vown ? m.vown[v] : find_unit(d, key.x, key.y, key.z);  // the emission's owner id: no probe
     if (owner < 0 || owner >= units) return;  // cannot happen for a vertex of this extraction
+    int edge[4], id[4], ci[4];
 #pragma unroll
-    for (int e = 0; e < 12; ++e) {
-        if (c_eshift[e][3] != axis) continue;
+    for (int k = 0; k < 4; ++k) {
+        const int e = c_axis_edges[axis][k];
         const int c[3] = {g[0] - c_eshift[e][0], g[1] - c_eshift[e][1], g[2] - c_eshift[e][2]};
         // the cube's unit is the owner or one of its -x/-y/-z neighbours (arithmetic shift: floor for negatives)
         const int ox = key.x - (c[0] >> 4), oy = key.y - (c[1] >> 4), oz = key.z - (c[2] >> 4);
-        const int id = m.nbr[owner * 16 + 8 + (ox << 2 | oy << 1 | oz)];
-        if (id < 0 || id >= units) continue;
-        const int ci = ((c[0] & 15) * 16 + (c[1] & 15)) * 16 + (c[2] & 15);
-        const int cube = m.cubes[(size_t)id * UNIT_VOX + ci];
-        if (cube == 0) continue;
-        start[nc] = m.tri_base[m.rank_of[id]] + m.ctri[(size_t)id * UNIT_VOX + ci];
-        cubev[nc] = cube;
-        edge[nc] = e;
-        ++nc;
+        edge[k] = e;
+        ci[k] = ((c[0] & 15) * 16 + (c[1] & 15)) * 16 + (c[2] & 15);
+        id[k] = m.nbr[owner * 16 + 8 + (ox << 2 | oy << 1 | oz)];
     }
-    // ascending triangle index (<= 4 cubes: insertion sort)
-    for (int i = 1; i < nc; ++i)
-        for (int j = i; j > 0 && start[j] < start[j - 1]; --j) {
-            const long long ts = start[j];
-            start[j] = start[j - 1], start[j - 1] = ts;
-            const int tc = cubev[j];
-            cubev[j] = cubev[j - 1], cubev[j - 1] = tc;
-            const int te = edge[j];
-            edge[j] = edge[j - 1], edge[j - 1] = te;
+    int cubev[4], rk[4], ct[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool ok = id[k] >= 0 && id[k] < units;
+        cubev[k] = ok ? (int)m.cubes[(size_t)id[k] * UNIT_VOX + ci[k]] : 0;
+        rk[k] = ok ? m.rank_of[id[k]] : 0;
+        ct[k] = ok ? (int)m.ctri[(size_t)id[k] * UNIT_VOX + ci[k]] : 0;
+    }
+    long long start[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) start[k] = cubev[k] ? m.tri_base[rk[k]] + ct[k] : 0x7FFFFFFFFFFFFFFFll;
+    // ascending triangle index: a 4-input sorting network (empty cubes sort last)
+    auto cswap = [&](int a, int b) {
+        if (start[b] < start[a]) {
+            const long long ts = start[a];
+            start[a] = start[b], start[b] = ts;
+            const int tc = cubev[a];
+            cubev[a] = cubev[b], cubev[b] = tc;
+            const int te = edge[a];
+            edge[a] = edge[b], edge[b] = te;
         }
+    };
+    cswap(0, 1);
+    cswap(2, 3);
+    cswap(0, 2);
+    cswap(1, 3);
+    cswap(1, 2);
     double n[3] = {0.0, 0.0, 0.0};
-    for (int i = 0; i < nc; ++i) {
-        long long tri = start[i];
-        for (int k = 0; k < 15 && c_tri[cubev[i]][k] != -1; k += 3, ++tri) {
-            const int e = edge[i];
-            if (c_tri[cubev[i]][k] != e && c_tri[cubev[i]][k + 1] != e && c_tri[cubev[i]][k + 2] != e) continue;
-            double tn[3];
-            triangle_normal(V, T[tri * 3], T[tri * 3 + 1], T[tri * 3 + 2], tn);
-            n[0] += tn[0];
-            n[1] += tn[1];
-            n[2] += tn[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (cubev[i]) {  // empty cubes sorted last
+            const int cube = cubev[i], e = edge[i], nt = c_ntri[cube];
+            // the cube's table triangles (its first nt rows, in order) that contain the edge: rows, then corners, sum
+            bool has[5];
+            int row[5][3];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int t0 = c_tri[cube][3 * k], t1 = c_tri[cube][3 * k + 1], t2 = c_tri[cube][3 * k + 2];
+                has[k] = k < nt && (t0 == e || t1 == e || t2 == e);
+                const long long tri = start[i] + k;
+#pragma unroll
+                for (int r = 0; r < 3; ++r) row[k][r] = has[k] ? T[tri * 3 + r] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                if (has[k]) {
+                    double tn[3];
+                    triangle_normal(V, row[k][0], row[k][1], row[k][2], tn);
+                    n[0] += tn[0];
+                    n[1] += tn[1];
+                    n[2] += tn[2];
+                }
         }
     }
     finish_vertex_normal(n);
@@ -744,6 +774,47 @@ ot_status ot_tsdf_mesh_vertex_normals(ot_tsdf* vol, int64_t serial, const double
     OT_HIP_TRY(hipEventRecord(vol->ev_normals, stream));
     vol->normals_pending = true;
     return OT_OK;
+}
+
+// reconstruct_rgbd_filter.py:112-132 of one volume in ONE host call: extract_triangle_mesh into the caller's arrays
+// (capacities guessed, as ot_tsdf_extract_triangle_mesh_into), then -- with no host work between the marching-cubes
+// totals and the sampler's first launch -- sample_points_uniformly(n_points, seed) + the z >= z_min mask (the fused
+// sampler, points and colours), and compute_vertex_normals of the mesh on `normals_stream` beside the sampling (the
+// sampling does not read them; a reader of `normals` waits for normals_stream).  On a capacity miss nothing is sampled
+// and OT_ERR_CAPACITY returns the totals (emit with ot_tsdf_emit_triangle_mesh, then sample as usual).  An empty mesh
+// samples nothing (*n_kept = 0; the reference skips it: reconstruct_rgbd_filter.py:115-117).
+ot_status ot_tsdf_extract_sample_min_z(ot_tsdf* vol, double* vertices, double* vertex_colors, int32_t* triangles,
+                                       int64_t capacity_vertices, int64_t capacity_triangles, double* vertex_normals,
+                                       void* normals_stream, int64_t n_points, uint64_t seed, double z_min,
+                                       double* out_xyz, double* out_rgb, int64_t* n_vertices, int64_t* n_triangles,
+                                       int64_t* n_kept, void* stream_) {
+    hipStream_t stream = S(stream_);
+    if (!vol || !n_kept || !out_xyz || n_points <= 0 || (out_rgb && !vertex_colors))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ExtractTriangleMesh] invalid arguments");
+    *n_kept = 0;
+    ot_status st = ot_tsdf_extract_triangle_mesh_into(vol, vertices, vertex_colors, triangles, capacity_vertices,
+                                                      capacity_triangles, n_vertices, n_triangles, stream_);
+    if (st != OT_OK) return st;
+    const int64_t nv = *n_vertices, nt = *n_triangles;
+    if (nv == 0 || nt == 0) return OT_OK;
+    if (!vol->ev_made) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_made, hipEventDisableTiming));
+    OT_HIP_TRY(hipEventRecord(vol->ev_made, stream));  // the mesh arrays are complete here
+    ot_mesh_sample_job job{vertices, nullptr, out_rgb ? vertex_colors : nullptr, nv, triangles, nt, out_xyz, nullptr,
+                           out_rgb};
+    hipStream_t hs = nullptr;
+    st = sample_min_z_enqueue(&job, 1, n_points, seed, z_min, stream, &hs);
+    if (st != OT_OK) return st;
+    if (vertex_normals) {  // queued once the sampling is (its chains' first passes are dispatched ahead of them)
+        hipStream_t ns = S(normals_stream);
+        OT_HIP_TRY(hipStreamWaitEvent(ns, vol->ev_made, 0));
+        st = ot_tsdf_mesh_vertex_normals(vol, vol->mesh.serial, vertices, nv, triangles, nt, vertex_normals, ns);
+        if (st != OT_OK) {
+            int64_t dummy = 0;
+            (void)sample_min_z_wait(hs, 1, &dummy);
+            return st;
+        }
+    }
+    return sample_min_z_wait(hs, 1, n_kept);
 }
 
 ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* vertex_colors, int32_t* triangles,

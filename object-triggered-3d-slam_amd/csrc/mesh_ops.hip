@@ -1217,6 +1217,15 @@ static ot_status min_z_wait(hipStream_t hs, int32_t n_jobs, int64_t* n_kept_host
     for (int j = 0; j < n_jobs; ++j) n_kept_host[j] = kept[j];
     return OT_OK;
 }
+// the fused extraction + sampling of one volume (mc.hip ot_tsdf_extract_sample_min_z) drives the same two phases
+ot_status sample_min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
+                               double z_min, hipStream_t stream, hipStream_t* hs) {
+    if (g_minz.active) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
+    return min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, (void*)stream, hs);
+}
+ot_status sample_min_z_wait(hipStream_t hs, int32_t n_jobs, int64_t* n_kept_host) {
+    return min_z_wait(hs, n_jobs, n_kept_host);
+}
 }  // namespace ot
 
 extern "C" {

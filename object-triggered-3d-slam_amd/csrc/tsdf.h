@@ -171,9 +171,6 @@ struct ot_tsdf {
     // batching of integrate_u16: frames per fused launch (ot_tsdf_set_batch; 64 = MAX_BATCH, measured best, §4)
     int batch_max = ot::MAX_BATCH;
     std::vector<ot::PendingFrame> pending;
-    void* batch_ws = nullptr;       // unused (kept for ABI of the struct layout)
-    size_t batch_ws_bytes = 0;
-    ot::BatchFrame* bframes = nullptr;     // device [MAX_BATCH]
     ot::BatchFrame* hbframes = nullptr;    // pinned host staging [2][MAX_BATCH]
     unsigned* hmail = nullptr;             // pinned coherent host mailbox [OT_MAIL_WORDS]: small read-backs stored
                                            // by a one-wave kernel (mail_words) instead of staged D2H copies
@@ -186,9 +183,24 @@ struct ot_tsdf {
     int early_frame = -1;
     hipEvent_t ev_mail = nullptr;  // behind a mailbox read-back that work queued after it must not delay
     int batch_pc = ot::C_BATCH_PAIRS;      // pair counter of the next batch (alternates 4, 5)
-    float2* bdm = nullptr;                 // device [batch][h][w] packed (depth, multiplier)
-    uint32_t* brgba = nullptr;             // device [batch][h][w] packed colour
-    int64_t bdepth_cap = 0;                // pixels (frames * h * w) the two buffers hold
+    // A batch's staging: per-frame parameters, packed (depth, multiplier) and colour per pixel, and the unit work list.
+    // Two sets: with the front end double-buffered (overlap, ot_tsdf_set_frontend_overlap: on by default for a spatially
+    // sharded volume, whose integrate is 1/N of the work) batch k+1's staging / touch / units run on the caller's stream
+    // while batch k's integrate runs on `istream`; otherwise set 0 only, everything on the caller's stream.
+    struct BatchSet {
+        ot::BatchFrame* bframes = nullptr;  // device [MAX_BATCH]
+        float2* bdm = nullptr;              // device [batch][h][w] packed (depth, multiplier)
+        uint32_t* brgba = nullptr;          // device [batch][h][w] packed colour
+        int64_t cap = 0;                    // pixels (frames * h * w) the two buffers hold
+        void* work = nullptr;               // UnitWork [hash_cap]; set 0 uses dev.work
+        hipEvent_t ev_units = nullptr;      // the set's units kernel (its integrate waits for it)
+        hipEvent_t ev_done = nullptr;       // the set's integrate (the set's next front end waits for it)
+    } bset[2];
+    int overlap_mode = -1;        // -1: on when sharded, 0 off, 1 on
+    int bset_next = 0;            // set of the next batch (alternates in overlap mode)
+    int last_set = -1;            // set of the last batch whose integrate ran on istream (joined by readers)
+    hipStream_t istream = nullptr;
+    int* wcount = nullptr;        // device [2]: the sets' work-list lengths (k_batch_units -> k_batch_integrate)
     // sorted-unit cache (rank -> id), valid for `sorted_units` units
     unsigned* sorted_ids = nullptr;
     int64_t sorted_units = -1;
@@ -202,6 +214,7 @@ struct ot_tsdf {
     // structure (mesh.ws, vk, vown): work that rewrites it or the units waits for this event first (wait_normals)
     hipEvent_t ev_normals = nullptr;
     bool normals_pending = false;
+    hipEvent_t ev_made = nullptr;  // ot_tsdf_extract_sample_min_z: the mesh arrays are complete (the normals wait on it)
     // kernel timing (events around the dominant integration kernel)
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
@@ -222,7 +235,13 @@ struct MailSrc {
     int n;
 };
 ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream);
-ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream);
+// integrate the queued frames; readers (join = true) also order `stream` after the last batch's integrate when it ran on
+// the volume's integrate stream (double-buffered front end)
+ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream, bool join = true);
 // order `stream` after the volume's deferred vertex normals, if any are still in flight
 ot_status wait_normals(ot_tsdf* vol, hipStream_t stream);
+// the fused sampler's two phases (mesh_ops.hip): queue the chains + emission on `stream`, then wait for the kept counts
+ot_status sample_min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
+                               double z_min, hipStream_t stream, hipStream_t* hs);
+ot_status sample_min_z_wait(hipStream_t hs, int32_t n_jobs, int64_t* n_kept_host);
 }  // namespace ot

@@ -365,12 +365,18 @@ struct UnitWork {
 // pool cannot hold is dropped (id -1, C_OVERFLOW; not counted) and integrated by the replay once the pool has grown.
 // REPLAY: units that already have an id were integrated by the batch's first pass: skipped (id -1, not counted).
 template <bool REPLAY>
+// wcount: where the integrate reads the batch's work-list length (the pair counter itself, or -- with the front end
+// double-buffered -- a per-set copy, since the next batch's units kernel zeroes the other pair counter while this
+// batch's integrate may still run)
 __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __restrict__ work, int pc,
-                                                     unsigned* __restrict__ early_mail) {
+                                                     unsigned* __restrict__ early_mail, int* __restrict__ wcount) {
     __shared__ unsigned long long red[4];
     const int n = d.counters[pc];
     // the other counter belongs to the next batch; the previous batch's integrate (its last reader) has finished
-    if (blockIdx.x == 0 && threadIdx.x == 0) d.counters[pc ^ 1] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        d.counters[pc ^ 1] = 0;
+        if (wcount) *wcount = n;
+    }
     unsigned long long pairs = 0;
     for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
         const int slot = d.bslots[t];
@@ -447,7 +453,8 @@ constexpr int RCP_N = 2048;  // 16 KiB (float64) / 8 KiB (float32) of LDS per wo
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes.
 template <bool C64, bool FAST>
 __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU) void k_batch_integrate(
-    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work, int pc) {
+    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
+    const int* __restrict__ wcount) {
     using CT = typename std::conditional<C64, double, float>::type;
     // one table per kernel: float64 reciprocals for the float64-colour kernel (its float32 ones are their roundings:
     // (float)RN64(1/n) == RN32(1/n) for every n <= 2^20, no double-rounding case -- tools/markstein_check.cpp),
@@ -462,7 +469,7 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
-    const int n = d.counters[pc];
+    const int n = *wcount;
     const int npx = p.W * p.H;
     unsigned upd = 0;  // per lane: <= BZ voxels x 64 frames x units per workgroup, far below 2^32
     {
@@ -1071,8 +1078,43 @@ static int integrate_grid(int variant) {
     return cache_c[dev];
 }
 
-static ot_status settle_batch(ot_tsdf* vol, const BatchTouchParams& tp, const IntegrateParams& ip0, unsigned tiles,
-                              int n, int pc, int variant, hipStream_t stream);
+// the context a batch's settle (and a replay) needs
+struct BatchCtx {
+    BatchTouchParams tp;
+    IntegrateParams ip0;
+    unsigned tiles;
+    int n, pc, variant, set;
+};
+static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stream);
+
+static bool overlap_on(const ot_tsdf* vol) {
+    return vol->overlap_mode > 0 || (vol->overlap_mode < 0 && vol->dev.shard_world > 1);
+}
+static void* set_work(ot_tsdf* vol, int s) { return s == 0 ? vol->dev.work : vol->bset[1].work; }
+
+// order `stream` after the last batch's integrate when it ran on the volume's integrate stream
+static ot_status join_integrate(ot_tsdf* vol, hipStream_t stream) {
+    if (vol->last_set >= 0) {
+        OT_HIP_TRY(hipStreamWaitEvent(stream, vol->bset[vol->last_set].ev_done, 0));
+        vol->last_set = -1;
+    }
+    return OT_OK;
+}
+
+// the second batch set, the integrate stream and the sets' events (once per volume)
+static ot_status ensure_overlap(ot_tsdf* vol) {
+    if (vol->istream) return OT_OK;
+    OT_HIP_TRY(hipStreamCreateWithFlags(&vol->istream, hipStreamNonBlocking));
+    if (!vol->wcount) OT_HIP_TRY(hipMalloc(&vol->wcount, sizeof(int) * 2));
+    if (!vol->bset[1].bframes) OT_HIP_TRY(hipMalloc(&vol->bset[1].bframes, sizeof(BatchFrame) * MAX_BATCH));
+    if (!vol->bset[1].work) OT_HIP_TRY(hipMalloc(&vol->bset[1].work, sizeof(UnitWork) * vol->hash_cap));
+    for (auto& b : vol->bset) {
+        if (!b.ev_units) OT_HIP_TRY(hipEventCreateWithFlags(&b.ev_units, hipEventDisableTiming));
+        if (!b.ev_done) OT_HIP_TRY(hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
+    }
+    note_alloc();
+    return OT_OK;
+}
 
 static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n, hipStream_t stream) {
     const ot_intrinsics& in = frames[0].intr;
@@ -1080,53 +1122,62 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     if (st != OT_OK) return st;
     st = ensure_mult(vol, &in, stream);
     if (st != OT_OK) return st;
+    const bool ovl = overlap_on(vol);
+    if (ovl && (st = ensure_overlap(vol)) != OT_OK) return st;
+    const int set = ovl ? vol->bset_next : 0;
+    if (ovl) vol->bset_next ^= 1;
+    auto& bs = vol->bset[set];
+    // the set's previous batch (two batches ago) must have finished its integrate before its buffers are restaged
+    // (an event never recorded counts as complete)
+    if (ovl) OT_HIP_TRY(hipStreamWaitEvent(stream, bs.ev_done, 0));
     const int64_t npx = (int64_t)in.width * in.height;
-    if (vol->bdepth_cap < npx * n) {
-        if (vol->bdm) {
+    if (bs.cap < npx * n) {
+        if (bs.bdm) {
             OT_HIP_TRY(hipStreamSynchronize(stream));
-            OT_HIP_TRY(hipFree(vol->bdm));
-            OT_HIP_TRY(hipFree(vol->brgba));
-            vol->bdm = nullptr;
-            vol->brgba = nullptr;
+            if (vol->istream) OT_HIP_TRY(hipStreamSynchronize(vol->istream));
+            OT_HIP_TRY(hipFree(bs.bdm));
+            OT_HIP_TRY(hipFree(bs.brgba));
+            bs.bdm = nullptr;
+            bs.brgba = nullptr;
         }
         const int64_t cap = npx * std::max(n, std::min(vol->batch_max, MAX_BATCH));
-        OT_HIP_TRY(hipMalloc(&vol->bdm, sizeof(float2) * cap));
-        OT_HIP_TRY(hipMalloc(&vol->brgba, sizeof(uint32_t) * cap));
-        vol->bdepth_cap = cap;
+        OT_HIP_TRY(hipMalloc(&bs.bdm, sizeof(float2) * cap));
+        OT_HIP_TRY(hipMalloc(&bs.brgba, sizeof(uint32_t) * cap));
+        bs.cap = cap;
     }
     // per-frame parameters: pinned host staging (double-buffered, event-guarded) -> device
     const int hb = vol->hb_next;
     vol->hb_next ^= 1;
     if (vol->hb_event[hb]) OT_HIP_TRY(hipEventSynchronize(vol->hb_event[hb]));
     BatchFrame* host = vol->hbframes + hb * MAX_BATCH;
-    const IntegrateParams ip0 = make_integrate_params(vol, nullptr, nullptr, vol->mult, &in, frames[0].extrinsic);
+    BatchCtx bc;
+    bc.ip0 = make_integrate_params(vol, nullptr, nullptr, vol->mult, &in, frames[0].extrinsic);
     for (int k = 0; k < n; ++k) {
         const PendingFrame& f = frames[k];
         BatchFrame& b = host[k];
         b.depth16 = f.depth;
         b.depthf = f.depth ? nullptr : f.depthf;
         b.color = (vol->color_type == OT_COLOR_RGB8) ? f.color : nullptr;
-        b.dm = vol->bdm + npx * k;
-        b.rgba = vol->brgba + npx * k;
+        b.dm = bs.bdm + npx * k;
+        b.rgba = bs.brgba + npx * k;
         double pose[16];
         inverse4(f.extrinsic, pose);
         for (int i = 0; i < 12; ++i) b.pose[i] = pose[i];
         float E[16];
         for (int i = 0; i < 16; ++i) E[i] = (float)f.extrinsic[i];
         for (int i = 0; i < 12; ++i) b.E[i] = E[i];
-        b.es[0] = E[0 * 4 + 2] * ip0.vl;
-        b.es[1] = E[1 * 4 + 2] * ip0.vl;
-        b.es[2] = E[2 * 4 + 2] * ip0.vl;
+        b.es[0] = E[0 * 4 + 2] * bc.ip0.vl;
+        b.es[1] = E[1 * 4 + 2] * bc.ip0.vl;
+        b.es[2] = E[2 * 4 + 2] * bc.ip0.vl;
         b.scale = (float)f.depth_scale;
         b.trunc = f.depth_trunc;
     }
-    OT_HIP_TRY(hipMemcpyAsync(vol->bframes, host, sizeof(BatchFrame) * n, hipMemcpyHostToDevice, stream));
+    OT_HIP_TRY(hipMemcpyAsync(bs.bframes, host, sizeof(BatchFrame) * n, hipMemcpyHostToDevice, stream));
     if (!vol->hb_event[hb]) OT_HIP_TRY(hipEventCreateWithFlags(&vol->hb_event[hb], hipEventDisableTiming));
     OT_HIP_TRY(hipEventRecord(vol->hb_event[hb], stream));
-    // batch pair count and the integrate's queue heads
     // this batch's pair counter: zeroed by reset, or by the previous batch's k_batch_units (no memset here)
     const int pc = vol->batch_pc;
-    BatchTouchParams tp;
+    BatchTouchParams& tp = bc.tp;
     tp.mult = vol->mult;
     tp.npx = npx;
     tp.pc = pc;
@@ -1141,46 +1192,64 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.trunc = vol->sdf_trunc;
     tp.unit_len = vol->unit_length;
     tp.slot_cap = (int)vol->hash_cap;
-    const unsigned tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
+    bc.tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
+    bc.n = n;
+    bc.pc = pc;
+    bc.set = set;
     hipEvent_t f0 = nullptr, f1 = nullptr;  // front end (staging + touch + units): the part a sharded volume repeats
     if (vol->profiling) {
         OT_HIP_TRY(hipEventCreate(&f0));
         OT_HIP_TRY(hipEventCreate(&f1));
         OT_HIP_TRY(hipEventRecord(f0, stream));
     }
-    hipLaunchKernelGGL(k_batch_touch<false>, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
-                       (const BatchFrame*)vol->bframes, tp, vol->dev, n);
-    hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc,
-                       vol->hmail + OT_MAIL_WORDS);
+    UnitWork* work = (UnitWork*)set_work(vol, set);
+    int* wcount = ovl ? vol->wcount + set : vol->dev.counters + pc;
+    hipLaunchKernelGGL(k_batch_touch<false>, dim3(bc.tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
+                       (const BatchFrame*)bs.bframes, tp, vol->dev, n);
+    hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, work, pc,
+                       vol->hmail + OT_MAIL_WORDS, ovl ? wcount : (int*)nullptr);
     if (!vol->ev_early) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_early, hipEventDisableTiming));
     OT_HIP_TRY(hipEventRecord(vol->ev_early, stream));
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
     const bool fast = !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
-    const int variant = (vol->color64 ? 2 : 0) + (fast ? 1 : 0);
-    const int grid = integrate_grid(variant);
+    bc.variant = (vol->color64 ? 2 : 0) + (fast ? 1 : 0);
+    const int grid = integrate_grid(bc.variant);
+    // overlap: the integrate on istream behind this set's units kernel (and the previous batch's integrate: same
+    // stream), so the caller's stream is free for the next batch's front end
+    hipStream_t is = stream;
+    if (ovl) {
+        OT_HIP_TRY(hipEventRecord(bs.ev_units, stream));
+        OT_HIP_TRY(hipStreamWaitEvent(vol->istream, bs.ev_units, 0));
+        is = vol->istream;
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
         OT_HIP_TRY(hipEventRecord(f1, stream));
         vol->prof_fe_events.emplace_back(f0, f1);
         OT_HIP_TRY(hipEventCreate(&e0));
         OT_HIP_TRY(hipEventCreate(&e1));
-        OT_HIP_TRY(hipEventRecord(e0, stream));
+        OT_HIP_TRY(hipEventRecord(e0, is));
     }
-    const BatchFrame* bf = vol->bframes;
-    const UnitWork* uw = (const UnitWork*)vol->dev.work;
-    void* args[] = {(void*)&bf, (void*)&ip0, (void*)&vol->dev, (void*)&uw, (void*)&pc};
-    OT_HIP_TRY(hipLaunchKernel(integrate_kernel(variant), dim3(grid), dim3(64 * INT_WG), args, 0, stream));
+    const BatchFrame* bf = bs.bframes;
+    const UnitWork* uw = work;
+    const int* wc = wcount;
+    void* args[] = {(void*)&bf, (void*)&bc.ip0, (void*)&vol->dev, (void*)&uw, (void*)&wc};
+    OT_HIP_TRY(hipLaunchKernel(integrate_kernel(bc.variant), dim3(grid), dim3(64 * INT_WG), args, 0, is));
     vol->batch_pc ^= 1;  // only once this batch's kernels are queued (its units kernel zeroes the other counter)
     OT_LAUNCH_CHECK();
     if (vol->profiling) {
-        OT_HIP_TRY(hipEventRecord(e1, stream));
+        OT_HIP_TRY(hipEventRecord(e1, is));
         vol->prof_events.emplace_back(e0, e1);
+    }
+    if (ovl) {
+        OT_HIP_TRY(hipEventRecord(bs.ev_done, is));
+        vol->last_set = set;
     }
     vol->frame_id += n;
     vol->sorted_frame = -1;
     vol->early_frame = vol->frame_id;  // the mailed counters are final for this frame count (see ev_early)
-    return settle_batch(vol, tp, ip0, tiles, n, pc, variant, stream);
+    return settle_batch(vol, bc, stream);
 }
 
 // ------------------------------------------------------------------------------------------ unbounded unit pool
@@ -1209,10 +1278,12 @@ static ot_status grow_pool(ot_tsdf* vol, int64_t need, int n_used, hipStream_t s
     ot_status st = wait_normals(vol, stream);
     if (st != OT_OK) return st;
     OT_HIP_TRY(hipStreamSynchronize(stream));
+    if (vol->istream) OT_HIP_TRY(hipStreamSynchronize(vol->istream));
     TsdfDev& d = vol->dev;
     TsdfDev nd = d;
     unsigned* nsorted = nullptr;
-    void* fresh[8] = {nullptr};
+    void* work1 = nullptr;
+    void* fresh[9] = {nullptr};
     auto alloc = [&](void** p, size_t bytes, int k) {
         const hipError_t e = hipMalloc(p, bytes);
         fresh[k] = *p;
@@ -1226,7 +1297,8 @@ static ot_status grow_pool(ot_tsdf* vol, int64_t need, int n_used, hipStream_t s
         (e = alloc((void**)&nd.hvals, sizeof(int) * cap, 4)) == hipSuccess &&
         (e = alloc((void**)&nd.fmask, sizeof(unsigned long long) * cap, 5)) == hipSuccess &&
         (e = alloc((void**)&nd.bslots, sizeof(int) * cap, 6)) == hipSuccess &&
-        (e = alloc((void**)&nd.work, 32 * cap, 7)) == hipSuccess) {
+        (e = alloc((void**)&nd.work, sizeof(UnitWork) * cap, 7)) == hipSuccess &&
+        (!vol->bset[1].work || (e = alloc(&work1, sizeof(UnitWork) * cap, 8)) == hipSuccess)) {
     }
     if (e != hipSuccess) {
         for (void* p : fresh)
@@ -1251,9 +1323,10 @@ static ot_status grow_pool(ot_tsdf* vol, int64_t need, int n_used, hipStream_t s
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(stream));
     for (void* p : {(void*)d.vox, (void*)d.unit_keys, (void*)vol->sorted_ids, (void*)d.hkeys, (void*)d.hvals,
-                    (void*)d.fmask, (void*)d.bslots, d.work})
+                    (void*)d.fmask, (void*)d.bslots, d.work, vol->bset[1].work})
         if (p) (void)hipFree(p);
     d = nd;
+    vol->bset[1].work = work1;
     vol->sorted_ids = nsorted;
     vol->max_units = nmax;
     vol->hash_cap = cap;
@@ -1267,8 +1340,7 @@ static ot_status grow_pool(ot_tsdf* vol, int64_t need, int n_used, hipStream_t s
 // the missing units (units that have an id were integrated and are skipped), integrate them with the batch's frames.
 // Units are independent and each sees the batch's frames in call order, so the volume equals an unbounded pool's.
 // A pool more than 3/4 full also grows here, ahead of need.
-static ot_status settle_batch(ot_tsdf* vol, const BatchTouchParams& tp0, const IntegrateParams& ip0, unsigned tiles,
-                              int n, int pc, int variant, hipStream_t stream) {
+static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stream) {
     for (int round = 0;; ++round) {
         OT_HIP_TRY(hipEventSynchronize(vol->ev_early));
         int c[N_COUNTERS];
@@ -1283,28 +1355,32 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchTouchParams& tp0, const I
         // ids below the old capacity were all handed out; the allocations past it were dropped (C_UNITS overshoots)
         const int used = (int)std::min<int64_t>(c[C_UNITS], vol->max_units);
         const int64_t need = std::max<int64_t>((int64_t)c[C_UNITS], vol->max_units) + 1;
-        ot_status st = grow_pool(vol, need, used, stream);
+        ot_status st = grow_pool(vol, need, used, stream);  // synchronises both of the volume's streams
         if (st != OT_OK) return st;
         int h[N_COUNTERS];
         OT_HIP_TRY(hipMemcpy(h, vol->dev.counters, sizeof(h), hipMemcpyDeviceToHost));
         h[C_UNITS] = used;
         h[C_OVERFLOW] = 0;
         h[C_HASHERR] &= ~1;
-        h[pc] = 0;  // the replay's touched-slot count (the batch's own pair counter; the next batch's stays zero)
+        h[bc.pc] = 0;  // the replay's touched-slot count (the batch's own pair counter; the next batch's stays zero)
         OT_HIP_TRY(hipMemcpy(vol->dev.counters, h, sizeof(h), hipMemcpyHostToDevice));
-        BatchTouchParams tp = tp0;
+        // the replay, all on the caller's stream, from the batch's set (its staging is intact: nothing restaged it)
+        BatchTouchParams tp = bc.tp;
         tp.slot_cap = (int)vol->hash_cap;
-        hipLaunchKernelGGL(k_batch_touch<true>, dim3(tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
-                           (const BatchFrame*)vol->bframes, tp, vol->dev, n);
-        hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, (UnitWork*)vol->dev.work, pc,
-                           vol->hmail + OT_MAIL_WORDS);
+        const BatchFrame* bf = vol->bset[bc.set].bframes;
+        UnitWork* work = (UnitWork*)set_work(vol, bc.set);
+        hipLaunchKernelGGL(k_batch_touch<true>, dim3(bc.tiles, (unsigned)((bc.n + TF - 1) / TF)), dim3(256), 0, stream,
+                           bf, tp, vol->dev, bc.n);
+        hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
+                           vol->hmail + OT_MAIL_WORDS, (int*)nullptr);
         OT_HIP_TRY(hipEventRecord(vol->ev_early, stream));
-        const BatchFrame* bf = vol->bframes;
-        const UnitWork* uw = (const UnitWork*)vol->dev.work;
-        void* args[] = {(void*)&bf, (void*)&ip0, (void*)&vol->dev, (void*)&uw, (void*)&pc};
-        OT_HIP_TRY(hipLaunchKernel(integrate_kernel(variant), dim3(integrate_grid(variant)), dim3(64 * INT_WG), args, 0,
-                                   stream));
+        const UnitWork* uw = work;
+        const int* wc = vol->dev.counters + bc.pc;
+        void* args[] = {(void*)&bf, (void*)&bc.ip0, (void*)&vol->dev, (void*)&uw, (void*)&wc};
+        OT_HIP_TRY(hipLaunchKernel(integrate_kernel(bc.variant), dim3(integrate_grid(bc.variant)), dim3(64 * INT_WG),
+                                   args, 0, stream));
         OT_LAUNCH_CHECK();
+        vol->last_set = -1;  // the replay ran on the caller's stream, after both streams drained
         vol->sorted_frame = -1;
     }
 }
@@ -1331,7 +1407,7 @@ ot_status wait_normals(ot_tsdf* vol, hipStream_t stream) {
     return OT_OK;
 }
 
-ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream) {
+ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream, bool join) {
     size_t i = 0;
     std::vector<PendingFrame> frames;
     frames.swap(vol->pending);
@@ -1347,7 +1423,7 @@ ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream) {
         if (st != OT_OK) return st;
         i += n;
     }
-    return OT_OK;
+    return join ? join_integrate(vol, stream) : OT_OK;
 }
 
 static ot_status counter_errors(const int* c) {
@@ -1507,7 +1583,7 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
     if ((e = hipMalloc(&d.fmask, sizeof(unsigned long long) * cap)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.bslots, sizeof(int) * cap)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.work, sizeof(UnitWork) * cap)) != hipSuccess) return cleanup(e);
-    if ((e = hipMalloc(&v->bframes, sizeof(BatchFrame) * MAX_BATCH)) != hipSuccess) return cleanup(e);
+    if ((e = hipMalloc(&v->bset[0].bframes, sizeof(BatchFrame) * MAX_BATCH)) != hipSuccess) return cleanup(e);
     if ((e = hipHostMalloc(&v->hbframes, sizeof(BatchFrame) * MAX_BATCH * 2, hipHostMallocDefault)) != hipSuccess)
         return cleanup(e);
     if ((e = hipHostMalloc(&v->hmail, sizeof(unsigned) * 2 * OT_MAIL_WORDS, hipHostMallocCoherent)) != hipSuccess)
@@ -1526,8 +1602,10 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     (void)hipDeviceSynchronize();
     TsdfDev& d = v->dev;
     ot_tsdf_set_profiling(v, 0);
-    void* ptrs[] = {d.hkeys, d.hvals, d.counters, d.stats, d.unit_keys, d.vox, v->mult, v->sorted_ids, v->batch_ws, v->mesh.ws, v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, v->mesh.vown, d.fmask, d.bslots, d.work,
-                    v->bframes, v->bdm, v->brgba};
+    void* ptrs[] = {d.hkeys, d.hvals, d.counters, d.stats, d.unit_keys, d.vox, v->mult, v->sorted_ids, v->mesh.ws,
+                    v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, v->mesh.vown, d.fmask, d.bslots, d.work,
+                    v->wcount, v->bset[0].bframes, v->bset[0].bdm, v->bset[0].brgba, v->bset[1].bframes,
+                    v->bset[1].bdm, v->bset[1].brgba, v->bset[1].work};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (v->hbframes) (void)hipHostFree(v->hbframes);
@@ -1537,7 +1615,13 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     if (v->ev_mail) (void)hipEventDestroy(v->ev_mail);
     if (v->ev_join) (void)hipEventDestroy(v->ev_join);
     if (v->ev_normals) (void)hipEventDestroy(v->ev_normals);
+    if (v->ev_made) (void)hipEventDestroy(v->ev_made);
     if (v->side) (void)hipStreamDestroy(v->side);
+    if (v->istream) (void)hipStreamDestroy(v->istream);
+    for (auto& b : v->bset) {
+        if (b.ev_units) (void)hipEventDestroy(b.ev_units);
+        if (b.ev_done) (void)hipEventDestroy(b.ev_done);
+    }
     for (hipEvent_t ev : v->hb_event)
         if (ev) (void)hipEventDestroy(ev);
     delete v;
@@ -1549,6 +1633,7 @@ ot_status ot_tsdf_reset(ot_tsdf* v) {
     TsdfDev& d = v->dev;
     OT_HIP_TRY(hipDeviceSynchronize());  // queued work on the volume (deferred normals included) first
     v->normals_pending = false;
+    v->last_set = -1;
     OT_HIP_TRY(hipMemset(d.hkeys, 0xFF, sizeof(unsigned long long) * v->hash_cap));
     OT_HIP_TRY(hipMemset(d.hvals, 0xFF, sizeof(int) * v->hash_cap));
     OT_HIP_TRY(hipMemset(d.fmask, 0, sizeof(unsigned long long) * v->hash_cap));
@@ -1603,7 +1688,8 @@ ot_status ot_tsdf_integrate(ot_tsdf* vol, const float* depth, const uint8_t* col
     f.depth_scale = 1.0;
     f.depth_trunc = 0.0;
     vol->pending.push_back(f);
-    if ((int)vol->pending.size() >= std::min(vol->batch_max, MAX_BATCH)) return tsdf_flush(vol, S(stream));
+    // a full queue is integrated; the integrate may keep running on the volume's integrate stream (overlap mode)
+    if ((int)vol->pending.size() >= std::min(vol->batch_max, MAX_BATCH)) return tsdf_flush(vol, S(stream), false);
     return OT_OK;
 }
 
@@ -1620,7 +1706,7 @@ ot_status ot_tsdf_integrate_u16(ot_tsdf* vol, const uint16_t* depth, const uint8
     f.depth_scale = depth_scale;
     f.depth_trunc = depth_trunc;
     vol->pending.push_back(f);
-    if ((int)vol->pending.size() >= std::min(vol->batch_max, MAX_BATCH)) return tsdf_flush(vol, S(stream));
+    if ((int)vol->pending.size() >= std::min(vol->batch_max, MAX_BATCH)) return tsdf_flush(vol, S(stream), false);
     return OT_OK;
 }
 
@@ -1652,6 +1738,17 @@ ot_status ot_tsdf_pending_frames(const ot_tsdf* vol, int32_t* n_host) {
 ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames) {
     if (!vol || max_frames < 1) return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] batch must be >= 1");
     vol->batch_max = max_frames;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_set_frontend_overlap(ot_tsdf* vol, int32_t mode) {
+    if (!vol || mode < -1 || mode > 1)
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] front-end overlap mode must be -1, 0 or 1");
+    ot_status st = tsdf_flush(vol, nullptr);  // queued frames (and a running integrate) under the old mode
+    if (st != OT_OK) return st;
+    if (vol->istream) OT_HIP_TRY(hipStreamSynchronize(vol->istream));
+    vol->last_set = -1;
+    vol->overlap_mode = mode;
     return OT_OK;
 }
 

@@ -356,9 +356,12 @@ def _reconstruct_points(R, cfg, label, o3d):
             R._integrate_frame(o3d, cfg, volume, intrinsic, colors, depths, poses, i)
         except Exception:
             pass
+    fused = getattr(volume, "extract_mesh_and_sample_min_z", None)
+    if fused is not None:  # extract, normals, sample_points_uniformly + the Z mask (:112-132) in one host call
+        _mesh, cloud = fused(cfg.n_samples, cfg.z_filter, cfg.sample_seed)
+        return None if cloud is None else cloud._xyz.dev()
     mesh = volume.extract_triangle_mesh()
     mesh.compute_vertex_normals()
     if R._mesh_empty(mesh):  # reference: len(mesh.vertices) == 0, without a writable host view
         return None
-    # sample_points_uniformly + the Z mask (reconstruct_rgbd_filter.py:123-132) in one pass
-    return mesh.sample_points_min_z(cfg.n_samples, cfg.z_filter)._xyz.dev()
+    return mesh.sample_points_min_z(cfg.n_samples, cfg.z_filter, cfg.sample_seed)._xyz.dev()

@@ -12,7 +12,8 @@ import numpy as np
 
 from .. import _device as D
 from .. import _lib as L
-from ..geometry import RGBDImage, TriangleMesh, _Arr
+from .. import streams as _streams
+from ..geometry import PointCloud, RGBDImage, TriangleMesh, _Arr
 
 
 class TSDFVolumeColorType(enum.IntEnum):
@@ -66,6 +67,11 @@ class ScalableTSDFVolume:
             except Exception:
                 pass
             self._h = None
+
+    def set_frontend_overlap(self, mode):
+        """Double-buffered batch front end (ot_tsdf_set_frontend_overlap): 1 on, 0 off, -1 (default) on when sharded.
+        Batch k+1's staging / touch run beside batch k's integrate; results are identical in every mode."""
+        L.call("ot_tsdf_set_frontend_overlap", self._h, int(mode))
 
     def set_batch(self, frames):
         L.call("ot_tsdf_set_batch", self._h, int(frames))
@@ -222,6 +228,68 @@ class ScalableTSDFVolume:
             raise RuntimeError("[ScalableTSDFVolume] import_border: shapes do not match export_border")
         L.call("ot_tsdf_import_border", self._h, n, D.ptr(keys), D.ptr(tsdf), D.ptr(weight), D.ptr(color),
                D.stream_ptr())
+
+    def extract_mesh_and_sample_min_z(self, number_of_points, z_min, seed=0, vertex_normals=True):
+        """reconstruct_rgbd_filter.py:112-132 in one host call (not an Open3D API): extract_triangle_mesh() ->
+        compute_vertex_normals() -> sample_points_uniformly(number_of_points) -> the rows with z >= z_min, points and
+        colours (the cloud TriangleMesh.sample_points_min_z returns).  Returns (mesh, cloud); cloud is None for an
+        empty mesh (the reference skips it, :115-117).  The marching-cubes totals go straight to the sampler's first
+        launch inside ot_tsdf_extract_sample_min_z (no Python between them); the vertex normals run beside the sampling
+        on a side stream and a reader of mesh.vertex_normals waits for them.  The first extraction of a volume (no
+        capacity guess yet) or a capacity miss takes the separate calls -- the same bits."""
+        if number_of_points <= 0:
+            raise RuntimeError("[SamplePointsUniformly] number_of_points <= 0")
+        cv, ct = getattr(self, "_mesh_cap", (0, 0))
+        if not (cv and ct):
+            return self._extract_then_sample(number_of_points, z_min, seed, vertex_normals)
+        torch = D.torch
+        rgb = self.color_type == TSDFVolumeColorType.RGB8
+        n = int(number_of_points)
+        V = D.empty((cv, 3), "float64")
+        VC = D.empty((cv, 3), "float64") if rgb else None
+        T = D.empty((ct, 3), "int32")
+        N = D.empty((cv, 3), "float64") if vertex_normals else None
+        P = D.empty((n, 3), "float64")
+        PC = D.empty((n, 3), "float64") if rgb else None
+        cur = torch.cuda.current_stream()
+        side = _streams.side_stream(cur) if vertex_normals else None
+        nv, nt, kept = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+        st = L.load().ot_tsdf_extract_sample_min_z(
+            self._h, D.ptr(V), D.ptr(VC), D.ptr(T), cv, ct, D.ptr(N), C.c_void_p(side.cuda_stream) if side else None,
+            n, C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), float(z_min), D.ptr(P), D.ptr(PC), C.byref(nv),
+            C.byref(nt), C.byref(kept), D.stream_ptr())
+        self._keep.clear()
+        if st == L.OT_ERR_CAPACITY and (nv.value or nt.value):  # the mesh outgrew the guess: the separate calls
+            self._mesh_cap = (nv.value + nv.value // 8 + 1024, nt.value + nt.value // 8 + 1024)
+            return self._extract_then_sample(number_of_points, z_min, seed, vertex_normals)
+        if st != L.OT_OK:
+            raise L.OTError(L.load().ot_last_error().decode())
+        self._mesh_cap = (nv.value + nv.value // 8 + 1024, nt.value + nt.value // 8 + 1024)
+        mesh = TriangleMesh()
+        mesh._v = _Arr(dev=V[:nv.value])
+        mesh._t = _Arr(dev=T[:nt.value])
+        if VC is not None:
+            mesh._vc = _Arr(dev=VC[:nv.value])
+        if nv.value == 0:
+            return mesh, None
+        if N is not None:
+            for t in (V, T, N):  # allocated on the caller's stream, used on the side stream
+                t.record_stream(side)
+            done = torch.cuda.Event()
+            done.record(side)
+            mesh._vn = _Arr(dev=N[:nv.value], ready=done)
+        pcd = PointCloud()
+        pcd._xyz = _Arr(dev=P[:kept.value])
+        pcd._rgb = _Arr(dev=PC[:kept.value]) if PC is not None else None
+        return mesh, pcd
+
+    def _extract_then_sample(self, number_of_points, z_min, seed, vertex_normals):
+        mesh = self.extract_triangle_mesh()
+        if vertex_normals:
+            mesh.compute_vertex_normals()
+        if not mesh.has_vertices():
+            return mesh, None
+        return mesh, mesh.sample_points_min_z(number_of_points, z_min, seed)
 
     def extract_triangle_mesh(self, with_keys=False):
         """ScalableTSDFVolume::ExtractTriangleMesh — GPU marching cubes (mc.hip).  with_keys: also return the merge

@@ -123,7 +123,7 @@ def _filtered_cloud(o3d, cfg, mesh):
     facade does both in one pass (TriangleMesh.sample_points_min_z: the same cloud); Open3D takes the reference's
     steps."""
     if hasattr(mesh, "sample_points_min_z"):
-        return mesh.sample_points_min_z(cfg.n_samples, cfg.z_filter)
+        return mesh.sample_points_min_z(cfg.n_samples, cfg.z_filter, cfg.sample_seed)
     pcd = mesh.sample_points_uniformly(number_of_points=cfg.n_samples)
     pts = np.asarray(pcd.points)
     cols = np.asarray(pcd.colors)
@@ -157,9 +157,18 @@ def reconstruct_object(label: str, cfg: ScanConfig, o3d=None, output: str = "poi
             _integrate_frame(o3d, cfg, volume, intrinsic, colors, depths, poses, i)
         except Exception as exc:  # reference: print and skip the frame
             _log(f"Skipping frame {i + 1} due to error: {exc}", log)
+    path = os.path.join(cfg.save_dir, f"{label}.ply")
+    fused = getattr(volume, "extract_mesh_and_sample_min_z", None)
+    if output == "points" and fused is not None:
+        # this package: :112-132 (extract, normals, sample, Z mask) in one host call, the same cloud
+        mesh, cloud = fused(cfg.n_samples, cfg.z_filter, cfg.sample_seed)
+        if cloud is None:
+            _log("Mesh is empty", log)
+            return None
+        o3d.io.write_point_cloud(path, cloud)
+        return path
     mesh = volume.extract_triangle_mesh()
     mesh.compute_vertex_normals()
-    path = os.path.join(cfg.save_dir, f"{label}.ply")
     if output == "mesh":
         o3d.io.write_triangle_mesh(path, mesh)
         return path
@@ -193,11 +202,18 @@ def reconstruct_range(name: str, start: int, end: int, cfg: ScanConfig, file_pre
             _log(f"Error on frame {i}: {exc}", log)
     if done == 0:
         return None
+    path = os.path.join(cfg.save_dir, f"{name}.ply")
+    fused = getattr(volume, "extract_mesh_and_sample_min_z", None)
+    if fused is not None:  # this package: extract, normals, sample and Z mask in one host call
+        mesh, cloud = fused(cfg.n_samples, cfg.z_filter, cfg.sample_seed)
+        if cloud is None:
+            return None
+        o3d.io.write_point_cloud(path, cloud)
+        return path
     mesh = volume.extract_triangle_mesh()
     mesh.compute_vertex_normals()
     if _mesh_empty(mesh):
         return None
-    path = os.path.join(cfg.save_dir, f"{name}.ply")
     o3d.io.write_point_cloud(path, _filtered_cloud(o3d, cfg, mesh))
     return path
 

@@ -92,11 +92,25 @@ struct Intr {
     double fx, fy, cx, cy;
 };
 
+/* Sensitivity probe (tools/parity_sensitivity.py): Eigen may compute camera_pose = extrinsic.inverse()
+ * with its vectorised 4x4 path, whose last bits can differ from the scalar cofactor restatement above.  Mode 1 / 2
+ * moves every entry of rows 0..2 of the pose by one ulp (direction by a fixed pattern / its opposite) to measure how
+ * many unit-touch decisions such a difference moves.  Mode 0 (the default) leaves the pose as computed. */
+static int g_pose_ulp_mode = 0;
+void perturb_pose(double* pose) {
+    if (!g_pose_ulp_mode) return;
+    for (int k = 0; k < 12; ++k) {
+        const bool up = (((k * 7 + 3) >> 1) & 1) ^ (g_pose_ulp_mode == 2);
+        pose[k] = std::nextafter(pose[k], up ? INFINITY : -INFINITY);
+    }
+}
+
 /* CreatePointCloudFromFloatDepthImage (Appendix A.2 / A.3(ii)). */
 int64_t unproject_impl(const float* depth, const uint8_t* color, const Intr& in, const double* extrinsic,
                        int stride, double* xyz, double* rgb) {
     double pose[16];
     inverse4(extrinsic, pose);
+    perturb_pose(pose);
     int64_t cnt = 0;
     for (int i = 0; i < in.h; i += stride) {
         for (int j = 0; j < in.w; j += stride) {
@@ -220,6 +234,7 @@ extern "C" {
 const char* oro_name(void) { return "otslam CPU oracle (restatement of Open3D semantics; parity unpinned)"; }
 
 void oro_inverse4(const double* m, double* out) { inverse4(m, out); }
+void oro_set_pose_ulp_mode(int mode) { g_pose_ulp_mode = mode; }
 
 /* Image::ConvertDepthToFloatImage (Appendix A.1). */
 void oro_depth_to_float(const uint16_t* in, float* out, int64_t n, double depth_scale, double depth_trunc) {

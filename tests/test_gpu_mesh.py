@@ -297,6 +297,45 @@ def test_deferred_normals_vs_later_volume_work(pkg, O, synth, seq16):
     assert_bitwise(np.asarray(mesh.vertex_normals), rN, "first mesh's normals after later work on the volume")
 
 
+def test_fused_extract_sample_min_z(pkg, O, synth, seq16):
+    """ScalableTSDFVolume.extract_mesh_and_sample_min_z (ot_tsdf_extract_sample_min_z: marching cubes, the fused
+    sampler and the vertex normals in one host call) gives the oracle's mesh, normals and Z-masked cloud -- on the
+    volume's first extraction (the separate calls), on a later one (the fused C entry), and on a capacity miss."""
+    depth, color, ext = seq16
+    intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth))
+    vol, ref = _volumes(pkg, O, synth, depth[:2], color[:2], ext[:2], 0.005)
+
+    def check(tag, seed):
+        mesh, cloud = vol.extract_mesh_and_sample_min_z(100000, 0.03, seed=seed)
+        V, VC, T = ref.extract_triangle_mesh()
+        assert_bitwise(np.asarray(mesh.vertices), V, f"vertices ({tag})")
+        assert_bitwise(np.asarray(mesh.vertex_colors), VC, f"vertex colours ({tag})")
+        assert_bitwise(np.asarray(mesh.triangles), T, f"triangles ({tag})")
+        P, _, PC = O.sample_points_uniformly(V, T, 100000, seed, VC=VC)
+        rx, rc = O.filter_min_z(P, PC, 0.03)
+        assert_bitwise(np.asarray(cloud.points), rx, f"fused cloud points ({tag})")
+        assert_bitwise(np.asarray(cloud.colors), rc, f"fused cloud colours ({tag})")
+        assert_bitwise(np.asarray(mesh.vertex_normals), O.vertex_normals(V, T), f"normals ({tag})")
+
+    def more(k):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], ref_intr(synth), ext[k])
+
+    check("first extraction: separate calls", 4)
+    more(2)
+    check("fused C entry", 5)
+    more(3)
+    vol._mesh_cap = (64, 64)  # a guess far too small: the capacity miss takes the separate calls
+    check("capacity miss", 6)
+    empty = pkg.pipelines.integration.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04,
+                                                         color_type=pkg.pipelines.integration.TSDFVolumeColorType.RGB8)
+    empty._mesh_cap = (1024, 1024)
+    mesh, cloud = empty.extract_mesh_and_sample_min_z(1000, 0.03)
+    assert cloud is None and not mesh.has_vertices()
+
+
 def test_sampling_batch_matches_single(pkg, O, synth, seq16, meshes):
     """TriangleMesh.sample_points_uniformly_batch: the per-mesh clouds equal the single-mesh calls (and the oracle)
     for meshes of different sizes sampled together."""

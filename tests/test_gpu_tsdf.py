@@ -344,6 +344,38 @@ def test_tsdf_pool_grows(pkg, O, gpu, synth, batch):
     assert_bitwise(np.asarray(m.triangles), T, "mesh triangles after pool growth")
 
 
+@pytest.mark.parametrize("batch,max_units", [(8, 0), (1, 0), (16, 64)])
+def test_frontend_overlap_bitexact(pkg, O, gpu, synth, batch, max_units):
+    """The double-buffered front end (batch k+1's staging / touch / units on the caller's stream beside batch k's
+    integrate on the volume's integrate stream; the default for sharded volumes) forced on for an unsharded volume:
+    70 frames in batches of 8 (9 batches, both staging sets reused), frame by frame, and with a 64-unit pool that
+    grows mid-scan (replay from the batch's own set) -- bitwise equal to the oracle, counters included."""
+    integ = _integration(pkg)
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=2), n_frames=70, frames=range(0, 70, 2 if batch == 1 else 1))
+    vol = integ.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                   batch_frames=batch, max_units=max_units)
+    vol.set_frontend_overlap(1)
+    ref = O.TSDF(0.005, 0.04, 1, 4)
+    for k in range(depth.shape[0]):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+            convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
+    assert _compare_volumes(vol, ref) > 1000
+    vol.reset()  # a reset after overlapped batches, then one more pass bit-exact again
+    ref2 = O.TSDF(0.005, 0.04, 1, 4)
+    for k in range(0, depth.shape[0], 3):
+        rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
+            pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+            convert_rgb_to_intensity=False)
+        vol.integrate(rgbd, intr, ext[k])
+        ref2.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
+    _compare_volumes(vol, ref2)
+
+
 def test_tsdf_pool_grows_on_import(pkg, gpu, synth, seq16):
     """import_units into a 64-unit volume makes room first (the rows are counted before the import kernel)."""
     integ = _integration(pkg)

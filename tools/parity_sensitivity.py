@@ -1,0 +1,130 @@
+"""How far can "bit-exact vs the oracle" sit from Open3D on the bench workloads?  (CPU only.)
+
+Parity against Open3D rests on two unpinned assumptions: camera_pose = extrinsic.inverse() by Eigen's
+SCALAR 4x4 path (Eigen may take its vectorised compute_inverse_size4, whose last bits differ), and no FMA contraction
+inside Open3D.  This tool measures their reach with the CPU oracle (test infrastructure):
+  pose+1ulp / pose-1ulp : every entry of rows 0..2 of each frame's pose moved by one ulp (two opposite patterns;
+                          oracle oro_set_pose_ulp_mode) -- a stand-in for a differently rounded inverse;
+  fma                   : the whole oracle compiled with -ffp-contract=fast -march=x86-64-v3 (FMA contracted
+                          wherever GCC may, the inverse included);
+on the configs[1] scan (256 frames, 640x480, 5 mm, sdf_trunc 0.04) and configs[3] object 0 (64 frames), each compared
+with the strict oracle: unit keys present in only one volume, voxels whose weight / tsdf / float64 colour differ, and
+the marching-cubes mesh (vertex and triangle counts, vertices not bitwise present in the other mesh).
+Usage: python tools/parity_sensitivity.py [--frames 256] > profiles/r05_parity_sensitivity.json"""
+import argparse
+import importlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle as O  # noqa: E402  (test infrastructure: this tool is a checker, never product)
+
+synth = importlib.import_module("object-triggered-3d-slam_amd.synth")
+FMA_LIB = "/tmp/otslam_sens/libotslam_oracle_fma.so"
+
+
+def build_fma():
+    os.makedirs(os.path.dirname(FMA_LIB), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=fast", "-march=x86-64-v3", "-fopenmp",
+                    "-shared", "-o", FMA_LIB, os.path.join(ROOT, "oracle", "otslam_oracle.cpp")], check=True)
+
+
+def use_lib(path):
+    O._lib = None
+    O._LIB_PATH = path
+    L = O.lib()
+    L.oro_set_pose_ulp_mode.argtypes = [O._i32]
+    L.oro_set_pose_ulp_mode.restype = None
+    return L
+
+
+def run(scan, voxel=0.005, trunc=0.04, depth_trunc=3.0):
+    depth, color, ext = scan
+    intr = synth.REF_INTRINSICS_640
+    vol = O.TSDF(voxel, trunc, 1, 4)
+    for k in range(depth.shape[0]):
+        vol.integrate(O.depth_to_float(depth[k], 1000.0, depth_trunc), color[k], intr, ext[k])
+    keys, tsdf, weight, col = vol.export()
+    V, VC, T = vol.extract_triangle_mesh()
+    return {"keys": keys, "tsdf": tsdf, "weight": weight, "color": col, "V": V, "T": T,
+            "updates": vol.total_updates()}
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view({4: np.uint32, 8: np.uint64}[a.dtype.itemsize])
+
+
+def compare(base, var):
+    kb = {tuple(k): i for i, k in enumerate(base["keys"].tolist())}
+    kv = {tuple(k): i for i, k in enumerate(var["keys"].tolist())}
+    common = sorted(set(kb) & set(kv))
+    ib = np.array([kb[k] for k in common], np.int64)
+    iv = np.array([kv[k] for k in common], np.int64)
+    wd = bits(base["weight"][ib]) != bits(var["weight"][iv])
+    td = bits(base["tsdf"][ib]) != bits(var["tsdf"][iv])
+    cd = (bits(base["color"][ib]) != bits(var["color"][iv])).any(axis=-1)
+    observed = int((base["weight"] > 0).sum())
+    same_w = ~wd  # voxels whose weight agrees: their tsdf / colour differ by rounding only
+    tdiff = np.abs(base["tsdf"][ib].astype(np.float64) - var["tsdf"][iv].astype(np.float64))[same_w]
+    cdiff = np.abs(base["color"][ib] - var["color"][iv])[same_w]
+    mesh_err = {}
+    if base["V"].shape == var["V"].shape and np.array_equal(base["T"], var["T"]):  # same topology, canonical order
+        dv = np.abs(base["V"] - var["V"])
+        mesh_err = {"mesh_topology_identical": True, "vertex_max_abs_diff_m": float(dv.max()),
+                    "vertex_max_rel_diff": float((dv / np.maximum(np.abs(base["V"]), 1e-300)).max())}
+    vb = {r.tobytes() for r in np.ascontiguousarray(base["V"])}
+    vv = [r.tobytes() for r in np.ascontiguousarray(var["V"])]
+    return {"units_base": len(kb), "units_only_in_base": len(set(kb) - set(kv)),
+            "units_only_in_variant": len(set(kv) - set(kb)),
+            "observed_voxels_base": observed, "voxels_weight_differs": int(wd.sum()),
+            "voxels_tsdf_differs": int(td.sum()), "voxels_colour_differs": int(cd.sum()),
+            "voxel_updates_base": int(base["updates"]), "voxel_updates_variant": int(var["updates"]),
+            "mesh_vertices_base": int(base["V"].shape[0]), "mesh_vertices_variant": int(var["V"].shape[0]),
+            "mesh_triangles_base": int(base["T"].shape[0]), "mesh_triangles_variant": int(var["T"].shape[0]),
+            "variant_vertices_not_in_base": int(sum(1 for r in vv if r not in vb)),
+            "tsdf_max_abs_diff_same_weight": float(tdiff.max()) if tdiff.size else 0.0,
+            "colour_max_abs_diff_same_weight": float(cdiff.max()) if cdiff.size else 0.0, **mesh_err}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=256)
+    ap.add_argument("--object-frames", type=int, default=64)
+    a = ap.parse_args()
+    t0 = time.time()
+    scans = {"configs[1] scan (Scene seed 0), %d frames, 5 mm" % a.frames:
+             synth.make_sequence_parallel(synth.Scene(seed=0), n_frames=a.frames, intr=synth.REF_INTRINSICS_640,
+                                          workers=8),
+             "configs[3] object 0, %d frames, 5 mm" % a.object_frames:
+             synth.make_sequence(synth.object_scene(0), n_frames=a.object_frames)}
+    build_fma()
+    out = {"tool": "tools/parity_sensitivity.py", "omp_threads": os.environ.get("OMP_NUM_THREADS"), "workloads": {}}
+    base_lib = os.path.join(ROOT, "oracle", "libotslam_oracle.so")
+    for name, scan in scans.items():
+        L = use_lib(base_lib)
+        L.oro_set_pose_ulp_mode(0)
+        base = run(scan)
+        res = {}
+        for label, lib, mode in (("pose+1ulp", base_lib, 1), ("pose-1ulp", base_lib, 2), ("fma", FMA_LIB, 0),
+                                 ("fma+pose+1ulp", FMA_LIB, 1)):
+            L = use_lib(lib)
+            L.oro_set_pose_ulp_mode(mode)
+            res[label] = compare(base, run(scan))
+            L.oro_set_pose_ulp_mode(0)
+            print(name, label, json.dumps(res[label]), file=sys.stderr, flush=True)
+        out["workloads"][name] = res
+    use_lib(base_lib)
+    out["seconds"] = round(time.time() - t0, 1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
