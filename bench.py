@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--voxel", type=float, default=0.005)
     ap.add_argument("--sdf-trunc", type=float, default=0.04)
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
+    ap.add_argument("--overlap", type=int, default=-1, choices=(-1, 0, 1),
+                    help="headline volume's batch front end double-buffered beside the previous integrate "
+                         "(ot_tsdf_set_frontend_overlap; -1 = library default: on only for sharded volumes)")
     ap.add_argument("--cpu-frames", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--sustain", type=float, default=12.0,
                     help="seconds of sustained headline steps after the timed ones (0 = skip): >= 12 s so a 5-s busy "
@@ -194,6 +197,7 @@ def main():
     L.call("ot_tsdf_set_color_precision", vol, args.color_bits)  # 64 is already the default; explicit for the record
     if args.batch > 0:
         L.call("ot_tsdf_set_batch", vol, args.batch)
+    L.call("ot_tsdf_set_frontend_overlap", vol, args.overlap)
     frame_bytes = W * H
     dptrs = [C.c_void_p(d_depth.data_ptr() + k * frame_bytes * 2) for k in range(args.frames)]
     cptrs = [C.c_void_p(d_color.data_ptr() + k * frame_bytes * 3) for k in range(args.frames)]
@@ -510,36 +514,36 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
             "frontend_note": "every rank stages and unprojects every frame (undivided); the integrate divides by units"}
 
 
-def shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, headline_ms, worlds=(2, 4, 8)):
+def shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, headline_ms, worlds=(1, 2, 4, 8)):
     """SURVEY 8(e) measured on one GPU: the headline step (reset + the 256-frame scan + flush) of a volume that keeps
     only rank r's units (ot_tsdf_set_shard(r, N)), for every rank r of N = 2, 4, 8, with the double-buffered front end
     (the sharded default: batch k+1's staging / touch beside batch k's integrate) and, for comparison, without it.  A
-    rank's step on an N-GPU node is this time (its shard, its front end, nothing shared with the other ranks), so
-    headline_ms / max over r is the strong-scaling speed-up of one object before the halo extraction."""
+    rank's step on an N-GPU node is this time (its shard, its front end, nothing shared with the other ranks), so the
+    unsharded step (N = 1, the same method) / max over r is the strong-scaling speed-up of one object before the halo
+    extraction.  The resident scan goes in with ot_tsdf_integrate_u16_frames (one host call per scan, the bits of
+    256 per-frame calls): at 1/8 of the integrate a rank's GPU step is shorter than 256 ctypes round trips."""
     W, H = intr.width, intr.height
     npx = W * H
-    dptrs = [C.c_void_p(d_depth.data_ptr() + k * npx * 2) for k in range(args.frames)]
-    cptrs = [C.c_void_p(d_color.data_ptr() + k * npx * 3) for k in range(args.frames)]
-    eptrs = [ext[k].ctypes.data_as(C.c_void_p) for k in range(args.frames)]
-    integrate, pintr = lib.ot_tsdf_integrate_u16, C.byref(intr)
+    integrate_frames, pintr = lib.ot_tsdf_integrate_u16_frames, C.byref(intr)
+    dp, cp, ep = d_depth.data_ptr(), d_color.data_ptr(), ext.ctypes.data
     out = {}
     for N in worlds:
         per_mode = {}
-        for mode in (1, 0):
+        for mode in ((1, 0) if N > 1 else (0,)):
             worst, units = 0.0, []
             for r in range(N):
                 vol = C.c_void_p()
                 L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
                 try:
                     L.call("ot_tsdf_set_color_precision", vol, args.color_bits)
-                    L.call("ot_tsdf_set_shard", vol, r, N)
+                    if N > 1:
+                        L.call("ot_tsdf_set_shard", vol, r, N)
                     L.call("ot_tsdf_set_frontend_overlap", vol, mode)
 
                     def step():
                         L.call("ot_tsdf_reset_async", vol, stream)
-                        for k in range(args.frames):
-                            if integrate(vol, dptrs[k], cptrs[k], pintr, eptrs[k], 1000.0, 3.0, stream):
-                                raise RuntimeError(lib.ot_last_error().decode())
+                        if integrate_frames(vol, args.frames, dp, cp, pintr, ep, 1000.0, 3.0, stream):
+                            raise RuntimeError(lib.ot_last_error().decode())
                         L.call("ot_tsdf_flush", vol, stream)
 
                     for _ in range(3):
@@ -555,12 +559,17 @@ def shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, h
                     units.append(nu.value)
                 finally:
                     L.call("ot_tsdf_destroy", vol)
-            per_mode["overlap" if mode else "serial"] = {"rank_step_ms_max": round(worst, 4),
-                                                         "speedup": round(headline_ms / worst, 2) if worst else None}
+            per_mode["overlap" if mode else "serial"] = {"rank_step_ms_max": round(worst, 4)}
         per_mode["units_per_rank_min_max"] = [min(units), max(units)]
         out[str(N)] = per_mode
-    return {"method": "every rank's shard of the headline scan timed on this GPU (reset + 256 frames + flush, "
-                      f"{args.shard_steps} steps after 3 warm-up), max over ranks; speedup = headline ms_per_step / that",
+    base = out["1"]["serial"]["rank_step_ms_max"]
+    for N, per_mode in out.items():
+        for m in ("overlap", "serial"):
+            if m in per_mode and per_mode[m]["rank_step_ms_max"]:
+                per_mode[m]["speedup"] = round(base / per_mode[m]["rank_step_ms_max"], 2)
+    return {"method": "every rank's shard of the headline scan timed on this GPU (reset + 256 frames in one "
+                      f"ot_tsdf_integrate_u16_frames call + flush, {args.shard_steps} steps after 3 warm-up), max over "
+                      "ranks; speedup = the unsharded volume's step (N = 1, same method) / that",
             "headline_ms_per_step": round(headline_ms, 4), "worlds": out}
 
 

@@ -57,3 +57,15 @@ def test_stale_or_other_workload_pmc_is_refused(tmp_path):
     assert traffic is None and "workload" in note
     missing = types.SimpleNamespace(traffic=str(tmp_path / "absent.json"))
     assert bench._traffic(missing, L, "k_batch_integrate", {})[0] is None
+
+
+def test_spatial_amdahl_caps_and_measured():
+    """bench.spatial_amdahl: the serial (F + I/N) and double-buffered (max(F, I/N)) caps from the per-batch front end F
+    and integrate I, with the measured per-rank steps carried beside them."""
+    bench, _ = _bench_and_lib()
+    out = bench.spatial_amdahl(0.1, 0.7, {"worlds": {"8": {"overlap": {"speedup": 6.1}}}})
+    assert out["speedup_cap_serial"]["8"] == round(0.8 / (0.1 + 0.7 / 8), 2)
+    assert out["speedup_cap_overlap"]["8"] == round(0.8 / 0.1, 2)
+    assert out["speedup_cap_overlap"]["2"] == round(0.8 / 0.35, 2)
+    assert out["measured"]["worlds"]["8"]["overlap"]["speedup"] == 6.1
+    assert bench.spatial_amdahl(0.0, 0.7) is None

@@ -78,8 +78,11 @@ def compare(base, var):
     mesh_err = {}
     if base["V"].shape == var["V"].shape and np.array_equal(base["T"], var["T"]):  # same topology, canonical order
         dv = np.abs(base["V"] - var["V"])
+        row = dv.max(axis=1)
         mesh_err = {"mesh_topology_identical": True, "vertex_max_abs_diff_m": float(dv.max()),
-                    "vertex_max_rel_diff": float((dv / np.maximum(np.abs(base["V"]), 1e-300)).max())}
+                    "vertex_abs_diff_m_p50_p99_p9999": [float(np.percentile(row, q)) for q in (50, 99, 99.99)],
+                    "vertices_off_by_more_than_1e-6_m": int((row > 1e-6).sum()),
+                    "vertices_off_by_more_than_1e-4_m": int((row > 1e-4).sum())}
     vb = {r.tobytes() for r in np.ascontiguousarray(base["V"])}
     vv = [r.tobytes() for r in np.ascontiguousarray(var["V"])]
     return {"units_base": len(kb), "units_only_in_base": len(set(kb) - set(kv)),
@@ -91,6 +94,8 @@ def compare(base, var):
             "mesh_triangles_base": int(base["T"].shape[0]), "mesh_triangles_variant": int(var["T"].shape[0]),
             "variant_vertices_not_in_base": int(sum(1 for r in vv if r not in vb)),
             "tsdf_max_abs_diff_same_weight": float(tdiff.max()) if tdiff.size else 0.0,
+            "tsdf_abs_diff_p99_same_weight": float(np.percentile(tdiff, 99)) if tdiff.size else 0.0,
+            "voxels_tsdf_off_by_more_than_1e-4": int((tdiff > 1e-4).sum()),
             "colour_max_abs_diff_same_weight": float(cdiff.max()) if cdiff.size else 0.0, **mesh_err}
 
 

@@ -39,6 +39,11 @@ int main(int argc, char** argv) {
     const int R = argc > 4 ? atoi(argv[4]) : 1;  // stage-1 block radius in cells
     const int zorder = argc > 5 ? atoi(argv[5]) : 0;  // 1: own z-cell first inside a column
     const int flat = argc > 6 ? atoi(argv[6]) : 0;  // 1: the lane's slots as one flattened lockstep stream
+    // > 1: candidates in per-lane batches of this many (one gather step each), each batch sorted (a B-input network),
+    // then inserted in ascending order while ANY lane of the wave still accepts its next one (a sorted batch's
+    // acceptances are a prefix per lane, so a wave's insertion steps per batch = its largest prefix)
+    const int batch = argc > 7 ? atoi(argv[7]) : 0;
+    long long batch_steps = 0, batch_ins_steps = 0;
     const double h = hm * 0.005;
     double mn[3] = {1e30, 1e30, 1e30};
     for (size_t i = 0; i < n; ++i)
@@ -162,6 +167,37 @@ int main(int argc, char** argv) {
                 act[l] = ex * ex + ey * ey + ez * ez < best[l][K - 1];
                 if (act[l]) maxlen = std::max(maxlen, plan[l][u].second - plan[l][u].first);
             }
+            if (batch > 1) {
+                for (int s0 = 0; s0 < maxlen; s0 += batch) {
+                    int wave_ins = 0;
+                    for (int l = 0; l < nl; ++l) {
+                        if (!act[l]) continue;
+                        const int len = plan[l][u].second - plan[l][u].first;
+                        std::vector<double> bd;
+                        for (int s = s0; s < s0 + batch && s < len; ++s) {
+                            const size_t j = w0 + l, m = plan[l][u].first + s;
+                            const double d0 = S[j * 3] - S[m * 3], d1 = S[j * 3 + 1] - S[m * 3 + 1],
+                                         d2 = S[j * 3 + 2] - S[m * 3 + 2];
+                            bd.push_back((d0 * d0 + d1 * d1) + d2 * d2);
+                            ++tot_cand;
+                        }
+                        std::sort(bd.begin(), bd.end());
+                        int acc = 0;
+                        for (double d : bd) {
+                            if (!(d < best[l][K - 1])) break;
+                            ++acc;
+                            ++tot_ins;
+                            auto& b = best[l];
+                            b[K - 1] = d;
+                            for (int i = K - 1; i > 0 && b[i] < b[i - 1]; --i) std::swap(b[i], b[i - 1]);
+                        }
+                        wave_ins = std::max(wave_ins, acc);
+                    }
+                    ++batch_steps;
+                    batch_ins_steps += wave_ins;
+                }
+                continue;
+            }
             for (int s = 0; s < maxlen; ++s) {
                 bool any = false;
                 for (int l = 0; l < nl; ++l) {
@@ -217,6 +253,13 @@ int main(int argc, char** argv) {
            wave_ins_steps / nw, 100.0 * wave_ins_steps / std::max<long long>(wave_steps, 1), 100.0 * unsettled / nq,
            (12.0 * wave_steps + 42.0 * wave_ins_steps) / nq);
     printf("   flat %d: wave steps with a column transition %.1f\n", flat, trans_steps / nw);
+    if (batch > 1) {
+        const int ce = batch == 2 ? 1 : batch == 4 ? 5 : batch == 8 ? 19 : batch == 16 ? 60 : batch * batch / 2;
+        printf("   batch %d: per wave %.1f batch steps, %.1f insertion steps (%.2f per batch) | VALU model "
+               "(12/cand-slot x %d + %d/sort + 42/ins-step) per query %.1f\n", batch, batch_steps / nw,
+               batch_ins_steps / nw, (double)batch_ins_steps / std::max<long long>(batch_steps, 1), batch, 2 * ce,
+               ((12.0 * batch + 2.0 * ce) * batch_steps + 42.0 * batch_ins_steps) / nq);
+    }
     printf("   stage-2 wave steps per wave %.1f -> model incl. stage 2 (54/step) per query %.1f\n", stage2_steps / nw,
            (12.0 * wave_steps + 42.0 * wave_ins_steps + 54.0 * stage2_steps) / nq);
 }
