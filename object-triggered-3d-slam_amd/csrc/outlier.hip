@@ -264,6 +264,32 @@ __device__ inline void scan_range(const double* __restrict__ P, const double q[3
     }
 }
 
+// Sorting network for the first KMAX candidates of a query (its own column's first ones): Batcher's odd-even merge
+// sort for 32 inputs restricted to the comparators among the first KMAX positions -- valid because inputs past KMAX
+// would be +inf, which every comparator keeps at the higher index (checked exhaustively for 20 inputs with the 0-1
+// principle when generated).  103 compare-exchanges instead of KMAX sequential insertions of ~2 KMAX min / max each.
+constexpr unsigned char k_net20[103][2] = {  // compile-time indices: the list stays in registers
+    {0, 1}, {2, 3}, {4, 5}, {6, 7}, {8, 9}, {10, 11}, {12, 13}, {14, 15}, {16, 17}, {18, 19}, {0, 2}, {1, 3}, {4, 6},
+    {5, 7}, {8, 10}, {9, 11}, {12, 14}, {13, 15}, {16, 18}, {17, 19}, {1, 2}, {5, 6}, {9, 10}, {13, 14}, {17, 18},
+    {0, 4}, {1, 5}, {2, 6}, {3, 7}, {8, 12}, {9, 13}, {10, 14}, {11, 15}, {2, 4}, {3, 5}, {10, 12}, {11, 13}, {1, 2},
+    {3, 4}, {5, 6}, {9, 10}, {11, 12}, {13, 14}, {17, 18}, {0, 8}, {1, 9}, {2, 10}, {3, 11}, {4, 12}, {5, 13},
+    {6, 14}, {7, 15}, {4, 8}, {5, 9}, {6, 10}, {7, 11}, {2, 4}, {3, 5}, {6, 8}, {7, 9}, {10, 12}, {11, 13}, {1, 2},
+    {3, 4}, {5, 6}, {7, 8}, {9, 10}, {11, 12}, {13, 14}, {17, 18}, {0, 16}, {1, 17}, {2, 18}, {3, 19}, {8, 16},
+    {9, 17}, {10, 18}, {11, 19}, {4, 8}, {5, 9}, {6, 10}, {7, 11}, {12, 16}, {13, 17}, {14, 18}, {15, 19}, {2, 4},
+    {3, 5}, {6, 8}, {7, 9}, {10, 12}, {11, 13}, {14, 16}, {15, 17}, {1, 2}, {3, 4}, {5, 6}, {7, 8}, {9, 10},
+    {11, 12}, {13, 14}, {15, 16}, {17, 18}};
+template <int KMAX>
+__device__ inline void sort_net(double (&v)[KMAX]) {
+    static_assert(KMAX == 20, "network for 20 inputs");
+#pragma unroll
+    for (int c = 0; c < 103; ++c) {
+        const int a = k_net20[c][0], b = k_net20[c][1];
+        const double lo = dmin(v[a], v[b]), hi = dmax(v[a], v[b]);
+        v[a] = lo;
+        v[b] = hi;
+    }
+}
+
 template <int KMAX>
 __device__ inline void topk_reset(double (&best)[KMAX], int kk) {
 #pragma unroll
@@ -365,7 +391,7 @@ __device__ inline int64_t xcd_block() {
     return x * per + (x < rem ? x : rem) + (b >> 3);
 }
 
-template <int KMAX, int R>
+template <int KMAX, int R, bool NETFILL = true>
 __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, double* avg, SorPend pd) {
     constexpr int W = 2 * R + 1;
     const int64_t j = xcd_block() * 256 + threadIdx.x;
@@ -384,12 +410,25 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     double lo[3], hi[3];
     cell_fracs(g, q, o, cc, lo, hi);
     long long have = 0;
+    // The own column's first KMAX candidates fill the empty list at once: their distances, +inf past the column's end,
+    // sorted by a network -- the list 20 sequential insertions would leave (each of the first KMAX is accepted, the
+    // list holding +inf), so every later decision and the final sum are the same bits.  Only for lists of KMAX (kk <
+    // KMAX lists keep their -inf padding and the sequential fill)
+    int m0 = 0;
+    if constexpr (KMAX == 20 && NETFILL) {
+        const int2 se = rr[R == 1 ? c_cols3[0] : c_cols5[0]];
+        m0 = kk == KMAX ? min(KMAX, se.y - se.x) : 0;
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i)
+            if (i < m0) best[i] = d2_l2(q, g.sxyz + (int64_t)(se.x + i) * 3);
+        sort_net<KMAX>(best);
+    }
     for (int u = 0; u < W * W; ++u) {
         const int t = R == 1 ? c_cols3[u] : c_cols5[u];
         const int dx = t / W - R, dy = t % W - R;
         const int2 se = rr[t];
         const double ex = face_gap(lo[0], hi[0], dx, g.h), ey = face_gap(lo[1], hi[1], dy, g.h);
-        if (!(ex * ex + ey * ey >= best[KMAX - 1])) scan_range<KMAX>(g.sxyz, q, se.x, se.y, best);
+        if (!(ex * ex + ey * ey >= best[KMAX - 1])) scan_range<KMAX>(g.sxyz, q, se.x + (u == 0 ? m0 : 0), se.y, best);
         have += se.y - se.x;
     }
     const double guard = block_guard(g, q, o, cc, (double)R);
@@ -963,6 +1002,9 @@ ot_status build_grid_sorted(const double* xyz, const unsigned long long* ckeys, 
     return OT_OK;
 }
 
+// test hook otx_sor_netfill: 0 = the sequential fill of the stage-1 list (A/B timing and parity of the network fill)
+static bool g_sor_netfill = true;
+
 ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_neighbors, double std_ratio,
                      double* avg, double* stats, hipStream_t stream, int slot0) {
     const int F = gb.g.nframes;
@@ -993,8 +1035,12 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
     const unsigned rgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid / 4, 1), 2048);
 #define OT_SOR_LAUNCH(KM)                                                                                           \
     do {                                                                                                            \
-        hipLaunchKernelGGL((k_sor_knn<KM, SOR_BLOCK_R>), dim3(grid), dim3(256), 0, stream, gb.g, n,                 \
-                           (int)nb_neighbors, avg, pd);                                                             \
+        if (g_sor_netfill)                                                                                          \
+            hipLaunchKernelGGL((k_sor_knn<KM, SOR_BLOCK_R, true>), dim3(grid), dim3(256), 0, stream, gb.g, n,       \
+                               (int)nb_neighbors, avg, pd);                                                         \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_sor_knn<KM, SOR_BLOCK_R, false>), dim3(grid), dim3(256), 0, stream, gb.g, n,      \
+                               (int)nb_neighbors, avg, pd);                                                         \
         hipLaunchKernelGGL((k_sor_knn_rest<KM, SOR_BLOCK_R>), dim3(rgrid), dim3(256), 0, stream, gb.g,              \
                            (int)nb_neighbors, avg, pd, pd3);                                                        \
         hipLaunchKernelGGL((k_sor_knn_wave<KM>), dim3(1024), dim3(64), 0, stream, gb.g, (int)nb_neighbors, avg, pd3); \
@@ -1096,6 +1142,15 @@ static ot_status single_frame_grid(const double* xyz, int64_t n, double h, const
     // build_grid_frames synchronises the stream before returning, so org / off outlive their copies
     return build_grid_frames(xyz, n, 1, (const int*)(fr + 32), (const double*)fr, h, dims, nbr, stream, gb, 22);
 }
+
+extern "C" {
+// test / diagnostic hook (not part of the drop-in boundary): 1 (default) = stage 1 fills its list with the own
+// column's first 20 candidates through a sorting network, 0 = by sequential insertion (same bits)
+ot_status otx_sor_netfill(int32_t on) {
+    ot::g_sor_netfill = on != 0;
+    return OT_OK;
+}
+}  // extern "C"
 
 extern "C" {
 

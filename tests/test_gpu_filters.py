@@ -236,16 +236,20 @@ def hd_voxels(O, synth, gpu):
     return O.voxel_down_sample(xyz, rgb, 0.005)[0]
 
 
-def test_sor_bench_scale_bitexact(pkg, O, hd_voxels):
-    """The bench's SOR(20, 2.0) on ~270k voxels: mean kNN distances and kept indices bit-exact."""
+@pytest.mark.parametrize("netfill", [1, 0])
+def test_sor_bench_scale_bitexact(pkg, O, hd_voxels, netfill):
+    """The bench's SOR(20, 2.0) on ~270k voxels: mean kNN distances and kept indices bit-exact -- with stage 1's list
+    filled by the sorting network (the default) and by sequential insertion (otx_sor_netfill(0))."""
     ds = hd_voxels
     L = pkg._lib
+    L.call("otx_sor_netfill", netfill)
     d = torch.from_numpy(ds).cuda()
     idx = torch.empty(ds.shape[0], dtype=torch.int64, device="cuda")
     avg = torch.empty(ds.shape[0], dtype=torch.float64, device="cuda")
     n = C.c_int64(0)
     L.call("ot_remove_statistical_outlier", C.c_void_p(d.data_ptr()), ds.shape[0], 20, 2.0,
            C.c_void_p(idx.data_ptr()), C.c_void_p(avg.data_ptr()), C.byref(n), None)
+    L.call("otx_sor_netfill", 1)
     ridx, ravg = O.remove_statistical_outlier(ds, 20, 2.0)
     assert_bitwise(avg.cpu().numpy(), ravg, "SOR mean kNN distance (bench scale)")
     assert_bitwise(idx[:n.value].cpu().numpy(), ridx, "SOR kept indices (bench scale)")
