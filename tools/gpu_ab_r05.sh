@@ -11,3 +11,11 @@ timeout -k 10 400 python3 -u tools/filter_batch_time.py --frames 128 --batches 6
     > gpurun_out/${T}_netfill.log 2>&1 || { echo NETFILL_FAILED; tail -20 gpurun_out/${T}_netfill.log; exit 1; }
 grep -E "netfill|batch 64" gpurun_out/${T}_netfill.log
 bash tools/gpu_ab_overlap.sh
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+for ov in 1 0; do
+  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T}_shard8_ov$ov -o run -- python3 -u \
+      tools/shard_trace.py --world 8 --overlap $ov > gpurun_out/${T}_shard8_ov$ov.log 2>&1 || { echo SHARDTRACE_FAILED; tail -20 gpurun_out/${T}_shard8_ov$ov.log; exit 1; }
+  grep "ms/step" gpurun_out/${T}_shard8_ov$ov.log
+  python3 tools/shard_trace.py --report gpurun_out/${T}_shard8_ov$ov/run_kernel_trace.csv > gpurun_out/${T}_shard8_ov${ov}_timeline.txt 2>&1
+  head -40 gpurun_out/${T}_shard8_ov${ov}_timeline.txt
+done

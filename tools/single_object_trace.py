@@ -4,6 +4,7 @@ the last repetition (durations and the idle gaps between kernels).  Tool only.
 
   rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 tools/single_object_trace.py
   python3 tools/single_object_trace.py --report DIR/run_kernel_trace.csv
+  python3 tools/single_object_trace.py --separate     (the facade's separate extract / normals / sample calls)
   python3 tools/single_object_trace.py --no-normals   (diagnostic: the same object without compute_vertex_normals, i.e.
                                                        what the normals' side-stream kernel costs the critical path)
 """
@@ -73,6 +74,8 @@ def main(normals=True):
     def one():
         vol.reset()
         lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
+        if normals and "--separate" not in sys.argv:  # bench.py's path: one host call from the totals to the sampler
+            return vol.extract_mesh_and_sample_min_z(100000, 0.03)[1]
         mesh = vol.extract_triangle_mesh()
         if normals:
             mesh.compute_vertex_normals()
