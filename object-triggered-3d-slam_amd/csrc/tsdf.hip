@@ -451,11 +451,12 @@ constexpr int RCP_N = 2048;  // 16 KiB (float64) / 8 KiB (float32) of LDS per wo
 // whatever its registers); the parts of a unit run on one XCD.  Work items are assigned by a static grid stride that
 // every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes.
-template <bool C64, bool FAST>
+template <bool C64, bool FAST, int ZB = BZ>
 __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
     const int* __restrict__ wcount) {
     using CT = typename std::conditional<C64, double, float>::type;
+    constexpr int PARTS = 4 * (UNIT_RES / ZB) / INT_WG;  // workgroups per unit (INT_PARTS at the default ZB)
     // one table per kernel: float64 reciprocals for the float64-colour kernel (its float32 ones are their roundings:
     // (float)RN64(1/n) == RN32(1/n) for every n <= 2^20, no double-rounding case -- tools/markstein_check.cpp),
     // float32 ones otherwise
@@ -471,16 +472,16 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
     const int lane = threadIdx.x & 63;
     const int n = *wcount;
     const int npx = p.W * p.H;
-    unsigned upd = 0;  // per lane: <= BZ voxels x 64 frames x units per workgroup, far below 2^32
+    unsigned upd = 0;  // per lane: <= ZB voxels x 64 frames x units per workgroup, far below 2^32
     {
         const int b = blockIdx.x;
-        // work item = (unit, part): the INT_PARTS parts of a unit are items 8 apart, so they run on one XCD (blocks
+        // work item = (unit, part): the PARTS parts of a unit are items 8 apart, so they run on one XCD (blocks
         // are dealt round-robin over the 8 XCDs) at about the same time and share its L2's copy of the footprint
-        const int items = INT_PARTS == 1 ? n : ((n + 7) / 8) * 8 * INT_PARTS;
+        const int items = PARTS == 1 ? n : ((n + 7) / 8) * 8 * PARTS;
         for (int it = b; it < items; it += gridDim.x) {
-            const int u = INT_PARTS == 1 ? it : (it / (8 * INT_PARTS)) * 8 + (it & 7);
-            if (INT_PARTS > 1 && u >= n) continue;
-            const int part = INT_PARTS == 1 ? 0 : (it >> 3) % INT_PARTS;
+            const int u = PARTS == 1 ? it : (it / (8 * PARTS)) * 8 + (it & 7);
+            if (PARTS > 1 && u >= n) continue;
+            const int part = PARTS == 1 ? 0 : (it >> 3) % PARTS;
             const int s = __builtin_amdgcn_readfirstlane(part * INT_WG + (int)(threadIdx.x >> 6));  // slice of this wave
             const UnitWork& w = work[u];
             const int ent = w.id;
@@ -491,16 +492,16 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                 // wave = 8 x 8 columns: a square patch of the unit's xy plane projects to fewer pixel rows
                 const int x = (s & 2) * 4 + (lane >> 3), y = (s & 1) * 8 + (lane & 7);
                 const int col = x * 16 + y;
-                const int z0 = (s >> 2) * BZ;
+                const int z0 = (s >> 2) * ZB;
                 float* base = d.vox + (size_t)id * (C64 ? UNIT_FLOATS_C64 : UNIT_FLOATS);
                 // colour plane c of voxel vi: float32 planes addressed from base (one address register for the
                 // whole record: a separate colour pointer costs ~34 VGPRs in this kernel), float64 through a buffer
                 // resource over the record's float64 planes
                 const __amdgpu_buffer_rsrc_t col64 = make_rsrc(base + 2 * UNIT_VOX, 3 * UNIT_VOX * 8);
-                float ts[BZ], wt[BZ];
-                CT cr[BZ], cg[BZ], cb[BZ];
+                float ts[ZB], wt[ZB];
+                CT cr[ZB], cg[ZB], cb[ZB];
 #pragma unroll
-                for (int k = 0; k < BZ; ++k) {
+                for (int k = 0; k < ZB; ++k) {
                     const int vi = (z0 + k) * 256 + col;
                     if (fresh) {
                         ts[k] = wt[k] = 0.0f;
@@ -546,11 +547,11 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                         pc[1] += es1;
                         pc[2] += es2;
                     }
-                    // phase A: projections of the BZ voxels
-                    int pixv[BZ];
-                    float pcz[BZ];
+                    // phase A: projections of the ZB voxels
+                    int pixv[ZB];
+                    float pcz[ZB];
 #pragma unroll
-                    for (int k = 0; k < BZ; ++k) {
+                    for (int k = 0; k < ZB; ++k) {
                         const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
                         // Certified fast projection.  Only floor(u), floor(v) and the bound tests are used, so
                         // u = nu * rcp(z) decides them exactly unless u lies within proj_eps of an integer (the
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                             u_f = ((nu / pc[2]) + p.cx) + 0.5f;
                             v_f = ((nv / pc[2]) + p.cy) + 0.5f;
                         }
-                        // non-short-circuit test keeps all BZ projections in one basic block
+                        // non-short-circuit test keeps all ZB projections in one basic block
                         const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) &
                                         (v_f < p.safe_h);
                         pixv[k] = ok ? (int)__umul24((unsigned)(int)v_f, (unsigned)p.W) + (int)u_f : -1;
@@ -577,9 +578,9 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                     }
                     // phase B: every depth gather issued before any use (buffer loads: wave-uniform resource +
                     // 32-bit byte offset, no per-lane 64-bit address math)
-                    float dv[BZ], mv[BZ];
+                    float dv[ZB], mv[ZB];
 #pragma unroll
-                    for (int k = 0; k < BZ; ++k) {
+                    for (int k = 0; k < ZB; ++k) {
                         dv[k] = mv[k] = 0.0f;
                         if (pixv[k] >= 0) {  // lanes projecting outside the image issue no gather
                             const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
@@ -588,11 +589,11 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                         }
                     }
                     // phase C: the depth test; colour gathered only by the lanes whose voxel updates
-                    bool doitv[BZ];
-                    float sdfv[BZ];
-                    uint32_t cv[BZ];
+                    bool doitv[ZB];
+                    float sdfv[ZB];
+                    uint32_t cv[ZB];
 #pragma unroll
-                    for (int k = 0; k < BZ; ++k) {
+                    for (int k = 0; k < ZB; ++k) {
                         sdfv[k] = (dv[k] - pcz[k]) * mv[k];
                         doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
                         cv[k] = 0u;
@@ -600,7 +601,7 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                     }
                     // phase D: updates in frame order (select form: identical values, no exec-mask branches)
 #pragma unroll
-                    for (int k = 0; k < BZ; ++k) {
+                    for (int k = 0; k < ZB; ++k) {
                         const bool doit = doitv[k];
                         const float sv = sdfv[k] * p.trunc_inv;
                         const float tn = (sv < 1.0f) ? sv : 1.0f;
@@ -658,7 +659,7 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                 // a slice none of whose voxels updated in this batch still holds its HBM values (fresh ones: zeros)
                 if (!fresh && !__any(upd != upd0)) continue;
 #pragma unroll
-                for (int k = 0; k < BZ; ++k) {
+                for (int k = 0; k < ZB; ++k) {
                     const int vi = (z0 + k) * 256 + col;
                     base[vi] = ts[k];
                     base[UNIT_VOX + vi] = wt[k];
@@ -1054,18 +1055,23 @@ static ot_status check_frame(const ot_tsdf* vol, const void* depth, const uint8_
 // static stride (0.77 vs 0.72 ms per launch; 6x / 12x / 16x / 32x: within 2 %, slower).
 constexpr int INT_GRID_MULT = 8;
 
-// the integrate instantiation of a batch: colour precision 64 (bit 1), reciprocal table (bit 0)
+// the integrate instantiation of a batch: colour precision 64 (bit 1), reciprocal table (bit 0), fine slices (bit 2:
+// 2 voxels per lane along z, 32 waves per unit instead of 16 -- for batches with few units, below)
+static int g_int_fine = -1;  // test hook otx_integrate_fine: -1 by the batch's size (default), 0 coarse, 1 fine
 static const void* integrate_kernel(int variant) {
-    static const void* const k[4] = {(const void*)k_batch_integrate<false, false>, (const void*)k_batch_integrate<false, true>,
-                                     (const void*)k_batch_integrate<true, false>, (const void*)k_batch_integrate<true, true>};
-    return k[variant & 3];
+    static const void* const k[8] = {
+        (const void*)k_batch_integrate<false, false>, (const void*)k_batch_integrate<false, true>,
+        (const void*)k_batch_integrate<true, false>, (const void*)k_batch_integrate<true, true>,
+        (const void*)k_batch_integrate<false, false, 2>, (const void*)k_batch_integrate<false, true, 2>,
+        (const void*)k_batch_integrate<true, false, 2>, (const void*)k_batch_integrate<true, true, 2>};
+    return k[variant & 7];
 }
 
 static int integrate_grid(int variant) {
-    static int cache[4][64] = {{0}};
+    static int cache[8][64] = {{0}};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 4096;
-    int* cache_c = cache[variant & 3];
+    int* cache_c = cache[variant & 7];
     if (!cache_c[dev]) {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, integrate_kernel(variant), 64 * INT_WG, 0) !=
@@ -1214,6 +1220,19 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
     const bool fast = !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
     bc.variant = (vol->color64 ? 2 : 0) + (fast ? 1 : 0);
+    // Few units (a spatial shard, a small object): a (unit, quarter) item is a chain of the batch's frames, ~60 us at 64
+    // frames whatever the unit count, so a batch with fewer items than ~3 rounds of resident workgroups is bound by
+    // that chain (r05c: a 1/8 shard's integrate 150-180 us per 64 frames against 720 / 8).  Such batches take twice
+    // the items of half the length (2 voxels per lane along z: the same per-voxel arithmetic, the same bits).  The
+    // unit count of a batch is known on the device only: the previous batch's (mailed) stands in for it, and a
+    // sharded volume's first batch counts as small from 4 ranks on.
+    {
+        const int resident = integrate_grid(bc.variant) / INT_GRID_MULT;
+        const int64_t est = vol->last_batch_slots >= 0 ? vol->last_batch_slots
+                                                       : (vol->dev.shard_world >= 4 ? 0 : (int64_t)1 << 30);
+        const bool fine = g_int_fine > 0 || (g_int_fine < 0 && est * INT_PARTS < 3 * (int64_t)resident);
+        if (fine) bc.variant |= 4;
+    }
     const int grid = integrate_grid(bc.variant);
     // overlap: the integrate on istream behind this set's units kernel (and the previous batch's integrate: same
     // stream), so the caller's stream is free for the next batch's front end
@@ -1345,6 +1364,7 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
         OT_HIP_TRY(hipEventSynchronize(vol->ev_early));
         int c[N_COUNTERS];
         std::memcpy(c, vol->hmail + OT_MAIL_WORDS, sizeof(c));
+        vol->last_batch_slots = c[bc.pc];  // units the batch touched: the next batch's item estimate
         const bool short_of_room = c[C_OVERFLOW] != 0 || (c[C_HASHERR] & 1) != 0;
         if (!short_of_room) {
             if ((int64_t)c[C_UNITS] * 4 > vol->max_units * 3)
@@ -1668,6 +1688,7 @@ ot_status ot_tsdf_reset_async(ot_tsdf* v, void* stream_) {
     v->frame_id = 0;
     v->imported = false;
     v->early_frame = -1;
+    v->last_batch_slots = -1;
     v->sorted_frame = -1;
     v->sorted_units = -1;
     v->mesh.nv = v->mesh.nt = 0;
@@ -1907,6 +1928,13 @@ ot_status otx_tsdf_stats(ot_tsdf* vol, uint64_t* out4) {
     ot_status st = tsdf_flush(vol, nullptr);
     if (st != OT_OK) return st;
     OT_HIP_TRY(hipMemcpy(out4, vol->dev.stats, sizeof(uint64_t) * 4, hipMemcpyDeviceToHost));
+    return OT_OK;
+}
+
+// test hook: the integrate's slice granularity (-1 = by the batch's estimated unit count, 0 = 4 voxels per lane along z
+// always, 1 = 2 always): A/B timing and the parity of both instantiations
+ot_status otx_integrate_fine(int32_t mode) {
+    g_int_fine = mode < 0 ? -1 : (mode ? 1 : 0);
     return OT_OK;
 }
 

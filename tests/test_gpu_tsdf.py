@@ -160,6 +160,21 @@ def test_tsdf_integrate_bitexact(pkg, O, gpu, synth, seq16, voxel, batch):
     assert n > 300
 
 
+@pytest.mark.parametrize("fine", [0, 1])
+def test_integrate_granularity_bitexact(pkg, O, gpu, synth, fine):
+    """Both slice granularities of k_batch_integrate (4 voxels per lane along z, 16 waves per unit; or 2, 32 waves --
+    taken for batches with few units) forced for every batch: 40 frames at 5 mm in 16-frame batches, bitwise vs the
+    oracle (keys, tsdf, weight, float64 colour, counters)."""
+    L = pkg._lib
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=80, frames=range(0, 80, 2))
+    L.call("otx_integrate_fine", fine)
+    try:
+        vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005, batch=16)
+        assert _compare_volumes(vol, ref) > 1000
+    finally:
+        L.call("otx_integrate_fine", -1)
+
+
 @pytest.mark.parametrize("batch", [1, None])
 def test_tsdf_odd_resolution(pkg, O, gpu, synth, batch):
     """A 321x243 camera (width not a multiple of 4: the staging kernel's per-pixel path; odd sample grid at
