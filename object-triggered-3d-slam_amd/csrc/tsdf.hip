@@ -429,6 +429,58 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
     }
 }
 
+// Phases A and B of one frame for a lane's ZB voxels: the certified projections and the depth gathers (no voxel state
+// read) -- the fine slices' frame skew issues them for frame f+1 before frame f's updates (k_batch_integrate).  The same
+// arithmetic as the phases inside the coarse loop.
+template <int ZB>
+__device__ __forceinline__ void frame_tap(const BatchFrame& fr, const IntegrateParams& p, int npx, float px, float py,
+                                          float pz, int z0, int (&pixv)[ZB], float (&pcz)[ZB], float (&dv)[ZB],
+                                          float (&mv)[ZB]) {
+    const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(fr.dm, npx * 8);
+    float pc[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const float a = fr.E[r * 4 + 0] * px;
+        const float b = fr.E[r * 4 + 1] * py;
+        const float c = fr.E[r * 4 + 2] * pz;
+        pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
+    }
+    const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
+    for (int k = 0; k < z0; ++k) {  // wave-uniform: advance to this slice's first voxel
+        pc[0] += es0;
+        pc[1] += es1;
+        pc[2] += es2;
+    }
+#pragma unroll
+    for (int k = 0; k < ZB; ++k) {
+        const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
+        const float rz = __builtin_amdgcn_rcpf(pc[2]);
+        float u_f = (nu * rz + p.cx) + 0.5f;
+        float v_f = (nv * rz + p.cy) + 0.5f;
+        const bool sure = !(pc[2] > 0.0f) || ((int)(fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
+                                              (int)(fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
+        if (!sure) {
+            u_f = ((nu / pc[2]) + p.cx) + 0.5f;
+            v_f = ((nv / pc[2]) + p.cy) + 0.5f;
+        }
+        const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) & (v_f < p.safe_h);
+        pixv[k] = ok ? (int)__umul24((unsigned)(int)v_f, (unsigned)p.W) + (int)u_f : -1;
+        pcz[k] = pc[2];
+        pc[0] += es0;
+        pc[1] += es1;
+        pc[2] += es2;
+    }
+#pragma unroll
+    for (int k = 0; k < ZB; ++k) {
+        dv[k] = mv[k] = 0.0f;
+        if (pixv[k] >= 0) {
+            const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
+            dv[k] = __uint_as_float(raw.x);
+            mv[k] = __uint_as_float(raw.y);
+        }
+    }
+}
+
 // Occupancy: the integrate lives on it: 64 VGPRs, 8 waves per SIMD for both colour precisions with
 // quarter-unit workgroups (float64 colour at 5 / 6 / 8 waves: 0.426 / 0.428 / 0.414 ms per 32-frame launch; the IEEE-
 // division float64 kernel needs more registers and runs at 5).  Measured and settled: lanes whose voxel
@@ -527,133 +579,231 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                 const float py = (p.half + p.vl * (float)y) + oy;
                 const float pz = p.half + oz;
                 const unsigned upd0 = upd;
-                for (unsigned long long m = mask; m; m &= m - 1) {
-                    const int f = __ffsll((long long)m) - 1;
-                    const BatchFrame& fr = frames[f];
-                    const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(fr.dm, npx * 8);
-                    const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
-                    const bool use_color = fr.color != nullptr;
-                    float pc[3];
+                if constexpr (ZB == 2) {
+                    // Frame skew (the fine slices serve batches with few units, whose waves cannot hide a frame's
+                    // dependent gathers behind other waves): frame f's colour gathers and frame f+1's projections and
+                    // depth gathers are issued together, before frame f's updates -- one memory round trip per frame
+                    // on the wave's chain instead of two.  The taps read no voxel state, so the order of the updates
+                    // (and every bit) is the unskewed loop's.
+                    unsigned long long m = mask;  // non-empty: a listed slot was touched by some frame of the batch
+                    int f = __ffsll((long long)m) - 1;
+                    int pixv[ZB], pixv_n[ZB];
+                    float pcz[ZB], dv[ZB], mv[ZB], pcz_n[ZB], dv_n[ZB], mv_n[ZB];
+                    frame_tap<ZB>(frames[f], p, npx, px, py, pz, z0, pixv, pcz, dv, mv);
+                    for (;;) {
+                        m &= m - 1;
+                        const int fn = m ? __ffsll((long long)m) - 1 : -1;  // wave-uniform
+                        const BatchFrame& fr = frames[f];
+                        const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
+                        const bool use_color = fr.color != nullptr;
+                        // phase C: the depth test; colour gathered only by the lanes whose voxel updates
+                        bool doitv[ZB];
+                        float sdfv[ZB];
+                        uint32_t cv[ZB];
 #pragma unroll
-                    for (int r = 0; r < 3; ++r) {
-                        const float a = fr.E[r * 4 + 0] * px;
-                        const float b = fr.E[r * 4 + 1] * py;
-                        const float c = fr.E[r * 4 + 2] * pz;
-                        pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
-                    }
-                    const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
-                    for (int k = 0; k < z0; ++k) {  // wave-uniform: advance to this slice's first voxel
-                        pc[0] += es0;
-                        pc[1] += es1;
-                        pc[2] += es2;
-                    }
-                    // phase A: projections of the ZB voxels
-                    int pixv[ZB];
-                    float pcz[ZB];
-#pragma unroll
-                    for (int k = 0; k < ZB; ++k) {
-                        const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
-                        // Certified fast projection.  Only floor(u), floor(v) and the bound tests are used, so
-                        // u = nu * rcp(z) decides them exactly unless u lies within proj_eps of an integer (the
-                        // bound tests 0.0001 and W - 0.0001 sit 1e-4 from integers); those rare waves redo the
-                        // IEEE quotients.
-                        const float rz = __builtin_amdgcn_rcpf(pc[2]);
-                        float u_f = (nu * rz + p.cx) + 0.5f;
-                        float v_f = (nv * rz + p.cy) + 0.5f;
-                        const bool sure = !(pc[2] > 0.0f) ||
-                                          ((int)(fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
-                                           (int)(fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
-                        if (!sure) {
-                            u_f = ((nu / pc[2]) + p.cx) + 0.5f;
-                            v_f = ((nv / pc[2]) + p.cy) + 0.5f;
+                        for (int k = 0; k < ZB; ++k) {
+                            sdfv[k] = (dv[k] - pcz[k]) * mv[k];
+                            doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
+                            cv[k] = 0u;
+                            if (use_color && doitv[k])
+                                cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
                         }
-                        // non-short-circuit test keeps all ZB projections in one basic block
-                        const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) &
-                                        (v_f < p.safe_h);
-                        pixv[k] = ok ? (int)__umul24((unsigned)(int)v_f, (unsigned)p.W) + (int)u_f : -1;
-                        pcz[k] = pc[2];
-                        pc[0] += es0;
-                        pc[1] += es1;
-                        pc[2] += es2;
-                    }
-                    // phase B: every depth gather issued before any use (buffer loads: wave-uniform resource +
-                    // 32-bit byte offset, no per-lane 64-bit address math)
-                    float dv[ZB], mv[ZB];
+                        if (fn >= 0) frame_tap<ZB>(frames[fn], p, npx, px, py, pz, z0, pixv_n, pcz_n, dv_n, mv_n);
+                        // phase D: updates in frame order (select form: identical values, no exec-mask branches)
 #pragma unroll
-                    for (int k = 0; k < ZB; ++k) {
-                        dv[k] = mv[k] = 0.0f;
-                        if (pixv[k] >= 0) {  // lanes projecting outside the image issue no gather
-                            const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
-                            dv[k] = __uint_as_float(raw.x);
-                            mv[k] = __uint_as_float(raw.y);
-                        }
-                    }
-                    // phase C: the depth test; colour gathered only by the lanes whose voxel updates
-                    bool doitv[ZB];
-                    float sdfv[ZB];
-                    uint32_t cv[ZB];
-#pragma unroll
-                    for (int k = 0; k < ZB; ++k) {
-                        sdfv[k] = (dv[k] - pcz[k]) * mv[k];
-                        doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
-                        cv[k] = 0u;
-                        if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
-                    }
-                    // phase D: updates in frame order (select form: identical values, no exec-mask branches)
-#pragma unroll
-                    for (int k = 0; k < ZB; ++k) {
-                        const bool doit = doitv[k];
-                        const float sv = sdfv[k] * p.trunc_inv;
-                        const float tn = (sv < 1.0f) ? sv : 1.0f;
-                        const float wv = wt[k];
-                        const float w1 = wv + 1.0f;
-                        const float ta = ts[k] * wv + tn;
-                        float tsn;  // (tsdf * w + t) / (w + 1): the IEEE quotient, tsdf bit-exact
-                        // one table read per voxel for the tsdf and the colour quotients (round 3: +0.8 %)
-                        const double y64 = (FAST && C64) ? s_r64[(int)w1] : 0.0;
-                        if constexpr (FAST) {
-                            const float y = C64 ? (float)y64 : s_r32[(int)w1];
-                            const float q0 = ta * y;
-                            tsn = __builtin_fmaf(__builtin_fmaf(-w1, q0, ta), y, q0);
-                        } else {
-                            tsn = ta / w1;
-                        }
-                        ts[k] = doit ? tsn : ts[k];
-                        if (use_color) {
-                            if constexpr (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
-                                {  // every lane, in select form (skipping voxels without an updating lane: slower)
-                                    const double wd = (double)wv, w1d = (double)w1;
-                                    const double ar = cr[k] * wd + (double)(cv[k] & 0xFFu);
-                                    const double ag = cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu);
-                                    const double ab = cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu);
-                                    double nr, ng, nb;
-                                    if constexpr (FAST) {
-                                        const double y = y64;
-                                        const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
-                                        nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
-                                        ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
-                                        nb = __builtin_fma(__builtin_fma(-w1d, q0b, ab), y, q0b);
-                                    } else {
-                                        nr = ar / w1d;
-                                        ng = ag / w1d;
-                                        nb = ab / w1d;
+                        for (int k = 0; k < ZB; ++k) {
+                            const bool doit = doitv[k];
+                            const float sv = sdfv[k] * p.trunc_inv;
+                            const float tn = (sv < 1.0f) ? sv : 1.0f;
+                            const float wv = wt[k];
+                            const float w1 = wv + 1.0f;
+                            const float ta = ts[k] * wv + tn;
+                            float tsn;  // (tsdf * w + t) / (w + 1): the IEEE quotient, tsdf bit-exact
+                            // one table read per voxel for the tsdf and the colour quotients (round 3: +0.8 %)
+                            const double y64 = (FAST && C64) ? s_r64[(int)w1] : 0.0;
+                            if constexpr (FAST) {
+                                const float y = C64 ? (float)y64 : s_r32[(int)w1];
+                                const float q0 = ta * y;
+                                tsn = __builtin_fmaf(__builtin_fmaf(-w1, q0, ta), y, q0);
+                            } else {
+                                tsn = ta / w1;
+                            }
+                            ts[k] = doit ? tsn : ts[k];
+                            if (use_color) {
+                                if constexpr (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
+                                    {  // every lane, in select form (skipping voxels without an updating lane: slower)
+                                        const double wd = (double)wv, w1d = (double)w1;
+                                        const double ar = cr[k] * wd + (double)(cv[k] & 0xFFu);
+                                        const double ag = cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu);
+                                        const double ab = cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu);
+                                        double nr, ng, nb;
+                                        if constexpr (FAST) {
+                                            const double y = y64;
+                                            const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
+                                            nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
+                                            ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
+                                            nb = __builtin_fma(__builtin_fma(-w1d, q0b, ab), y, q0b);
+                                        } else {
+                                            nr = ar / w1d;
+                                            ng = ag / w1d;
+                                            nb = ab / w1d;
+                                        }
+                                        cr[k] = doit ? nr : cr[k];
+                                        cg[k] = doit ? ng : cg[k];
+                                        cb[k] = doit ? nb : cb[k];
                                     }
+                                } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
+                                    const float rw = __builtin_amdgcn_rcpf(w1);
+                                    const float nr = ((float)cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
+                                    const float ng = ((float)cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
+                                    const float nb = ((float)cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
                                     cr[k] = doit ? nr : cr[k];
                                     cg[k] = doit ? ng : cg[k];
                                     cb[k] = doit ? nb : cb[k];
                                 }
-                            } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
-                                const float rw = __builtin_amdgcn_rcpf(w1);
-                                const float nr = ((float)cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
-                                const float ng = ((float)cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
-                                const float nb = ((float)cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
-                                cr[k] = doit ? nr : cr[k];
-                                cg[k] = doit ? ng : cg[k];
-                                cb[k] = doit ? nb : cb[k];
+                            }
+                            wt[k] = doit ? w1 : wv;
+                            upd += doit ? 1u : 0u;
+                        }
+                        if (fn < 0) break;
+                        f = fn;
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            pixv[k] = pixv_n[k];
+                            pcz[k] = pcz_n[k];
+                            dv[k] = dv_n[k];
+                            mv[k] = mv_n[k];
+                        }
+                    }
+                } else {
+                    for (unsigned long long m = mask; m; m &= m - 1) {
+                        const int f = __ffsll((long long)m) - 1;
+                        const BatchFrame& fr = frames[f];
+                        const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(fr.dm, npx * 8);
+                        const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
+                        const bool use_color = fr.color != nullptr;
+                        float pc[3];
+#pragma unroll
+                        for (int r = 0; r < 3; ++r) {
+                            const float a = fr.E[r * 4 + 0] * px;
+                            const float b = fr.E[r * 4 + 1] * py;
+                            const float c = fr.E[r * 4 + 2] * pz;
+                            pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
+                        }
+                        const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
+                        for (int k = 0; k < z0; ++k) {  // wave-uniform: advance to this slice's first voxel
+                            pc[0] += es0;
+                            pc[1] += es1;
+                            pc[2] += es2;
+                        }
+                        // phase A: projections of the ZB voxels
+                        int pixv[ZB];
+                        float pcz[ZB];
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
+                            // Certified fast projection.  Only floor(u), floor(v) and the bound tests are used, so
+                            // u = nu * rcp(z) decides them exactly unless u lies within proj_eps of an integer (the
+                            // bound tests 0.0001 and W - 0.0001 sit 1e-4 from integers); those rare waves redo the
+                            // IEEE quotients.
+                            const float rz = __builtin_amdgcn_rcpf(pc[2]);
+                            float u_f = (nu * rz + p.cx) + 0.5f;
+                            float v_f = (nv * rz + p.cy) + 0.5f;
+                            const bool sure = !(pc[2] > 0.0f) ||
+                                              ((int)(fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
+                                               (int)(fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
+                            if (!sure) {
+                                u_f = ((nu / pc[2]) + p.cx) + 0.5f;
+                                v_f = ((nv / pc[2]) + p.cy) + 0.5f;
+                            }
+                            // non-short-circuit test keeps all ZB projections in one basic block
+                            const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) &
+                                            (v_f < p.safe_h);
+                            pixv[k] = ok ? (int)__umul24((unsigned)(int)v_f, (unsigned)p.W) + (int)u_f : -1;
+                            pcz[k] = pc[2];
+                            pc[0] += es0;
+                            pc[1] += es1;
+                            pc[2] += es2;
+                        }
+                        // phase B: every depth gather issued before any use (buffer loads: wave-uniform resource +
+                        // 32-bit byte offset, no per-lane 64-bit address math)
+                        float dv[ZB], mv[ZB];
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            dv[k] = mv[k] = 0.0f;
+                            if (pixv[k] >= 0) {  // lanes projecting outside the image issue no gather
+                                const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
+                                dv[k] = __uint_as_float(raw.x);
+                                mv[k] = __uint_as_float(raw.y);
                             }
                         }
-                        wt[k] = doit ? w1 : wv;
-                        upd += doit ? 1u : 0u;
+                        // phase C: the depth test; colour gathered only by the lanes whose voxel updates
+                        bool doitv[ZB];
+                        float sdfv[ZB];
+                        uint32_t cv[ZB];
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            sdfv[k] = (dv[k] - pcz[k]) * mv[k];
+                            doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
+                            cv[k] = 0u;
+                            if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
+                        }
+                        // phase D: updates in frame order (select form: identical values, no exec-mask branches)
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            const bool doit = doitv[k];
+                            const float sv = sdfv[k] * p.trunc_inv;
+                            const float tn = (sv < 1.0f) ? sv : 1.0f;
+                            const float wv = wt[k];
+                            const float w1 = wv + 1.0f;
+                            const float ta = ts[k] * wv + tn;
+                            float tsn;  // (tsdf * w + t) / (w + 1): the IEEE quotient, tsdf bit-exact
+                            // one table read per voxel for the tsdf and the colour quotients (round 3: +0.8 %)
+                            const double y64 = (FAST && C64) ? s_r64[(int)w1] : 0.0;
+                            if constexpr (FAST) {
+                                const float y = C64 ? (float)y64 : s_r32[(int)w1];
+                                const float q0 = ta * y;
+                                tsn = __builtin_fmaf(__builtin_fmaf(-w1, q0, ta), y, q0);
+                            } else {
+                                tsn = ta / w1;
+                            }
+                            ts[k] = doit ? tsn : ts[k];
+                            if (use_color) {
+                                if constexpr (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
+                                    {  // every lane, in select form (skipping voxels without an updating lane: slower)
+                                        const double wd = (double)wv, w1d = (double)w1;
+                                        const double ar = cr[k] * wd + (double)(cv[k] & 0xFFu);
+                                        const double ag = cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu);
+                                        const double ab = cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu);
+                                        double nr, ng, nb;
+                                        if constexpr (FAST) {
+                                            const double y = y64;
+                                            const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
+                                            nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
+                                            ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
+                                            nb = __builtin_fma(__builtin_fma(-w1d, q0b, ab), y, q0b);
+                                        } else {
+                                            nr = ar / w1d;
+                                            ng = ag / w1d;
+                                            nb = ab / w1d;
+                                        }
+                                        cr[k] = doit ? nr : cr[k];
+                                        cg[k] = doit ? ng : cg[k];
+                                        cb[k] = doit ? nb : cb[k];
+                                    }
+                                } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
+                                    const float rw = __builtin_amdgcn_rcpf(w1);
+                                    const float nr = ((float)cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
+                                    const float ng = ((float)cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
+                                    const float nb = ((float)cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                                    cr[k] = doit ? nr : cr[k];
+                                    cg[k] = doit ? ng : cg[k];
+                                    cb[k] = doit ? nb : cb[k];
+                                }
+                            }
+                            wt[k] = doit ? w1 : wv;
+                            upd += doit ? 1u : 0u;
+                        }
                     }
                 }
                 // a slice none of whose voxels updated in this batch still holds its HBM values (fresh ones: zeros)

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--overlap", type=int, default=-1)
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--fine", type=int, default=-1, help="otx_integrate_fine: -1 auto, 0 coarse, 1 fine slices")
     ap.add_argument("--report")
     a = ap.parse_args()
     if a.report:
@@ -53,6 +54,7 @@ def main():
     if a.world > 1:
         L.call("ot_tsdf_set_shard", vol, a.rank, a.world)
     L.call("ot_tsdf_set_frontend_overlap", vol, a.overlap)
+    L.call("otx_integrate_fine", a.fine)
 
     def step():
         L.call("ot_tsdf_reset_async", vol, s_)
@@ -68,7 +70,8 @@ def main():
     for _ in range(a.reps):
         step()
     torch.cuda.synchronize()
-    print(f"world {a.world} rank {a.rank} overlap {a.overlap}: {(time.perf_counter() - t0) * 1e3 / a.reps:.4f} ms/step")
+    print(f"world {a.world} rank {a.rank} overlap {a.overlap} fine {a.fine}: "
+          f"{(time.perf_counter() - t0) * 1e3 / a.reps:.4f} ms/step")
     step()  # the report's last repetition ends at this step's reset
     torch.cuda.synchronize()
     L.call("ot_tsdf_destroy", vol)
