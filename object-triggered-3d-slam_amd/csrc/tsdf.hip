@@ -514,10 +514,19 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
     // float32 ones otherwise
     __shared__ float s_r32[(FAST && !C64) ? RCP_N + 1 : 1];
     __shared__ double s_r64[(FAST && C64) ? RCP_N + 1 : 1];
+    // work item = (unit, part): the PARTS parts of a unit are items 8 apart, so they run on one XCD (blocks are dealt
+    // round-robin over the 8 XCDs) at about the same time and share its L2's copy of the footprint.
+    // The grid is sized for large batches (8x the resident workgroups): a workgroup without an item leaves before
+    // building the reciprocal table -- for a batch of few units (a spatial shard) the idle workgroups' tables had cost
+    // more than the integrate itself (r05e: a 1/8 shard's 64-frame batch 165-200 us whatever its slicing)
+    {
+        const int n0 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(wcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if ((int)blockIdx.x >= (PARTS == 1 ? n0 : ((n0 + 7) / 8) * 8 * PARTS)) return;
+    }
     if constexpr (FAST) {
-        for (int n = threadIdx.x; n <= RCP_N; n += 64 * INT_WG) {
-            if constexpr (C64) s_r64[n] = 1.0 / (double)n;  // IEEE (correctly rounded) quotients
-            else s_r32[n] = 1.0f / (float)n;
+        for (int r = threadIdx.x; r <= RCP_N; r += 64 * INT_WG) {
+            if constexpr (C64) s_r64[r] = 1.0 / (double)r;  // IEEE (correctly rounded) quotients
+            else s_r32[r] = 1.0f / (float)r;
         }
         __syncthreads();
     }
@@ -527,8 +536,6 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
     unsigned upd = 0;  // per lane: <= ZB voxels x 64 frames x units per workgroup, far below 2^32
     {
         const int b = blockIdx.x;
-        // work item = (unit, part): the PARTS parts of a unit are items 8 apart, so they run on one XCD (blocks
-        // are dealt round-robin over the 8 XCDs) at about the same time and share its L2's copy of the footprint
         const int items = PARTS == 1 ? n : ((n + 7) / 8) * 8 * PARTS;
         for (int it = b; it < items; it += gridDim.x) {
             const int u = PARTS == 1 ? it : (it / (8 * PARTS)) * 8 + (it & 7);
