@@ -196,7 +196,7 @@ struct ot_tsdf {
         hipEvent_t ev_units = nullptr;      // the set's units kernel (its integrate waits for it)
         hipEvent_t ev_done = nullptr;       // the set's integrate (the set's next front end waits for it)
     } bset[2];
-    int overlap_mode = -1;        // -1: on when sharded, 0 off, 1 on
+    int overlap_mode = -1;        // -1: on when sharded over >= 4 ranks, 0 off, 1 on
     int64_t last_batch_slots = -1;  // units the last batch touched (mailed): the next batch's integrate granularity
     int bset_next = 0;            // set of the next batch (alternates in overlap mode)
     int last_set = -1;            // set of the last batch whose integrate ran on istream (joined by readers)

@@ -1250,8 +1250,10 @@ struct BatchCtx {
 };
 static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stream);
 
+// auto (-1): from 4 shards on (r05f, rank 0 of the configs[1] scan: 1/4 shard 1.41 vs 1.56 ms per step, 1/8 1.08 vs
+// 1.16 ms; at 2 shards the co-running front end slows the larger integrate more than it hides: 2.22 vs 2.19 ms)
 static bool overlap_on(const ot_tsdf* vol) {
-    return vol->overlap_mode > 0 || (vol->overlap_mode < 0 && vol->dev.shard_world > 1);
+    return vol->overlap_mode > 0 || (vol->overlap_mode < 0 && vol->dev.shard_world >= 4);
 }
 static void* set_work(ot_tsdf* vol, int s) { return s == 0 ? vol->dev.work : vol->bset[1].work; }
 
@@ -1377,17 +1379,20 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
     const bool fast = !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
     bc.variant = (vol->color64 ? 2 : 0) + (fast ? 1 : 0);
-    // Few units (a spatial shard, a small object): a (unit, quarter) item is a chain of the batch's frames, ~60 us at 64
-    // frames whatever the unit count, so a batch with fewer items than ~3 rounds of resident workgroups is bound by
-    // that chain (r05c: a 1/8 shard's integrate 150-180 us per 64 frames against 720 / 8).  Such batches take twice
-    // the items of half the length (2 voxels per lane along z: the same per-voxel arithmetic, the same bits).  The
-    // unit count of a batch is known on the device only: the previous batch's (mailed) stands in for it, and a
-    // sharded volume's first batch counts as small from 4 ranks on.
+    // Few units (a spatial shard, a small object): a (unit, quarter) item is a chain of the batch's frames, each frame
+    // two dependent gather round trips plus ~270 dependent VALU instructions, so a batch too small to fill the GPU is
+    // bound by that chain -- ~130 us per 64 frames whatever the unit count (tools/shard_scaling.py, r05g: rank 0 of
+    // 16 / 32 / 64 shards 142 / 134 / 132 us).  Such batches take the fine slices (2 voxels per lane along z, twice
+    // the items, the next frame's gathers issued beside this frame's colour gathers: 107 / 90 / 85 us; the same
+    // per-voxel arithmetic, the same bits).  With a quarter of the GPU's resident workgroups in items or more the
+    // coarse slices are as fast or faster (1/8 shard 167 / 167 us, 1/4 242 / 280 us).  The unit count of a batch is
+    // known on the device only: the previous batch's (mailed) stands in for it, and a sharded volume's first batch
+    // counts as small from 16 ranks on.
     {
         const int resident = integrate_grid(bc.variant) / INT_GRID_MULT;
         const int64_t est = vol->last_batch_slots >= 0 ? vol->last_batch_slots
-                                                       : (vol->dev.shard_world >= 4 ? 0 : (int64_t)1 << 30);
-        const bool fine = g_int_fine > 0 || (g_int_fine < 0 && est * INT_PARTS < 3 * (int64_t)resident);
+                                                       : (vol->dev.shard_world >= 16 ? 0 : (int64_t)1 << 30);
+        const bool fine = g_int_fine > 0 || (g_int_fine < 0 && est * INT_PARTS * 4 < (int64_t)resident * 3);
         if (fine) bc.variant |= 4;
     }
     const int grid = integrate_grid(bc.variant);

@@ -69,7 +69,8 @@ class ScalableTSDFVolume:
             self._h = None
 
     def set_frontend_overlap(self, mode):
-        """Double-buffered batch front end (ot_tsdf_set_frontend_overlap): 1 on, 0 off, -1 (default) on when sharded.
+        """Double-buffered batch front end (ot_tsdf_set_frontend_overlap): 1 on, 0 off, -1 (default) on when the volume is
+        sharded over 4 or more ranks.
         Batch k+1's staging / touch run beside batch k's integrate; results are identical in every mode."""
         L.call("ot_tsdf_set_frontend_overlap", self._h, int(mode))
 
