@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
 }
 
 // Phases A and B of one frame for a lane's ZB voxels: the certified projections and the depth gathers (no voxel state
-// read) -- the fine slices' frame skew issues them for frame f+2 before frame f's updates (k_batch_integrate).  The same
+// read) -- the fine slices' frame skew issues them for frame f+1 before frame f's updates (k_batch_integrate).  The same
 // arithmetic as the phases inside the coarse loop.
 template <int ZB>
 __device__ __forceinline__ void frame_tap(const BatchFrame& fr, const IntegrateParams& p, int npx, float px, float py,
@@ -481,24 +481,6 @@ __device__ __forceinline__ void frame_tap(const BatchFrame& fr, const IntegrateP
     }
 }
 
-// Phase C of one frame for a lane's ZB voxels from its tap: the depth test and, for the lanes whose voxel updates, the
-// colour gather (no voxel state read) -- the fine slices' frame skew issues it for frame f+1 before frame f's updates.
-template <int ZB>
-__device__ __forceinline__ void frame_test(const BatchFrame& fr, const IntegrateParams& p, int npx,
-                                           const int (&pixv)[ZB], const float (&pcz)[ZB], const float (&dv)[ZB],
-                                           const float (&mv)[ZB], bool (&doitv)[ZB], float (&sdfv)[ZB],
-                                           uint32_t (&cv)[ZB]) {
-    const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
-    const bool use_color = fr.color != nullptr;
-#pragma unroll
-    for (int k = 0; k < ZB; ++k) {
-        sdfv[k] = (dv[k] - pcz[k]) * mv[k];
-        doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
-        cv[k] = 0u;
-        if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
-    }
-}
-
 // Occupancy: the integrate lives on it: 64 VGPRs, 8 waves per SIMD for both colour precisions with
 // quarter-unit workgroups (float64 colour at 5 / 6 / 8 waves: 0.426 / 0.428 / 0.414 ms per 32-frame launch; the IEEE-
 // division float64 kernel needs more registers and runs at 5).  Measured and settled: lanes whose voxel
@@ -522,7 +504,7 @@ constexpr int RCP_N = 2048;  // 16 KiB (float64) / 8 KiB (float32) of LDS per wo
 // every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes.
 template <bool C64, bool FAST, int ZB = BZ>
-__global__ __launch_bounds__(64 * INT_WG, ZB == 2 ? 4 : ((C64 && !FAST) ? 5 : INT_WAVES_PER_EU)) void k_batch_integrate(
+__global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
     const int* __restrict__ wcount) {
     using CT = typename std::conditional<C64, double, float>::type;
@@ -605,39 +587,35 @@ __global__ __launch_bounds__(64 * INT_WG, ZB == 2 ? 4 : ((C64 && !FAST) ? 5 : IN
                 const float pz = p.half + oz;
                 const unsigned upd0 = upd;
                 if constexpr (ZB == 2) {
-                    // Two-deep frame skew (the fine slices serve batches with few units, whose waves cannot hide a
-                    // frame's dependent gathers behind other waves): before frame f's updates each iteration issues
-                    // frame f+2's projections and depth gathers and frame f+1's depth test and colour gathers, so a
-                    // frame's two gather round trips overlap the updates of the two frames before it.  Taps and tests
-                    // read no voxel state: the updates (and every bit) are the unskewed loop's, in frame order.
+                    // Frame skew (the fine slices serve batches with few units, whose waves cannot hide a frame's
+                    // dependent gathers behind other waves): frame f's colour gathers and frame f+1's projections and
+                    // depth gathers are issued together, before frame f's updates -- one memory round trip per frame
+                    // on the wave's chain instead of two.  The taps read no voxel state, so the order of the updates
+                    // (and every bit) is the unskewed loop's.
                     unsigned long long m = mask;  // non-empty: a listed slot was touched by some frame of the batch
-                    int f0 = __ffsll((long long)m) - 1;
-                    m &= m - 1;
-                    int f1 = m ? __ffsll((long long)m) - 1 : -1;  // wave-uniform
-                    if (m) m &= m - 1;
-                    int pix1[ZB], pix2[ZB];
-                    float pcz1[ZB], dv1[ZB], mv1[ZB], pcz2[ZB], dv2[ZB], mv2[ZB];
-                    bool doit0[ZB], doit1[ZB];
-                    float sdf0[ZB], sdf1[ZB];
-                    uint32_t cv0[ZB], cv1[ZB];
-                    frame_tap<ZB>(frames[f0], p, npx, px, py, pz, z0, pix1, pcz1, dv1, mv1);
-                    frame_test<ZB>(frames[f0], p, npx, pix1, pcz1, dv1, mv1, doit0, sdf0, cv0);
-                    bool use0 = frames[f0].color != nullptr, use1 = false;
-                    if (f1 >= 0) frame_tap<ZB>(frames[f1], p, npx, px, py, pz, z0, pix1, pcz1, dv1, mv1);
+                    int f = __ffsll((long long)m) - 1;
+                    int pixv[ZB], pixv_n[ZB];
+                    float pcz[ZB], dv[ZB], mv[ZB], pcz_n[ZB], dv_n[ZB], mv_n[ZB];
+                    frame_tap<ZB>(frames[f], p, npx, px, py, pz, z0, pixv, pcz, dv, mv);
                     for (;;) {
-                        const int f2 = m ? __ffsll((long long)m) - 1 : -1;  // wave-uniform
-                        if (m) m &= m - 1;
-                        if (f2 >= 0) frame_tap<ZB>(frames[f2], p, npx, px, py, pz, z0, pix2, pcz2, dv2, mv2);
-                        if (f1 >= 0) {
-                            frame_test<ZB>(frames[f1], p, npx, pix1, pcz1, dv1, mv1, doit1, sdf1, cv1);
-                            use1 = frames[f1].color != nullptr;
-                        }
+                        m &= m - 1;
+                        const int fn = m ? __ffsll((long long)m) - 1 : -1;  // wave-uniform
+                        const BatchFrame& fr = frames[f];
+                        const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
+                        const bool use_color = fr.color != nullptr;
+                        // phase C: the depth test; colour gathered only by the lanes whose voxel updates
                         bool doitv[ZB];
                         float sdfv[ZB];
                         uint32_t cv[ZB];
 #pragma unroll
-                        for (int k = 0; k < ZB; ++k) doitv[k] = doit0[k], sdfv[k] = sdf0[k], cv[k] = cv0[k];
-                        const bool use_color = use0;
+                        for (int k = 0; k < ZB; ++k) {
+                            sdfv[k] = (dv[k] - pcz[k]) * mv[k];
+                            doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
+                            cv[k] = 0u;
+                            if (use_color && doitv[k])
+                                cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
+                        }
+                        if (fn >= 0) frame_tap<ZB>(frames[fn], p, npx, px, py, pz, z0, pixv_n, pcz_n, dv_n, mv_n);
                         // phase D: updates in frame order (select form: identical values, no exec-mask branches)
 #pragma unroll
                         for (int k = 0; k < ZB; ++k) {
@@ -694,13 +672,14 @@ __global__ __launch_bounds__(64 * INT_WG, ZB == 2 ? 4 : ((C64 && !FAST) ? 5 : IN
                             wt[k] = doit ? w1 : wv;
                             upd += doit ? 1u : 0u;
                         }
-                        if (f1 < 0) break;
-                        f1 = f2;
-                        use0 = use1;
+                        if (fn < 0) break;
+                        f = fn;
 #pragma unroll
                         for (int k = 0; k < ZB; ++k) {
-                            doit0[k] = doit1[k], sdf0[k] = sdf1[k], cv0[k] = cv1[k];
-                            pix1[k] = pix2[k], pcz1[k] = pcz2[k], dv1[k] = dv2[k], mv1[k] = mv2[k];
+                            pixv[k] = pixv_n[k];
+                            pcz[k] = pcz_n[k];
+                            dv[k] = dv_n[k];
+                            mv[k] = mv_n[k];
                         }
                     }
                 } else {
