@@ -16,11 +16,12 @@ timeout -k 10 400 python3 bench.py > gpurun_out/${T}_bench.log 2>&1 || { echo BE
 tail -1 gpurun_out/${T}_bench.log > gpurun_out/${T}_bench.json
 python3 -c "
 import json; d=json.load(open('gpurun_out/${T}_bench.json'))
-print('value', d['value'], 'ms/step', d['ms_per_step'], 'roofline', d['roofline'].get('frac'), d['roofline'].get('kernel_ms'))
+print('value', d['value'], 'ms/step', d['ms_per_step'], 'roofline', d['roofline'].get('frac'), d['roofline'].get('kernel_ms_avg'))
 print('filtered', d['filtered']['ms_per_frame'], 'objects', d['objects']['ms'], d['objects']['single_object_ms'], d['objects']['objects_over_single'])"
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof_h -o bench -- python3 bench.py \
-    --objects 0 --hybrid-objects 0 --filter-frames 0 --cpu-frames 0 > gpurun_out/${T}_bench_prof_h.log 2>&1 \
+    --objects 0 --hybrid-objects 0 --filter-frames 0 --cpu-frames 0 --sustain 0 --shard-steps 0 --color32 0 \
+    > gpurun_out/${T}_bench_prof_h.log 2>&1 \
     || { echo PROF_FAILED; tail -30 gpurun_out/${T}_bench_prof_h.log; exit 1; }
 tail -1 gpurun_out/${T}_bench_prof_h.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_fb_prof -o run -- python3 -u \
@@ -30,4 +31,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${T
     tools/single_object_trace.py > gpurun_out/${T}_obj_trace.log 2>&1 || { echo TRACE_FAILED; tail -20 gpurun_out/${T}_obj_trace.log; exit 1; }
 python3 tools/single_object_trace.py --report gpurun_out/${T}_obj_trace/run_kernel_trace.csv > gpurun_out/${T}_obj_timeline.txt 2>&1
 grep -E "single object|units" gpurun_out/${T}_obj_trace.log || true
+grep -E "k_batch_integrate|k_sor_knn<" gpurun_out/${T}_prof_h/*stats.csv gpurun_out/${T}_fb_prof/*stats.csv | cut -c1-200 || true
 echo DONE

@@ -28,9 +28,10 @@ BASE_CFG = {"voxel": 0.005, "frames": 256, "batch": 0}
 
 def short_name(full):
     base = full.split("(")[0].split("::")[-1]
-    if base.startswith("k_batch_integrate<"):  # <C64, FAST>: the reciprocal-table kernel keeps the bench's name
+    if base.startswith("k_batch_integrate<"):  # <C64, FAST, ZB>: the reciprocal-table coarse kernel keeps the bench's name
         args = [a.strip() for a in base[base.index("<") + 1:base.rindex(">")].split(",")]
-        return f"k_batch_integrate<{args[0]}>" + ("" if len(args) < 2 or args[1] == "true" else "[ieee]")
+        return f"k_batch_integrate<{args[0]}>" + ("" if len(args) < 2 or args[1] == "true" else "[ieee]") + \
+            ("[fine]" if len(args) > 2 and args[2] == "2" else "")
     return base.split("<")[0]
 
 

@@ -8,7 +8,7 @@
 # Output: gpurun_out/pmc_<w>_<i>/ and profiles/pmc_traffic.json (tagged with the source hash of this build).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
-HEAD_ARGS="--steps 2 --warmup 1 --sustain 0 --cpu-frames 0 --filter-frames 0 --objects 0 --hybrid-objects 0 --color32 0"
+HEAD_ARGS="--steps 2 --warmup 1 --sustain 0 --cpu-frames 0 --filter-frames 0 --objects 0 --hybrid-objects 0 --color32 0 --shard-steps 0"
 FILT_ARGS="--frames 128 --batches 64 --reps 1"  # the bench times 64-frame batches (--filter-batch 64)
 TRAFFIC=("FETCH_SIZE" "WRITE_SIZE")
 DIAG=("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES"
