@@ -141,6 +141,8 @@ TEST_SIGNATURES = {
     "otx_unit_sort_radix": [_i32],
     "otx_sor_netfill": [_i32],
     "otx_integrate_fine": [_i32],
+    "otx_mc_emit_fork": [_i32],
+    "otx_normals_at": [_i32],
     "otx_sampler_hi_stream": [_i32],
     "otx_sort_pairs_u64_u32": [_p, _p, _p, _p, _i64, _i32, _p],
     "otx_sort_segments_u32_u32": [_p, _p, _p, _p, _p, _i32, _i32, _p],

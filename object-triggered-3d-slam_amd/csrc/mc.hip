@@ -243,10 +243,10 @@ __device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z
     }
 }
 
-__global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, double vl, double* V, double* VC) {
-    const int r = blockIdx.x;
+// one unit's vertices (rank r): one lane per edge-bitmask word w
+__device__ __forceinline__ void mc_vertices_unit(const TsdfDev& d, const McDev& m, double vl, double* V, double* VC,
+                                                 int r, int w) {
     const int id = (int)m.sorted_ids[r];
-    const int w = threadIdx.x;
     unsigned bits = m.eflags[(size_t)id * EWORDS + w];
     if (!bits) return;
     long long vid = m.vert_base[r] + m.wprefix[(size_t)id * EWORDS + w];
@@ -307,12 +307,11 @@ __device__ inline int edge_vid(const McDev& m, const int* snbr, const long long*
     return (int)(sbase[o] + m.wprefix[(size_t)owner * EWORDS + word] + __popc(below));
 }
 
-__global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_t* T) {
+// one unit's triangles (rank r): 256 lanes, one (x, y) column of 16 cubes each
+__device__ __forceinline__ void mc_triangles_unit(const TsdfDev& d, const McDev& m, int32_t* T, int r, int t) {
     __shared__ int snbr[8];
     __shared__ long long sbase[8];
-    const int r = blockIdx.x;
     const int id = (int)m.sorted_ids[r];
-    const int t = threadIdx.x;
     const int ukey[3] = {d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]};
     if (t < 8) {
         const int o = m.nbr[id * 16 + t];
@@ -361,6 +360,26 @@ __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_
             }
             ++out;
         }
+    }
+}
+
+__global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, double vl, double* V, double* VC) {
+    mc_vertices_unit(d, m, vl, V, VC, blockIdx.x, threadIdx.x);
+}
+__global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_t* T) {
+    mc_triangles_unit(d, m, T, blockIdx.x, threadIdx.x);
+}
+// The emission in ONE launch: workgroups [0, U) the triangles (their upper 128 lanes leave at once; a barrier counts
+// only the waves still running), [U, 2U) the vertices.  Replaces the vertices on the side stream beside the triangles:
+// that fork and join cost the GPU ~25 us of idle queue time per extraction (tools/event_gap.hip, r05j)
+__global__ __launch_bounds__(EWORDS) void k_mc_emit(TsdfDev d, McDev m, int U, double vl, double* V, double* VC,
+                                                    int32_t* T) {
+    const int b = blockIdx.x;
+    if (b < U) {
+        if (threadIdx.x >= 256) return;
+        mc_triangles_unit(d, m, T, b, threadIdx.x);
+    } else {
+        mc_vertices_unit(d, m, vl, V, VC, b - U, threadIdx.x);
     }
 }
 
@@ -460,10 +479,12 @@ __global__ __launch_bounds__(256) void k_mc_vnormals(TsdfDev d, McDev m, int64_t
 // the extraction's two exclusive scans (triangle and vertex counts per unit, U of each) in one launch: block 0 scans
 // the triangle counts, block 1 the vertex counts, 4096 per round (4 consecutive per thread) with a carried total --
 // one ~5 us launch instead of a library scan's two launches per array (U is a few thousand units).  Each block mails
-// its array's total (triangles, vertices) to the volume's pinned mailbox: the host's read-back needs no launch of its own
+// its array's total (triangles, vertices) to the volume's pinned mailbox, then `seq` to its sequence word (seqw[block]):
+// the host spins on those (mail_wait), with no launch or event of its own
 __global__ __launch_bounds__(1024) void k_mc_scan2(const long long* __restrict__ c0, long long* __restrict__ b0,
                                                   const long long* __restrict__ c1, long long* __restrict__ b1,
-                                                  int n, long long* __restrict__ totals) {
+                                                  int n, long long* __restrict__ totals, unsigned* __restrict__ seqw,
+                                                  unsigned seq) {
     const long long* in = blockIdx.x ? c1 : c0;
     long long* out = blockIdx.x ? b1 : b0;
     __shared__ long long wsum[16];
@@ -502,10 +523,18 @@ __global__ __launch_bounds__(1024) void k_mc_scan2(const long long* __restrict__
         if (t == 0) s_carry += tot;
         __syncthreads();
     }
-    if (t == 0) totals[blockIdx.x] = s_carry;
+    if (t == 0) {
+        totals[blockIdx.x] = s_carry;
+        __threadfence_system();  // the total reaches the host before the sequence word
+        __hip_atomic_store(seqw + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 static std::atomic<bool> g_tables_uploaded{false};
+static bool g_mc_emit_fork = false;  // test hook otx_mc_emit_fork: the two-stream emission (round 4) for A/B timing
+// ot_tsdf_extract_sample_min_z: where the vertex normals may start -- 0 right after the emission, 1 beside the area-sum
+// walk, 2 beside the CDF walk (test hook otx_normals_at)
+static int g_normals_at = 2;
 static std::mutex g_tables_mutex;
 
 static ot_status upload_tables() {  // once per process (one process per GPU), safe from concurrent host threads
@@ -594,19 +623,20 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
     OT_LAUNCH_CHECK();
     if (U > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] too many units");
     // the scans mail the triangle and vertex totals (hmail words 0..3)
+    const unsigned seq = ++vol->mc_seq;
     hipLaunchKernelGGL(k_mc_scan2, dim3(2), dim3(1024), 0, stream, (const long long*)m.tri_cnt, m.tri_base,
-                       (const long long*)m.vert_cnt, m.vert_base, (int)U, (long long*)vol->hmail);
+                       (const long long*)m.vert_cnt, m.vert_base, (int)U, (long long*)vol->hmail,
+                       vol->hmail + MAIL_SEQ_MC, seq);
     OT_LAUNCH_CHECK();
     mb.ws_units = U;
     if (spec) {  // the host waits for the read-back only, the speculative work runs behind it
-        if (!vol->ev_mail) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_mail, hipEventDisableTiming));
-        OT_HIP_TRY(hipEventRecord(vol->ev_mail, stream));
         st = spec(m);
         if (st != OT_OK) return st;
-        OT_HIP_TRY(hipEventSynchronize(vol->ev_mail));
-    } else {
-        OT_HIP_TRY(hipStreamSynchronize(stream));
     }
+    // the totals' sequence words, not an event: an event between the scans and the emission idles the GPU (tsdf.h)
+    st = mail_wait(vol->hmail + MAIL_SEQ_MC, seq, stream);
+    if (st == OT_OK) st = mail_wait(vol->hmail + MAIL_SEQ_MC + 1, seq, stream);
+    if (st != OT_OK) return st;
     long long totals[2];
     std::memcpy(totals, vol->hmail, sizeof(totals));
     const int64_t nt = totals[0], nv = totals[1];
@@ -653,18 +683,24 @@ static ot_status mc_emit_launch(ot_tsdf* vol, McDev m, int64_t nv, double* V, do
     const unsigned g = (unsigned)vol->mesh.ws_units;
     ot_status st = wait_normals(vol, stream);  // the emission rewrites vk / vown, which deferred normals read
     if (st != OT_OK) return st;
-    if (!vol->side) {
+    if (g_mc_emit_fork && !vol->side) {
         OT_HIP_TRY(hipStreamCreateWithFlags(&vol->side, hipStreamNonBlocking));
         OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_fork, hipEventDisableTiming));
         OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_join, hipEventDisableTiming));
     }
-    OT_HIP_TRY(hipEventRecord(vol->ev_fork, stream));
-    OT_HIP_TRY(hipStreamWaitEvent(vol->side, vol->ev_fork, 0));
-    hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, vol->side, vol->dev, m, vol->voxel_length, V,
-                       vol->color_type == OT_COLOR_RGB8 ? VC : nullptr);
-    OT_HIP_TRY(hipEventRecord(vol->ev_join, vol->side));
-    hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, T);
-    OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_join, 0));
+    double* vc = vol->color_type == OT_COLOR_RGB8 ? VC : nullptr;
+    if (g_mc_emit_fork) {
+        OT_HIP_TRY(hipEventRecord(vol->ev_fork, stream));
+        OT_HIP_TRY(hipStreamWaitEvent(vol->side, vol->ev_fork, 0));
+        hipLaunchKernelGGL(k_mc_vertices, dim3(g), dim3(EWORDS), 0, vol->side, vol->dev, m, vol->voxel_length, V, vc);
+        OT_HIP_TRY(hipEventRecord(vol->ev_join, vol->side));
+        hipLaunchKernelGGL(k_mc_triangles, dim3(g), dim3(256), 0, stream, vol->dev, m, T);
+        OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_join, 0));
+    } else {
+        if (g > 0x3FFFFFFFu) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] too many units");
+        hipLaunchKernelGGL(k_mc_emit, dim3(2 * g), dim3(EWORDS), 0, stream, vol->dev, m, (int)g, vol->voxel_length, V,
+                           vc, T);
+    }
     OT_LAUNCH_CHECK();
     if (VC && vol->color_type != OT_COLOR_RGB8)
         OT_HIP_TRY(hipMemsetAsync(VC, 0, sizeof(double) * 3 * (size_t)std::min<int64_t>(nv, m.cap_v), stream));
@@ -798,11 +834,15 @@ ot_status ot_tsdf_extract_sample_min_z(ot_tsdf* vol, double* vertices, double* v
     const int64_t nv = *n_vertices, nt = *n_triangles;
     if (nv == 0 || nt == 0) return OT_OK;
     if (!vol->ev_made) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_made, hipEventDisableTiming));
-    OT_HIP_TRY(hipEventRecord(vol->ev_made, stream));  // the mesh arrays are complete here
+    // ev_made: the mesh arrays are complete (the normals wait on it).  Recorded where the normals cost the sampling
+    // least: not right after the emission -- there they took the CUs from the chains' wide first passes (bsum, guess,
+    // chunk, runs: 33 -> 66 us, r05k) -- but just before one of its single-wave walks (g_normals_at)
+    const int at = vertex_normals ? g_normals_at : 0;
+    if (vertex_normals && at == 0) OT_HIP_TRY(hipEventRecord(vol->ev_made, stream));
     ot_mesh_sample_job job{vertices, nullptr, out_rgb ? vertex_colors : nullptr, nv, triangles, nt, out_xyz, nullptr,
                            out_rgb};
     hipStream_t hs = nullptr;
-    st = sample_min_z_enqueue(&job, 1, n_points, seed, z_min, stream, &hs);
+    st = sample_min_z_enqueue(&job, 1, n_points, seed, z_min, stream, &hs, at ? vol->ev_made : nullptr, at);
     if (st != OT_OK) return st;
     if (vertex_normals) {  // queued once the sampling is (its chains' first passes are dispatched ahead of them)
         hipStream_t ns = S(normals_stream);
@@ -839,6 +879,19 @@ ot_status ot_tsdf_fetch_triangle_mesh(ot_tsdf* vol, double* vertices, double* ve
     }
     if (mb.nt > 0 && triangles)
         OT_HIP_TRY(hipMemcpyAsync(triangles, mb.t, sizeof(int32_t) * 3 * mb.nt, hipMemcpyDefault, stream));
+    return OT_OK;
+}
+
+// test hook: where ot_tsdf_extract_sample_min_z lets the vertex normals start (0 / 1 / 2, g_normals_at)
+ot_status otx_normals_at(int32_t at) {
+    if (at < 0 || at > 2) return fail(OT_ERR_INVALID_ARGUMENT, "otx_normals_at: 0, 1 or 2");
+    g_normals_at = at;
+    return OT_OK;
+}
+
+// test hook: 1 = the emission as two kernels on two streams (fork / join by events), 0 = one launch (default)
+ot_status otx_mc_emit_fork(int32_t on) {
+    g_mc_emit_fork = on != 0;
     return OT_OK;
 }
 

@@ -698,7 +698,10 @@ __global__ __launch_bounds__(256) void k_chain_emit(const ChainJob* __restrict__
 // prologue (true): chunk sums, binade guesses, integer chunk sums and flags; false: the caller produced those
 // (k_chain_cdf_prep)
 template <bool CDF>
-void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream, bool prologue = true) {
+// mark (nullable): recorded on `stream` just before the walk -- a single wave per chain, the rest of the GPU idle --
+// for work on another stream to start beside it (the fused extraction's vertex normals)
+void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream, bool prologue = true,
+                   hipEvent_t mark = nullptr) {
     const int64_t nb = (max_n + CH - 1) / CH;
     const dim3 grid((unsigned)((nb + 3) / 4), (unsigned)n_jobs);
     if (prologue) {
@@ -707,6 +710,7 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
         hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
     }
     hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
+    if (mark) (void)hipEventRecord(mark, stream);  // (a failure is the thread's last error: the caller's launch check)
     // metadata staged in LDS when every job's chunks fit (max_n bounds them all)
     if (nb <= WALK_LDS_CHUNKS) {
         const size_t lds_bytes = (size_t)nb * 17 + 16;
@@ -1041,7 +1045,7 @@ static ot_status hi_stream_fork(hipStream_t caller, hipStream_t* out) {
 static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, size_t extra, size_t upload,
                              const std::function<void(char*, char*)>& fill, size_t zero_off, size_t zero_bytes,
                              hipStream_t stream, std::vector<double*>& cdf, std::vector<long long*>& ncum,
-                             char** extra_dev) {
+                             char** extra_dev, hipEvent_t mark = nullptr, int mark_at = 0) {
     if (g_minz.active) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
     size_t bytes = 256;
     int64_t max_nt = 0;
@@ -1107,11 +1111,11 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
                                cdf[j]);
         }
     }
-    launch_chains<false>(djobs, n_jobs, max_nt, stream);
+    launch_chains<false>(djobs, n_jobs, max_nt, stream, true, mark_at == 1 ? mark : nullptr);
     const int64_t max_nb = (max_nt + CH - 1) / CH;
     hipLaunchKernelGGL(k_chain_cdf_prep, dim3((unsigned)((max_nb + 3) / 4), (unsigned)n_jobs), dim3(256), 0, stream,
                        (const ChainJob*)djobs, (const ChainJob*)(djobs + n_jobs));
-    launch_chains<true>(djobs + n_jobs, n_jobs, max_nt, stream, false);
+    launch_chains<true>(djobs + n_jobs, n_jobs, max_nt, stream, false, mark_at == 2 ? mark : nullptr);
     OT_LAUNCH_CHECK();
     return OT_OK;
 }
@@ -1154,7 +1158,8 @@ namespace ot {
 // The fused sampler's launches (on the caller's stream); the kept counts land in pinned slot 1 once it drains.  *hs:
 // the stream to wait on.
 static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
-                               double z_min, void* stream_, hipStream_t* hs) {
+                               double z_min, void* stream_, hipStream_t* hs, hipEvent_t mark = nullptr,
+                               int mark_at = 0) {
     hipStream_t stream = S(stream_);
     if (g_sampler_hi) {
         ot_status fst = hi_stream_fork(S(stream_), &stream);
@@ -1193,7 +1198,7 @@ static ot_status min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, i
     for (int j = 0; j < n_jobs; ++j)
         if (jobs[j].n_triangles > 0x7FFFFFFF) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] too many triangles");
     ot_status st = sample_cdfs(jobs, n_jobs, total, up_bytes, fill, zero_off, zero_end - zero_off, stream, cdf, ncum,
-                               &extra);
+                               &extra, mark, mark_at);
     if (st != OT_OK) return st;
     const MinZJob* djobs = (const MinZJob*)extra;
     const double* const* dcdf = (const double* const*)(djobs + n_jobs);
@@ -1219,9 +1224,9 @@ static ot_status min_z_wait(hipStream_t hs, int32_t n_jobs, int64_t* n_kept_host
 }
 // the fused extraction + sampling of one volume (mc.hip ot_tsdf_extract_sample_min_z) drives the same two phases
 ot_status sample_min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
-                               double z_min, hipStream_t stream, hipStream_t* hs) {
+                               double z_min, hipStream_t stream, hipStream_t* hs, hipEvent_t mark, int mark_at) {
     if (g_minz.active) return fail(OT_ERR_INVALID_ARGUMENT, "[SamplePointsUniformly] an async sampling is pending");
-    return min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, (void*)stream, hs);
+    return min_z_enqueue(jobs, n_jobs, n_points, seed, z_min, (void*)stream, hs, mark, mark_at);
 }
 ot_status sample_min_z_wait(hipStream_t hs, int32_t n_jobs, int64_t* n_kept_host) {
     return min_z_wait(hs, n_jobs, n_kept_host);

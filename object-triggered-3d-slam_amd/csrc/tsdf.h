@@ -108,6 +108,10 @@ __host__ __device__ inline void border_voxel(int b, int& x, int& y, int& z) {
 
 constexpr int MAX_BATCH = 64;      // frames per fused launch (one bit each in fmask)
 constexpr int OT_MAIL_WORDS = 64;  // capacity of the pinned host mailbox (4-B words per read-back, mail_words)
+// sequence words of the kernels that mail on their own (mail_wait): the marching-cubes scans (words 62, 63: one per
+// scan block) and the units kernel's counters (the last word of the second half)
+constexpr int MAIL_SEQ_MC = OT_MAIL_WORDS - 2;
+constexpr int MAIL_SEQ_UNITS = 2 * OT_MAIL_WORDS - 1;
 
 // per-frame parameters of a batch (device resident)
 struct BatchFrame {
@@ -174,14 +178,17 @@ struct ot_tsdf {
     ot::BatchFrame* hbframes = nullptr;    // pinned host staging [2][MAX_BATCH]
     unsigned* hmail = nullptr;             // pinned coherent host mailbox [OT_MAIL_WORDS]: small read-backs stored
                                            // by a one-wave kernel (mail_words) instead of staged D2H copies
-    hipEvent_t hb_event[2] = {nullptr, nullptr};
+    // staging half of the next batch; a batch's parameter copy has run once its units kernel has mailed (settle_batch
+    // waits for that before integrate_batch returns), so the halves need no event
     int hb_next = 0;
     // the counters as the last batch's units kernel left them (the integrate does not change them), mailed by its last
-    // workgroup to hmail + OT_MAIL_WORDS: an extraction reads the unit count behind `ev_early` instead of waiting for
-    // the integrate (valid while early_frame == frame_id, no reset or import since)
-    hipEvent_t ev_early = nullptr;
+    // workgroup to hmail + OT_MAIL_WORDS, then sequence number `units_seq` to word MAIL_SEQ_UNITS: the host spins on
+    // that word (mail_wait) instead of an event behind the units kernel -- an event recorded between two kernels of a
+    // stream idles the GPU ~4 us (tools/event_gap.hip, r05j) -- and an extraction reads the unit count without waiting
+    // for the integrate (valid while early_frame == frame_id, no reset or import since)
+    unsigned units_seq = 0;
     int early_frame = -1;
-    hipEvent_t ev_mail = nullptr;  // behind a mailbox read-back that work queued after it must not delay
+    unsigned mc_seq = 0;  // the marching-cubes totals' sequence number (words MAIL_SEQ_MC, MAIL_SEQ_MC + 1)
     int batch_pc = ot::C_BATCH_PAIRS;      // pair counter of the next batch (alternates 4, 5)
     // A batch's staging: per-frame parameters, packed (depth, multiplier) and colour per pixel, and the unit work list.
     // Two sets: with the front end double-buffered (overlap, ot_tsdf_set_frontend_overlap: on by default for a spatially
@@ -236,13 +243,18 @@ struct MailSrc {
     int n;
 };
 ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream);
+// spin until a kernel on `stream` stores `seq` to the mailbox word (system-scope release after its mailed values); the
+// stream is polled now and then, so a fault or a drained stream without the mail ends the wait with an error
+ot_status mail_wait(const unsigned* word, unsigned seq, hipStream_t stream);
 // integrate the queued frames; readers (join = true) also order `stream` after the last batch's integrate when it ran on
 // the volume's integrate stream (double-buffered front end)
 ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream, bool join = true);
 // order `stream` after the volume's deferred vertex normals, if any are still in flight
 ot_status wait_normals(ot_tsdf* vol, hipStream_t stream);
-// the fused sampler's two phases (mesh_ops.hip): queue the chains + emission on `stream`, then wait for the kept counts
+// the fused sampler's two phases (mesh_ops.hip): queue the chains + emission on `stream`, then wait for the kept counts.
+// mark (nullable) is recorded on `stream` just before the area-sum walk (mark_at 1) or the CDF walk (mark_at 2)
 ot_status sample_min_z_enqueue(const ot_mesh_sample_job* jobs, int32_t n_jobs, int64_t n_points, uint64_t seed,
-                               double z_min, hipStream_t stream, hipStream_t* hs);
+                               double z_min, hipStream_t stream, hipStream_t* hs, hipEvent_t mark = nullptr,
+                               int mark_at = 0);
 ot_status sample_min_z_wait(hipStream_t hs, int32_t n_jobs, int64_t* n_kept_host);
 }  // namespace ot

@@ -368,8 +368,10 @@ template <bool REPLAY>
 // wcount: where the integrate reads the batch's work-list length (the pair counter itself, or -- with the front end
 // double-buffered -- a per-set copy, since the next batch's units kernel zeroes the other pair counter while this
 // batch's integrate may still run)
+// early_mail: hmail + OT_MAIL_WORDS; its last word (MAIL_SEQ_UNITS) receives `seq` once the counters are stored
 __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __restrict__ work, int pc,
-                                                     unsigned* __restrict__ early_mail, int* __restrict__ wcount) {
+                                                     unsigned* __restrict__ early_mail, int* __restrict__ wcount,
+                                                     unsigned seq) {
     __shared__ unsigned long long red[4];
     const int n = d.counters[pc];
     // the other counter belongs to the next batch; the previous batch's integrate (its last reader) has finished
@@ -422,10 +424,16 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
         s_last = atomicAdd(&d.counters[C_UNITS_DONE], 1) == (int)gridDim.x - 1;
     }
     __syncthreads();
-    if (s_last && threadIdx.x < N_COUNTERS) {  // every workgroup's counter atomics are done: mail the final values
-        const int v = __hip_atomic_load(&d.counters[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        early_mail[threadIdx.x] = threadIdx.x == C_UNITS_DONE ? 0u : (unsigned)v;
-        if (threadIdx.x == C_UNITS_DONE) d.counters[C_UNITS_DONE] = 0;
+    if (s_last && threadIdx.x < 64) {  // every workgroup's counter atomics are done: wave 0 mails the final values
+        if (threadIdx.x < N_COUNTERS) {
+            const int v = __hip_atomic_load(&d.counters[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            early_mail[threadIdx.x] = threadIdx.x == C_UNITS_DONE ? 0u : (unsigned)v;
+            if (threadIdx.x == C_UNITS_DONE) d.counters[C_UNITS_DONE] = 0;
+        }
+        __threadfence_system();  // the values reach the host before the sequence word
+        if (threadIdx.x == 0)
+            __hip_atomic_store(early_mail + (MAIL_SEQ_UNITS - OT_MAIL_WORDS), seq, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1311,9 +1319,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         bs.cap = cap;
     }
     // per-frame parameters: pinned host staging (double-buffered, event-guarded) -> device
-    const int hb = vol->hb_next;
+    const int hb = vol->hb_next;  // (the last batch from this half was copied: settle_batch saw its units kernel mail)
     vol->hb_next ^= 1;
-    if (vol->hb_event[hb]) OT_HIP_TRY(hipEventSynchronize(vol->hb_event[hb]));
     BatchFrame* host = vol->hbframes + hb * MAX_BATCH;
     BatchCtx bc;
     bc.ip0 = make_integrate_params(vol, nullptr, nullptr, vol->mult, &in, frames[0].extrinsic);
@@ -1338,8 +1345,6 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         b.trunc = f.depth_trunc;
     }
     OT_HIP_TRY(hipMemcpyAsync(bs.bframes, host, sizeof(BatchFrame) * n, hipMemcpyHostToDevice, stream));
-    if (!vol->hb_event[hb]) OT_HIP_TRY(hipEventCreateWithFlags(&vol->hb_event[hb], hipEventDisableTiming));
-    OT_HIP_TRY(hipEventRecord(vol->hb_event[hb], stream));
     // this batch's pair counter: zeroed by reset, or by the previous batch's k_batch_units (no memset here)
     const int pc = vol->batch_pc;
     BatchTouchParams& tp = bc.tp;
@@ -1372,9 +1377,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     hipLaunchKernelGGL(k_batch_touch<false>, dim3(bc.tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
                        (const BatchFrame*)bs.bframes, tp, vol->dev, n);
     hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, work, pc,
-                       vol->hmail + OT_MAIL_WORDS, ovl ? wcount : (int*)nullptr);
-    if (!vol->ev_early) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_early, hipEventDisableTiming));
-    OT_HIP_TRY(hipEventRecord(vol->ev_early, stream));
+                       vol->hmail + OT_MAIL_WORDS, ovl ? wcount : (int*)nullptr, ++vol->units_seq);
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
     const bool fast = !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
@@ -1429,7 +1432,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     }
     vol->frame_id += n;
     vol->sorted_frame = -1;
-    vol->early_frame = vol->frame_id;  // the mailed counters are final for this frame count (see ev_early)
+    vol->early_frame = vol->frame_id;  // the mailed counters are final for this frame count (see units_seq)
     return settle_batch(vol, bc, stream);
 }
 
@@ -1514,8 +1517,8 @@ static ot_status grow_pool(ot_tsdf* vol, int64_t need, int n_used, hipStream_t s
     return OT_OK;
 }
 
-// After each batch: the counters its units kernel mailed (behind ev_early: the host waits for the units kernel, not for
-// the integrate queued behind it, so the GPU keeps its queue).  Units the pool could not hold (C_OVERFLOW), or keys the
+// After each batch: the counters its units kernel mailed (mail_wait on units_seq: the host waits for the units kernel,
+// not for the integrate queued behind it, so the GPU keeps its queue).  Units the pool could not hold (C_OVERFLOW), or keys the
 // hash could not hold (C_HASHERR bit 0), were skipped by the batch's integrate: grow, then replay the batch for exactly
 // those units -- touch again from the staged depths (still resident: the next batch has not been staged yet), allocate
 // the missing units (units that have an id were integrated and are skipped), integrate them with the batch's frames.
@@ -1523,7 +1526,8 @@ static ot_status grow_pool(ot_tsdf* vol, int64_t need, int n_used, hipStream_t s
 // A pool more than 3/4 full also grows here, ahead of need.
 static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stream) {
     for (int round = 0;; ++round) {
-        OT_HIP_TRY(hipEventSynchronize(vol->ev_early));
+        ot_status ws = mail_wait(vol->hmail + MAIL_SEQ_UNITS, vol->units_seq, stream);
+        if (ws != OT_OK) return ws;
         int c[N_COUNTERS];
         std::memcpy(c, vol->hmail + OT_MAIL_WORDS, sizeof(c));
         vol->last_batch_slots = c[bc.pc];  // units the batch touched: the next batch's item estimate
@@ -1554,8 +1558,7 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
         hipLaunchKernelGGL(k_batch_touch<true>, dim3(bc.tiles, (unsigned)((bc.n + TF - 1) / TF)), dim3(256), 0, stream,
                            bf, tp, vol->dev, bc.n);
         hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
-                           vol->hmail + OT_MAIL_WORDS, (int*)nullptr);
-        OT_HIP_TRY(hipEventRecord(vol->ev_early, stream));
+                           vol->hmail + OT_MAIL_WORDS, (int*)nullptr, ++vol->units_seq);
         const UnitWork* uw = work;
         const int* wc = vol->dev.counters + bc.pc;
         void* args[] = {(void*)&bf, (void*)&bc.ip0, (void*)&vol->dev, (void*)&uw, (void*)&wc};
@@ -1623,11 +1626,26 @@ __global__ void k_mail_words(MailSrc s, unsigned* __restrict__ out) {
 }
 
 ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
-    if (s.n > OT_MAIL_WORDS) return fail(OT_ERR_INVALID_ARGUMENT, "mailbox overflow");
+    if (s.n > MAIL_SEQ_MC) return fail(OT_ERR_INVALID_ARGUMENT, "mailbox overflow");
     hipLaunchKernelGGL(k_mail_words, dim3(1), dim3(64), 0, stream, s, vol->hmail);
     OT_LAUNCH_CHECK();
     OT_HIP_TRY(hipStreamSynchronize(stream));
     return OT_OK;
+}
+
+ot_status mail_wait(const unsigned* word, unsigned seq, hipStream_t stream) {
+    for (unsigned it = 1;; ++it) {
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return OT_OK;
+        if ((it & 1023u) == 0) {  // every ~10-50 us: has the stream faulted, or drained without the mail?
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return OT_OK;
+                return fail(OT_ERR_HIP, "mailbox: the stream drained without the kernel's mail");
+            }
+            if (q != hipErrorNotReady) OT_HIP_TRY(q);
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 static ot_status check_errors(ot_tsdf* vol, hipStream_t stream) {
@@ -1644,9 +1662,10 @@ ot_status tsdf_sorted_units(ot_tsdf* vol, hipStream_t stream, int64_t* n_units) 
     ot_status st = tsdf_flush(vol, stream);
     if (st != OT_OK) return st;
     int c[N_COUNTERS];  // error flags and the unit count in one read-back (the pinned mailbox)
-    if (vol->early_frame == vol->frame_id && !vol->imported && vol->ev_early) {
-        // mailed by the last batch's units kernel: wait for that kernel only, not for the integrate behind it
-        OT_HIP_TRY(hipEventSynchronize(vol->ev_early));
+    if (vol->early_frame == vol->frame_id && !vol->imported && vol->units_seq != 0) {
+        // mailed by the last batch's units kernel (settle_batch saw it): not waiting for the integrate behind it
+        st = mail_wait(vol->hmail + MAIL_SEQ_UNITS, vol->units_seq, stream);
+        if (st != OT_OK) return st;
         std::memcpy(c, vol->hmail + OT_MAIL_WORDS, sizeof(c));
     } else {
         MailSrc ms;
@@ -1770,6 +1789,7 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
         return cleanup(e);
     if ((e = hipHostMalloc(&v->hmail, sizeof(unsigned) * 2 * OT_MAIL_WORDS, hipHostMallocCoherent)) != hipSuccess)
         return cleanup(e);
+    std::memset(v->hmail, 0, sizeof(unsigned) * 2 * OT_MAIL_WORDS);  // sequence words start below every seq sent (>= 1)
     ot_status st = ot_tsdf_reset(v);
     if (st != OT_OK) {
         ot_tsdf_destroy(v);
@@ -1793,8 +1813,6 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     if (v->hbframes) (void)hipHostFree(v->hbframes);
     if (v->hmail) (void)hipHostFree(v->hmail);
     if (v->ev_fork) (void)hipEventDestroy(v->ev_fork);
-    if (v->ev_early) (void)hipEventDestroy(v->ev_early);
-    if (v->ev_mail) (void)hipEventDestroy(v->ev_mail);
     if (v->ev_join) (void)hipEventDestroy(v->ev_join);
     if (v->ev_normals) (void)hipEventDestroy(v->ev_normals);
     if (v->ev_made) (void)hipEventDestroy(v->ev_made);
@@ -1804,8 +1822,6 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
         if (b.ev_units) (void)hipEventDestroy(b.ev_units);
         if (b.ev_done) (void)hipEventDestroy(b.ev_done);
     }
-    for (hipEvent_t ev : v->hb_event)
-        if (ev) (void)hipEventDestroy(ev);
     delete v;
     return OT_OK;
 }

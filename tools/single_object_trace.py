@@ -5,6 +5,9 @@ the last repetition (durations and the idle gaps between kernels).  Tool only.
   rocprofv3 --kernel-trace --output-format csv -d DIR -o run -- python3 tools/single_object_trace.py
   python3 tools/single_object_trace.py --report DIR/run_kernel_trace.csv
   python3 tools/single_object_trace.py --separate     (the facade's separate extract / normals / sample calls)
+  python3 tools/single_object_trace.py --normals-at N (A/B: the normals start after the emission (0), beside the
+                                                       area-sum walk (1) or the CDF walk (2, default))
+  python3 tools/single_object_trace.py --fork         (A/B: the marching-cubes emission as two kernels on two streams)
   python3 tools/single_object_trace.py --no-normals   (diagnostic: the same object without compute_vertex_normals, i.e.
                                                        what the normals' side-stream kernel costs the critical path)
 """
@@ -21,6 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PKG = "object-triggered-3d-slam_amd"
 REPS = 8
+AFTER_PASSES = 6 + 6 + 6 + 1  # volume resets after the timed repetitions (see main)
 
 
 def report(path):
@@ -29,10 +33,13 @@ def report(path):
         for r in csv.DictReader(fh):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], int(r.get("Stream_Id", 0) or 0)))
     rows.sort()
-    # every repetition starts with the volume reset (k_tsdf_clear); the statistics pass after the timed repetitions
-    # starts with one too: the last timed repetition lies between the last two
+    # every repetition starts with the volume reset (k_tsdf_clear), and so does every pass of main()'s later loops (6
+    # host-timing passes of the timed sequence, 6 of the separate calls, 6 host-breakdown passes of the separate calls,
+    # the final statistics pass): the last timed
+    # repetition (the path bench.py times) lies between the 20th- and 19th-last clears
     clears = [i for i, r in enumerate(rows) if "k_tsdf_clear" in r[2]]
-    last = rows[clears[-2]:clears[-1]] if len(clears) >= 2 else rows[len(rows) - len(rows) // REPS:]
+    after = AFTER_PASSES
+    last = rows[clears[-after - 1]:clears[-after]]
     t0 = last[0][0]
     busy = {}
     prev_end = t0
@@ -59,6 +66,10 @@ def main(normals=True):
     lib = L.load()
     if "--hi" in sys.argv:  # A/B: the fused sampler on a greatest-priority stream, as before late round 4
         L.call("otx_sampler_hi_stream", 1)
+    if "--normals-at" in sys.argv:  # A/B: where the fused call lets the vertex normals start (0 / 1 / 2)
+        L.call("otx_normals_at", int(sys.argv[sys.argv.index("--normals-at") + 1]))
+    if "--fork" in sys.argv:  # A/B: the round-4 emission (vertices on the side stream, fork / join by events)
+        L.call("otx_mc_emit_fork", 1)
     intr_t = synth.REF_INTRINSICS_640
     W, H = intr_t[0], intr_t[1]
     intr = L.ot_intrinsics(W, H, *intr_t[2:])
@@ -88,7 +99,26 @@ def main(normals=True):
         one()
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t) * 1e3)
-    # host side of the same call sequence: when each call returns (no synchronisation in between), medians over 5
+    # host side of the timed (fused) sequence: when each call returns, medians over 5 (reset, integrate, fused call,
+    # final synchronize)
+    fmarks = []
+    for _ in range(6):
+        torch.cuda.synchronize()
+        t = [time.perf_counter()]
+        vol.reset()
+        t.append(time.perf_counter())
+        lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
+        t.append(time.perf_counter())
+        if normals and "--separate" not in sys.argv:
+            vol.extract_mesh_and_sample_min_z(100000, 0.03)
+        t.append(time.perf_counter())
+        torch.cuda.synchronize()
+        t.append(time.perf_counter())
+        fmarks.append(np.diff(np.array(t)) * 1e6)
+    med = np.median(np.array(fmarks[1:]), axis=0)
+    print("host us per call of the timed sequence (reset, integrate, fused extract+sample, final sync):",
+          [round(float(x), 1) for x in med])
+    # host side of the separate call sequence: when each call returns (no synchronisation in between), medians over 5
     marks = []
     for _ in range(6):
         torch.cuda.synchronize()
@@ -142,7 +172,9 @@ def main(normals=True):
           [round(float(x), 1) for x in med])
     print("stream priority range (least, greatest):", torch.cuda.Stream.priority_range())
     print("single object ms (median of last 5)" + ("" if normals else ", WITHOUT normals") +
-          (", sampler on the greatest-priority stream" if "--hi" in sys.argv else "") + ":", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
+          (", sampler on the greatest-priority stream" if "--hi" in sys.argv else "") +
+          (", two-stream emission" if "--fork" in sys.argv else "") +
+          (f", normals at {sys.argv[sys.argv.index('--normals-at') + 1]}" if "--normals-at" in sys.argv else "") + ":", round(float(np.median(ts[3:])), 3), [round(x, 3) for x in ts])
     # the volume's size against configs[1]'s (integrate occupancy): units, voxel updates, unit integrations
     vol.reset()
     lib.ot_tsdf_integrate_u16_frames(vol._h, ext.shape[0], dp, cp, intr_ref, ep, 1000.0, 3.0, s_)
