@@ -534,7 +534,7 @@ static std::atomic<bool> g_tables_uploaded{false};
 static bool g_mc_emit_fork = false;  // test hook otx_mc_emit_fork: the two-stream emission (round 4) for A/B timing
 // ot_tsdf_extract_sample_min_z: where the vertex normals may start -- 0 right after the emission, 1 beside the area-sum
 // walk, 2 beside the CDF walk (test hook otx_normals_at)
-static int g_normals_at = 2;
+static int g_normals_at = 1;
 static std::mutex g_tables_mutex;
 
 static ot_status upload_tables() {  // once per process (one process per GPU), safe from concurrent host threads
@@ -835,8 +835,9 @@ ot_status ot_tsdf_extract_sample_min_z(ot_tsdf* vol, double* vertices, double* v
     if (nv == 0 || nt == 0) return OT_OK;
     if (!vol->ev_made) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_made, hipEventDisableTiming));
     // ev_made: the mesh arrays are complete (the normals wait on it).  Recorded where the normals cost the sampling
-    // least: not right after the emission -- there they took the CUs from the chains' wide first passes (bsum, guess,
-    // chunk, runs: 33 -> 66 us, r05k) -- but just before one of its single-wave walks (g_normals_at)
+    // least: just before the area-sum walk, a single wave per chain with the rest of the GPU idle (g_normals_at 1).
+    // Right after the emission the normals' launch landed among the chains' wide first passes and the stream stalled
+    // 27 us twice (one object 1.571 vs 1.536 ms kernel span, r05m); beside the CDF walk (2) 1.592 vs 1.587 ms wall
     const int at = vertex_normals ? g_normals_at : 0;
     if (vertex_normals && at == 0) OT_HIP_TRY(hipEventRecord(vol->ev_made, stream));
     ot_mesh_sample_job job{vertices, nullptr, out_rgb ? vertex_colors : nullptr, nv, triangles, nt, out_xyz, nullptr,
