@@ -276,7 +276,11 @@ class ScalableTSDFVolume:
         if N is not None:
             for t in (V, T, N):  # allocated on the caller's stream, used on the side stream
                 t.record_stream(side)
-            done = torch.cuda.Event()
+            # one event per volume, re-recorded by each call: a reader of an older mesh's normals then waits for a
+            # later point of the same in-order side stream (never too early), and no event is created per call
+            done = getattr(self, "_normals_done", None)
+            if done is None:
+                done = self._normals_done = torch.cuda.Event()
             done.record(side)
             mesh._vn = _Arr(dev=N[:nv.value], ready=done)
         pcd = PointCloud()

@@ -336,6 +336,36 @@ def test_fused_extract_sample_min_z(pkg, O, synth, seq16):
     assert cloud is None and not mesh.has_vertices()
 
 
+@pytest.mark.parametrize("fork,normals_at", [(0, 0), (0, 2), (1, 1)])
+def test_fused_call_schedules_bitexact(pkg, O, synth, seq16, gpu, fork, normals_at):
+    """The scheduling knobs of the fused call change no bit: the marching-cubes emission as one launch (default) or as
+    two kernels on two streams (otx_mc_emit_fork), and the vertex normals started right after the emission, beside the
+    area-sum walk (default) or beside the CDF walk (otx_normals_at) -- each against the oracle, twice on one volume."""
+    L = pkg._lib
+    depth, color, ext = seq16
+    vol, ref = _volumes(pkg, O, synth, depth[:3], color[:3], ext[:3], 0.005)
+    V, VC, T = ref.extract_triangle_mesh()
+    P, _, PC = O.sample_points_uniformly(V, T, 50000, 9, VC=VC)
+    rx, rc = O.filter_min_z(P, PC, 0.03)
+    VN = O.vertex_normals(V, T)
+    vol.extract_mesh_and_sample_min_z(50000, 0.03, seed=9)  # the first extraction (separate calls) sets the guess
+    L.call("otx_mc_emit_fork", fork)
+    L.call("otx_normals_at", normals_at)
+    try:
+        for rep in range(2):
+            mesh, cloud = vol.extract_mesh_and_sample_min_z(50000, 0.03, seed=9)
+            tag = f"fork {fork}, normals at {normals_at}, pass {rep}"
+            assert_bitwise(np.asarray(mesh.vertices), V, f"vertices ({tag})")
+            assert_bitwise(np.asarray(mesh.vertex_colors), VC, f"vertex colours ({tag})")
+            assert_bitwise(np.asarray(mesh.triangles), T, f"triangles ({tag})")
+            assert_bitwise(np.asarray(cloud.points), rx, f"cloud points ({tag})")
+            assert_bitwise(np.asarray(cloud.colors), rc, f"cloud colours ({tag})")
+            assert_bitwise(np.asarray(mesh.vertex_normals), VN, f"normals ({tag})")
+    finally:
+        L.call("otx_mc_emit_fork", 0)
+        L.call("otx_normals_at", 1)
+
+
 def test_sampling_batch_matches_single(pkg, O, synth, seq16, meshes):
     """TriangleMesh.sample_points_uniformly_batch: the per-mesh clouds equal the single-mesh calls (and the oracle)
     for meshes of different sizes sampled together."""
