@@ -168,6 +168,15 @@ __device__ inline T wave_sum(T v) {
     return v;
 }
 
+__device__ inline int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int u = __shfl_xor(v, o, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
 // Decoupled look-back (single-pass prefix over the tiles of one chain), run by ONE whole wave of the tile's
 // workgroup: publishes the tile's aggregate, reads its predecessors' status words 64 at a time (lane i: tile - 1 - i),
 // folds every aggregate up to the nearest inclusive prefix, publishes its own inclusive prefix and returns the

@@ -29,6 +29,11 @@ __constant__ int c_eshift[12][4];
 __constant__ int c_e2v[12][2];
 __constant__ int c_shift[8][3];
 __constant__ unsigned char c_ntri[256];  // triangles per cube configuration (from c_tri)
+__constant__ unsigned c_cinfo[256];      // per cube configuration: the edges its triangles use (bits 0-11), ntri << 12
+// OT_MC_EDGE_SHIFT as a compile-time table: the emission's unrolled loop over a cube's 12 edges folds each edge's shift
+// into constants instead of loading it per corner (upload_tables checks it against the header's)
+constexpr int kEdgeShift[12][4] = {{0, 0, 0, 0}, {1, 0, 0, 1}, {0, 1, 0, 0}, {0, 0, 0, 1}, {0, 0, 1, 0}, {1, 0, 1, 1},
+                                   {0, 1, 1, 0}, {0, 0, 1, 1}, {0, 0, 0, 2}, {1, 0, 0, 2}, {1, 1, 0, 2}, {0, 1, 0, 2}};
 
 constexpr int EWORDS = (UNIT_VOX * 3) / 32;  // 384 bitmask words per unit
 constexpr int T17 = 17;
@@ -109,7 +114,9 @@ __global__ __launch_bounds__(256) void k_mc_prepare(TsdfDev d, McDev m) {
 
 __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
     // Classification needs only two predicates per voxel (weight == 0, tsdf < 0): one flag byte each in LDS
-    // (4.9 KiB per 17^3 tile instead of 39 KiB of floats), so many more units are resident per CU.
+    // (4.9 KiB per 17^3 tile instead of 39 KiB of floats), so many more units are resident per CU.  (Flag bytes written
+    // by k_mc_prepare from a coalesced read of each unit, and the tiles staged from them instead of the floats:
+    // classify 89 -> 59 us, but prepare 8 -> 53 us, r05u -- not kept.)
     __shared__ unsigned char sB[T17 * T17 * T17];
     __shared__ unsigned sflags[EWORDS];  // this unit's own edge bits; edges owned by a +1 neighbour go to HBM directly
     __shared__ int snbr[8];
@@ -243,11 +250,16 @@ __device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z
     }
 }
 
-// one unit's vertices (rank r): one lane per edge-bitmask word w
+// one unit's vertices (rank r): one lane per edge-bitmask word w.  The unit's +x / +y / +z neighbour ids are staged in
+// LDS with the words (not one dependent global load per vertex before its neighbour voxel's loads).  (A wave per unit,
+// each lane walking six words, measured 193 vs 109 us for the emission, r05t: fewer waves, longer chains.)
 __device__ __forceinline__ void mc_vertices_unit(const TsdfDev& d, const McDev& m, double vl, double* V, double* VC,
                                                  int r, int w) {
+    __shared__ int s_vnbr[8];
     const int id = (int)m.sorted_ids[r];
+    if (w < 8) s_vnbr[w] = m.nbr[id * 16 + w];
     unsigned bits = m.eflags[(size_t)id * EWORDS + w];
+    __syncthreads();
     if (!bits) return;
     long long vid = m.vert_base[r] + m.wprefix[(size_t)id * EWORDS + w];
     const int kx = d.unit_keys[id * 3], ky = d.unit_keys[id * 3 + 1], kz = d.unit_keys[id * 3 + 2];
@@ -262,7 +274,7 @@ __device__ __forceinline__ void mc_vertices_unit(const TsdfDev& d, const McDev& 
         double c0[3], c1[3];
         voxel_value(d, id, x, y, z, f0f, c0);
         int x1 = x + (axis == 0), y1 = y + (axis == 1), z1 = z + (axis == 2);
-        const int nid = m.nbr[id * 16 + (((x1 >> 4) << 2) | ((y1 >> 4) << 1) | (z1 >> 4))];
+        const int nid = s_vnbr[((x1 >> 4) << 2) | ((y1 >> 4) << 1) | (z1 >> 4)];
         if (nid < 0) {  // cannot happen for a valid cube (its corners have weight > 0); never read out of bounds
             f1f = f0f;
             c1[0] = c0[0], c1[1] = c0[1], c1[2] = c0[2];
@@ -292,19 +304,13 @@ __device__ __forceinline__ void mc_vertices_unit(const TsdfDev& d, const McDev& 
     }
 }
 
-// sbase: the 8 owner units' first vertex (vert_base of their rank), read once per workgroup, so a triangle corner costs
-// two independent loads (the owner's edge word and its prefix) instead of a rank -> base chain behind them
-__device__ inline int edge_vid(const McDev& m, const int* snbr, const long long* sbase, int x, int y, int z, int e) {
-    const int ox = x + c_eshift[e][0], oy = y + c_eshift[e][1], oz = z + c_eshift[e][2];
-    const int o = ((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4);
-    const int owner = snbr[o];
-    const int local = (ox & 15) * 256 + (oy & 15) * 16 + (oz & 15);
-    const int bit = local * 3 + c_eshift[e][3];
-    const int word = bit >> 5;
-    if (owner < 0) return 0;
-    const unsigned wbits = m.eflags[(size_t)owner * EWORDS + word];
-    const unsigned below = wbits & ((1u << (bit & 31)) - 1u);
-    return (int)(sbase[o] + m.wprefix[(size_t)owner * EWORDS + word] + __popc(below));
+// v[e] for a per-lane e in [0, 12): a select tree (a register array indexed by a per-lane value would go to scratch)
+__device__ __forceinline__ int pick12(const int (&v)[12], int e) {
+    const bool b0 = e & 1, b1 = e & 2;
+    const int p0 = b0 ? v[1] : v[0], p1 = b0 ? v[3] : v[2], p2 = b0 ? v[5] : v[4], p3 = b0 ? v[7] : v[6];
+    const int p4 = b0 ? v[9] : v[8], p5 = b0 ? v[11] : v[10];
+    const int q0 = b1 ? p1 : p0, q1 = b1 ? p3 : p2, q2 = b1 ? p5 : p4;
+    return (e & 8) ? q2 : ((e & 4) ? q1 : q0);
 }
 
 // one unit's triangles (rank r): 256 lanes, one (x, y) column of 16 cubes each
@@ -340,14 +346,49 @@ __device__ __forceinline__ void mc_triangles_unit(const TsdfDev& d, const McDev&
         dst[0] = make_uint4(off[0], off[1], off[2], off[3]);
         dst[1] = make_uint4(off[4], off[5], off[6], off[7]);
     }
+    // per non-empty cube two round trips: its table row and edge set, then the owner words and prefixes of every edge
+    // it uses (the 12 edges unrolled, each shift a constant), all issued before any is used; a corner's vertex id is
+    // sbase (the owner's first vertex) + the word's prefix + the set bits below its own -- the cut edges' ids are
+    // formed once per cube, not once per corner
     const int x = t >> 4, y = t & 15;
     for (int z = 0; z < UNIT_RES; ++z) {
         const int cube = (int)((cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu);
         if (cube == 0) continue;
-        for (int k = 0; k < 15 && c_tri[cube][k] != -1; k += 3) {
-            const int a = edge_vid(m, snbr, sbase, x, y, z, c_tri[cube][k]);
-            const int b = edge_vid(m, snbr, sbase, x, y, z, c_tri[cube][k + 1]);
-            const int c = edge_vid(m, snbr, sbase, x, y, z, c_tri[cube][k + 2]);
+        const int4 row = *reinterpret_cast<const int4*>(&c_tri[cube][0]);
+        const unsigned info = c_cinfo[cube];
+        unsigned wb[12];
+        int wp[12];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) {
+            const int ox = x + kEdgeShift[e][0], oy = y + kEdgeShift[e][1], oz = z + kEdgeShift[e][2];
+            const int o = ((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4);
+            const int owner = snbr[o];
+            const int word = (((ox & 15) * 256 + (oy & 15) * 16 + (oz & 15)) * 3 + kEdgeShift[e][3]) >> 5;
+            wb[e] = 0u;
+            wp[e] = 0;
+            if (((info >> e) & 1u) && owner >= 0) {
+                wb[e] = m.eflags[(size_t)owner * EWORDS + word];
+                wp[e] = m.wprefix[(size_t)owner * EWORDS + word];
+            }
+        }
+        int vid[12];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) {
+            const int ox = x + kEdgeShift[e][0], oy = y + kEdgeShift[e][1], oz = z + kEdgeShift[e][2];
+            const int o = ((ox >> 4) << 2) | ((oy >> 4) << 1) | (oz >> 4);
+            const int bit = ((ox & 15) * 256 + (oy & 15) * 16 + (oz & 15)) * 3 + kEdgeShift[e][3];
+            const unsigned below = wb[e] & ((1u << (bit & 31)) - 1u);
+            vid[e] = snbr[o] < 0 ? 0 : (int)(sbase[o] + wp[e] + __popc(below));
+        }
+        const int nt = (int)(info >> 12);
+        const unsigned rw[4] = {(unsigned)row.x, (unsigned)row.y, (unsigned)row.z, (unsigned)row.w};
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k >= nt) break;
+            const int ea = (int)((rw[(3 * k) >> 2] >> (((3 * k) & 3) * 8)) & 0xFFu);
+            const int eb = (int)((rw[(3 * k + 1) >> 2] >> (((3 * k + 1) & 3) * 8)) & 0xFFu);
+            const int ec = (int)((rw[(3 * k + 2) >> 2] >> (((3 * k + 2) & 3) * 8)) & 0xFFu);
+            const int a = pick12(vid, ea), b = pick12(vid, eb), c = pick12(vid, ec);
             if (out < m.cap_t) {
                 T[out * 3 + 0] = a;
                 T[out * 3 + 1] = c;
@@ -552,6 +593,17 @@ static ot_status upload_tables() {  // once per process (one process per GPU), s
         ntri[c] = (unsigned char)n;
     }
     OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_ntri), ntri, sizeof(ntri)));
+    unsigned cinfo[256];
+    for (int c = 0; c < 256; ++c) {
+        unsigned em = 0u;
+        for (int k = 0; k < 3 * ntri[c]; ++k) em |= 1u << OT_MC_TRI_TABLE[c][k];
+        cinfo[c] = em | ((unsigned)ntri[c] << 12);
+    }
+    OT_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_cinfo), cinfo, sizeof(cinfo)));
+    for (int e = 0; e < 12; ++e)
+        for (int a = 0; a < 4; ++a)
+            if (kEdgeShift[e][a] != OT_MC_EDGE_SHIFT[e][a])
+                return fail(OT_ERR_INVALID_ARGUMENT, "marching cubes: kEdgeShift differs from OT_MC_EDGE_SHIFT");
     g_tables_uploaded.store(true, std::memory_order_release);
     return OT_OK;
 }

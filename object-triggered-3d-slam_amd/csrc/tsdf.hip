@@ -334,22 +334,37 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
     }
     __syncthreads();
     // only the entries this tile filled (listed by their inserting lanes), not the whole table
+    // The slots this batch touches first get a place in its list through ONE counter atomic per wave (ballot, the
+    // first such lane adds the wave's count, each lane takes its rank): a batch's thousands of first touches on one
+    // counter word no longer serialise in L2 one lane at a time
     const int nused = s_nused;
-    for (int t = tid; t < nused; t += 256) {
-        const int e = s_used[t];
-        const unsigned long long key = s_keys[e];
-        const int slot = hash_insert(d, key);
-        if (slot < 0) {
-            atomicOr(&d.counters[C_HASHERR], 1);
-            continue;
+    for (int t0 = 0; t0 < nused; t0 += 256) {  // block-uniform trip count: every lane reaches the ballot
+        const int t = t0 + tid;
+        bool fresh = false;
+        int slot = -1;
+        if (t < nused) {
+            const int e = s_used[t];
+            slot = hash_insert(d, s_keys[e]);
+            if (slot < 0) {
+                atomicOr(&d.counters[C_HASHERR], 1);
+            } else {
+                const unsigned long long m = s_masks[e];
+                if ((d.fmask[slot] & m) != m)  // fast path; a stale read only costs the atomic below
+                    fresh = atomicOr(&d.fmask[slot], m) == 0ull;
+            }
         }
-        const unsigned long long m = s_masks[e];
-        if ((d.fmask[slot] & m) == m) continue;  // fast path; a stale read only costs the atomic below
-        const unsigned long long old = atomicOr(&d.fmask[slot], m);
-        if (old == 0ull) {
-            const int pos = atomicAdd(&d.counters[p.pc], 1);
-            if (pos < p.slot_cap) d.bslots[pos] = slot;
-            else atomicOr(&d.counters[C_HASHERR], 1);
+        int cnt;
+        const int rank = wave_excl_count(fresh, cnt);
+        if (cnt) {  // wave-uniform
+            const int leader = __ffsll((long long)__ballot(fresh)) - 1;
+            int base = 0;
+            if ((int)lane_id() == leader) base = atomicAdd(&d.counters[p.pc], cnt);
+            base = __builtin_amdgcn_readlane(base, leader);
+            if (fresh) {
+                const int pos = base + rank;
+                if (pos < p.slot_cap) d.bslots[pos] = slot;
+                else atomicOr(&d.counters[C_HASHERR], 1);
+            }
         }
     }
 }
@@ -393,15 +408,31 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
         if (wcount) *wcount = n;
     }
     unsigned long long pairs = 0;
-    for (int t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
-        const int slot = d.bslots[t];
+    // the new units' key bounds (note_unit_key's counters), reduced over the wave before its atomics: a fresh volume
+    // allocates thousands of units in one batch, and one atomic per unit on six shared words serialised in L2
+    int kmax[3] = {0, 0, 0}, kneg[3] = {0, 0, 0};  // 0: none (the counters hold k + KEY_BIAS + 1 >= 1)
+    // block-uniform trip count, so every lane reaches the wave's one allocation atomic (ballot + rank, as the touch)
+    for (int t0 = blockIdx.x * 256; t0 < n; t0 += gridDim.x * 256) {
+        const int t = t0 + (int)threadIdx.x;
+        const bool live = t < n;
+        const int slot = live ? d.bslots[t] : 0;
+        int id = live ? d.hvals[slot] : 0;
+        int cnt;
+        const int rank = wave_excl_count(live && id < 0, cnt);
+        if (cnt) {  // wave-uniform
+            const int leader = __ffsll((long long)__ballot(live && id < 0)) - 1;
+            int base = 0;
+            if ((int)lane_id() == leader) base = atomicAdd(&d.counters[C_UNITS], cnt);
+            base = __builtin_amdgcn_readlane(base, leader);
+            if (live && id < 0) id = -2 - (base + rank);  // the new id, encoded below -1 until it is checked
+        }
+        if (!live) continue;
         const unsigned long long mask = d.fmask[slot];
         d.fmask[slot] = 0ull;
         int kx, ky, kz;
         unpack_key(d.hkeys[slot], kx, ky, kz);
-        int id = d.hvals[slot];
-        if (id < 0) {
-            id = atomicAdd(&d.counters[C_UNITS], 1);
+        if (id <= -2) {
+            id = -2 - id;
             if (id >= d.max_units) {
                 atomicOr(&d.counters[C_OVERFLOW], 1);
                 id = -1;
@@ -410,7 +441,12 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
                 d.unit_keys[id * 3 + 0] = kx;
                 d.unit_keys[id * 3 + 1] = ky;
                 d.unit_keys[id * 3 + 2] = kz;
-                note_unit_key(d, kx, ky, kz);
+                const int k3[3] = {kx, ky, kz};
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    kmax[a] = max(kmax[a], k3[a] + KEY_BIAS + 1);
+                    kneg[a] = max(kneg[a], KEY_BIAS - k3[a] + 1);
+                }
                 id |= (int)0x80000000u;
             }
         } else if (REPLAY) {
@@ -425,6 +461,18 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
         w.pad = 0ull;
         work[t] = w;
         if (id != -1) pairs += (unsigned long long)__popcll(mask);
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        kmax[a] = wave_max(kmax[a]);
+        kneg[a] = wave_max(kneg[a]);
+    }
+    if (lane_id() == 0) {  // before this workgroup's done ticket below: the last workgroup mails the final bounds
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            if (kmax[a]) atomicMax(&d.counters[C_KMAX + a], kmax[a]);
+            if (kneg[a]) atomicMax(&d.counters[C_KNEG + a], kneg[a]);
+        }
     }
     pairs = wave_sum(pairs);
     if (lane_id() == 0) red[threadIdx.x >> 6] = pairs;
