@@ -135,33 +135,58 @@ __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
     if (t < 8) snbr[t] = m.nbr[id * 16 + t];
     for (int w = t; w < EWORDS; w += 256) sflags[w] = 0u;
     __syncthreads();
-    // tile staging in the pool's memory order (z, x, y with y fastest), so a wave's loads are contiguous runs;
-    // all of a lane's loads are issued before any is consumed (the staging is latency-bound otherwise)
-    constexpr int NT = T17 * T17 * T17, NIT = (NT + 255) / 256;
-    float fv[NIT], wv[NIT];
+    // Tile staging, every load of a lane issued before any is consumed: the unit's own 16^3 voxels as lane t's y-row
+    // (z = t >> 4, x = t & 15: 16 contiguous floats, four 16-B loads per plane), then one voxel per lane of each +x /
+    // +y / +z neighbour face and the 49 voxels of the three +edges and the corner (lanes 0-48).  (Round 4 staged the
+    // 17^3 positions in pool order, 20 scalar load pairs per lane: 88-91 us per configs[3] object.)  A missing
+    // neighbour reads as weight 0.
+    const auto flag = [](float f, float w) { return (unsigned char)((w == 0.0f ? 1 : 0) | (f < 0.0f ? 2 : 0)); };
+    {
+        const int a = t >> 4, b = t & 15;
+        const float* own = unit_base(d, id);
+        const float4* tp = reinterpret_cast<const float4*>(own) + t * 4;
+        const float4* wp = reinterpret_cast<const float4*>(own + UNIT_VOX) + t * 4;
+        float4 tv[4], wv[4];
 #pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-        const int c = t + i * 256;
-        fv[i] = 0.0f;
-        wv[i] = 0.0f;
-        if (c < NT) {
-            const int lz = c / (T17 * T17), lx = (c / T17) % T17, ly = c % T17;
-            const int nid = snbr[((lx >> 4) << 2) | ((ly >> 4) << 1) | (lz >> 4)];
-            if (nid >= 0) {
-                const float* base = unit_base(d, nid);
-                const int vi = (lz & 15) * 256 + (lx & 15) * 16 + (ly & 15);
-                fv[i] = base[vi];
-                wv[i] = base[UNIT_VOX + vi];
-            }
+        for (int k = 0; k < 4; ++k) {
+            tv[k] = tp[k];
+            wv[k] = wp[k];
         }
-    }
+        // faces: +y (lz a, lx b, ly 16), +x (lz a, lx 16, ly b), +z (lz 16, lx a, ly b)
+        float fy = 0.0f, wy = 0.0f, fx = 0.0f, wx = 0.0f, fz = 0.0f, wz = 0.0f, fe = 0.0f, we = 0.0f;
+        const int ny = snbr[2], nx = snbr[4], nz = snbr[1];
+        if (ny >= 0) {
+            fy = unit_base(d, ny)[a * 256 + b * 16];
+            wy = unit_base(d, ny)[UNIT_VOX + a * 256 + b * 16];
+        }
+        if (nx >= 0) {
+            fx = unit_base(d, nx)[a * 256 + b];
+            wx = unit_base(d, nx)[UNIT_VOX + a * 256 + b];
+        }
+        if (nz >= 0) {
+            fz = unit_base(d, nz)[a * 16 + b];
+            wz = unit_base(d, nz)[UNIT_VOX + a * 16 + b];
+        }
+        // edges: (16, 16, lz = t) in n6, (16, ly = t - 16, 16) in n5, (lx = t - 32, 16, 16) in n3, the corner in n7
+        int ne = -1, ve = 0, se = 0;
+        if (t < 16) ne = snbr[6], ve = t * 256, se = (16 * T17 + 16) * T17 + t;
+        else if (t < 32) ne = snbr[5], ve = t - 16, se = (16 * T17 + (t - 16)) * T17 + 16;
+        else if (t < 48) ne = snbr[3], ve = (t - 32) * 16, se = ((t - 32) * T17 + 16) * T17 + 16;
+        else if (t == 48) ne = snbr[7], ve = 0, se = (16 * T17 + 16) * T17 + 16;
+        if (ne >= 0) {
+            fe = unit_base(d, ne)[ve];
+            we = unit_base(d, ne)[UNIT_VOX + ve];
+        }
+        const float f16[16] = {tv[0].x, tv[0].y, tv[0].z, tv[0].w, tv[1].x, tv[1].y, tv[1].z, tv[1].w,
+                               tv[2].x, tv[2].y, tv[2].z, tv[2].w, tv[3].x, tv[3].y, tv[3].z, tv[3].w};
+        const float w16[16] = {wv[0].x, wv[0].y, wv[0].z, wv[0].w, wv[1].x, wv[1].y, wv[1].z, wv[1].w,
+                               wv[2].x, wv[2].y, wv[2].z, wv[2].w, wv[3].x, wv[3].y, wv[3].z, wv[3].w};
 #pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-        const int c = t + i * 256;
-        if (c < NT) {
-            const int lz = c / (T17 * T17), lx = (c / T17) % T17, ly = c % T17;
-            sB[(lx * T17 + ly) * T17 + lz] = (unsigned char)((wv[i] == 0.0f ? 1 : 0) | (fv[i] < 0.0f ? 2 : 0));
-        }
+        for (int y = 0; y < 16; ++y) sB[(b * T17 + y) * T17 + a] = flag(f16[y], w16[y]);
+        sB[(b * T17 + 16) * T17 + a] = flag(fy, wy);
+        sB[(16 * T17 + b) * T17 + a] = flag(fx, wx);
+        sB[(a * T17 + b) * T17 + 16] = flag(fz, wz);
+        if (t <= 48) sB[se] = flag(fe, we);
     }
     __syncthreads();
     const int x = t >> 4, y = t & 15;
