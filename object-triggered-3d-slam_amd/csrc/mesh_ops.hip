@@ -95,17 +95,9 @@ __global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V,
 }
 // k_tri_areas that also lands the sampler's uploaded tables (blob words -> dst) and zeroes its look-back words
 // (zwords at zero) from block 0: the chains' table upload and the status memset ride on the first kernel of the chain
-// instead of two launches of their own (~5 us each on one object's latency chain).  The argument blob comes in two
-// sizes: a one-object table fits 512 B, and the 3-KiB one delayed the kernel's start ~6 us behind the kernel before
-// it (one object's timeline, r05v; a bigger kernel-argument segment is written and fetched per launch)
-template <int W>
-struct ArgWords {
-    unsigned long long w[W];
-};
-constexpr int BLOB_SMALL_WORDS = 64;
-template <int W>
+// instead of two launches of their own (~5 us each on one object's latency chain)
 __global__ __launch_bounds__(256) void k_tri_areas_blob(const double* __restrict__ V, const int32_t* __restrict__ T,
-                                                        int64_t nt, double* __restrict__ area, ArgWords<W> b,
+                                                        int64_t nt, double* __restrict__ area, ArgBlob b,
                                                         unsigned long long* __restrict__ dst, int words,
                                                         unsigned long long* __restrict__ zero, int zwords) {
     if (blockIdx.x == 0) {
@@ -1109,21 +1101,11 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
         const int64_t nt = jobs[j].n_triangles;
         const dim3 grid((unsigned)((nt + 255) / 256));
         if (blob && j == 0) {
-            const int words = (int)((blob_bytes + 7) / 8);
-            unsigned long long* zw = (unsigned long long*)(*extra_dev + zero_off);
-            if (words <= BLOB_SMALL_WORDS) {
-                ArgWords<BLOB_SMALL_WORDS> b;
-                std::memcpy(b.w, up, blob_bytes);
-                hipLaunchKernelGGL(k_tri_areas_blob<BLOB_SMALL_WORDS>, grid, dim3(256), 0, stream, jobs[j].vertices,
-                                   jobs[j].triangles, nt, cdf[j], b, (unsigned long long*)djobs, words, zw,
-                                   (int)(zero_bytes / 8));
-            } else {
-                ArgWords<UPLOAD_ARG_BYTES / 8> b;
-                std::memcpy(b.w, up, blob_bytes);
-                hipLaunchKernelGGL(k_tri_areas_blob<UPLOAD_ARG_BYTES / 8>, grid, dim3(256), 0, stream,
-                                   jobs[j].vertices, jobs[j].triangles, nt, cdf[j], b, (unsigned long long*)djobs,
-                                   words, zw, (int)(zero_bytes / 8));
-            }
+            ArgBlob b;
+            std::memcpy(b.w, up, blob_bytes);
+            hipLaunchKernelGGL(k_tri_areas_blob, grid, dim3(256), 0, stream, jobs[j].vertices, jobs[j].triangles, nt,
+                               cdf[j], b, (unsigned long long*)djobs, (int)((blob_bytes + 7) / 8),
+                               (unsigned long long*)(*extra_dev + zero_off), (int)(zero_bytes / 8));
         } else {
             hipLaunchKernelGGL(k_tri_areas, grid, dim3(256), 0, stream, jobs[j].vertices, jobs[j].triangles, nt,
                                cdf[j]);
