@@ -734,7 +734,8 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
             pcds = pkg.geometry.TriangleMesh.sample_points_min_z_batch([parts[j] for j in range(len(dev))], 100000,
                                                                       0.03)
         clouds = [p._xyz.dev() for p in pcds]
-        # one collective, counts in-band: every rank holds <= ceil(objects / N) objects of <= 100k points
+        # every rank holds <= ceil(objects / N) objects of <= 100k points: one collective with the counts in-band while
+        # that padded bound stays small (distributed.CAPPED_MAX_BYTES), else a count exchange and a tight gather
         merged = D.merge_object_clouds(clouds, capacity=((args.objects + world - 1) // world) * 100000)
         sizes["local"] = sum(int(c.shape[0]) for c in clouds)
         return merged
@@ -770,7 +771,7 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t1)
         single = round(float(np.median(ts)) * 1e3, 3)
-    merge = _merge_label(world)
+    merge = _merge_label(world, ((args.objects + world - 1) // world) * 100000)
     return {"workload": f"configs[3]: {args.objects} object scans x {args.object_frames} 640x480 frames, "
                         f"{args.voxel * 1000:g} mm TSDF -> mesh -> normals -> 100k samples + z mask (one pass) per object "
                         f"({'one host call from the mesh totals to the sampler' if fused else 'batched sampling'}), "
@@ -784,12 +785,16 @@ def objects_pipeline(args, L, lib, synth, torch, dist, rank, world, ids, scans):
             "objects_over_single": round(dt * 1e3 / single, 2) if single else None}
 
 
-def _merge_label(world):
-    """the collective a merge actually runs at this world size / backend"""
+def _merge_label(world, capacity=None):
+    """the collectives a merge actually runs at this world size / backend / capacity bound (merge_object_clouds takes
+    the padded single collective only while it stays under distributed.CAPPED_MAX_BYTES)"""
     if world == 1:
         return "local concatenation (N=1: no process group, no collective)"
-    return ("one RCCL all-gather over xGMI (counts in-band)" if COLL_DEV == "cuda"
-            else "one gloo all-gather (counts in-band)")
+    D = importlib.import_module(PKG + ".distributed")
+    lib = "RCCL" if COLL_DEV == "cuda" else "gloo"
+    if capacity is not None and D.capped_fits(capacity, 3):
+        return f"one {lib} all-gather (counts in-band)" + (" over xGMI" if lib == "RCCL" else "")
+    return f"a {lib} all-gather of the row counts, one host read, a {lib} all-gather of the rows"
 
 
 def hybrid_fusion(args, L, synth, torch, dist, rank, world):
@@ -842,7 +847,7 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
             L.call("ot_occupancy_to_points", C.c_void_p(d_base.data_ptr()), 1024, 1024, 100, 0.05, -25.6, -25.6,
                    C.c_void_p(occ.data_ptr()), C.byref(nq), stream)
             stats["changed_cells"] = ch.value
-        merged = Dm.merge_object_clouds(objs, capacity=cap)  # one collective, counts in-band
+        merged = Dm.merge_object_clouds(objs, capacity=cap)  # counts in-band while the padding is small
         if rank == 0:
             merged = torch.cat([occ[:nq.value], merged], 0)
         stats.update(added=added, removed=removed)
@@ -855,7 +860,7 @@ def hybrid_fusion(args, L, synth, torch, dist, rank, world):
         dist.all_reduce(t)
     return {"workload": f"configs[4]: 1024x1024 occupancy grid @ 5 cm + {args.hybrid_objects} object clouds, "
                         "change detection vs the saved map (smart_paste grid merge + 2 cm voxel-key diff per object), "
-                        f"hybrid cloud assembled over {world} GPU(s), merge: {_merge_label(world)}",
+                        f"hybrid cloud assembled over {world} GPU(s), merge: {_merge_label(world, cap)}",
             "ms": round(dt * 1e3, 3), "mpoints_per_s": round(int(t.item()) / dt / 1e6, 2),
             "merged_points": int(merged.shape[0]) if rank == 0 else None,
             "changed_grid_cells": stats.get("changed_cells"), "added_keys_rank0": stats.get("added"),
