@@ -87,11 +87,25 @@ __device__ inline double tri_area(const double* __restrict__ V, const int32_t* _
     const double c2 = x[0] * y[1] - x[1] * y[0];
     return 0.5 * sqrt((c0 * c0 + c1 * c1) + c2 * c2);
 }
-__global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V, const int32_t* __restrict__ T,
-                                                   int64_t nt, double* __restrict__ area) {
+// bsum (nullable): the block's 256 areas are chunk blockIdx.x of the area-sum chain (CHAIN_CH values per chunk), and
+// their approximate sum -- only a binade guess for the chain walk, any order will do -- is k_chain_bsum's output, formed
+// here instead of in a launch of its own
+__device__ inline void areas_block(const double* __restrict__ V, const int32_t* __restrict__ T, int64_t nt,
+                                   double* __restrict__ area, double* __restrict__ bsum) {
+    static_assert(CHAIN_CH == 256, "one areas workgroup per chain chunk");
+    __shared__ double s_w[4];
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= nt) return;
-    area[t] = tri_area(V, T, t);
+    const double a = t < nt ? tri_area(V, T, t) : 0.0;
+    if (t < nt) area[t] = a;
+    if (!bsum) return;  // grid-uniform
+    const double w = wave_sum(a);
+    if (lane_id() == 0) s_w[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+}
+__global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V, const int32_t* __restrict__ T,
+                                                   int64_t nt, double* __restrict__ area, double* __restrict__ bsum) {
+    areas_block(V, T, nt, area, bsum);
 }
 // k_tri_areas that also lands the sampler's uploaded tables (blob words -> dst) and zeroes its look-back words
 // (zwords at zero) from block 0: the chains' table upload and the status memset ride on the first kernel of the chain
@@ -99,14 +113,13 @@ __global__ __launch_bounds__(256) void k_tri_areas(const double* __restrict__ V,
 __global__ __launch_bounds__(256) void k_tri_areas_blob(const double* __restrict__ V, const int32_t* __restrict__ T,
                                                         int64_t nt, double* __restrict__ area, ArgBlob b,
                                                         unsigned long long* __restrict__ dst, int words,
-                                                        unsigned long long* __restrict__ zero, int zwords) {
+                                                        unsigned long long* __restrict__ zero, int zwords,
+                                                        double* __restrict__ bsum) {
     if (blockIdx.x == 0) {
         for (int i = threadIdx.x; i < words; i += 256) dst[i] = b.w[i];
         for (int i = threadIdx.x; i < zwords; i += 256) zero[i] = 0ull;
     }
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= nt) return;
-    area[t] = tri_area(V, T, t);
+    areas_block(V, T, nt, area, bsum);
 }
 
 // Open3D's sequential recurrences (GetSurfaceArea: s = (((a0 + a1) + a2) + ...), then the CDF loop
@@ -700,12 +713,13 @@ __global__ __launch_bounds__(256) void k_chain_emit(const ChainJob* __restrict__
 template <bool CDF>
 // mark (nullable): recorded on `stream` just before the walk -- a single wave per chain, the rest of the GPU idle --
 // for work on another stream to start beside it (the fused extraction's vertex normals)
+// bsum_done: the chunk sums were formed by the kernel that produced the values (the sampler's areas)
 void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t stream, bool prologue = true,
-                   hipEvent_t mark = nullptr) {
+                   hipEvent_t mark = nullptr, bool bsum_done = false) {
     const int64_t nb = (max_n + CH - 1) / CH;
     const dim3 grid((unsigned)((nb + 3) / 4), (unsigned)n_jobs);
     if (prologue) {
-        hipLaunchKernelGGL(k_chain_bsum, grid, dim3(256), 0, stream, djobs);
+        if (!bsum_done) hipLaunchKernelGGL(k_chain_bsum, grid, dim3(256), 0, stream, djobs);
         hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(1024), 0, stream, djobs);
         hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
     }
@@ -1105,13 +1119,13 @@ static ot_status sample_cdfs(const ot_mesh_sample_job* jobs, int32_t n_jobs, siz
             std::memcpy(b.w, up, blob_bytes);
             hipLaunchKernelGGL(k_tri_areas_blob, grid, dim3(256), 0, stream, jobs[j].vertices, jobs[j].triangles, nt,
                                cdf[j], b, (unsigned long long*)djobs, (int)((blob_bytes + 7) / 8),
-                               (unsigned long long*)(*extra_dev + zero_off), (int)(zero_bytes / 8));
+                               (unsigned long long*)(*extra_dev + zero_off), (int)(zero_bytes / 8), chain[j].bsum);
         } else {
             hipLaunchKernelGGL(k_tri_areas, grid, dim3(256), 0, stream, jobs[j].vertices, jobs[j].triangles, nt,
-                               cdf[j]);
+                               cdf[j], chain[j].bsum);
         }
     }
-    launch_chains<false>(djobs, n_jobs, max_nt, stream, true, mark_at == 1 ? mark : nullptr);
+    launch_chains<false>(djobs, n_jobs, max_nt, stream, true, mark_at == 1 ? mark : nullptr, true);
     const int64_t max_nb = (max_nt + CH - 1) / CH;
     hipLaunchKernelGGL(k_chain_cdf_prep, dim3((unsigned)((max_nb + 3) / 4), (unsigned)n_jobs), dim3(256), 0, stream,
                        (const ChainJob*)djobs, (const ChainJob*)(djobs + n_jobs));
@@ -1302,7 +1316,8 @@ ot_status ot_mesh_get_surface_area(const double* V, int64_t nv, const int32_t* T
     jb.x = area, jb.n = nt, jb.out = sum;
     char* cur = chain_aux((char*)(area + nt2), nt, jb);
     ChainJob* djob = (ChainJob*)cur;
-    hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, V, T, nt, area);
+    hipLaunchKernelGGL(k_tri_areas, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, V, T, nt, area,
+                       (double*)nullptr);
     OT_HIP_TRY(hipMemcpyAsync(djob, &jb, sizeof(ChainJob), hipMemcpyHostToDevice, stream));
     launch_chains<false>(djob, 1, nt, stream);
     OT_LAUNCH_CHECK();

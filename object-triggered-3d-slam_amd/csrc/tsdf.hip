@@ -1847,7 +1847,9 @@ ot_status ot_tsdf_create(double voxel_length, double sdf_trunc, int32_t color_ty
     if ((e = hipMalloc(&d.bslots, sizeof(int) * cap)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&d.work, sizeof(UnitWork) * cap)) != hipSuccess) return cleanup(e);
     if ((e = hipMalloc(&v->bset[0].bframes, sizeof(BatchFrame) * MAX_BATCH)) != hipSuccess) return cleanup(e);
-    if ((e = hipHostMalloc(&v->hbframes, sizeof(BatchFrame) * MAX_BATCH * 2, hipHostMallocDefault)) != hipSuccess)
+    // coherent: k_copy_frames reads the staging straight from host memory, and non-coherent host memory may be cached
+    // by the GPU (the halves are rewritten every other batch)
+    if ((e = hipHostMalloc(&v->hbframes, sizeof(BatchFrame) * MAX_BATCH * 2, hipHostMallocCoherent)) != hipSuccess)
         return cleanup(e);
     if ((e = hipHostMalloc(&v->hmail, sizeof(unsigned) * 2 * OT_MAIL_WORDS, hipHostMallocCoherent)) != hipSuccess)
         return cleanup(e);
