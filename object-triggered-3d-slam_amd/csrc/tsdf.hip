@@ -14,6 +14,7 @@
 // holds, the pool and the hash grow (records copied, keys rehashed) and the batch's dropped units are integrated
 // again from its staged frames (settle_batch), so the result is the one an unbounded pool gives.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <type_traits>
 
@@ -1695,16 +1696,28 @@ ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
     return OT_OK;
 }
 
+// The stream is polled only once the wait has lasted 20 ms (then every ~1 ms): a stream query puts commands on the
+// stream's queue, and while the host spins the queue already holds the work launched after the mailing kernel -- polling
+// every ~20 us had left ~6 us of idle GPU behind that work at each wait (host launch trace against the kernel trace,
+// tools/launch_lag.py, r05ah: the gaps before the unit sort and before the sampler)
 ot_status mail_wait(const unsigned* word, unsigned seq, hipStream_t stream) {
+    using clk = std::chrono::steady_clock;
+    clk::time_point next{};
     for (unsigned it = 1;; ++it) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return OT_OK;
-        if ((it & 1023u) == 0) {  // every ~10-50 us: has the stream faulted, or drained without the mail?
-            const hipError_t q = hipStreamQuery(stream);
-            if (q == hipSuccess) {
-                if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return OT_OK;
-                return fail(OT_ERR_HIP, "mailbox: the stream drained without the kernel's mail");
+        if ((it & 1023u) == 0) {
+            const clk::time_point now = clk::now();
+            if (it == 1024u) {
+                next = now + std::chrono::milliseconds(20);
+            } else if (now >= next) {  // has the stream faulted, or drained without the mail?
+                next = now + std::chrono::milliseconds(1);
+                const hipError_t q = hipStreamQuery(stream);
+                if (q == hipSuccess) {
+                    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return OT_OK;
+                    return fail(OT_ERR_HIP, "mailbox: the stream drained without the kernel's mail");
+                }
+                if (q != hipErrorNotReady) OT_HIP_TRY(q);
             }
-            if (q != hipErrorNotReady) OT_HIP_TRY(q);
         }
         __builtin_ia32_pause();
     }
