@@ -191,7 +191,7 @@ struct ot_tsdf {
     unsigned mc_seq = 0;  // the marching-cubes totals' sequence number (words MAIL_SEQ_MC, MAIL_SEQ_MC + 1)
     int batch_pc = ot::C_BATCH_PAIRS;      // pair counter of the next batch (alternates 4, 5)
     // A batch's staging: per-frame parameters, packed (depth, multiplier) and colour per pixel, and the unit work list.
-    // Two sets: with the front end double-buffered (overlap, ot_tsdf_set_frontend_overlap: on by default for a spatially
+    // Two sets: with the front end double-buffered (overlap, ot_tsdf_set_frontend_overlap: off by default, measured slower
     // sharded volume, whose integrate is 1/N of the work) batch k+1's staging / touch / units run on the caller's stream
     // while batch k's integrate runs on `istream`; otherwise set 0 only, everything on the caller's stream.
     struct BatchSet {
@@ -203,7 +203,7 @@ struct ot_tsdf {
         hipEvent_t ev_units = nullptr;      // the set's units kernel (its integrate waits for it)
         hipEvent_t ev_done = nullptr;       // the set's integrate (the set's next front end waits for it)
     } bset[2];
-    int overlap_mode = -1;        // -1: on when sharded over >= 4 ranks, 0 off, 1 on
+    int overlap_mode = -1;        // -1 (default) and 0 off, 1 on
     int64_t last_batch_slots = -1;  // units the last batch touched (mailed): the next batch's integrate granularity
     int bset_next = 0;            // set of the next batch (alternates in overlap mode)
     int last_set = -1;            // set of the last batch whose integrate ran on istream (joined by readers)

@@ -1322,9 +1322,11 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
 
 // auto (-1): from 4 shards on (r05f, rank 0 of the configs[1] scan: 1/4 shard 1.41 vs 1.56 ms per step, 1/8 1.08 vs
 // 1.16 ms; at 2 shards the co-running front end slows the larger integrate more than it hides: 2.22 vs 2.19 ms)
-static bool overlap_on(const ot_tsdf* vol) {
-    return vol->overlap_mode > 0 || (vol->overlap_mode < 0 && vol->dev.shard_world >= 4);
-}
+// Off unless asked for: with the batch's events gone from the serial path (mailbox waits, a kernel for the frame
+// parameters) the serial front end beat the double-buffered one at every shard count -- rank steps 2.146 / 1.532 /
+// 1.165 ms against 2.195 / 1.587 / 1.230 ms at 2 / 4 / 8 ranks (r05aj, bench.py spatial_amdahl.measured): the overlap's
+// cross-stream events cost more than the co-running front end saves
+static bool overlap_on(const ot_tsdf* vol) { return vol->overlap_mode > 0; }
 static void* set_work(ot_tsdf* vol, int s) { return s == 0 ? vol->dev.work : vol->bset[1].work; }
 
 // order `stream` after the last batch's integrate when it ran on the volume's integrate stream

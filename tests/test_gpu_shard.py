@@ -12,13 +12,15 @@ from conftest import assert_bitwise, ref_intr
 pytestmark = pytest.mark.gpu
 
 
-def _integrate(pkg, seq, voxel, shard=None):
+def _integrate(pkg, seq, voxel, shard=None, overlap=None):
     depth, color, ext = seq
     integ = pkg.pipelines.integration
     intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(importlib.import_module(pkg.__name__ + ".synth")))
     vol = integ.ScalableTSDFVolume(voxel_length=voxel, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
     if shard is not None:
         vol.set_shard(*shard)
+    if overlap is not None:
+        vol.set_frontend_overlap(overlap)
     for k in range(depth.shape[0]):
         rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
             pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
@@ -31,11 +33,11 @@ def _host(t):
     return t.cpu().numpy()
 
 
-@pytest.mark.parametrize("voxel,world", [(0.01, 3), (0.005, 8)])
-def test_shard_union_bitexact(pkg, seq16, gpu, voxel, world):
+@pytest.mark.parametrize("voxel,world,overlap", [(0.01, 3, None), (0.005, 8, 1)])
+def test_shard_union_bitexact(pkg, seq16, gpu, voxel, world, overlap):
     full = _integrate(pkg, seq16, voxel)
     fk, ft, fw, fc = (_host(a) for a in full.export_units())
-    parts = [_integrate(pkg, seq16, voxel, (r, world)) for r in range(world)]
+    parts = [_integrate(pkg, seq16, voxel, (r, world), overlap) for r in range(world)]
     exports = [[_host(a) for a in v.export_units()] for v in parts]
     counts = [e[0].shape[0] for e in exports]
     assert sum(counts) == fk.shape[0] and min(counts) > 0.5 * fk.shape[0] / world

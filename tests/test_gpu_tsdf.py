@@ -362,7 +362,7 @@ def test_tsdf_pool_grows(pkg, O, gpu, synth, batch):
 @pytest.mark.parametrize("batch,max_units", [(8, 0), (1, 0), (16, 64)])
 def test_frontend_overlap_bitexact(pkg, O, gpu, synth, batch, max_units):
     """The double-buffered front end (batch k+1's staging / touch / units on the caller's stream beside batch k's
-    integrate on the volume's integrate stream; the default for sharded volumes) forced on for an unsharded volume:
+    integrate on the volume's integrate stream; off by default) forced on for an unsharded volume:
     70 frames in batches of 8 (9 batches, both staging sets reused), frame by frame, and with a 64-unit pool that
     grows mid-scan (replay from the batch's own set) -- bitwise equal to the oracle, counters included."""
     integ = _integration(pkg)
