@@ -141,6 +141,7 @@ TEST_SIGNATURES = {
     "otx_unit_sort_radix": [_i32],
     "otx_sor_netfill": [_i32],
     "otx_integrate_fine": [_i32],
+    "otx_touch_stage_blocks": [_i32],
     "otx_mc_emit_fork": [_i32],
     "otx_normals_at": [_i32],
     "otx_sampler_hi_stream": [_i32],

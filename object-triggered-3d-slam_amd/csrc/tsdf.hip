@@ -212,6 +212,8 @@ struct BatchTouchParams {
     const float* mult;  // fused staging (k_batch_touch stages the batch's pixels too): ray multipliers
     int64_t npx;        // pixels per frame
     int pc;             // this batch's pair counter index
+    int tiles;          // touch workgroups per frame group (blockIdx.x below it)
+    int stage_blocks;   // staging-only workgroups per frame group after them (0: each touch workgroup stages a share)
 };
 
 __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int pc, int x, int y, int z) {
@@ -263,6 +265,26 @@ __device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* m
     return false;
 }
 
+// staging share `part` of `parts` of the pixels of frame group `grp`
+__device__ inline void stage_share(const BatchFrame* __restrict__ frames, const BatchTouchParams& p, int nframes,
+                                   int grp, int part, int parts) {
+    const int64_t quads = (p.npx + 3) >> 2;
+    const int64_t per = (quads + parts - 1) / parts;
+    const int64_t q0 = (int64_t)part * per, q1 = q0 + per < quads ? q0 + per : quads;
+    for (int f = grp * TF; f < grp * TF + TF && f < nframes; ++f)
+        prep_range(frames[f], p.mult, q0 + threadIdx.x, q1, p.npx);
+}
+
+// Staging (every pixel of the batch: HBM streaming) and the touch (stride samples: LDS merges and global hash atomics)
+// as separate workgroups: stage_blocks > 0 staging-only workgroups follow each frame group's touch tiles in the grid
+// (blockIdx.x >= tiles), so the touches' global atomics are spread over the time the staging streams.  Measured
+// (tools/touch_stage_ab.py, front end per 64-frame batch): every touch workgroup staging a share first (stage_blocks 0,
+// the round-4 form) 115 us, 1 / 2 / 4 / 8 staging workgroups per tile 120 / 111 / 112 / 122 us (r05aq, r05ar: step
+// -1.2 % at 2); all touch workgroups dispatched first and the staging after them 123-128 us (r05as: the touches'
+// atomics then contend at once).  The touch reads raw depth itself, so nothing in it waits on the staging stores.
+// Every rank of a spatially sharded volume stages every pixel: integrating from the raw frames instead (a u16 depth +
+// a multiplier-table gather per voxel visit) made the integrate 1.9x slower per unit (round 4,
+// tools/shard_frontend.py), more than the staging it saves.
 // REPLAY (settle_batch, after the pool grew): the batch's touch again from its STAGED depths (the caller's frames may be
 // gone by then; the staged depth is exactly the value the first pass computed from them), no staging.
 template <bool REPLAY>
@@ -273,28 +295,27 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
     __shared__ int s_used[LTAB];
     __shared__ int s_nused;
     const int tid = threadIdx.x;
+    const int tile = (int)blockIdx.x, grp = (int)blockIdx.y;
+    if constexpr (!REPLAY) {
+        if (p.stage_blocks > 0 && tile >= p.tiles) {  // block-uniform
+            stage_share(frames, p, nframes, grp, tile - p.tiles, p.stage_blocks);
+            return;
+        }
+    }
     for (int e = tid; e < LTAB; e += 256) {
         s_keys[e] = KEY_EMPTY;
         s_masks[e] = 0ull;
     }
     if (tid == 0) s_nused = 0;
-    // Fused staging: this workgroup also stages a contiguous 1/gridDim.x of the pixels of each of its frames (the
-    // touch below reads raw depth itself, so nothing here waits on these stores; as a separate launch the staging
-    // measured 7 us slower per 64 frames).  Every rank of a spatially sharded volume stages every pixel:
-    // integrating from the raw frames instead (a u16 depth + a multiplier-table gather per voxel visit) made the
-    // integrate 1.9x slower per unit (round 4, tools/shard_frontend.py), more than the staging it saves
+    // (stage_blocks 0) this touch workgroup also stages a contiguous 1/tiles of its frames' pixels
     if constexpr (!REPLAY) {
-        const int64_t quads = (p.npx + 3) >> 2;
-        const int64_t per = (quads + gridDim.x - 1) / gridDim.x;
-        const int64_t q0 = (int64_t)blockIdx.x * per, q1 = q0 + per < quads ? q0 + per : quads;
-        for (int f = blockIdx.y * TF; f < blockIdx.y * TF + TF && f < nframes; ++f)
-            prep_range(frames[f], p.mult, q0 + tid, q1, p.npx);
+        if (p.stage_blocks == 0) stage_share(frames, p, nframes, grp, tile, p.tiles);
     }
     __syncthreads();
     const int tiles_x = (p.ws + TT - 1) / TT;
-    const int sx = (blockIdx.x % tiles_x) * TT + (tid & (TT - 1));
-    const int sy = (blockIdx.x / tiles_x) * TT + (tid / TT);
-    const int f0 = blockIdx.y * TF;
+    const int sx = (tile % tiles_x) * TT + (tid & (TT - 1));
+    const int sy = (tile / tiles_x) * TT + (tid / TT);
+    const int f0 = grp * TF;
     if (sx < p.ws && sy < p.hs) {
         const int r = sy * p.stride, c = sx * p.stride;
         for (int f = f0; f < f0 + TF && f < nframes; ++f) {
@@ -1285,6 +1306,7 @@ constexpr int INT_GRID_MULT = 8;
 // the integrate instantiation of a batch: colour precision 64 (bit 1), reciprocal table (bit 0), fine slices (bit 2:
 // 2 voxels per lane along z, 32 waves per unit instead of 16 -- for batches with few units, below)
 static int g_int_fine = -1;  // test hook otx_integrate_fine: -1 by the batch's size (default), 0 coarse, 1 fine
+static int g_stage_blocks = -1;  // test hook otx_touch_stage_blocks: staging-only touch workgroups (-1: 2 per tile)
 static const void* integrate_kernel(int variant) {
     static const void* const k[8] = {
         (const void*)k_batch_integrate<false, false>, (const void*)k_batch_integrate<false, true>,
@@ -1428,6 +1450,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.unit_len = vol->unit_length;
     tp.slot_cap = (int)vol->hash_cap;
     bc.tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
+    tp.tiles = (int)bc.tiles;
+    tp.stage_blocks = g_stage_blocks < 0 ? 2 * (int)bc.tiles : g_stage_blocks;
     bc.n = n;
     bc.pc = pc;
     bc.set = set;
@@ -1439,8 +1463,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     }
     UnitWork* work = (UnitWork*)set_work(vol, set);
     int* wcount = ovl ? vol->wcount + set : vol->dev.counters + pc;
-    hipLaunchKernelGGL(k_batch_touch<false>, dim3(bc.tiles, (unsigned)((n + TF - 1) / TF)), dim3(256), 0, stream,
-                       (const BatchFrame*)bs.bframes, tp, vol->dev, n);
+    hipLaunchKernelGGL(k_batch_touch<false>, dim3(bc.tiles + (unsigned)tp.stage_blocks, (unsigned)((n + TF - 1) / TF)),
+                       dim3(256), 0, stream, (const BatchFrame*)bs.bframes, tp, vol->dev, n);
     hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, work, pc,
                        vol->hmail + OT_MAIL_WORDS, ovl ? wcount : (int*)nullptr, ++vol->units_seq);
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
@@ -2192,6 +2216,14 @@ ot_status otx_tsdf_stats(ot_tsdf* vol, uint64_t* out4) {
 // always, 1 = 2 always): A/B timing and the parity of both instantiations
 ot_status otx_integrate_fine(int32_t mode) {
     g_int_fine = mode < 0 ? -1 : (mode ? 1 : 0);
+    return OT_OK;
+}
+
+// test hook: the batch touch's staging-only workgroups per frame group (-1 = two per touch tile, the default;
+// 0 = every touch workgroup stages a share first): A/B timing and the parity of both forms
+ot_status otx_touch_stage_blocks(int32_t blocks) {
+    if (blocks > 4096) return fail(OT_ERR_INVALID_ARGUMENT, "otx_touch_stage_blocks: at most 4096");
+    g_stage_blocks = blocks < 0 ? -1 : blocks;
     return OT_OK;
 }
 

@@ -175,6 +175,25 @@ def test_integrate_granularity_bitexact(pkg, O, gpu, synth, fine):
         L.call("otx_integrate_fine", -1)
 
 
+@pytest.mark.parametrize("blocks", [0, 7, -1])
+def test_touch_staging_forms_bitexact(pkg, O, gpu, synth, blocks):
+    """The batch touch's staging by separate staging-only workgroups (-1: two per touch tile, the default; 7: a
+    count that does not divide the frame) and by the touch workgroups themselves (0): 40 frames at 5 mm in 16-frame
+    batches and the odd 321x243 camera (per-pixel staging tail), bitwise vs the oracle."""
+    L = pkg._lib
+    L.call("otx_touch_stage_blocks", blocks)
+    try:
+        depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=80, frames=range(0, 80, 2))
+        vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005, batch=16)
+        assert _compare_volumes(vol, ref) > 1000
+        intr_t = (321, 243, 283.1, 283.4, 161.7, 120.2)
+        depth, color, ext = synth.make_sequence(n_frames=12, frames=[0, 2, 5, 9], intr=intr_t)
+        vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, batch=None, intr_t=intr_t)
+        assert _compare_volumes(vol, ref) > 100
+    finally:
+        L.call("otx_touch_stage_blocks", -1)
+
+
 @pytest.mark.parametrize("batch", [1, None])
 def test_tsdf_odd_resolution(pkg, O, gpu, synth, batch):
     """A 321x243 camera (width not a multiple of 4: the staging kernel's per-pixel path; odd sample grid at
