@@ -142,6 +142,7 @@ TEST_SIGNATURES = {
     "otx_sor_netfill": [_i32],
     "otx_integrate_fine": [_i32],
     "otx_touch_stage_blocks": [_i32],
+    "otx_touch_frames": [_i32],
     "otx_mc_emit_fork": [_i32],
     "otx_normals_at": [_i32],
     "otx_sampler_hi_stream": [_i32],

@@ -214,6 +214,7 @@ struct BatchTouchParams {
     int pc;             // this batch's pair counter index
     int tiles;          // touch workgroups per frame group (blockIdx.x below it)
     int stage_blocks;   // staging-only workgroups per frame group after them (0: each touch workgroup stages a share)
+    int tf;             // frames per group (TF)
 };
 
 __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int pc, int x, int y, int z) {
@@ -243,7 +244,11 @@ __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, i
 // every distinct unit of the tile does ONE global hash insert + ONE atomicOr of its merged mask.  A key that does
 // not fit the LDS table falls back to the direct global path.
 constexpr int TT = 16;          // tile edge in samples
-constexpr int TF = 4;        // frames per workgroup (64-frame batches: +1 % step vs 2; 8 / 16: -0.7 / -9 %)
+// frames per workgroup: 2 since the staging-only workgroups (r05au / r05av, tools/touch_stage_ab.py: unsharded step
+// within 0.2 % of 4, a rank of 8 shards 3 % faster -- front end 99 vs 105 us per batch; 8: +10 %); with every touch
+// workgroup staging a share first, 4 was 1 % faster than 2 (round 3)
+constexpr int TF = 2;
+static int g_touch_tf = TF;  // test hook otx_touch_frames: frames per touch workgroup (A/B timing)
 constexpr int LTAB = 1024;   // LDS table entries (16 B each + a 4-B slot in the list of used entries)
 
 __device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* masks, int* used, int* nused,
@@ -271,7 +276,7 @@ __device__ inline void stage_share(const BatchFrame* __restrict__ frames, const 
     const int64_t quads = (p.npx + 3) >> 2;
     const int64_t per = (quads + parts - 1) / parts;
     const int64_t q0 = (int64_t)part * per, q1 = q0 + per < quads ? q0 + per : quads;
-    for (int f = grp * TF; f < grp * TF + TF && f < nframes; ++f)
+    for (int f = grp * p.tf; f < grp * p.tf + p.tf && f < nframes; ++f)
         prep_range(frames[f], p.mult, q0 + threadIdx.x, q1, p.npx);
 }
 
@@ -315,10 +320,10 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
     const int tiles_x = (p.ws + TT - 1) / TT;
     const int sx = (tile % tiles_x) * TT + (tid & (TT - 1));
     const int sy = (tile / tiles_x) * TT + (tid / TT);
-    const int f0 = grp * TF;
+    const int f0 = grp * p.tf;
     if (sx < p.ws && sy < p.hs) {
         const int r = sy * p.stride, c = sx * p.stride;
-        for (int f = f0; f < f0 + TF && f < nframes; ++f) {
+        for (int f = f0; f < f0 + p.tf && f < nframes; ++f) {
             const BatchFrame& fr = frames[f];
             const int64_t pix = (int64_t)r * p.W + c;  // the staged depth, computed as the staging does
             const float df = REPLAY ? fr.dm[pix].x : fr.depth16 ? prep_depth(fr, fr.depth16[pix]) : fr.depthf[pix];
@@ -1452,6 +1457,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     bc.tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
     tp.tiles = (int)bc.tiles;
     tp.stage_blocks = g_stage_blocks < 0 ? 2 * (int)bc.tiles : g_stage_blocks;
+    tp.tf = g_touch_tf;
     bc.n = n;
     bc.pc = pc;
     bc.set = set;
@@ -1463,7 +1469,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     }
     UnitWork* work = (UnitWork*)set_work(vol, set);
     int* wcount = ovl ? vol->wcount + set : vol->dev.counters + pc;
-    hipLaunchKernelGGL(k_batch_touch<false>, dim3(bc.tiles + (unsigned)tp.stage_blocks, (unsigned)((n + TF - 1) / TF)),
+    hipLaunchKernelGGL(k_batch_touch<false>, dim3(bc.tiles + (unsigned)tp.stage_blocks, (unsigned)((n + tp.tf - 1) / tp.tf)),
                        dim3(256), 0, stream, (const BatchFrame*)bs.bframes, tp, vol->dev, n);
     hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, work, pc,
                        vol->hmail + OT_MAIL_WORDS, ovl ? wcount : (int*)nullptr, ++vol->units_seq);
@@ -1644,7 +1650,7 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
         tp.slot_cap = (int)vol->hash_cap;
         const BatchFrame* bf = vol->bset[bc.set].bframes;
         UnitWork* work = (UnitWork*)set_work(vol, bc.set);
-        hipLaunchKernelGGL(k_batch_touch<true>, dim3(bc.tiles, (unsigned)((bc.n + TF - 1) / TF)), dim3(256), 0, stream,
+        hipLaunchKernelGGL(k_batch_touch<true>, dim3(bc.tiles, (unsigned)((bc.n + tp.tf - 1) / tp.tf)), dim3(256), 0, stream,
                            bf, tp, vol->dev, bc.n);
         hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
                            vol->hmail + OT_MAIL_WORDS, (int*)nullptr, ++vol->units_seq);
@@ -2224,6 +2230,13 @@ ot_status otx_integrate_fine(int32_t mode) {
 ot_status otx_touch_stage_blocks(int32_t blocks) {
     if (blocks > 4096) return fail(OT_ERR_INVALID_ARGUMENT, "otx_touch_stage_blocks: at most 4096");
     g_stage_blocks = blocks < 0 ? -1 : blocks;
+    return OT_OK;
+}
+
+// test hook: frames per touch workgroup (1..64, default TF): A/B timing and the parity of other groupings
+ot_status otx_touch_frames(int32_t tf) {
+    if (tf < 1 || tf > MAX_BATCH) return fail(OT_ERR_INVALID_ARGUMENT, "otx_touch_frames: 1..64");
+    g_touch_tf = tf;
     return OT_OK;
 }
 

@@ -175,13 +175,15 @@ def test_integrate_granularity_bitexact(pkg, O, gpu, synth, fine):
         L.call("otx_integrate_fine", -1)
 
 
-@pytest.mark.parametrize("blocks", [0, 7, -1])
-def test_touch_staging_forms_bitexact(pkg, O, gpu, synth, blocks):
+@pytest.mark.parametrize("blocks,tf", [(0, 2), (7, 2), (-1, 4), (-1, 3), (-1, 8)])
+def test_touch_staging_forms_bitexact(pkg, O, gpu, synth, blocks, tf):
     """The batch touch's staging by separate staging-only workgroups (-1: two per touch tile, the default; 7: a
     count that does not divide the frame) and by the touch workgroups themselves (0): 40 frames at 5 mm in 16-frame
-    batches and the odd 321x243 camera (per-pixel staging tail), bitwise vs the oracle."""
+    batches and the odd 321x243 camera (per-pixel staging tail), bitwise vs the oracle; with 4 frames per touch
+    workgroup (the default 2, and 3 -- a ragged last group -- 4 and 8)."""
     L = pkg._lib
     L.call("otx_touch_stage_blocks", blocks)
+    L.call("otx_touch_frames", tf)
     try:
         depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=80, frames=range(0, 80, 2))
         vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005, batch=16)
@@ -192,6 +194,7 @@ def test_touch_staging_forms_bitexact(pkg, O, gpu, synth, blocks):
         assert _compare_volumes(vol, ref) > 100
     finally:
         L.call("otx_touch_stage_blocks", -1)
+        L.call("otx_touch_frames", 2)
 
 
 @pytest.mark.parametrize("batch", [1, None])

@@ -1,7 +1,7 @@
 """A/B of the batch touch's staging forms (tool): the headline scan (configs[1], 256 frames, 64-frame batches), the
 unsharded volume and rank 0 of 8 shards, with otx_touch_stage_blocks 0 (every touch workgroup stages a share first) or
 N staging-only workgroups per frame group (FORMS, comma-separated; a 640x480 frame at stride 4 has 80 touch tiles, and
--1 is the default, 2 per tile); per form
+-1 is the default, 2 per tile; an optional ':F' sets the frames per touch workgroup, default 2); per form
 the front end's mean time per batch (ot_tsdf_frontend_time, HIP events around staging + touch + units) and the step
 (reset + 256 frames + flush, HIP events), forms interleaved over rounds so drift hits them alike."""
 import ctypes as C
@@ -14,7 +14,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PKG = "object-triggered-3d-slam_amd"
-FORMS = tuple(int(x) for x in os.environ.get("FORMS", "0,40,-1,160").split(","))
+FORMS = tuple(tuple(int(v) for v in (x + ":2").split(":")[:2]) for x in os.environ.get("FORMS", "0,-1:2,-1:4").split(","))
 
 
 def main():
@@ -46,7 +46,8 @@ def main():
 
         for rnd in range(3):
             for form in FORMS:
-                L.call("otx_touch_stage_blocks", form)
+                L.call("otx_touch_stage_blocks", form[0])
+                L.call("otx_touch_frames", form[1])
                 for _ in range(2):
                     step()
                 L.call("ot_tsdf_set_profiling", vol, 1)
@@ -65,12 +66,13 @@ def main():
                 r = res.setdefault((N, form), {"fe": [], "step": []})
                 r["fe"].append(fm.value / max(fb.value, 1) * 1e3)
                 r["step"].append(e0.elapsed_time(e1) / 10)
-                print(f"round {rnd} N {N} form {form:4d}: front end {r['fe'][-1]:6.1f} us/batch  step "
+                print(f"round {rnd} N {N} form {form[0]:4d}:{form[1]}: front end {r['fe'][-1]:6.1f} us/batch  step "
                       f"{r['step'][-1]:.4f} ms", flush=True)
         L.call("ot_tsdf_destroy", vol)
     L.call("otx_touch_stage_blocks", -1)
+    L.call("otx_touch_frames", 2)
     for (N, form), r in sorted(res.items()):
-        print(f"N {N} form {form:4d}: front end median {np.median(r['fe']):6.1f} us/batch  step median "
+        print(f"N {N} form {form[0]:4d}:{form[1]}: front end median {np.median(r['fe']):6.1f} us/batch  step median "
               f"{np.median(r['step']):.4f} ms")
 
 
