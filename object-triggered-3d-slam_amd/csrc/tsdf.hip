@@ -435,6 +435,10 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
         d.counters[pc ^ 1] = 0;
         if (wcount) *wcount = n;
     }
+    // only the workgroups that have slots take part (a batch's few thousand units need a tenth of the grid): the rest
+    // leave before the done ticket below, which the last of the active ones draws
+    const int active = min((int)gridDim.x, max(1, (n + 255) / 256));
+    if ((int)blockIdx.x >= active) return;  // block-uniform
     unsigned long long pairs = 0;
     // the new units' key bounds (note_unit_key's counters), reduced over the wave before its atomics: a fresh volume
     // allocates thousands of units in one batch, and one atomic per unit on six shared words serialised in L2
@@ -445,6 +449,9 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
         const bool live = t < n;
         const int slot = live ? d.bslots[t] : 0;
         int id = live ? d.hvals[slot] : 0;
+        // requested with the id, ahead of the allocation atomic (the compiler keeps loads behind an atomic)
+        const unsigned long long mask = live ? d.fmask[slot] : 0ull;
+        const unsigned long long hkey = live ? d.hkeys[slot] : 0ull;
         int cnt;
         const int rank = wave_excl_count(live && id < 0, cnt);
         if (cnt) {  // wave-uniform
@@ -455,10 +462,9 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
             if (live && id < 0) id = -2 - (base + rank);  // the new id, encoded below -1 until it is checked
         }
         if (!live) continue;
-        const unsigned long long mask = d.fmask[slot];
         d.fmask[slot] = 0ull;
         int kx, ky, kz;
-        unpack_key(d.hkeys[slot], kx, ky, kz);
+        unpack_key(hkey, kx, ky, kz);
         if (id <= -2) {
             id = -2 - id;
             if (id >= d.max_units) {
@@ -510,7 +516,7 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
         const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
         if (tot) atomicAdd(&d.stats[S_UNIT_INTEGRATIONS], tot);
         __threadfence();
-        s_last = atomicAdd(&d.counters[C_UNITS_DONE], 1) == (int)gridDim.x - 1;
+        s_last = atomicAdd(&d.counters[C_UNITS_DONE], 1) == active - 1;
     }
     __syncthreads();
     if (s_last && threadIdx.x < 64) {  // every workgroup's counter atomics are done: wave 0 mails the final values
