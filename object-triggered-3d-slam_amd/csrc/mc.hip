@@ -97,19 +97,24 @@ __device__ inline int find_unit(const TsdfDev& d, int x, int y, int z) {
     return -1;
 }
 
-__global__ __launch_bounds__(256) void k_mc_prepare(TsdfDev d, McDev m) {
-    const int r = blockIdx.x;
+// 16 units per workgroup, 16 lanes each (one workgroup per unit spent most of its ~8 us dispatching 5.6k workgroups of
+// one object's mesh): lane q < 16 of a unit looks up neighbour combination q, and the 16 lanes clear the unit's 384
+// edge words with 16-B stores
+constexpr int PREP_UNITS = 16;
+static_assert(EWORDS % 64 == 0, "16 lanes x 16-B stores cover a unit's edge words");
+__global__ __launch_bounds__(256) void k_mc_prepare(TsdfDev d, McDev m, int U) {
+    const int t = threadIdx.x, q16 = t & 15;
+    const int r = (int)blockIdx.x * PREP_UNITS + (t >> 4);
+    if (r >= U) return;
     const int id = (int)m.sorted_ids[r];
-    const int t = threadIdx.x;
-    if (t < 16) {
-        const int sg = t < 8 ? 1 : -1, q = t & 7;
-        const int dx = sg * ((q >> 2) & 1), dy = sg * ((q >> 1) & 1), dz = sg * (q & 1);
-        m.nbr[id * 16 + t] = q == 0 ? id
-                                    : find_unit(d, d.unit_keys[id * 3] + dx, d.unit_keys[id * 3 + 1] + dy,
-                                                d.unit_keys[id * 3 + 2] + dz);
-    }
-    if (t == 0) m.rank_of[id] = r;
-    for (int w = t; w < EWORDS; w += 256) m.eflags[(size_t)id * EWORDS + w] = 0u;
+    const int sg = q16 < 8 ? 1 : -1, q = q16 & 7;
+    const int dx = sg * ((q >> 2) & 1), dy = sg * ((q >> 1) & 1), dz = sg * (q & 1);
+    m.nbr[id * 16 + q16] = q == 0 ? id
+                                  : find_unit(d, d.unit_keys[id * 3] + dx, d.unit_keys[id * 3 + 1] + dy,
+                                              d.unit_keys[id * 3 + 2] + dz);
+    if (q16 == 0) m.rank_of[id] = r;
+    uint4* ef = reinterpret_cast<uint4*>(m.eflags + (size_t)id * EWORDS);
+    for (int w = q16; w < EWORDS / 4; w += 16) ef[w] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
@@ -236,24 +241,34 @@ __global__ __launch_bounds__(256) void k_mc_classify(TsdfDev d, McDev m) {
     }
 }
 
-// per-unit exclusive popcount prefix of the 384 bitmask words (6 waves, one word per lane)
-__global__ __launch_bounds__(EWORDS) void k_mc_count(McDev m) {
-    __shared__ int wsum[EWORDS / 64];
-    const int r = blockIdx.x;
+// per-unit exclusive popcount prefix of the 384 bitmask words: one wave per unit, 6 consecutive words per lane, 4 units
+// per workgroup (one 384-thread workgroup per unit spent most of its ~10 us dispatching one object's 5.6k workgroups)
+constexpr int CNT_UNITS = 4;
+constexpr int CNT_PER_LANE = EWORDS / 64;
+static_assert(CNT_PER_LANE == 6, "3 x 8-B loads per lane");
+__global__ __launch_bounds__(64 * CNT_UNITS) void k_mc_count(McDev m, int U) {
+    const int lane = (int)lane_id();
+    const int r = (int)blockIdx.x * CNT_UNITS + ((int)threadIdx.x >> 6);
+    if (r >= U) return;  // wave-uniform
     const int id = (int)m.sorted_ids[r];
-    const int t = threadIdx.x;
-    const int pc = __popc(m.eflags[(size_t)id * EWORDS + t]);
-    int inc = wave_incl_scan(pc);
-    if (lane_id() == 63) wsum[t >> 6] = inc;
-    __syncthreads();
-    int off = 0, tot = 0;
+    const uint2* ef = reinterpret_cast<const uint2*>(m.eflags + (size_t)id * EWORDS + lane * CNT_PER_LANE);
+    int pc[CNT_PER_LANE], loc = 0;
 #pragma unroll
-    for (int w = 0; w < EWORDS / 64; ++w) {
-        if (w < (t >> 6)) off += wsum[w];
-        tot += wsum[w];
+    for (int k = 0; k < CNT_PER_LANE / 2; ++k) {
+        const uint2 v = ef[k];
+        pc[2 * k] = __popc(v.x);
+        pc[2 * k + 1] = __popc(v.y);
+        loc += pc[2 * k] + pc[2 * k + 1];
     }
-    m.wprefix[(size_t)id * EWORDS + t] = off + inc - pc;
-    if (t == 0) m.vert_cnt[r] = tot;
+    const int inc = wave_incl_scan(loc);
+    int run = inc - loc;
+    int* wp = m.wprefix + (size_t)id * EWORDS + lane * CNT_PER_LANE;
+#pragma unroll
+    for (int k = 0; k < CNT_PER_LANE; ++k) {
+        wp[k] = run;
+        run += pc[k];
+    }
+    if (lane == 63) m.vert_cnt[r] = inc;
 }
 
 // tsdf and colour of one voxel; colour from the float64 pool when the volume keeps it (exact: a float colour widens
@@ -694,9 +709,9 @@ static ot_status mc_count(ot_tsdf* vol, hipStream_t stream, int64_t* n_vertices,
     m.tk = nullptr;
     mc_layout((char*)mb.ws, U, m);
     const unsigned g = (unsigned)U;
-    hipLaunchKernelGGL(k_mc_prepare, dim3(g), dim3(256), 0, stream, vol->dev, m);
+    hipLaunchKernelGGL(k_mc_prepare, dim3((g + PREP_UNITS - 1) / PREP_UNITS), dim3(256), 0, stream, vol->dev, m, (int)U);
     hipLaunchKernelGGL(k_mc_classify, dim3(g), dim3(256), 0, stream, vol->dev, m);
-    hipLaunchKernelGGL(k_mc_count, dim3(g), dim3(EWORDS), 0, stream, m);
+    hipLaunchKernelGGL(k_mc_count, dim3((g + CNT_UNITS - 1) / CNT_UNITS), dim3(64 * CNT_UNITS), 0, stream, m, (int)U);
     OT_LAUNCH_CHECK();
     if (U > 0x7FFFFFFF) return fail(OT_ERR_CAPACITY, "[ExtractTriangleMesh] too many units");
     // the scans mail the triangle and vertex totals (hmail words 0..3)
