@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
     ap.add_argument("--overlap", type=int, default=-1, choices=(-1, 0, 1),
                     help="headline volume's batch front end double-buffered beside the previous integrate "
-                         "(ot_tsdf_set_frontend_overlap; -1 = library default: on only for sharded volumes)")
+                         "(ot_tsdf_set_frontend_overlap; opt-in: 1 on, 0 and -1 (library default) off at every shard count)")
     ap.add_argument("--cpu-frames", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--sustain", type=float, default=12.0,
                     help="seconds of sustained headline steps after the timed ones (0 = skip): >= 12 s so a 5-s busy "
@@ -517,7 +517,8 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
 def shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, headline_ms, worlds=(1, 2, 4, 8)):
     """SURVEY 8(e) measured on one GPU: the headline step (reset + the 256-frame scan + flush) of a volume that keeps
     only rank r's units (ot_tsdf_set_shard(r, N)), for every rank r of N = 2, 4, 8, with the double-buffered front end
-    (the sharded default: batch k+1's staging / touch beside batch k's integrate) and, for comparison, without it.  A
+    (opt-in, mode 1: batch k+1's staging / touch beside batch k's integrate) and without it (the default at every
+    shard count).  A
     rank's step on an N-GPU node is this time (its shard, its front end, nothing shared with the other ranks), so the
     unsharded step (N = 1, the same method) / max over r is the strong-scaling speed-up of one object before the halo
     extraction.  The resident scan goes in with ot_tsdf_integrate_u16_frames (one host call per scan, the bits of

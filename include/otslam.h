@@ -194,7 +194,7 @@ ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames);
  * a second stream of the volume (two staging sets); readers (num_units, export, extraction, flush, reset) order the
  * caller's stream after the last integrate.  -1 (default) and 0: off (measured slower than the serial front end at 2, 4
  * and 8 shards since round 5: the two streams' events cost more than the overlap saves).  Results are identical in
- * every mode. */
+ * every mode.  Fails with OT_ERR_INVALID_ARGUMENT while frames are queued (flush on their stream first). */
 ot_status ot_tsdf_set_frontend_overlap(ot_tsdf* vol, int32_t mode);
 
 /* Number of allocated volume units.  Queued frames are integrated first, on `stream`; synchronises `stream`. */

@@ -24,7 +24,7 @@
 
 namespace ot {
 
-__constant__ signed char c_tri[256][16];
+alignas(16) __constant__ signed char c_tri[256][16];  // rows are read as one 16-B word (k_mc_emit's triangles)
 __constant__ int c_eshift[12][4];
 __constant__ int c_e2v[12][2];
 __constant__ int c_shift[8][3];
@@ -353,8 +353,33 @@ __device__ __forceinline__ int pick12(const int (&v)[12], int e) {
     return (e & 8) ? q2 : ((e & 4) ? q1 : q0);
 }
 
-// one unit's triangles (rank r): 256 lanes, one (x, y) column of 16 cubes each
+// exclusive scan over an NT-thread workgroup (every thread of the workgroup must call it: two barriers)
+template <int NT>
+__device__ inline int block_excl_scan_n(int v, int& total) {
+    __shared__ int wsum[NT / 64];
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+    const int inc = wave_incl_scan(v);
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const int s = wsum[w];
+        if (w < wid) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return off + inc - v;
+}
+
+// one unit's triangles (rank r): lanes [0, 256) one (x, y) column of 16 cubes each.  An NT-thread workgroup (k_mc_emit
+// runs the triangles in its 384-lane workgroups) keeps lanes >= 256 through the scan's barriers with no column, so every
+// thread of the workgroup reaches every barrier (no reliance on exited waves leaving the barrier count)
+template <int NT>
 __device__ __forceinline__ void mc_triangles_unit(const TsdfDev& d, const McDev& m, int32_t* T, int r, int t) {
+    static_assert(NT >= 256 && NT % 64 == 0, "a unit's 256 columns need >= 256 lanes");
+    const bool col = t < 256;
     __shared__ int snbr[8];
     __shared__ long long sbase[8];
     const int id = (int)m.sorted_ids[r];
@@ -364,13 +389,15 @@ __device__ __forceinline__ void mc_triangles_unit(const TsdfDev& d, const McDev&
         snbr[t] = o;
         sbase[t] = o >= 0 ? m.vert_base[m.rank_of[o]] : 0;
     }
-    const uint4 q = *reinterpret_cast<const uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16);
+    uint4 q = make_uint4(0u, 0u, 0u, 0u);
+    if (col) q = *reinterpret_cast<const uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16);
     const unsigned cw[4] = {q.x, q.y, q.z, q.w};
     int cnt = 0;
 #pragma unroll
     for (int z = 0; z < UNIT_RES; ++z) cnt += c_ntri[(cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu];
     int total;
-    const int pre = block_excl_scan_256(cnt, total);  // contains __syncthreads (snbr visible after)
+    const int pre = block_excl_scan_n<NT>(cnt, total);  // contains __syncthreads (snbr visible after)
+    if (!col) return;  // no barrier below
     long long out = m.tri_base[r] + pre;
     {  // per cube its first triangle inside the unit (<= 5 * 4096 < 2^16): the vertex-normal walk's index
         unsigned off[8];
@@ -448,17 +475,16 @@ __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, doub
     mc_vertices_unit(d, m, vl, V, VC, blockIdx.x, threadIdx.x);
 }
 __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_t* T) {
-    mc_triangles_unit(d, m, T, blockIdx.x, threadIdx.x);
+    mc_triangles_unit<256>(d, m, T, blockIdx.x, threadIdx.x);
 }
-// The emission in ONE launch: workgroups [0, U) the triangles (their upper 128 lanes leave at once; a barrier counts
-// only the waves still running), [U, 2U) the vertices.  Replaces the vertices on the side stream beside the triangles:
+// The emission in ONE launch: workgroups [0, U) the triangles (their upper 128 lanes take part in the scan's barriers
+// with no column, then leave), [U, 2U) the vertices.  Replaces the vertices on the side stream beside the triangles:
 // that fork and join cost the GPU ~25 us of idle queue time per extraction (tools/event_gap.hip, r05j)
 __global__ __launch_bounds__(EWORDS) void k_mc_emit(TsdfDev d, McDev m, int U, double vl, double* V, double* VC,
                                                     int32_t* T) {
     const int b = blockIdx.x;
     if (b < U) {
-        if (threadIdx.x >= 256) return;
-        mc_triangles_unit(d, m, T, b, threadIdx.x);
+        mc_triangles_unit<EWORDS>(d, m, T, b, threadIdx.x);
     } else {
         mc_vertices_unit(d, m, vl, V, VC, b - U, threadIdx.x);
     }

@@ -14,7 +14,9 @@
 // holds, the pool and the hash grow (records copied, keys rehashed) and the batch's dropped units are integrated
 // again from its staged frames (settle_batch), so the result is the one an unbounded pool gives.
 #include <algorithm>
+#include <sched.h>
 #include <chrono>
+#include <thread>
 #include <cstring>
 #include <type_traits>
 
@@ -1738,27 +1740,41 @@ ot_status mail_words(ot_tsdf* vol, const MailSrc& s, hipStream_t stream) {
 // The stream is polled only once the wait has lasted 20 ms (then every ~1 ms): a stream query puts commands on the
 // stream's queue, and while the host spins the queue already holds the work launched after the mailing kernel -- polling
 // every ~20 us had left ~6 us of idle GPU behind that work at each wait (host launch trace against the kernel trace,
-// tools/launch_lag.py, r05ah: the gaps before the unit sort and before the sampler)
+// tools/launch_lag.py, r05ah: the gaps before the unit sort and before the sampler).
+// Host CPU bound: the loop spins with `pause` only for the first ~50 us -- the mails the headline
+// waits for arrive within that (the units kernel ~10 us after the touch, the marching-cubes totals) -- then yields the
+// core on every check (sched_yield: a rank's other threads and RCCL's proxy threads get it), and past 2 ms sleeps
+// 20 us per check, so 8 ranks x 2 object streams waiting on a long kernel do not hold 16 cores at 100 %.
 ot_status mail_wait(const unsigned* word, unsigned seq, hipStream_t stream) {
     using clk = std::chrono::steady_clock;
-    clk::time_point next{};
+    const clk::time_point t0 = clk::now();
+    const clk::time_point t_yield = t0 + std::chrono::microseconds(50);
+    const clk::time_point t_sleep = t0 + std::chrono::milliseconds(2);
+    clk::time_point next = t0 + std::chrono::milliseconds(20);
     for (unsigned it = 1;; ++it) {
         if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return OT_OK;
-        if ((it & 1023u) == 0) {
-            const clk::time_point now = clk::now();
-            if (it == 1024u) {
-                next = now + std::chrono::milliseconds(20);
-            } else if (now >= next) {  // has the stream faulted, or drained without the mail?
-                next = now + std::chrono::milliseconds(1);
-                const hipError_t q = hipStreamQuery(stream);
-                if (q == hipSuccess) {
-                    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return OT_OK;
-                    return fail(OT_ERR_HIP, "mailbox: the stream drained without the kernel's mail");
-                }
-                if (q != hipErrorNotReady) OT_HIP_TRY(q);
-            }
+        const bool spin = (it & 63u) != 0;
+        if (spin && it < (1u << 20)) {  // the clock is read every 64 polls while spinning
+            __builtin_ia32_pause();
+            continue;
         }
-        __builtin_ia32_pause();
+        const clk::time_point now = clk::now();
+        if (now < t_yield) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        it = 1u << 20;  // from here every poll reads the clock
+        if (now >= next) {  // has the stream faulted, or drained without the mail?
+            next = now + std::chrono::milliseconds(1);
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return OT_OK;
+                return fail(OT_ERR_HIP, "mailbox: the stream drained without the kernel's mail");
+            }
+            if (q != hipErrorNotReady) OT_HIP_TRY(q);
+        }
+        if (now < t_sleep) sched_yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
 }
 
@@ -2059,9 +2075,12 @@ ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames) {
 ot_status ot_tsdf_set_frontend_overlap(ot_tsdf* vol, int32_t mode) {
     if (!vol || mode < -1 || mode > 1)
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] front-end overlap mode must be -1, 0 or 1");
-    ot_status st = tsdf_flush(vol, nullptr);  // queued frames (and a running integrate) under the old mode
-    if (st != OT_OK) return st;
-    if (vol->istream) OT_HIP_TRY(hipStreamSynchronize(vol->istream));
+    // the mode changes only on a drained volume: queued frames would be staged on whichever stream this call named,
+    // not the one their producers ran on -- flush or read the volume on the frames' stream first
+    if (!vol->pending.empty())
+        return fail(OT_ERR_INVALID_ARGUMENT,
+                    "[ScalableTSDFVolume] front-end overlap can change only with no queued frames (flush first)");
+    if (vol->istream) OT_HIP_TRY(hipStreamSynchronize(vol->istream));  // a running integrate of the old mode
     vol->last_set = -1;
     vol->overlap_mode = mode;
     return OT_OK;

@@ -3,7 +3,7 @@ meshes.  File decode is host work in the reference too (reconstruct_rgbd_filter.
 timed hot path; arrays are uploaded to HBM by the first kernel that needs them.
 
 PLY layout follows Open3D's writer: binary_little_endian, vertex x/y/z as double, nx/ny/nz double,
-red/green/blue uchar (round(clip(c, 0, 1) * 255)), faces as `list uchar int vertex_indices`.
+red/green/blue uchar (std::round(clip(c, 0, 1) * 255), half away from zero), faces as `list uchar int vertex_indices`.
 """
 from __future__ import annotations
 
@@ -47,7 +47,16 @@ _PLY_TYPES = {"char": "i1", "int8": "i1", "uchar": "u1", "uint8": "u1", "short":
 
 
 def _color_to_u8(c):
-    return np.round(np.clip(c, 0.0, 1.0) * 255.0).astype(np.uint8)
+    """Open3D's utility::ColorToUint8 (written by write_point_cloud, reconstruct_rgbd_filter.py:140, and
+    hybrid_map.py:121): uint8_t(std::round(std::min(1., std::max(0., c)) * 255.)).  std::max(0., NaN) is 0 and
+    std::round rounds half AWAY from zero (np.round rounds half to even, which differs at k + 0.5).  x = v * 255 is
+    one float64 rounding, as in C++; on [0, 255] x - floor(x) is exact, so the tie test is exact too."""
+    c = np.asarray(c, np.float64)
+    v = np.where(c > 0.0, c, 0.0)       # std::max(0., c): (0. < c) ? c : 0.
+    v = np.where(v < 1.0, v, 1.0)       # std::min(1., v): (v < 1.) ? v : 1.
+    x = v * 255.0
+    f = np.floor(x)
+    return (f + (x - f >= 0.5)).astype(np.uint8)
 
 
 def _write_ply(filename, V, N=None, Cc=None, T=None):

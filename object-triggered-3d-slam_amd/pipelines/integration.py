@@ -71,7 +71,9 @@ class ScalableTSDFVolume:
     def set_frontend_overlap(self, mode):
         """Double-buffered batch front end (ot_tsdf_set_frontend_overlap): 1 on, 0 and -1 (default) off -- measured slower
         than the serial front end at 2, 4 and 8 shards.
-        Batch k+1's staging / touch run beside batch k's integrate; results are identical in every mode."""
+        Batch k+1's staging / touch run beside batch k's integrate; results are identical in every mode.  Queued
+        frames are integrated first, on the facade's stream (the C call refuses a volume with queued frames)."""
+        self.flush()
         L.call("ot_tsdf_set_frontend_overlap", self._h, int(mode))
 
     def set_batch(self, frames):
@@ -273,6 +275,8 @@ class ScalableTSDFVolume:
             mesh._vc = _Arr(dev=VC[:nv.value])
         if nv.value == 0:
             return mesh, None
+        if nt.value == 0:  # vertices but no triangles (marching cubes cannot emit this): Open3D's sampler raises
+            raise RuntimeError("[SamplePointsUniformly] Input mesh has no triangles.")
         if N is not None:
             for t in (V, T, N):  # allocated on the caller's stream, used on the side stream
                 t.record_stream(side)
