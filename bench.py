@@ -259,6 +259,9 @@ def main():
     fms, fbatches = C.c_double(0.0), C.c_int64(0)  # each batch's front end (staging + touch + unit headers)
     L.call("ot_tsdf_frontend_time", vol, C.byref(fms), C.byref(fbatches))
     L.call("ot_tsdf_set_profiling", vol, 0)
+    # the step's batches (the profiled step began with a reset): units touched per batch and how many were new
+    sb, sub, sfresh = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+    L.call("ot_tsdf_batch_stats", vol, C.byref(sb), C.byref(sub), C.byref(sfresh))
 
     frames_total = world * args.frames * args.steps
     value = frames_total / elapsed
@@ -295,9 +298,25 @@ def main():
     if hbm_achieved:  # kept under the old names too (round-3/4 records)
         roofline["hbm_achieved"] = roofline["achieved"]
         roofline["hbm_frac"] = roofline["frac"]
+        roofline["traffic_level"] = ("L2-miss (fabric) bytes: FETCH_SIZE / WRITE_SIZE count the requests that leave "
+                                     "the XCD's L2, including those the Infinity Cache (MALL) then serves "
+                                     "(MI355X_MICROARCH.md), so the DRAM bytes may be lower and `frac` is an upper "
+                                     "bound on the HBM fraction")
+    # compulsory bytes per launch: the touched units' state read once (units new in the batch
+    # start from zero: not read) and written once, plus the batch's staged frames read once (8-B depth / multiplier +
+    # 4-B colour per pixel) -- what a kernel that re-fetched nothing would move
+    rec = 4096 * (32 if args.color_bits == 64 else 20)
+    if sb.value > 0 and klaunch.value > 0:
+        comp = ((2 * sub.value - sfresh.value) * rec + 12.0 * W * H * args.frames) / klaunch.value
+        roofline["compulsory_bytes"] = round(comp)
+        roofline["compulsory_basis"] = (f"per launch: (2 x {sub.value / sb.value:.0f} touched units - "
+                                        f"{sfresh.value / sb.value:.0f} new) x {rec} B records + 12 B x W x H x frames "
+                                        "of staged pixels (ot_tsdf_batch_stats over one step)")
+        if traffic:
+            roofline["traffic_over_compulsory"] = round(traffic / comp, 3)
     ient, _ = _pmc_entry(args, L, kname, pmc_cfg)
     # the ceilings that actually bind this kernel: vector-ALU issue and the vector-memory data path (PMC, same build)
-    for key in ("valu_busy_frac", "ta_busy_frac", "td_busy_frac"):
+    for key in ("valu_busy_frac", "ta_busy_frac", "td_busy_frac", "tcc_hit_frac"):
         if ient and ient.get(key) is not None:
             roofline[key] = round(ient[key], 4)
     if ient and ient.get("valu_busy_frac") is not None:
@@ -451,7 +470,7 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
         v = integ.ScalableTSDFVolume(voxel_length=args.voxel, sdf_trunc=args.sdf_trunc,
                                      color_type=integ.TSDFVolumeColorType.RGB8)
         if shard:
-            v.set_shard(rank, world)
+            v.set_shard_sector(rank, world, scan_centre_xy(ext))
         if args.batch > 0:
             v.set_batch(args.batch)
         return v
@@ -502,44 +521,55 @@ def spatial_shard(args, L, lib, synth, torch, dist, rank, world, units_rank0):
                      torch.equal(mesh._vc.dev(), m0._vc.dev()))
         del ref
     return {"workload": f"configs[1] scan (seed 0) as ONE object spatially sharded over {world} GPU(s): unit owner = "
-                        f"hash(ownership block key) mod {world}, blocks of {4 if world <= 4 else 2}^3 units "
-                        "(tsdf.h unit_owner), every rank integrates every frame into its own units; marching cubes "
-                        "with a border halo routed to the owners of the -x/-y/-z neighbours",
+                        f"the unit centre's azimuth sector (1/{world} of the turn) around the mean camera position "
+                        "(tsdf.h unit_owner, ot_tsdf_set_shard_sector), every rank integrates every frame into its own "
+                        "units and stages only the image tiles they project to; marching cubes with a border halo "
+                        "routed to the owners of the -x/-y/-z neighbours",
             "scaling": "strong", "frames_per_s": round(args.frames * 1.0 / dt, 1), "ms_per_step": round(dt * 1e3, 3),
             "units_per_rank_min": min(cnt), "units_per_rank_max": max(cnt), "assemble_ms": round(t_asm * 1e3, 2),
             "assemble_bytes": border_bytes, "allgather_border_bytes": allgather_border, "whole_unit_bytes": whole,
             "mesh_vertices": int(mesh._v.dev().shape[0]), "mesh_matches_unsharded": match,
             "frontend_ms_per_batch_max": round(float(per[:, 0].max()), 5),
             "integrate_ms_per_batch_max": round(float(per[:, 1].max()), 5),
-            "frontend_note": "every rank stages and unprojects every frame (undivided); the integrate divides by units"}
+            "frontend_note": "every rank unprojects every stride sample; staging divides by the tiles its units project "
+                             "to (split front end); the integrate divides by units"}
+
+
+def scan_centre_xy(ext):
+    """The centre of a ring scan for sector ownership: the mean camera position (x, y) over the frames (camera centre
+    = -R^T t of each world->camera extrinsic).  A reference caller knows it as the ScanObject goal's x, y."""
+    e = np.asarray(ext, np.float64).reshape(-1, 4, 4)
+    c = -np.einsum("nji,nj->ni", e[:, :3, :3], e[:, :3, 3])
+    return float(c[:, 0].mean()), float(c[:, 1].mean())
 
 
 def shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, headline_ms, worlds=(1, 2, 4, 8)):
     """SURVEY 8(e) measured on one GPU: the headline step (reset + the 256-frame scan + flush) of a volume that keeps
-    only rank r's units (ot_tsdf_set_shard(r, N)), for every rank r of N = 2, 4, 8, with the double-buffered front end
-    (opt-in, mode 1: batch k+1's staging / touch beside batch k's integrate) and without it (the default at every
-    shard count).  A
-    rank's step on an N-GPU node is this time (its shard, its front end, nothing shared with the other ranks), so the
-    unsharded step (N = 1, the same method) / max over r is the strong-scaling speed-up of one object before the halo
-    extraction.  The resident scan goes in with ot_tsdf_integrate_u16_frames (one host call per scan, the bits of
-    256 per-frame calls): at 1/8 of the integrate a rank's GPU step is shorter than 256 ctypes round trips."""
-    W, H = intr.width, intr.height
-    npx = W * H
+    only rank r's units, for every rank r of N = 2, 4, 8, under both ownerships: `blocks` (ot_tsdf_set_shard: hashed
+    blocks of units) and `sectors` (ot_tsdf_set_shard_sector: azimuth sectors around the scan centre, the product
+    choice since round 6) -- both on the split front end (a sharded volume stages only the image tiles its batch's
+    units project to).  A rank's step on an N-GPU node is this time (its shard, its front end, nothing shared with the
+    other ranks), so the unsharded step (N = 1, the same method) / max over r is the strong-scaling speed-up of one
+    object before the halo extraction.  The resident scan goes in with ot_tsdf_integrate_u16_frames (one host call
+    per scan, the bits of 256 per-frame calls): at 1/8 of the integrate a rank's GPU step is shorter than 256 ctypes
+    round trips."""
+    cx, cy = scan_centre_xy(ext[:args.frames])
     integrate_frames, pintr = lib.ot_tsdf_integrate_u16_frames, C.byref(intr)
     dp, cp, ep = d_depth.data_ptr(), d_color.data_ptr(), ext.ctypes.data
     out = {}
     for N in worlds:
         per_mode = {}
-        for mode in ((1, 0) if N > 1 else (0,)):
+        for mode in (("blocks", "sectors") if N > 1 else ("unsharded",)):
             worst, units = 0.0, []
             for r in range(N):
                 vol = C.c_void_p()
                 L.call("ot_tsdf_create", args.voxel, args.sdf_trunc, L.OT_COLOR_RGB8, 16, 4, 0, C.byref(vol))
                 try:
                     L.call("ot_tsdf_set_color_precision", vol, args.color_bits)
-                    if N > 1:
+                    if mode == "blocks":
                         L.call("ot_tsdf_set_shard", vol, r, N)
-                    L.call("ot_tsdf_set_frontend_overlap", vol, mode)
+                    elif mode == "sectors":
+                        L.call("ot_tsdf_set_shard_sector", vol, r, N, cx, cy)
 
                     def step():
                         L.call("ot_tsdf_reset_async", vol, stream)
@@ -560,27 +590,26 @@ def shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, h
                     units.append(nu.value)
                 finally:
                     L.call("ot_tsdf_destroy", vol)
-            per_mode["overlap" if mode else "serial"] = {"rank_step_ms_max": round(worst, 4)}
-        per_mode["units_per_rank_min_max"] = [min(units), max(units)]
+            per_mode[mode] = {"rank_step_ms_max": round(worst, 4), "units_per_rank_min_max": [min(units), max(units)]}
         out[str(N)] = per_mode
-    base = out["1"]["serial"]["rank_step_ms_max"]
+    base = out["1"]["unsharded"]["rank_step_ms_max"]
     for N, per_mode in out.items():
-        for m in ("overlap", "serial"):
-            if m in per_mode and per_mode[m]["rank_step_ms_max"]:
-                per_mode[m]["speedup"] = round(base / per_mode[m]["rank_step_ms_max"], 2)
+        for m in per_mode.values():
+            if m["rank_step_ms_max"]:
+                m["speedup"] = round(base / m["rank_step_ms_max"], 2)
     return {"method": "every rank's shard of the headline scan timed on this GPU (reset + 256 frames in one "
                       f"ot_tsdf_integrate_u16_frames call + flush, {args.shard_steps} steps after 3 warm-up), max over "
-                      "ranks; speedup = the unsharded volume's step (N = 1, same method) / that",
+                      "ranks; speedup = the unsharded volume's step (N = 1, same method) / that; sectors centred on "
+                      f"the mean camera position ({cx:.4f}, {cy:.4f})",
             "headline_ms_per_step": round(headline_ms, 4), "worlds": out}
 
 
 def spatial_amdahl(frontend_ms, integrate_ms, measured=None):
-    """Amdahl bound of ONE object spatially sharded over N GPUs, from this run's per-batch device times:
-    every rank stages every pixel of every frame and unprojects every stride sample (the front end: staging + touch +
-    unit headers; only the touch's hash inserts divide), while the integrate divides by the units each rank owns.
-    Speed-up cap at N = (F + I) / (F + I / N).  Integrating from the raw frames instead of staging them (no per-rank
-    staging) was measured: the integrate gets 1.9x slower per unit (two gathers per voxel visit instead of one), more
-    than the staging it saves."""
+    """Amdahl bound of ONE object spatially sharded over N GPUs, from this run's per-batch device times
+    of the UNSHARDED volume: if every rank repeated the whole front end (staging + touch + unit headers) while the
+    integrate divides by the units each rank owns, the speed-up at N would be capped at (F + I) / (F + I / N).  Since
+    round 6 a sharded rank's front end is split and stages only the tiles its units project to (sector ownership:
+    ~1/N of the pixels of a ring scan), so `measured` (every rank's shard timed) can pass this cap."""
     F, I = frontend_ms, integrate_ms
     if F <= 0 or I <= 0:
         return None

@@ -197,6 +197,12 @@ ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames);
  * every mode.  Fails with OT_ERR_INVALID_ARGUMENT while frames are queued (flush on their stream first). */
 ot_status ot_tsdf_set_frontend_overlap(ot_tsdf* vol, int32_t mode);
 
+/* Batch statistics since the last reset (measurement; not an Open3D API): integrate batches run, the units they touched
+ * summed over batches, and how many of those were new in their batch (allocated by it: their state starts at zero and
+ * is not read).  Frames still queued are not counted (flush first).  The bench's compulsory-bytes figure of the integrate kernel:
+ * (2 x unit_batches - new_units) unit records + the staged pixels. */
+ot_status ot_tsdf_batch_stats(ot_tsdf* vol, int64_t* batches, int64_t* unit_batches, int64_t* new_units);
+
 /* Number of allocated volume units.  Queued frames are integrated first, on `stream`; synchronises `stream`. */
 ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n_units_host, void* stream);
 /* Cumulative voxel updates and volume-unit integrations since create/reset (flushes on `stream`, synchronises it). */
@@ -248,6 +254,13 @@ ot_status ot_tsdf_set_shard(ot_tsdf* vol, int32_t rank, int32_t world);
  * of the block key).  Set by ot_tsdf_set_shard to 2 (4^3 units) up to 4 ranks and 1 beyond; call after it, before the
  * first integrate. */
 ot_status ot_tsdf_set_shard_block(ot_tsdf* vol, int32_t log2_units);
+/* Sector ownership (round 6): the unit is owned by the azimuth sector (world equal sectors of the pseudo-angle; the true
+ * 90 / 45 degree sectors at 4 / 8 ranks) of its centre around the scan centre (cx, cy) in metres -- for a ring scan the
+ * look-at point, e.g. the ScanObject goal's x, y (otslam_interfaces/action/ScanObject.action) or the mean camera
+ * position.  Each frame then sees a contiguous arc of a rank's units, so a sharded rank stages only the image tiles its
+ * units project to (the split front end: tools/shard_sector_model.py).  Integer arithmetic on the unit
+ * key only: results are exact for any centre.  Call instead of ot_tsdf_set_shard, before the first integrate. */
+ot_status ot_tsdf_set_shard_sector(ot_tsdf* vol, int32_t rank, int32_t world, double cx, double cy);
 /* Border-halo routing: per border row key int32 [n][3] (export_border's), the bitmask (bit r = rank r,
  * world <= 64) of the other ranks that own one of the unit's 7 -x/-y/-z neighbours -- the only ranks whose marching
  * cubes can read the row.  Device pointers; ordered on `stream`. */

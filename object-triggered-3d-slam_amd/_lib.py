@@ -81,6 +81,8 @@ SIGNATURES = {
     "ot_tsdf_import_units_color64": [_p, _i64, _p, _p, _p, _p, _p],
     "ot_tsdf_set_shard": [_p, _i32, _i32],
     "ot_tsdf_set_shard_block": [_p, _i32],
+    "ot_tsdf_set_shard_sector": [_p, _i32, _i32, _d, _d],
+    "ot_tsdf_batch_stats": [_p, _pi64, _pi64, _pi64],
     "ot_tsdf_border_destinations": [_p, _i64, _p, _p, _p],
     "ot_tsdf_mesh_serial": [_p, _pi64],
     "ot_tsdf_mesh_vertex_normals": [_p, _i64, _p, _i64, _p, _i64, _p, _p],
@@ -143,6 +145,8 @@ TEST_SIGNATURES = {
     "otx_integrate_fine": [_i32],
     "otx_touch_stage_blocks": [_i32],
     "otx_touch_frames": [_i32],
+    "otx_split_frontend": [_i32],
+    "otx_integrate_depth": [_i32],
     "otx_mc_emit_fork": [_i32],
     "otx_normals_at": [_i32],
     "otx_sampler_hi_stream": [_i32],

@@ -56,20 +56,41 @@ struct TsdfDev {
     int shard_rank;   // spatial sharding of one volume over `shard_world` GPUs: this volume keeps only the units
     int shard_world;  // with owner(key) == shard_rank (<= 1: no sharding)
     int shard_shift;  // ownership granularity: blocks of 2^shift units per axis share an owner
+    int shard_mode;   // SHARD_BLOCKS: hashed blocks of 2^shift units; SHARD_SECTORS: azimuth sectors around a centre
+    int shard_cx2, shard_cy2;  // sector centre in half units (round(2 * centre / unit_length)) per axis
 };
+constexpr int SHARD_BLOCKS = 0;
+constexpr int SHARD_SECTORS = 1;
 
-// owner rank of a unit: a hash of its block key (unit key >> shard_shift per axis), independent of the
-// table's slot hash mix64(key), so a shard's keys still spread over all slots.  Blocks of units keep most marching-cubes
-// neighbours on one rank (the border halo only crosses block faces) while still balancing the ranks' units.
-__host__ __device__ inline int unit_owner(int shard_world, int shard_shift, int x, int y, int z) {
-    const unsigned long long bk = pack_key(x >> shard_shift, y >> shard_shift, z >> shard_shift);
-    return (int)((unsigned)(mix64(bk + 0x9E3779B97F4A7C15ull) >> 32) % (unsigned)shard_world);
+// owner rank of a unit, a function of its key alone (exact on host and device: integers only).
+// SHARD_BLOCKS: a hash of its block key (unit key >> shard_shift per axis), independent of the table's slot hash
+// mix64(key), so a shard's keys still spread over all slots.  Blocks of units keep most marching-cubes neighbours on one
+// rank (the border halo only crosses block faces) while still balancing the ranks' units.
+// SHARD_SECTORS (round 6): the azimuth sector of the unit's centre around the scan centre (x, y).  A ring scan's frames
+// each see a contiguous arc of the object, so a rank's units project into a fraction of every frame and its front end
+// stages only those tiles (tools/shard_sector_model.py: 0.23 of the pixels at 8 ranks against 0.54 for blocks).  The
+// sector is floor(N * pa / 4) of the pseudo-angle pa = quadrant + a / (a + b) in [0, 4), exact in int64 (the octants at
+// N = 8 and the quadrants at N = 4 are the true 45 / 90 degree sectors); the centre point itself goes to sector 0.
+__host__ __device__ inline int unit_sector(long long X, long long Y, int n) {
+    if (X == 0 && Y == 0) return 0;
+    long long a, b, q;
+    if (X > 0 && Y >= 0) { q = 0; a = Y; b = X; }
+    else if (X <= 0 && Y > 0) { q = 1; a = -X; b = Y; }
+    else if (X < 0 && Y <= 0) { q = 2; a = -Y; b = -X; }
+    else { q = 3; a = X; b = -Y; }
+    return (int)(((q * (a + b) + a) * (long long)n) / (4 * (a + b)));
+}
+__host__ __device__ inline int unit_owner(const TsdfDev& d, int x, int y, int z) {
+    if (d.shard_mode == SHARD_SECTORS)
+        return unit_sector(2ll * x + 1 - d.shard_cx2, 2ll * y + 1 - d.shard_cy2, d.shard_world);
+    const unsigned long long bk = pack_key(x >> d.shard_shift, y >> d.shard_shift, z >> d.shard_shift);
+    return (int)((unsigned)(mix64(bk + 0x9E3779B97F4A7C15ull) >> 32) % (unsigned)d.shard_world);
 }
 __host__ __device__ inline bool unit_owned(const TsdfDev& d, unsigned long long key) {
     if (d.shard_world <= 1) return true;
     int x, y, z;
     unpack_key(key, x, y, z);
-    return unit_owner(d.shard_world, d.shard_shift, x, y, z) == d.shard_rank;
+    return unit_owner(d, x, y, z) == d.shard_rank;
 }
 
 // a newly allocated unit widens the volume's key bounds (read back with the counters: the sorted-unit order packs keys
@@ -204,6 +225,16 @@ struct ot_tsdf {
         hipEvent_t ev_done = nullptr;       // the set's integrate (the set's next front end waits for it)
     } bset[2];
     int overlap_mode = -1;        // -1 (default) and 0 off, 1 on
+    // Split front end of a sharded volume (round 6): the touch stages nothing (only each stride sample's own pixel, for a
+    // replay), k_stage_mask marks the image tiles the batch's owned units can project to, k_stage_tiles stages those.
+    unsigned* tmask = nullptr;    // device [2 parities][MAX_BATCH][tile rows][words per row]
+    int64_t tmask_words = 0;      // words per parity
+    int tmask_w = 0, tmask_h = 0;  // the image size the masks are laid out for
+    int tmask_par = 0;            // parity of the next split batch (the other one is cleared by its mask kernel)
+    int split_mode = -1;          // -1 (default): split for sharded volumes; 0 off; 1 on (test hook)
+    // batch statistics since reset (ot_tsdf_batch_stats; the bench's compulsory-bytes figure): batches, units touched
+    // summed over batches, units new in their batch; units the last batch left (-1: unknown after an import)
+    int64_t stat_batches = 0, stat_unit_batches = 0, stat_fresh = 0, stat_prev_units = 0;
     int64_t last_batch_slots = -1;  // units the last batch touched (mailed): the next batch's integrate granularity
     int bset_next = 0;            // set of the next batch (alternates in overlap mode)
     int last_set = -1;            // set of the last batch whose integrate ran on istream (joined by readers)

@@ -14,11 +14,13 @@
 // holds, the pool and the hash grow (records copied, keys rehashed) and the batch's dropped units are integrated
 // again from its staged frames (settle_batch), so the result is the one an unbounded pool gives.
 #include <algorithm>
+#include <cmath>
 #include <sched.h>
 #include <chrono>
 #include <thread>
 #include <cstring>
 #include <type_traits>
+#include <utility>
 
 #include "compact.h"
 #include "sort.h"
@@ -217,6 +219,8 @@ struct BatchTouchParams {
     int tiles;          // touch workgroups per frame group (blockIdx.x below it)
     int stage_blocks;   // staging-only workgroups per frame group after them (0: each touch workgroup stages a share)
     int tf;             // frames per group (TF)
+    int sample_stage;   // split front end (stage_blocks < 0): each stride sample stores its own pixel's staged pair
+                        // (a replay touch reads it; k_stage_tiles stages only the owned units' footprints)
 };
 
 __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int pc, int x, int y, int z) {
@@ -329,6 +333,9 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
             const BatchFrame& fr = frames[f];
             const int64_t pix = (int64_t)r * p.W + c;  // the staged depth, computed as the staging does
             const float df = REPLAY ? fr.dm[pix].x : fr.depth16 ? prep_depth(fr, fr.depth16[pix]) : fr.depthf[pix];
+            if constexpr (!REPLAY) {
+                if (p.sample_stage) fr.dm[pix] = make_float2(df, p.mult[pix]);  // what the staging writes there
+            }
             if (!(df > 0.0f)) continue;
             const double z = (double)df;
             const double x = ((double)c - p.cx) * z / p.fx;
@@ -534,6 +541,116 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
     }
 }
 
+// ------------------------------------------------------------------------------------ split front end (sharded)
+// A rank of a spatially sharded volume integrates only its own units, so it reads only the pixels those units project
+// to.  With sector ownership (tsdf.h unit_owner) that is a fraction of every frame (tools/shard_sector_model.py, the
+// configs[1] ring scan: 0.23 of the 32x16 tiles at 8 ranks; 0.54 with hashed blocks), so the front end splits:
+// touch (no staging) -> units -> k_stage_mask (the tiles each (owned unit, frame) pair can project to) -> k_stage_tiles
+// (only those tiles).  The staged values are a pure function of the pixel, so staging a superset changes no bit.
+constexpr int STX = 32, STY = 16;  // staging tile: 32 pixels (one 8-lane group of quads per row) x 16 rows
+struct StageMaskParams {
+    int W, H, tiles_x, tiles_y, wpr;  // wpr: 32-bit mask words per tile row
+    float fx, fy, cx, cy, vl, half;
+    double unit_len;
+    int nframes;
+};
+// Footprint of a unit in a frame: the voxel centres span the box [p(0), p(15)] per axis (the integrate's own float
+// expressions for x, y = 0 and 15; z from the unit origin by 15 voxel lengths), so in exact arithmetic their projections
+// lie in the projected corners' bounding box (the box is in front of the camera).  The integrate's float projection of a
+// voxel differs from the exact one by < 0.02 px here (|pc| error ~6e-6 m at z >= 0.05 m); the box is widened by 2 px
+// and any corner nearer than 5 cm marks the whole frame.
+__global__ __launch_bounds__(256) void k_stage_mask(const BatchFrame* __restrict__ frames, StageMaskParams q,
+                                                    const UnitWork* __restrict__ work, const int* __restrict__ wcount,
+                                                    unsigned* __restrict__ mask, unsigned* __restrict__ other,
+                                                    int other_words) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < other_words; i += gridDim.x * 256) other[i] = 0u;  // next batch's
+    const int n = __builtin_amdgcn_readfirstlane(*wcount);
+    const int lane = threadIdx.x & 63;
+    for (int u = blockIdx.x * 4 + (int)(threadIdx.x >> 6); u < n; u += gridDim.x * 4) {  // one wave per unit
+        const UnitWork& w = work[u];
+        const unsigned long long m = w.mask;
+        if (lane >= q.nframes || !((m >> lane) & 1ull)) continue;
+        const BatchFrame& fr = frames[lane];
+        const float ox = (float)((double)w.kx * q.unit_len);
+        const float oy = (float)((double)w.ky * q.unit_len);
+        const float oz = (float)((double)w.kz * q.unit_len);
+        const double xs[2] = {(double)((q.half + q.vl * 0.0f) + ox), (double)((q.half + q.vl * 15.0f) + ox)};
+        const double ys[2] = {(double)((q.half + q.vl * 0.0f) + oy), (double)((q.half + q.vl * 15.0f) + oy)};
+        const double zs[2] = {(double)(q.half + oz), (double)(q.half + oz) + 15.0 * (double)q.vl};
+        bool full = false;
+        double umin = 1e300, umax = -1e300, vmin = 1e300, vmax = -1e300;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const double px = xs[c & 1], py = ys[(c >> 1) & 1], pz = zs[c >> 2];
+            double pc[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+                pc[r] = (double)fr.E[r * 4 + 0] * px + (double)fr.E[r * 4 + 1] * py + (double)fr.E[r * 4 + 2] * pz +
+                        (double)fr.E[r * 4 + 3];
+            if (!(pc[2] >= 0.05)) {
+                full = true;
+            } else {
+                const double uf = (double)q.fx * pc[0] / pc[2] + (double)q.cx + 0.5;
+                const double vf = (double)q.fy * pc[1] / pc[2] + (double)q.cy + 0.5;
+                umin = fmin(umin, uf), umax = fmax(umax, uf), vmin = fmin(vmin, vf), vmax = fmax(vmax, vf);
+            }
+        }
+        int u0 = 0, u1 = q.W - 1, v0 = 0, v1 = q.H - 1;
+        if (!full) {
+            if (umax < -2.0 || vmax < -2.0 || umin > (double)q.W + 2.0 || vmin > (double)q.H + 2.0) continue;
+            u0 = max(0, (int)floor(umin) - 2), u1 = min(q.W - 1, (int)floor(umax) + 2);
+            v0 = max(0, (int)floor(vmin) - 2), v1 = min(q.H - 1, (int)floor(vmax) + 2);
+            if (u0 > u1 || v0 > v1) continue;
+        }
+        const int tx0 = u0 / STX, tx1 = u1 / STX, ty0 = v0 / STY, ty1 = v1 / STY;
+        unsigned* row = mask + (size_t)lane * q.tiles_y * q.wpr;
+        for (int ty = ty0; ty <= ty1; ++ty)
+            for (int k = tx0 >> 5; k <= (tx1 >> 5); ++k) {
+                const int a = max(tx0, k * 32) - k * 32, b = min(tx1, k * 32 + 31) - k * 32;  // bits [a, b]
+                const unsigned bits = (b == 31 ? ~0u : ((1u << (b + 1)) - 1u)) & ~((1u << a) - 1u);
+                atomicOr(row + ty * q.wpr + k, bits);
+            }
+    }
+}
+
+// stage the marked tiles: one wave per tile, 8 lanes per row of 32 pixels (8 quads), 8 rows per step
+__global__ __launch_bounds__(256) void k_stage_tiles(const BatchFrame* __restrict__ frames, const float* __restrict__ mult,
+                                                     const unsigned* __restrict__ mask, int W, int H, int tiles_x,
+                                                     int tiles_y, int wpr, int64_t npx) {
+    const int f = blockIdx.y;
+    const int t = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (t >= tiles_x * tiles_y) return;
+    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    if (!((mask[((size_t)f * tiles_y + ty) * wpr + (tx >> 5)] >> (tx & 31)) & 1u)) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int x0 = tx * STX, x1 = min(W, x0 + STX);
+    const int y0 = ty * STY, y1 = min(H, y0 + STY);
+    const BatchFrame& fr = frames[f];
+    for (int r = y0 + (lane >> 3); r < y1; r += 8) {
+        const int64_t qa = ((int64_t)r * W + x0) >> 2, qb = ((int64_t)r * W + x1 - 1) >> 2;
+        for (int64_t qq = qa + (lane & 7); qq <= qb; qq += 8) prep_quad(fr, mult, qq * 4, npx);
+    }
+}
+
+// compile-time loops over slot indices (std::integral_constant arguments): f(0), ..., f(N - 1); static_all stops at the
+// first false
+template <int N, class F>
+__device__ __forceinline__ void static_for(F& f) {
+    if constexpr (N > 0) {
+        static_for<N - 1>(f);
+        f(std::integral_constant<int, N - 1>{});
+    }
+}
+template <int N, class F>
+__device__ __forceinline__ bool static_all(F& f) {
+    if constexpr (N == 0) {
+        return true;
+    } else {
+        if (!static_all<N - 1>(f)) return false;
+        return f(std::integral_constant<int, N - 1>{});
+    }
+}
+
 // Phases A and B of one frame for a lane's ZB voxels: the certified projections and the depth gathers (no voxel state
 // read) -- the fine slices' frame skew issues them for frame f+1 before frame f's updates (k_batch_integrate).  The same
 // arithmetic as the phases inside the coarse loop.
@@ -608,8 +725,8 @@ constexpr int RCP_N = 2048;  // 16 KiB (float64) / 8 KiB (float32) of LDS per wo
 // whatever its registers); the parts of a unit run on one XCD.  Work items are assigned by a static grid stride that
 // every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes.
-template <bool C64, bool FAST, int ZB = BZ>
-__global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU) void k_batch_integrate(
+template <bool C64, bool FAST, int ZB = BZ, int KT = 1>
+__global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : (ZB == 2 ? 4 : INT_WAVES_PER_EU)) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
     const int* __restrict__ wcount) {
     using CT = typename std::conditional<C64, double, float>::type;
@@ -692,46 +809,62 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                 const float pz = p.half + oz;
                 const unsigned upd0 = upd;
                 if constexpr (ZB == 2) {
-                    // Frame skew (the fine slices serve batches with few units, whose waves cannot hide a frame's
-                    // dependent gathers behind other waves): frame f's colour gathers and frame f+1's projections and
-                    // depth gathers are issued together, before frame f's updates -- one memory round trip per frame
-                    // on the wave's chain instead of two.  The taps read no voxel state, so the order of the updates
-                    // (and every bit) is the unskewed loop's.
-                    unsigned long long m = mask;  // non-empty: a listed slot was touched by some frame of the batch
-                    int f = __ffsll((long long)m) - 1;
-                    int pixv[ZB], pixv_n[ZB];
-                    float pcz[ZB], dv[ZB], mv[ZB], pcz_n[ZB], dv_n[ZB], mv_n[ZB];
-                    frame_tap<ZB>(frames[f], p, npx, px, py, pz, z0, pixv, pcz, dv, mv);
-                    for (;;) {
-                        m &= m - 1;
-                        const int fn = m ? __ffsll((long long)m) - 1 : -1;  // wave-uniform
-                        const BatchFrame& fr = frames[f];
+                    // Frame pipeline (the fine slices serve batches with few units, whose waves cannot hide a frame's
+                    // dependent gathers behind other waves: the wave's chain of frames IS the batch's time).  Every
+                    // load of a frame is state-independent -- the projections and depth gathers (tap), the depth test,
+                    // clamped tsdf term and colour gather (stage C) -- only the running means (stage D) read the
+                    // voxel state.  So frame f+KT's tap and frame f+KC's stage C are issued before frame f's update,
+                    // from KT + 1 register slots (the loop is unrolled over the slots so every slot is a fixed
+                    // register set: a rotating copy would wait for the loads in flight).  The updates still run in
+                    // frame order with the same arithmetic: the bits are the unpipelined loop's.  KT = 1, KC = 0 is the
+                    // round-5 one-frame skew.
+                    constexpr int KC = KT - 1, RS = KT + 1;
+                    unsigned long long mt = mask;  // frames not yet tapped
+                    int fs[RS];                     // frame of each slot (wave-uniform), -1: past the last frame
+                    int pixv[RS][ZB];
+                    float pcz[RS][ZB], dv[RS][ZB], mv[RS][ZB], tnv[RS][ZB];
+                    uint32_t cv[RS][ZB];
+                    bool dov[RS][ZB];
+                    auto tap = [&](auto J) __attribute__((always_inline)) {
+                        constexpr int j = decltype(J)::value;
+                        if (mt) {
+                            const int f = __ffsll((long long)mt) - 1;
+                            mt &= mt - 1;
+                            fs[j] = f;
+                            frame_tap<ZB>(frames[f], p, npx, px, py, pz, z0, pixv[j], pcz[j], dv[j], mv[j]);
+                        } else {
+                            fs[j] = -1;
+                        }
+                    };
+                    auto stage_c = [&](auto J) __attribute__((always_inline)) {
+                        constexpr int j = decltype(J)::value;
+                        if (fs[j] < 0) return;
+                        const BatchFrame& fr = frames[fs[j]];
                         const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
                         const bool use_color = fr.color != nullptr;
-                        // phase C: the depth test; colour gathered only by the lanes whose voxel updates
-                        bool doitv[ZB];
-                        float sdfv[ZB];
-                        uint32_t cv[ZB];
 #pragma unroll
                         for (int k = 0; k < ZB; ++k) {
-                            sdfv[k] = (dv[k] - pcz[k]) * mv[k];
-                            doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
-                            cv[k] = 0u;
-                            if (use_color && doitv[k])
-                                cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
+                            const float sdf = (dv[j][k] - pcz[j][k]) * mv[j][k];
+                            dov[j][k] = (pixv[j][k] >= 0) & (dv[j][k] > 0.0f) & (sdf > -p.trunc);
+                            const float sv = sdf * p.trunc_inv;
+                            tnv[j][k] = (sv < 1.0f) ? sv : 1.0f;
+                            cv[j][k] = 0u;
+                            if (use_color && dov[j][k])
+                                cv[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[j][k] * 4, 0, 0);
                         }
-                        if (fn >= 0) frame_tap<ZB>(frames[fn], p, npx, px, py, pz, z0, pixv_n, pcz_n, dv_n, mv_n);
-                        // phase D: updates in frame order (select form: identical values, no exec-mask branches)
+                    };
+                    auto stage_d = [&](auto J) __attribute__((always_inline)) -> bool {
+                        constexpr int j = decltype(J)::value;
+                        if (fs[j] < 0) return false;
+                        const bool use_color = frames[fs[j]].color != nullptr;
 #pragma unroll
                         for (int k = 0; k < ZB; ++k) {
-                            const bool doit = doitv[k];
-                            const float sv = sdfv[k] * p.trunc_inv;
-                            const float tn = (sv < 1.0f) ? sv : 1.0f;
+                            const bool doit = dov[j][k];
+                            const float tn = tnv[j][k];
                             const float wv = wt[k];
                             const float w1 = wv + 1.0f;
                             const float ta = ts[k] * wv + tn;
-                            float tsn;  // (tsdf * w + t) / (w + 1): the IEEE quotient, tsdf bit-exact
-                            // one table read per voxel for the tsdf and the colour quotients (round 3: +0.8 %)
+                            float tsn;
                             const double y64 = (FAST && C64) ? s_r64[(int)w1] : 0.0;
                             if constexpr (FAST) {
                                 const float y = C64 ? (float)y64 : s_r32[(int)w1];
@@ -742,33 +875,32 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                             }
                             ts[k] = doit ? tsn : ts[k];
                             if (use_color) {
-                                if constexpr (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
-                                    {  // every lane, in select form (skipping voxels without an updating lane: slower)
-                                        const double wd = (double)wv, w1d = (double)w1;
-                                        const double ar = cr[k] * wd + (double)(cv[k] & 0xFFu);
-                                        const double ag = cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu);
-                                        const double ab = cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu);
-                                        double nr, ng, nb;
-                                        if constexpr (FAST) {
-                                            const double y = y64;
-                                            const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
-                                            nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
-                                            ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
-                                            nb = __builtin_fma(__builtin_fma(-w1d, q0b, ab), y, q0b);
-                                        } else {
-                                            nr = ar / w1d;
-                                            ng = ag / w1d;
-                                            nb = ab / w1d;
-                                        }
-                                        cr[k] = doit ? nr : cr[k];
-                                        cg[k] = doit ? ng : cg[k];
-                                        cb[k] = doit ? nb : cb[k];
+                                const uint32_t c = cv[j][k];
+                                if constexpr (C64) {
+                                    const double wd = (double)wv, w1d = (double)w1;
+                                    const double ar = cr[k] * wd + (double)(c & 0xFFu);
+                                    const double ag = cg[k] * wd + (double)((c >> 8) & 0xFFu);
+                                    const double ab = cb[k] * wd + (double)((c >> 16) & 0xFFu);
+                                    double nr, ng, nb;
+                                    if constexpr (FAST) {
+                                        const double y = y64;
+                                        const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
+                                        nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
+                                        ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
+                                        nb = __builtin_fma(__builtin_fma(-w1d, q0b, ab), y, q0b);
+                                    } else {
+                                        nr = ar / w1d;
+                                        ng = ag / w1d;
+                                        nb = ab / w1d;
                                     }
-                                } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
+                                    cr[k] = doit ? nr : cr[k];
+                                    cg[k] = doit ? ng : cg[k];
+                                    cb[k] = doit ? nb : cb[k];
+                                } else {
                                     const float rw = __builtin_amdgcn_rcpf(w1);
-                                    const float nr = ((float)cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
-                                    const float ng = ((float)cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
-                                    const float nb = ((float)cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                                    const float nr = ((float)cr[k] * wv + (float)(c & 0xFFu)) * rw;
+                                    const float ng = ((float)cg[k] * wv + (float)((c >> 8) & 0xFFu)) * rw;
+                                    const float nb = ((float)cb[k] * wv + (float)((c >> 16) & 0xFFu)) * rw;
                                     cr[k] = doit ? nr : cr[k];
                                     cg[k] = doit ? ng : cg[k];
                                     cb[k] = doit ? nb : cb[k];
@@ -777,15 +909,20 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : INT_WAVES_PER_EU)
                             wt[k] = doit ? w1 : wv;
                             upd += doit ? 1u : 0u;
                         }
-                        if (fn < 0) break;
-                        f = fn;
-#pragma unroll
-                        for (int k = 0; k < ZB; ++k) {
-                            pixv[k] = pixv_n[k];
-                            pcz[k] = pcz_n[k];
-                            dv[k] = dv_n[k];
-                            mv[k] = mv_n[k];
-                        }
+                        return true;
+                    };
+                    // one iteration = frame f in slot J: stage C of f + KC, the tap of f + KT (into the slot frame f - 1
+                    // left), the update of f
+                    auto iter = [&](auto J) __attribute__((always_inline)) -> bool {
+                        constexpr int j = decltype(J)::value;
+                        stage_c(std::integral_constant<int, (j + KC) % RS>{});
+                        tap(std::integral_constant<int, (j + KT) % RS>{});
+                        return stage_d(J);
+                    };
+                    // prologue: taps of the first KT frames, stage C of the first KC
+                    static_for<KT>(tap);
+                    static_for<KC>(stage_c);
+                    while (static_all<RS>(iter)) {
                     }
                 } else {
                     for (unsigned long long m = mask; m; m &= m - 1) {
@@ -1088,7 +1225,7 @@ __global__ __launch_bounds__(256) void k_border_dest(TsdfDev d, int64_t n, const
     if (d.shard_world > 1)
         for (int t = 1; t < 8; ++t) {
             const int nx = x - ((t >> 2) & 1), ny = y - ((t >> 1) & 1), nz = z - (t & 1);
-            if (key_in_range(nx, ny, nz)) m |= 1ull << unit_owner(d.shard_world, d.shard_shift, nx, ny, nz);
+            if (key_in_range(nx, ny, nz)) m |= 1ull << unit_owner(d, nx, ny, nz);
         }
     mask[r] = m & ~(1ull << d.shard_rank);
 }
@@ -1321,20 +1458,31 @@ constexpr int INT_GRID_MULT = 8;
 // 2 voxels per lane along z, 32 waves per unit instead of 16 -- for batches with few units, below)
 static int g_int_fine = -1;  // test hook otx_integrate_fine: -1 by the batch's size (default), 0 coarse, 1 fine
 static int g_stage_blocks = -1;  // test hook otx_touch_stage_blocks: staging-only touch workgroups (-1: 2 per tile)
+// bits 3-4 of a fine variant: the frame pipeline's depth KT - 1 (k_batch_integrate's ZB == 2 loop)
+static int g_int_depth = -1;  // test hook otx_integrate_depth: -1 the default (INT_FINE_KT), else KT in 1..3
+constexpr int INT_FINE_KT = 1;
 static const void* integrate_kernel(int variant) {
-    static const void* const k[8] = {
+    static const void* const k[20] = {
         (const void*)k_batch_integrate<false, false>, (const void*)k_batch_integrate<false, true>,
         (const void*)k_batch_integrate<true, false>, (const void*)k_batch_integrate<true, true>,
-        (const void*)k_batch_integrate<false, false, 2>, (const void*)k_batch_integrate<false, true, 2>,
-        (const void*)k_batch_integrate<true, false, 2>, (const void*)k_batch_integrate<true, true, 2>};
-    return k[variant & 7];
+        (const void*)k_batch_integrate<false, false, 2, 1>, (const void*)k_batch_integrate<false, true, 2, 1>,
+        (const void*)k_batch_integrate<true, false, 2, 1>, (const void*)k_batch_integrate<true, true, 2, 1>,
+        nullptr, nullptr, nullptr, nullptr,
+        (const void*)k_batch_integrate<false, false, 2, 2>, (const void*)k_batch_integrate<false, true, 2, 2>,
+        (const void*)k_batch_integrate<true, false, 2, 2>, (const void*)k_batch_integrate<true, true, 2, 2>,
+        nullptr, nullptr, nullptr, nullptr};
+    static const void* const k3[4] = {
+        (const void*)k_batch_integrate<false, false, 2, 3>, (const void*)k_batch_integrate<false, true, 2, 3>,
+        (const void*)k_batch_integrate<true, false, 2, 3>, (const void*)k_batch_integrate<true, true, 2, 3>};
+    if ((variant & 4) && ((variant >> 3) & 3) == 2) return k3[variant & 3];
+    return k[(variant & 4) ? (variant & 7) + 8 * ((variant >> 3) & 1) : (variant & 3)];
 }
 
 static int integrate_grid(int variant) {
-    static int cache[8][64] = {{0}};
+    static int cache[32][64] = {{0}};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 4096;
-    int* cache_c = cache[variant & 7];
+    int* cache_c = cache[variant & 31];
     if (!cache_c[dev]) {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, integrate_kernel(variant), 64 * INT_WG, 0) !=
@@ -1353,6 +1501,9 @@ struct BatchCtx {
     IntegrateParams ip0;
     unsigned tiles;
     int n, pc, variant, set;
+    bool split = false;         // split front end: a replay stages its units' tiles too (units the full hash dropped
+    StageMaskParams sq{};       // were in no work list of the first pass, so their footprints were never staged)
+    unsigned* smask = nullptr;  // the batch's tile masks (its parity)
 };
 static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stream);
 
@@ -1363,6 +1514,30 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
 // 1.165 ms against 2.195 / 1.587 / 1.230 ms at 2 / 4 / 8 ranks (r05aj, bench.py spatial_amdahl.measured): the overlap's
 // cross-stream events cost more than the co-running front end saves
 static bool overlap_on(const ot_tsdf* vol) { return vol->overlap_mode > 0; }
+// the split front end: sharded volumes (its masks are single-stream state: not with the double-buffered front end)
+static int g_split = -1;  // test hook otx_split_frontend: -1 by the volume (default), 0 never, 1 always (unsharded too)
+static bool split_on(const ot_tsdf* vol) {
+    if (overlap_on(vol)) return false;
+    const int mode = g_split >= 0 ? g_split : vol->split_mode;
+    return mode > 0 || (mode < 0 && vol->dev.shard_world > 1);
+}
+// tile masks for w x h frames, both parities zero (each split batch's mask kernel clears the other parity for the next)
+static ot_status ensure_tmask(ot_tsdf* vol, int w, int h, hipStream_t stream) {
+    if (vol->tmask && vol->tmask_w == w && vol->tmask_h == h) return OT_OK;
+    const int64_t words = (int64_t)MAX_BATCH * ((h + STY - 1) / STY) * (((w + STX - 1) / STX + 31) / 32);
+    if (vol->tmask) {
+        OT_HIP_TRY(hipStreamSynchronize(stream));
+        OT_HIP_TRY(hipFree(vol->tmask));
+        vol->tmask = nullptr;
+    }
+    OT_HIP_TRY(hipMalloc(&vol->tmask, sizeof(unsigned) * 2 * words));
+    OT_HIP_TRY(hipMemsetAsync(vol->tmask, 0, sizeof(unsigned) * 2 * words, stream));
+    vol->tmask_words = words;
+    vol->tmask_w = w, vol->tmask_h = h;
+    vol->tmask_par = 0;
+    note_alloc();
+    return OT_OK;
+}
 static void* set_work(ot_tsdf* vol, int s) { return s == 0 ? vol->dev.work : vol->bset[1].work; }
 
 // order `stream` after the last batch's integrate when it ran on the volume's integrate stream
@@ -1467,6 +1642,13 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.tiles = (int)bc.tiles;
     tp.stage_blocks = g_stage_blocks < 0 ? 2 * (int)bc.tiles : g_stage_blocks;
     tp.tf = g_touch_tf;
+    // sharded volume: split front end (touch without staging -> units -> tile mask -> staging of the marked tiles)
+    const bool split = split_on(vol);
+    tp.sample_stage = split ? 1 : 0;
+    if (split) {
+        tp.stage_blocks = -1;
+        if ((st = ensure_tmask(vol, in.width, in.height, stream)) != OT_OK) return st;
+    }
     bc.n = n;
     bc.pc = pc;
     bc.set = set;
@@ -1478,10 +1660,34 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     }
     UnitWork* work = (UnitWork*)set_work(vol, set);
     int* wcount = ovl ? vol->wcount + set : vol->dev.counters + pc;
-    hipLaunchKernelGGL(k_batch_touch<false>, dim3(bc.tiles + (unsigned)tp.stage_blocks, (unsigned)((n + tp.tf - 1) / tp.tf)),
+    hipLaunchKernelGGL(k_batch_touch<false>,
+                       dim3(bc.tiles + (unsigned)std::max(0, tp.stage_blocks), (unsigned)((n + tp.tf - 1) / tp.tf)),
                        dim3(256), 0, stream, (const BatchFrame*)bs.bframes, tp, vol->dev, n);
     hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, work, pc,
                        vol->hmail + OT_MAIL_WORDS, ovl ? wcount : (int*)nullptr, ++vol->units_seq);
+    if (split) {
+        StageMaskParams q;
+        q.W = in.width;
+        q.H = in.height;
+        q.tiles_x = (in.width + STX - 1) / STX;
+        q.tiles_y = (in.height + STY - 1) / STY;
+        q.wpr = (q.tiles_x + 31) / 32;
+        q.fx = bc.ip0.fx, q.fy = bc.ip0.fy, q.cx = bc.ip0.cx, q.cy = bc.ip0.cy;
+        q.vl = bc.ip0.vl, q.half = bc.ip0.half;
+        q.unit_len = vol->unit_length;
+        q.nframes = n;
+        unsigned* cur = vol->tmask + (size_t)vol->tmask_par * vol->tmask_words;
+        unsigned* oth = vol->tmask + (size_t)(vol->tmask_par ^ 1) * vol->tmask_words;
+        vol->tmask_par ^= 1;
+        bc.split = true;
+        bc.sq = q;
+        bc.smask = cur;
+        hipLaunchKernelGGL(k_stage_mask, dim3(256), dim3(256), 0, stream, (const BatchFrame*)bs.bframes, q,
+                           (const UnitWork*)work, (const int*)wcount, cur, oth, (int)vol->tmask_words);
+        hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)((q.tiles_x * q.tiles_y + 3) / 4), (unsigned)n), dim3(256), 0,
+                           stream, (const BatchFrame*)bs.bframes, (const float*)vol->mult, (const unsigned*)cur,
+                           in.width, in.height, q.tiles_x, q.tiles_y, q.wpr, npx);
+    }
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
     const bool fast = !vol->imported && (int64_t)vol->frame_id + n < RCP_N;
@@ -1500,7 +1706,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         const int64_t est = vol->last_batch_slots >= 0 ? vol->last_batch_slots
                                                        : (vol->dev.shard_world >= 16 ? 0 : (int64_t)1 << 30);
         const bool fine = g_int_fine > 0 || (g_int_fine < 0 && est * INT_PARTS * 4 < (int64_t)resident * 3);
-        if (fine) bc.variant |= 4;
+        if (fine) bc.variant |= 4 | (((g_int_depth > 0 ? g_int_depth : INT_FINE_KT) - 1) << 3);
     }
     const int grid = integrate_grid(bc.variant);
     // overlap: the integrate on istream behind this set's units kernel (and the previous batch's integrate: same
@@ -1635,8 +1841,14 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
         int c[N_COUNTERS];
         std::memcpy(c, vol->hmail + OT_MAIL_WORDS, sizeof(c));
         vol->last_batch_slots = c[bc.pc];  // units the batch touched: the next batch's item estimate
+        if (round == 0) {
+            ++vol->stat_batches;
+            vol->stat_unit_batches += c[bc.pc];
+        }
         const bool short_of_room = c[C_OVERFLOW] != 0 || (c[C_HASHERR] & 1) != 0;
         if (!short_of_room) {
+            if (vol->stat_prev_units >= 0) vol->stat_fresh += c[C_UNITS] - vol->stat_prev_units;
+            vol->stat_prev_units = c[C_UNITS];
             if ((int64_t)c[C_UNITS] * 4 > vol->max_units * 3)
                 return grow_pool(vol, (int64_t)c[C_UNITS] * 2, c[C_UNITS], stream);
             return OT_OK;
@@ -1663,6 +1875,14 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
                            bf, tp, vol->dev, bc.n);
         hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
                            vol->hmail + OT_MAIL_WORDS, (int*)nullptr, ++vol->units_seq);
+        if (bc.split) {  // the replayed units' tiles, from the caller's frames (valid until this flush returns)
+            hipLaunchKernelGGL(k_stage_mask, dim3(256), dim3(256), 0, stream, (const BatchFrame*)bf, bc.sq,
+                               (const UnitWork*)work, (const int*)(vol->dev.counters + bc.pc), bc.smask,
+                               (unsigned*)nullptr, 0);
+            hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)((bc.sq.tiles_x * bc.sq.tiles_y + 3) / 4), (unsigned)bc.n),
+                               dim3(256), 0, stream, bf, (const float*)vol->mult, (const unsigned*)bc.smask, bc.sq.W,
+                               bc.sq.H, bc.sq.tiles_x, bc.sq.tiles_y, bc.sq.wpr, (int64_t)bc.sq.W * bc.sq.H);
+        }
         const UnitWork* uw = work;
         const int* wc = vol->dev.counters + bc.pc;
         void* args[] = {(void*)&bf, (void*)&bc.ip0, (void*)&vol->dev, (void*)&uw, (void*)&wc};
@@ -1939,7 +2159,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     void* ptrs[] = {d.hkeys, d.hvals, d.counters, d.stats, d.unit_keys, d.vox, v->mult, v->sorted_ids, v->mesh.ws,
                     v->mesh.v, v->mesh.c, v->mesh.t, v->mesh.vk, v->mesh.tk, v->mesh.vown, d.fmask, d.bslots, d.work,
                     v->wcount, v->bset[0].bframes, v->bset[0].bdm, v->bset[0].brgba, v->bset[1].bframes,
-                    v->bset[1].bdm, v->bset[1].brgba, v->bset[1].work};
+                    v->bset[1].bdm, v->bset[1].brgba, v->bset[1].work, v->tmask};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (v->hbframes) (void)hipHostFree(v->hbframes);
@@ -1975,6 +2195,7 @@ ot_status ot_tsdf_reset(ot_tsdf* v) {
     v->imported = false;
     v->early_frame = -1;
     v->pending.clear();
+    v->stat_batches = v->stat_unit_batches = v->stat_fresh = v->stat_prev_units = 0;
     v->sorted_frame = -1;
     v->sorted_units = -1;
     v->mesh.nv = v->mesh.nt = 0;
@@ -1999,6 +2220,7 @@ ot_status ot_tsdf_reset_async(ot_tsdf* v, void* stream_) {
     v->imported = false;
     v->early_frame = -1;
     v->last_batch_slots = -1;
+    v->stat_batches = v->stat_unit_batches = v->stat_fresh = v->stat_prev_units = 0;
     v->sorted_frame = -1;
     v->sorted_units = -1;
     v->mesh.nv = v->mesh.nt = 0;
@@ -2099,6 +2321,14 @@ ot_status ot_tsdf_num_units(ot_tsdf* vol, int64_t* n, void* stream_) {
     OT_HIP_TRY(hipMemcpyAsync(&nu, vol->dev.counters + C_UNITS, sizeof(int), hipMemcpyDeviceToHost, stream));
     OT_HIP_TRY(hipStreamSynchronize(stream));
     *n = std::min<int64_t>(nu, vol->max_units);
+    return OT_OK;
+}
+
+ot_status ot_tsdf_batch_stats(ot_tsdf* vol, int64_t* batches, int64_t* unit_batches, int64_t* new_units) {
+    if (!vol) return fail(OT_ERR_INVALID_ARGUMENT, "invalid arguments");
+    if (batches) *batches = vol->stat_batches;  // batches run (frames still queued are not counted: flush first)
+    if (unit_batches) *unit_batches = vol->stat_unit_batches;
+    if (new_units) *new_units = vol->stat_fresh;
     return OT_OK;
 }
 
@@ -2281,9 +2511,36 @@ ot_status ot_tsdf_set_shard(ot_tsdf* vol, int32_t rank, int32_t world) {
         return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] set the shard before the first integrate");
     vol->dev.shard_rank = rank;
     vol->dev.shard_world = world;
+    vol->dev.shard_mode = SHARD_BLOCKS;
     // ownership blocks: 4^3 units up to 4 ranks, 2^3 beyond (configs[1] scan, 5 mm: largest shard / mean 1.09 / 1.13 /
     // 1.09 at 2 / 4 / 8 ranks; border rows sent 0.42 / 0.25 / 0.24 of an all-gather's)
     vol->dev.shard_shift = world <= 4 ? 2 : 1;
+    return OT_OK;
+}
+
+ot_status ot_tsdf_set_shard_sector(ot_tsdf* vol, int32_t rank, int32_t world, double cx, double cy) {
+    if (!vol || world < 1 || rank < 0 || rank >= world || !std::isfinite(cx) || !std::isfinite(cy))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] shard needs 0 <= rank < world and a finite centre");
+    const double hx = std::nearbyint(2.0 * cx / vol->unit_length), hy = std::nearbyint(2.0 * cy / vol->unit_length);
+    if (std::fabs(hx) > (double)(1 << 22) || std::fabs(hy) > (double)(1 << 22))
+        return fail(OT_ERR_INVALID_ARGUMENT, "[ScalableTSDFVolume] sector centre out of the unit key range");
+    ot_status st = ot_tsdf_set_shard(vol, rank, world);
+    if (st != OT_OK) return st;
+    vol->dev.shard_mode = SHARD_SECTORS;
+    vol->dev.shard_cx2 = (int)hx;
+    vol->dev.shard_cy2 = (int)hy;
+    return OT_OK;
+}
+
+ot_status otx_integrate_depth(int32_t kt) {
+    if (kt != -1 && (kt < 1 || kt > 3)) return fail(OT_ERR_INVALID_ARGUMENT, "integrate pipeline depth must be -1 or 1..3");
+    g_int_depth = kt;
+    return OT_OK;
+}
+
+ot_status otx_split_frontend(int32_t mode) {
+    if (mode < -1 || mode > 1) return fail(OT_ERR_INVALID_ARGUMENT, "split front end mode must be -1, 0 or 1");
+    g_split = mode;
     return OT_OK;
 }
 
@@ -2333,6 +2590,7 @@ static ot_status import_units(ot_tsdf* vol, int64_t n, const int32_t* keys, cons
     OT_LAUNCH_CHECK();
     vol->sorted_units = -1;  // the sorted-unit cache no longer matches
     vol->imported = true;    // arbitrary state: the IEEE-division integrate from now on
+    vol->stat_prev_units = -1;
     vol->mesh.valid = false;
     st = check_errors(vol, stream);
     if (st != OT_OK) return st;
@@ -2399,6 +2657,7 @@ ot_status ot_tsdf_import_border(ot_tsdf* vol, int64_t n, const int32_t* keys, co
     OT_LAUNCH_CHECK();
     vol->sorted_units = -1;
     vol->imported = true;  // halo units hold other shards' state (read by marching cubes; kept exact anyway)
+    vol->stat_prev_units = -1;
     vol->mesh.valid = false;
     st = check_errors(vol, stream);
     if (st != OT_OK) return st;

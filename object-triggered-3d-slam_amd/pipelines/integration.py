@@ -189,6 +189,11 @@ class ScalableTSDFVolume:
         """Keep only the units owned by `rank` of `world` (spatial sharding of one object)."""
         L.call("ot_tsdf_set_shard", self._h, int(rank), int(world))
 
+    def set_shard_sector(self, rank, world, centre=(0.0, 0.0)):
+        """Keep only the units in azimuth sector `rank` of `world` around the scan centre (x, y) in metres
+        (ot_tsdf_set_shard_sector): a ring scan's rank then stages only the image tiles its units project to."""
+        L.call("ot_tsdf_set_shard_sector", self._h, int(rank), int(world), float(centre[0]), float(centre[1]))
+
     def set_shard_block(self, log2_units):
         """Ownership granularity of a sharded volume (ot_tsdf_set_shard_block): 2^log2_units units per axis."""
         L.call("ot_tsdf_set_shard_block", self._h, int(log2_units))

@@ -18,7 +18,7 @@ def _integrate(pkg, seq, voxel, shard=None, overlap=None):
     intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(importlib.import_module(pkg.__name__ + ".synth")))
     vol = integ.ScalableTSDFVolume(voxel_length=voxel, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8)
     if shard is not None:
-        vol.set_shard(*shard)
+        _set_shard(vol, shard)
     if overlap is not None:
         vol.set_frontend_overlap(overlap)
     for k in range(depth.shape[0]):
@@ -29,18 +29,31 @@ def _integrate(pkg, seq, voxel, shard=None, overlap=None):
     return vol
 
 
+def _set_shard(vol, shard):
+    """(rank, world): hashed ownership blocks; (rank, world, cx, cy): azimuth sectors around (cx, cy) (round 6)"""
+    if len(shard) == 4:
+        vol.set_shard_sector(shard[0], shard[1], shard[2:])
+    else:
+        vol.set_shard(*shard)
+
+
 def _host(t):
     return t.cpu().numpy()
 
 
-@pytest.mark.parametrize("voxel,world,overlap", [(0.01, 3, None), (0.005, 8, 1)])
-def test_shard_union_bitexact(pkg, seq16, gpu, voxel, world, overlap):
+@pytest.mark.parametrize("voxel,world,overlap,sector", [(0.01, 3, None, None), (0.005, 8, 1, None),
+                                                        (0.005, 8, None, (0.0, 0.0)), (0.01, 3, None, (0.13, -0.2)),
+                                                        (0.005, 4, None, (0.0, 0.0))])
+def test_shard_union_bitexact(pkg, seq16, gpu, voxel, world, overlap, sector):
+    """hashed blocks (split front end; the double-buffered one at 8 ranks) and azimuth sectors (split front end: the
+    touch stages nothing, only the tiles the rank's units project to are staged), centred and off-centre"""
     full = _integrate(pkg, seq16, voxel)
     fk, ft, fw, fc = (_host(a) for a in full.export_units())
-    parts = [_integrate(pkg, seq16, voxel, (r, world), overlap) for r in range(world)]
+    parts = [_integrate(pkg, seq16, voxel, (r, world) + tuple(sector or ()), overlap) for r in range(world)]
     exports = [[_host(a) for a in v.export_units()] for v in parts]
     counts = [e[0].shape[0] for e in exports]
-    assert sum(counts) == fk.shape[0] and min(counts) > 0.5 * fk.shape[0] / world
+    assert sum(counts) == fk.shape[0] and min(counts) > (0.5 if sector is None or sector == (0.0, 0.0) else 0.2) * \
+        fk.shape[0] / world
     keys = np.concatenate([e[0] for e in exports])
     order = np.lexsort((keys[:, 2], keys[:, 1], keys[:, 0]))
     assert_bitwise(keys[order], fk, "shard union keys")
@@ -66,8 +79,8 @@ def test_shard_import_mesh_bitexact(pkg, seq16, gpu):
     assert_bitwise(np.asarray(m1.vertex_colors), np.asarray(m0.vertex_colors), "merged-shard mesh colours")
 
 
-@pytest.mark.parametrize("world,precision", [(3, 64), (8, 32)])
-def test_shard_border_halo_mesh_bitexact(pkg, seq16, gpu, world, precision):
+@pytest.mark.parametrize("world,precision,sector", [(3, 64, None), (8, 32, None), (8, 64, (0.0, 0.0))])
+def test_shard_border_halo_mesh_bitexact(pkg, seq16, gpu, world, precision, sector):
     """SURVEY §8(e) border halo: every shard imports the other shards' border rows (721 low-face voxels per unit)
     it needs, extracts only its own units' cubes, and the partial meshes merge (distributed.merge_shard_meshes)
     into the unsharded mesh bit for bit -- without moving whole units."""
@@ -80,7 +93,7 @@ def test_shard_border_halo_mesh_bitexact(pkg, seq16, gpu, world, precision):
 
     full = make()
     m0 = full.extract_triangle_mesh()
-    shards = [make((r, world)) for r in range(world)]
+    shards = [make((r, world) + tuple(sector or ())) for r in range(world)]
     rows = [D.pack_border(*v.export_border()) for v in shards]
     import torch
 
@@ -107,7 +120,7 @@ def _integrate_p(pkg, seq, voxel, shard, precision):
     vol = integ.ScalableTSDFVolume(voxel_length=voxel, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
                                    color_precision=precision)
     if shard is not None:
-        vol.set_shard(*shard)
+        _set_shard(vol, shard)
     for k in range(depth.shape[0]):
         rgbd = pkg.geometry.RGBDImage.create_from_color_and_depth(
             pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
@@ -126,6 +139,43 @@ def test_shard_argument_errors(pkg, seq16, gpu):
     with pytest.raises(RuntimeError, match="rank < world"):
         fresh.set_shard(2, 2)
     fresh.set_shard(0, 1)  # world 1: no sharding
+    with pytest.raises(RuntimeError, match="finite centre"):
+        fresh.set_shard_sector(0, 2, (float("nan"), 0.0))
+    with pytest.raises(RuntimeError, match="before the first integrate"):
+        vol.set_shard_sector(0, 2)
+
+
+@pytest.mark.parametrize("sector", [None, (0.0, 0.0)])
+def test_split_frontend_pool_growth_bitexact(pkg, O, gpu, synth, sector):
+    """The split front end with a 64-unit pool: the first batch overflows, the pool grows and the dropped units are
+    integrated again from the staged frames (the replay touch reads each stride sample's staged pixel, which the
+    split touch writes; the dropped units' tiles were staged by the first pass).  Union of 4 shards == the oracle."""
+    integ = pkg.pipelines.integration
+    intr_t = ref_intr(synth)
+    intr = pkg.camera.PinholeCameraIntrinsic(*intr_t)
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=0), n_frames=256, frames=range(0, 64, 4), intr=intr_t)
+    ref = O.TSDF(0.005, 0.04, 1, 4)
+    for k in range(depth.shape[0]):
+        ref.integrate(O.depth_to_float(depth[k], 1000.0, 3.0), color[k], intr_t, ext[k])
+    rk, rt, rw, rc = ref.export()[:4]
+    world = 4
+    exports = []
+    for r in range(world):
+        vol = integ.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                       max_units=64, batch_frames=16)
+        _set_shard(vol, (r, world) + tuple(sector or ()))
+        for k in range(depth.shape[0]):
+            vol.integrate(pkg.geometry.RGBDImage.create_from_color_and_depth(
+                pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+                convert_rgb_to_intensity=False), intr, ext[k])
+        exports.append([_host(a) for a in vol.export_units()])
+    keys = np.concatenate([e[0] for e in exports])
+    order = np.lexsort((keys[:, 2], keys[:, 1], keys[:, 0]))
+    assert keys.shape[0] > 4 * 64
+    assert_bitwise(keys[order], rk, "split-front-end union keys after growth")
+    assert_bitwise(np.concatenate([e[1] for e in exports])[order], rt, "union tsdf")
+    assert_bitwise(np.concatenate([e[2] for e in exports])[order], rw, "union weight")
+    assert_bitwise(np.concatenate([e[3] for e in exports])[order], rc, "union colour")
 
 
 def test_border_api_errors(pkg, seq16, gpu):

@@ -160,19 +160,25 @@ def test_tsdf_integrate_bitexact(pkg, O, gpu, synth, seq16, voxel, batch):
     assert n > 300
 
 
-@pytest.mark.parametrize("fine", [0, 1])
-def test_integrate_granularity_bitexact(pkg, O, gpu, synth, fine):
+@pytest.mark.parametrize("fine,depth", [(0, -1), (1, 1), (1, 2), (1, 3)])
+def test_integrate_granularity_bitexact(pkg, O, gpu, synth, fine, depth):
     """Both slice granularities of k_batch_integrate (4 voxels per lane along z, 16 waves per unit; or 2, 32 waves --
-    taken for batches with few units) forced for every batch: 40 frames at 5 mm in 16-frame batches, bitwise vs the
-    oracle (keys, tsdf, weight, float64 colour, counters)."""
+    taken for batches with few units) forced for every batch, the fine one at every frame-pipeline depth (round 6:
+    frame f + KT's taps and f + KT - 1's colour gathers issued before frame f's update): 40 frames at 5 mm in 16-frame
+    batches (and a 3-frame batch: shorter than the pipeline), bitwise vs the oracle (keys, tsdf, weight, float64
+    colour, counters)."""
     L = pkg._lib
-    depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=80, frames=range(0, 80, 2))
+    depth_img, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=80, frames=range(0, 80, 2))
     L.call("otx_integrate_fine", fine)
+    L.call("otx_integrate_depth", depth)
     try:
-        vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005, batch=16)
+        vol, ref = _run_pair(pkg, O, synth, depth_img, color, ext, 0.005, batch=16)
         assert _compare_volumes(vol, ref) > 1000
+        vol, ref = _run_pair(pkg, O, synth, depth_img[:7], color[:7], ext[:7], 0.005, batch=3)
+        assert _compare_volumes(vol, ref) > 100
     finally:
         L.call("otx_integrate_fine", -1)
+        L.call("otx_integrate_depth", -1)
 
 
 @pytest.mark.parametrize("blocks,tf", [(0, 2), (7, 2), (-1, 4), (-1, 3), (-1, 8)])
@@ -195,6 +201,28 @@ def test_touch_staging_forms_bitexact(pkg, O, gpu, synth, blocks, tf):
     finally:
         L.call("otx_touch_stage_blocks", -1)
         L.call("otx_touch_frames", 2)
+
+
+@pytest.mark.parametrize("batch", [16, 1])
+def test_split_frontend_bitexact(pkg, O, gpu, synth, seq16, batch):
+    """The split front end (round 6: touch without staging, the batch units' footprint tiles marked, only those tiles
+    staged) forced on an unsharded volume, where every visible tile must be marked: 40 frames at 5 mm, the odd
+    321x243 camera (partial 32x16 tiles, quads straddling rows) and the float-depth path, bitwise vs the oracle."""
+    L = pkg._lib
+    L.call("otx_split_frontend", 1)
+    try:
+        depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=80, frames=range(0, 80, 2))
+        vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005, batch=batch)
+        assert _compare_volumes(vol, ref) > 1000
+        intr_t = (321, 243, 283.1, 283.4, 161.7, 120.2)
+        depth, color, ext = synth.make_sequence(n_frames=12, frames=[0, 2, 5, 9], intr=intr_t)
+        vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, batch=batch, intr_t=intr_t)
+        assert _compare_volumes(vol, ref) > 100
+        depth, color, ext = seq16
+        vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, float_path=True)
+        _compare_volumes(vol, ref)
+    finally:
+        L.call("otx_split_frontend", -1)
 
 
 @pytest.mark.parametrize("batch", [1, None])

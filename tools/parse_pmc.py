@@ -132,6 +132,11 @@ def main():
             ent["valu_busy_frac"] = k["SQ_ACTIVE_INST_VALU"] * 4.0 / 1024.0 / cyc
             ent["valu_insts_per_launch"] = k.get("SQ_INSTS_VALU")
             ent["dispatch_cycles"] = cyc
+        if k.get("TCC_HIT_sum") is not None and k.get("TCC_MISS_sum") is not None:
+            # L2 (TCC) hit share of the kernel's requests: the misses are what FETCH_SIZE counts as fabric traffic
+            h, m = k["TCC_HIT_sum"], k["TCC_MISS_sum"]
+            ent["tcc_hit"], ent["tcc_miss"] = h, m
+            ent["tcc_hit_frac"] = h / (h + m) if h + m > 0 else None
         if k.get("TA_TA_BUSY_sum") and k.get("GRBM_GUI_ACTIVE"):
             ent["ta_busy_frac"] = k["TA_TA_BUSY_sum"] / 256.0 / (k["GRBM_GUI_ACTIVE"] / 8.0)
             ent["td_busy_frac"] = k.get("TD_TD_BUSY_sum", 0) / 256.0 / (k["GRBM_GUI_ACTIVE"] / 8.0)
