@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
     ap.add_argument("--overlap", type=int, default=-1, choices=(-1, 0, 1),
                     help="headline volume's batch front end double-buffered beside the previous integrate "
-                         "(ot_tsdf_set_frontend_overlap; opt-in: 1 on, 0 and -1 (library default) off at every shard count)")
+                         "(ot_tsdf_set_frontend_overlap; -1 = library default: on for sharded volumes only, 0 off, 1 on)")
     ap.add_argument("--cpu-frames", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--sustain", type=float, default=12.0,
                     help="seconds of sustained headline steps after the timed ones (0 = skip): >= 12 s so a 5-s busy "
@@ -547,8 +547,8 @@ def shard_rank_steps(args, L, lib, torch, d_depth, d_color, ext, intr, stream, h
     """SURVEY 8(e) measured on one GPU: the headline step (reset + the 256-frame scan + flush) of a volume that keeps
     only rank r's units, for every rank r of N = 2, 4, 8, under both ownerships: `blocks` (ot_tsdf_set_shard: hashed
     blocks of units) and `sectors` (ot_tsdf_set_shard_sector: azimuth sectors around the scan centre, the product
-    choice since round 6) -- both on the split front end (a sharded volume stages only the image tiles its batch's
-    units project to).  A rank's step on an N-GPU node is this time (its shard, its front end, nothing shared with the
+    choice since round 6) -- both with the library's sharded defaults: the split front end (a sharded volume stages
+    only the image tiles its batch's units project to), double-buffered beside the previous batch's integrate.  A rank's step on an N-GPU node is this time (its shard, its front end, nothing shared with the
     other ranks), so the unsharded step (N = 1, the same method) / max over r is the strong-scaling speed-up of one
     object before the halo extraction.  The resident scan goes in with ot_tsdf_integrate_u16_frames (one host call
     per scan, the bits of 256 per-frame calls): at 1/8 of the integrate a rank's GPU step is shorter than 256 ctypes

@@ -192,9 +192,9 @@ ot_status ot_tsdf_set_batch(ot_tsdf* vol, int32_t max_frames);
 /* Double-buffered batch front end (spatial sharding of one object: reconstruct_rgbd_filter.py:88-109):
  * with mode 1 batch k+1's staging, touch and unit headers run on the caller's stream while batch k's integrate runs on
  * a second stream of the volume (two staging sets); readers (num_units, export, extraction, flush, reset) order the
- * caller's stream after the last integrate.  -1 (default) and 0: off (measured slower than the serial front end at 2, 4
- * and 8 shards since round 5: the two streams' events cost more than the overlap saves).  Results are identical in
- * every mode.  Fails with OT_ERR_INVALID_ARGUMENT while frames are queued (flush on their stream first). */
+ * caller's stream after the last integrate.  -1 (default): on for spatially sharded volumes (their split front end
+ * stages only their units' tiles; measured faster at 2, 4 and 8 ranks), off otherwise; 0 off; 1 on.
+ * Results are identical in every mode.  Fails with OT_ERR_INVALID_ARGUMENT while frames are queued (flush on their stream first). */
 ot_status ot_tsdf_set_frontend_overlap(ot_tsdf* vol, int32_t mode);
 
 /* Batch statistics since the last reset (measurement; not an Open3D API): integrate batches run, the units they touched

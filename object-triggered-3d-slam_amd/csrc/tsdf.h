@@ -90,6 +90,17 @@ __host__ __device__ inline bool unit_owned(const TsdfDev& d, unsigned long long 
     if (d.shard_world <= 1) return true;
     int x, y, z;
     unpack_key(key, x, y, z);
+    if (d.shard_mode == SHARD_SECTORS) {  // unit_sector(...) == rank without the division: 4 r s <= N v < 4 (r + 1) s
+        const long long X = 2ll * x + 1 - d.shard_cx2, Y = 2ll * y + 1 - d.shard_cy2;
+        if (X == 0 && Y == 0) return d.shard_rank == 0;
+        long long a, b, q;
+        if (X > 0 && Y >= 0) { q = 0; a = Y; b = X; }
+        else if (X <= 0 && Y > 0) { q = 1; a = -X; b = Y; }
+        else if (X < 0 && Y <= 0) { q = 2; a = -Y; b = -X; }
+        else { q = 3; a = X; b = -Y; }
+        const long long s = a + b, v = (q * s + a) * (long long)d.shard_world;
+        return v >= 4ll * d.shard_rank * s && v < 4ll * (d.shard_rank + 1) * s;
+    }
     return unit_owner(d, x, y, z) == d.shard_rank;
 }
 
@@ -227,10 +238,9 @@ struct ot_tsdf {
     int overlap_mode = -1;        // -1 (default) and 0 off, 1 on
     // Split front end of a sharded volume (round 6): the touch stages nothing (only each stride sample's own pixel, for a
     // replay), k_stage_mask marks the image tiles the batch's owned units can project to, k_stage_tiles stages those.
-    unsigned* tmask = nullptr;    // device [2 parities][MAX_BATCH][tile rows][words per row]
-    int64_t tmask_words = 0;      // words per parity
+    unsigned* tmask = nullptr;    // device [MAX_BATCH][tile rows][words per row]
+    int64_t tmask_words = 0;
     int tmask_w = 0, tmask_h = 0;  // the image size the masks are laid out for
-    int tmask_par = 0;            // parity of the next split batch (the other one is cleared by its mask kernel)
     int split_mode = -1;          // -1 (default): split for sharded volumes; 0 off; 1 on (test hook)
     // batch statistics since reset (ot_tsdf_batch_stats; the bench's compulsory-bytes figure): batches, units touched
     // summed over batches, units new in their batch; units the last batch left (-1: unknown after an import)

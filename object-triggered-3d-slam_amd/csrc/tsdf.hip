@@ -212,6 +212,7 @@ struct BatchTouchParams {
     int W, stride, ws, hs;
     double fx, fy, cx, cy;
     double trunc, unit_len;
+    double inv_unit;    // RN(1 / unit_len): floor_div's certified product
     int slot_cap;
     const float* mult;  // fused staging (k_batch_touch stages the batch's pixels too): ray multipliers
     int64_t npx;        // pixels per frame
@@ -222,6 +223,17 @@ struct BatchTouchParams {
     int sample_stage;   // split front end (stage_blocks < 0): each stride sample stores its own pixel's staged pair
                         // (a replay touch reads it; k_stage_tiles stages only the owned units' footprints)
 };
+
+// floor(RN(a / b)) -- Open3D's LocateVolumeUnit on a float64 quotient -- with one multiply in the common case: v =
+// RN(a * RN(1/b)) is within 2^-52 |a/b| of a/b (and RN(a/b) within 2^-53), so when v lies farther than 1e-14 |v| (+ an
+// absolute floor far below any unit index) from every integer, floor(v) is floor(RN(a/b)); otherwise the IEEE division.
+__device__ inline int floor_div(double a, double b, double inv_b) {
+    const double v = a * inv_b;
+    const double fv = floor(v);
+    const double eps = 1e-14 * fabs(v) + 1e-300;
+    if (v - fv > eps && (fv + 1.0) - v > eps) return (int)fv;
+    return (int)floor(a / b);
+}
 
 __device__ inline void touch_unit_batch(const TsdfDev& d, int f, int slot_cap, int pc, int x, int y, int z) {
     if (!key_in_range(x, y, z)) {
@@ -351,8 +363,8 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
             int lo[3], hi[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                lo[k] = (int)floor((q[k] - p.trunc) / p.unit_len);
-                hi[k] = (int)floor((q[k] + p.trunc) / p.unit_len);
+                lo[k] = floor_div(q[k] - p.trunc, p.unit_len, p.inv_unit);
+                hi[k] = floor_div(q[k] + p.trunc, p.unit_len, p.inv_unit);
             }
             const unsigned long long bit = 1ull << f;
             for (int ux = lo[0]; ux <= hi[0]; ++ux)
@@ -559,18 +571,23 @@ struct StageMaskParams {
 // lie in the projected corners' bounding box (the box is in front of the camera).  The integrate's float projection of a
 // voxel differs from the exact one by < 0.02 px here (|pc| error ~6e-6 m at z >= 0.05 m); the box is widened by 2 px
 // and any corner nearer than 5 cm marks the whole frame.
+// One workgroup per FRAME: its threads walk the batch's work list, each unit whose frame mask has this frame's bit ORs
+// its footprint's tiles into the frame's map in LDS, and the map is stored whole -- no global atomics (one per (unit,
+// frame, tile row) had contended on the frames' few words: 8-18 us per batch, r06e), nothing to clear between batches.
+constexpr int SM_WORDS = 2048;  // LDS map words: tile rows * words per row (8 KiB; 16K x 16K-pixel frames)
 __global__ __launch_bounds__(256) void k_stage_mask(const BatchFrame* __restrict__ frames, StageMaskParams q,
                                                     const UnitWork* __restrict__ work, const int* __restrict__ wcount,
-                                                    unsigned* __restrict__ mask, unsigned* __restrict__ other,
-                                                    int other_words) {
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < other_words; i += gridDim.x * 256) other[i] = 0u;  // next batch's
-    const int n = __builtin_amdgcn_readfirstlane(*wcount);
-    const int lane = threadIdx.x & 63;
-    for (int u = blockIdx.x * 4 + (int)(threadIdx.x >> 6); u < n; u += gridDim.x * 4) {  // one wave per unit
+                                                    unsigned* __restrict__ mask) {
+    __shared__ unsigned s_map[SM_WORDS];
+    const int f = blockIdx.x;
+    const int words = q.tiles_y * q.wpr;
+    for (int i = threadIdx.x; i < words; i += 256) s_map[i] = 0u;
+    __syncthreads();
+    const int n = *wcount;
+    const BatchFrame& fr = frames[f];
+    for (int u = threadIdx.x; u < n; u += 256) {
         const UnitWork& w = work[u];
-        const unsigned long long m = w.mask;
-        if (lane >= q.nframes || !((m >> lane) & 1ull)) continue;
-        const BatchFrame& fr = frames[lane];
+        if (!((w.mask >> f) & 1ull)) continue;
         const float ox = (float)((double)w.kx * q.unit_len);
         const float oy = (float)((double)w.ky * q.unit_len);
         const float oz = (float)((double)w.kz * q.unit_len);
@@ -590,8 +607,9 @@ __global__ __launch_bounds__(256) void k_stage_mask(const BatchFrame* __restrict
             if (!(pc[2] >= 0.05)) {
                 full = true;
             } else {
-                const double uf = (double)q.fx * pc[0] / pc[2] + (double)q.cx + 0.5;
-                const double vf = (double)q.fy * pc[1] / pc[2] + (double)q.cy + 0.5;
+                const double rz = 1.0 / pc[2];
+                const double uf = (double)q.fx * pc[0] * rz + (double)q.cx + 0.5;
+                const double vf = (double)q.fy * pc[1] * rz + (double)q.cy + 0.5;
                 umin = fmin(umin, uf), umax = fmax(umax, uf), vmin = fmin(vmin, vf), vmax = fmax(vmax, vf);
             }
         }
@@ -603,32 +621,46 @@ __global__ __launch_bounds__(256) void k_stage_mask(const BatchFrame* __restrict
             if (u0 > u1 || v0 > v1) continue;
         }
         const int tx0 = u0 / STX, tx1 = u1 / STX, ty0 = v0 / STY, ty1 = v1 / STY;
-        unsigned* row = mask + (size_t)lane * q.tiles_y * q.wpr;
         for (int ty = ty0; ty <= ty1; ++ty)
             for (int k = tx0 >> 5; k <= (tx1 >> 5); ++k) {
                 const int a = max(tx0, k * 32) - k * 32, b = min(tx1, k * 32 + 31) - k * 32;  // bits [a, b]
                 const unsigned bits = (b == 31 ? ~0u : ((1u << (b + 1)) - 1u)) & ~((1u << a) - 1u);
-                atomicOr(row + ty * q.wpr + k, bits);
+                atomicOr(&s_map[ty * q.wpr + k], bits);
             }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < words; i += 256) mask[(size_t)f * words + i] = s_map[i];
 }
 
-// stage the marked tiles: one wave per tile, 8 lanes per row of 32 pixels (8 quads), 8 rows per step
+// Stage the marked tiles: one workgroup per (tile row, frame); its lanes take the marked tiles' quads in turn (a row of
+// a 32-pixel tile is 8 quads, 9 slots when W % 4 != 0 lets a quad straddle the tile edge), so the work of a sparse row is
+// spread over all 256 lanes (one wave per tile left 77 % of the waves idle: 23 us per batch, r06e).  A quad staged
+// twice writes the same bytes.
+constexpr int ST_MAX_TILES_X = 256;
 __global__ __launch_bounds__(256) void k_stage_tiles(const BatchFrame* __restrict__ frames, const float* __restrict__ mult,
                                                      const unsigned* __restrict__ mask, int W, int H, int tiles_x,
                                                      int tiles_y, int wpr, int64_t npx) {
-    const int f = blockIdx.y;
-    const int t = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    if (t >= tiles_x * tiles_y) return;
-    const int ty = t / tiles_x, tx = t - ty * tiles_x;
-    if (!((mask[((size_t)f * tiles_y + ty) * wpr + (tx >> 5)] >> (tx & 31)) & 1u)) return;  // wave-uniform
-    const int lane = threadIdx.x & 63;
-    const int x0 = tx * STX, x1 = min(W, x0 + STX);
-    const int y0 = ty * STY, y1 = min(H, y0 + STY);
+    __shared__ int s_tx[ST_MAX_TILES_X];
+    __shared__ int s_m;
+    const int ty = blockIdx.x, f = blockIdx.y;
+    if (threadIdx.x == 0) s_m = 0;
+    __syncthreads();
+    const unsigned* row = mask + ((size_t)f * tiles_y + ty) * wpr;
+    for (int tx = threadIdx.x; tx < tiles_x; tx += 256)
+        if ((row[tx >> 5] >> (tx & 31)) & 1u) s_tx[atomicAdd(&s_m, 1)] = tx;
+    __syncthreads();
+    const int m = s_m;
+    if (m == 0) return;
+    const int y0 = ty * STY, rows = min(H, y0 + STY) - y0;
+    const int slots = (W & 3) ? STX / 4 + 1 : STX / 4;
+    const int per_tile = rows * slots;
     const BatchFrame& fr = frames[f];
-    for (int r = y0 + (lane >> 3); r < y1; r += 8) {
+    for (int i = threadIdx.x; i < m * per_tile; i += 256) {
+        const int t = i / per_tile, rem = i - t * per_tile;
+        const int r = y0 + rem / slots, kq = rem - (rem / slots) * slots;
+        const int x0 = s_tx[t] * STX, x1 = min(W, x0 + STX);
         const int64_t qa = ((int64_t)r * W + x0) >> 2, qb = ((int64_t)r * W + x1 - 1) >> 2;
-        for (int64_t qq = qa + (lane & 7); qq <= qb; qq += 8) prep_quad(fr, mult, qq * 4, npx);
+        if (qa + kq <= qb) prep_quad(fr, mult, (qa + kq) * 4, npx);
     }
 }
 
@@ -1507,21 +1539,25 @@ struct BatchCtx {
 };
 static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stream);
 
-// auto (-1): from 4 shards on (r05f, rank 0 of the configs[1] scan: 1/4 shard 1.41 vs 1.56 ms per step, 1/8 1.08 vs
-// 1.16 ms; at 2 shards the co-running front end slows the larger integrate more than it hides: 2.22 vs 2.19 ms)
-// Off unless asked for: with the batch's events gone from the serial path (mailbox waits, a kernel for the frame
-// parameters) the serial front end beat the double-buffered one at every shard count -- rank steps 2.146 / 1.532 /
-// 1.165 ms against 2.195 / 1.587 / 1.230 ms at 2 / 4 / 8 ranks (r05aj, bench.py spatial_amdahl.measured): the overlap's
-// cross-stream events cost more than the co-running front end saves
-static bool overlap_on(const ot_tsdf* vol) { return vol->overlap_mode > 0; }
-// the split front end: sharded volumes (its masks are single-stream state: not with the double-buffered front end)
+// auto (-1): on for sharded volumes (round 6, with their split front end: rank steps at 2 / 4 / 8 sector ranks 2.025 /
+// 1.383 / 1.024 ms with it against 2.117 / 1.416 / 1.050 without, r06h; 0.953 vs 0.985 at 8 with coarse slices, r06i),
+// off for whole volumes.  Round 5 had found it slower at every shard count when every rank still staged whole frames
+// (its cross-stream events cost more than the co-running front end saved: DESIGN_HISTORY.md D).
+static bool overlap_on(const ot_tsdf* vol) {
+    return vol->overlap_mode > 0 || (vol->overlap_mode < 0 && vol->dev.shard_world > 1);
+}
+// the split front end: sharded volumes.  Its tile masks are written and read on the caller's stream only (mask kernel,
+// then staging), so one buffer serves the double-buffered front end too: the integrate on istream never reads them.
 static int g_split = -1;  // test hook otx_split_frontend: -1 by the volume (default), 0 never, 1 always (unsharded too)
 static bool split_on(const ot_tsdf* vol) {
-    if (overlap_on(vol)) return false;
     const int mode = g_split >= 0 ? g_split : vol->split_mode;
     return mode > 0 || (mode < 0 && vol->dev.shard_world > 1);
 }
-// tile masks for w x h frames, both parities zero (each split batch's mask kernel clears the other parity for the next)
+// tile masks for w x h frames (each split batch's mask kernel writes its frames' maps whole)
+static bool tmask_fits(int w, int h) {
+    const int tx = (w + STX - 1) / STX;
+    return tx <= ST_MAX_TILES_X && (int64_t)((h + STY - 1) / STY) * ((tx + 31) / 32) <= SM_WORDS;
+}
 static ot_status ensure_tmask(ot_tsdf* vol, int w, int h, hipStream_t stream) {
     if (vol->tmask && vol->tmask_w == w && vol->tmask_h == h) return OT_OK;
     const int64_t words = (int64_t)MAX_BATCH * ((h + STY - 1) / STY) * (((w + STX - 1) / STX + 31) / 32);
@@ -1530,11 +1566,9 @@ static ot_status ensure_tmask(ot_tsdf* vol, int w, int h, hipStream_t stream) {
         OT_HIP_TRY(hipFree(vol->tmask));
         vol->tmask = nullptr;
     }
-    OT_HIP_TRY(hipMalloc(&vol->tmask, sizeof(unsigned) * 2 * words));
-    OT_HIP_TRY(hipMemsetAsync(vol->tmask, 0, sizeof(unsigned) * 2 * words, stream));
+    OT_HIP_TRY(hipMalloc(&vol->tmask, sizeof(unsigned) * words));
     vol->tmask_words = words;
     vol->tmask_w = w, vol->tmask_h = h;
-    vol->tmask_par = 0;
     note_alloc();
     return OT_OK;
 }
@@ -1637,13 +1671,14 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.cy = in.cy;
     tp.trunc = vol->sdf_trunc;
     tp.unit_len = vol->unit_length;
+    tp.inv_unit = 1.0 / vol->unit_length;
     tp.slot_cap = (int)vol->hash_cap;
     bc.tiles = (unsigned)(((tp.ws + TT - 1) / TT) * ((tp.hs + TT - 1) / TT));
     tp.tiles = (int)bc.tiles;
     tp.stage_blocks = g_stage_blocks < 0 ? 2 * (int)bc.tiles : g_stage_blocks;
     tp.tf = g_touch_tf;
     // sharded volume: split front end (touch without staging -> units -> tile mask -> staging of the marked tiles)
-    const bool split = split_on(vol);
+    const bool split = split_on(vol) && tmask_fits(in.width, in.height);
     tp.sample_stage = split ? 1 : 0;
     if (split) {
         tp.stage_blocks = -1;
@@ -1676,16 +1711,13 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         q.vl = bc.ip0.vl, q.half = bc.ip0.half;
         q.unit_len = vol->unit_length;
         q.nframes = n;
-        unsigned* cur = vol->tmask + (size_t)vol->tmask_par * vol->tmask_words;
-        unsigned* oth = vol->tmask + (size_t)(vol->tmask_par ^ 1) * vol->tmask_words;
-        vol->tmask_par ^= 1;
         bc.split = true;
         bc.sq = q;
-        bc.smask = cur;
-        hipLaunchKernelGGL(k_stage_mask, dim3(256), dim3(256), 0, stream, (const BatchFrame*)bs.bframes, q,
-                           (const UnitWork*)work, (const int*)wcount, cur, oth, (int)vol->tmask_words);
-        hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)((q.tiles_x * q.tiles_y + 3) / 4), (unsigned)n), dim3(256), 0,
-                           stream, (const BatchFrame*)bs.bframes, (const float*)vol->mult, (const unsigned*)cur,
+        bc.smask = vol->tmask;
+        hipLaunchKernelGGL(k_stage_mask, dim3((unsigned)n), dim3(256), 0, stream, (const BatchFrame*)bs.bframes, q,
+                           (const UnitWork*)work, (const int*)wcount, vol->tmask);
+        hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)q.tiles_y, (unsigned)n), dim3(256), 0, stream,
+                           (const BatchFrame*)bs.bframes, (const float*)vol->mult, (const unsigned*)vol->tmask,
                            in.width, in.height, q.tiles_x, q.tiles_y, q.wpr, npx);
     }
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
@@ -1703,8 +1735,12 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     // counts as small from 16 ranks on.
     {
         const int resident = integrate_grid(bc.variant) / INT_GRID_MULT;
-        const int64_t est = vol->last_batch_slots >= 0 ? vol->last_batch_slots
-                                                       : (vol->dev.shard_world >= 16 ? 0 : (int64_t)1 << 30);
+        // 2..15 ranks: coarse always.  A sector rank's batches swing between a few units and a full arc (r06e, rank 0
+        // of 8: 135 / 677 / 662 / 317 units), so the previous batch mispredicts: the 677-unit batch took 214 us fine
+        // against ~145 us coarse, and coarse-only steps were the faster (0.985 vs 1.053 ms, r06i)
+        const int64_t est = vol->dev.shard_world > 1 && vol->dev.shard_world < 16 ? (int64_t)1 << 30
+                            : vol->last_batch_slots >= 0 ? vol->last_batch_slots
+                                                         : (vol->dev.shard_world >= 16 ? 0 : (int64_t)1 << 30);
         const bool fine = g_int_fine > 0 || (g_int_fine < 0 && est * INT_PARTS * 4 < (int64_t)resident * 3);
         if (fine) bc.variant |= 4 | (((g_int_depth > 0 ? g_int_depth : INT_FINE_KT) - 1) << 3);
     }
@@ -1876,12 +1912,11 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
         hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
                            vol->hmail + OT_MAIL_WORDS, (int*)nullptr, ++vol->units_seq);
         if (bc.split) {  // the replayed units' tiles, from the caller's frames (valid until this flush returns)
-            hipLaunchKernelGGL(k_stage_mask, dim3(256), dim3(256), 0, stream, (const BatchFrame*)bf, bc.sq,
-                               (const UnitWork*)work, (const int*)(vol->dev.counters + bc.pc), bc.smask,
-                               (unsigned*)nullptr, 0);
-            hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)((bc.sq.tiles_x * bc.sq.tiles_y + 3) / 4), (unsigned)bc.n),
-                               dim3(256), 0, stream, bf, (const float*)vol->mult, (const unsigned*)bc.smask, bc.sq.W,
-                               bc.sq.H, bc.sq.tiles_x, bc.sq.tiles_y, bc.sq.wpr, (int64_t)bc.sq.W * bc.sq.H);
+            hipLaunchKernelGGL(k_stage_mask, dim3((unsigned)bc.n), dim3(256), 0, stream, (const BatchFrame*)bf, bc.sq,
+                               (const UnitWork*)work, (const int*)(vol->dev.counters + bc.pc), bc.smask);
+            hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)bc.sq.tiles_y, (unsigned)bc.n), dim3(256), 0, stream, bf,
+                               (const float*)vol->mult, (const unsigned*)bc.smask, bc.sq.W, bc.sq.H, bc.sq.tiles_x,
+                               bc.sq.tiles_y, bc.sq.wpr, (int64_t)bc.sq.W * bc.sq.H);
         }
         const UnitWork* uw = work;
         const int* wc = vol->dev.counters + bc.pc;

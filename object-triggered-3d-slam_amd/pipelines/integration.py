@@ -69,8 +69,8 @@ class ScalableTSDFVolume:
             self._h = None
 
     def set_frontend_overlap(self, mode):
-        """Double-buffered batch front end (ot_tsdf_set_frontend_overlap): 1 on, 0 and -1 (default) off -- measured slower
-        than the serial front end at 2, 4 and 8 shards.
+        """Double-buffered batch front end (ot_tsdf_set_frontend_overlap): 1 on, 0 off, -1 (default) on for sharded
+        volumes only (with their split front end it is the faster at 2, 4 and 8 ranks).
         Batch k+1's staging / touch run beside batch k's integrate; results are identical in every mode.  Queued
         frames are integrated first, on the facade's stream (the C call refuses a volume with queued frames)."""
         self.flush()

@@ -43,10 +43,11 @@ def _host(t):
 
 @pytest.mark.parametrize("voxel,world,overlap,sector", [(0.01, 3, None, None), (0.005, 8, 1, None),
                                                         (0.005, 8, None, (0.0, 0.0)), (0.01, 3, None, (0.13, -0.2)),
-                                                        (0.005, 4, None, (0.0, 0.0))])
+                                                        (0.005, 4, None, (0.0, 0.0)), (0.005, 8, 1, (0.0, 0.0))])
 def test_shard_union_bitexact(pkg, seq16, gpu, voxel, world, overlap, sector):
-    """hashed blocks (split front end; the double-buffered one at 8 ranks) and azimuth sectors (split front end: the
-    touch stages nothing, only the tiles the rank's units project to are staged), centred and off-centre"""
+    """hashed blocks and azimuth sectors (split front end: the touch stages nothing, only the tiles the rank's units
+    project to are staged), centred and off-centre; at 8 ranks also with the double-buffered front end (the split
+    front end on the caller's stream beside the previous batch's integrate on the volume's integrate stream)"""
     full = _integrate(pkg, seq16, voxel)
     fk, ft, fw, fc = (_host(a) for a in full.export_units())
     parts = [_integrate(pkg, seq16, voxel, (r, world) + tuple(sector or ()), overlap) for r in range(world)]

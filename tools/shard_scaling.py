@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--split", default="-1")
     ap.add_argument("--fine", default="-1")
     ap.add_argument("--depth", default="-1", help="fine integrate's frame-pipeline depth KT (otx_integrate_depth)")
+    ap.add_argument("--tf", default="2", help="frames per touch workgroup (otx_touch_frames)")
+    ap.add_argument("--overlap", default="0", help="double-buffered front end (ot_tsdf_set_frontend_overlap)")
+    ap.add_argument("--batch", default="64", help="frames per batch (ot_tsdf_set_batch)")
     ap.add_argument("--ranks", default="all")
     ap.add_argument("--steps", type=int, default=10)
     a = ap.parse_args()
@@ -46,7 +49,10 @@ def main():
     for N in [int(x) for x in a.worlds.split(",")]:
         for owner in (a.owners.split(",") if N > 1 else ["unsharded"]):
             for split in [int(x) for x in a.split.split(",")]:
-                for fine, depth in [(int(x), int(y)) for x in a.fine.split(",") for y in a.depth.split(",")]:
+                for fine, depth, tf, ov, bt in [(int(x), int(y), int(t), int(o), int(b)) for x in a.fine.split(",")
+                                                for y in a.depth.split(",") for t in a.tf.split(",")
+                                                for o in a.overlap.split(",") for b in a.batch.split(",")]:
+                    L.call("otx_touch_frames", tf)
                     L.call("otx_split_frontend", split)
                     L.call("otx_integrate_fine", fine)
                     L.call("otx_integrate_depth", depth)
@@ -58,6 +64,8 @@ def main():
                             L.call("ot_tsdf_set_shard", vol, r, N)
                         elif owner == "sectors":
                             L.call("ot_tsdf_set_shard_sector", vol, r, N, cx, cy)
+                        L.call("ot_tsdf_set_frontend_overlap", vol, ov)
+                        L.call("ot_tsdf_set_batch", vol, bt)
 
                         def step():
                             L.call("ot_tsdf_reset_async", vol, s_)
@@ -88,12 +96,13 @@ def main():
                         worst["fe"] = max(worst["fe"], fm.value / max(fb.value, 1) * 1e3)
                         worst["units"] = max(worst["units"], nu.value)
                         L.call("ot_tsdf_destroy", vol)
-                    print(f"N {N:2d} {owner:9s} split {split:2d} fine {fine:2d} depth {depth:2d}: step {worst['step']:.3f} ms  "
+                    print(f"N {N:2d} {owner:9s} split {split:2d} fine {fine:2d} depth {depth:2d} tf {tf} overlap {ov} batch {bt}: step {worst['step']:.3f} ms  "
                           f"units max {worst['units']:5d}  integrate {worst['int']:6.1f} us/batch  front end "
                           f"{worst['fe']:6.1f} us/batch", flush=True)
     L.call("otx_integrate_fine", -1)
     L.call("otx_integrate_depth", -1)
     L.call("otx_split_frontend", -1)
+    L.call("otx_touch_frames", 2)
 
 
 if __name__ == "__main__":
