@@ -146,6 +146,7 @@ TEST_SIGNATURES = {
     "otx_touch_stage_blocks": [_i32],
     "otx_touch_frames": [_i32],
     "otx_split_frontend": [_i32],
+    "otx_defer_integrate": [_i32],
     "otx_integrate_depth": [_i32],
     "otx_mc_emit_fork": [_i32],
     "otx_normals_at": [_i32],

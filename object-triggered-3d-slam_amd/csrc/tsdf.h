@@ -242,6 +242,13 @@ struct ot_tsdf {
     int64_t tmask_words = 0;
     int tmask_w = 0, tmask_h = 0;  // the image size the masks are laid out for
     int split_mode = -1;          // -1 (default): split for sharded volumes; 0 off; 1 on (test hook)
+    // Deferred integrate of a sharded volume's last batch (round 6): its front end ran, its integrate waits to be launched
+    // together with the next batch's touch (k_integrate_touch) or alone by the next flush.  dfr_ctx holds the batch's
+    // context (tsdf.hip BatchCtx), dfr_stream the stream its front end ran on.
+    bool dfr_on = false;
+    hipStream_t dfr_stream = nullptr;
+    hipEvent_t ev_dfr = nullptr;  // dfr_stream -> a flush on another stream
+    alignas(16) unsigned char dfr_ctx[1024];
     // batch statistics since reset (ot_tsdf_batch_stats; the bench's compulsory-bytes figure): batches, units touched
     // summed over batches, units new in their batch; units the last batch left (-1: unknown after an import)
     int64_t stat_batches = 0, stat_unit_batches = 0, stat_fresh = 0, stat_prev_units = 0;

@@ -310,16 +310,24 @@ __device__ inline void stage_share(const BatchFrame* __restrict__ frames, const 
 // tools/shard_frontend.py), more than the staging it saves.
 // REPLAY (settle_batch, after the pool grew): the batch's touch again from its STAGED depths (the caller's frames may be
 // gone by then; the staged depth is exactly the value the first pass computed from them), no staging.
-template <bool REPLAY>
-__global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restrict__ frames, BatchTouchParams p,
-                                                     TsdfDev d, int nframes) {
-    __shared__ unsigned long long s_keys[LTAB];
-    __shared__ unsigned long long s_masks[LTAB];
-    __shared__ int s_used[LTAB];
-    __shared__ int s_nused;
+// LDS of one touch workgroup (k_batch_touch, and the touch half of k_integrate_touch)
+struct TouchLds {
+    unsigned long long keys[LTAB];
+    unsigned long long masks[LTAB];
+    int used[LTAB];
+    int nused;
+};
+// STAGE: the staging code paths (stage_blocks >= 0) are compiled in; the split front end's touch has none (the touch half
+// of k_integrate_touch: without them it fits 64 VGPRs instead of 96)
+template <bool REPLAY, bool STAGE = !REPLAY>
+__device__ __forceinline__ void touch_body(const BatchFrame* __restrict__ frames, const BatchTouchParams& p,
+                                           const TsdfDev& d, int nframes, TouchLds& L, int tile, int grp) {
+    unsigned long long* s_keys = L.keys;
+    unsigned long long* s_masks = L.masks;
+    int* s_used = L.used;
+    int& s_nused = L.nused;
     const int tid = threadIdx.x;
-    const int tile = (int)blockIdx.x, grp = (int)blockIdx.y;
-    if constexpr (!REPLAY) {
+    if constexpr (STAGE) {
         if (p.stage_blocks > 0 && tile >= p.tiles) {  // block-uniform
             stage_share(frames, p, nframes, grp, tile - p.tiles, p.stage_blocks);
             return;
@@ -331,7 +339,7 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
     }
     if (tid == 0) s_nused = 0;
     // (stage_blocks 0) this touch workgroup also stages a contiguous 1/tiles of its frames' pixels
-    if constexpr (!REPLAY) {
+    if constexpr (STAGE) {
         if (p.stage_blocks == 0) stage_share(frames, p, nframes, grp, tile, p.tiles);
     }
     __syncthreads();
@@ -416,6 +424,19 @@ __global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restric
             }
         }
     }
+}
+
+template <bool REPLAY>
+__global__ __launch_bounds__(256) void k_batch_touch(const BatchFrame* __restrict__ frames, BatchTouchParams p,
+                                                     TsdfDev d, int nframes) {
+    __shared__ TouchLds lds;
+    touch_body<REPLAY>(frames, p, d, nframes, lds, (int)blockIdx.x, (int)blockIdx.y);
+}
+// the split front end's touch (no staging paths compiled in: 69 instead of 96 VGPRs)
+__global__ __launch_bounds__(256) void k_batch_touch_split(const BatchFrame* __restrict__ frames, BatchTouchParams p,
+                                                           TsdfDev d, int nframes) {
+    __shared__ TouchLds lds;
+    touch_body<false, false>(frames, p, d, nframes, lds, (int)blockIdx.x, (int)blockIdx.y);
 }
 
 // ------------------------------------------------------------------------------------------------ integrate
@@ -757,17 +778,23 @@ constexpr int RCP_N = 2048;  // 16 KiB (float64) / 8 KiB (float32) of LDS per wo
 // whatever its registers); the parts of a unit run on one XCD.  Work items are assigned by a static grid stride that
 // every wave derives on its own: no atomics, one barrier (the reciprocal table).
 // C64: colour state in float64 (Open3D's TSDFVoxel::color_ is Eigen::Vector3d), in the record's float64 planes.
-template <bool C64, bool FAST, int ZB = BZ, int KT = 1>
-__global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : (ZB == 2 ? 4 : INT_WAVES_PER_EU)) void k_batch_integrate(
-    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
-    const int* __restrict__ wcount) {
+// one table per kernel: float64 reciprocals for the float64-colour kernel (its float32 ones are their roundings:
+// (float)RN64(1/n) == RN32(1/n) for every n <= 2^20, no double-rounding case -- tools/markstein_check.cpp), float32
+// ones otherwise
+template <bool C64, bool FAST>
+struct RcpLds {
+    float r32[(FAST && !C64) ? RCP_N + 1 : 1];
+    double r64[(FAST && C64) ? RCP_N + 1 : 1];
+};
+// the integrate of a batch as workgroup `bid` of `nblk` (k_batch_integrate; the integrate half of k_integrate_touch)
+template <bool C64, bool FAST, int ZB, int KT>
+__device__ __forceinline__ void integrate_body(const BatchFrame* __restrict__ frames, const IntegrateParams& p,
+                                               const TsdfDev& d, const UnitWork* __restrict__ work,
+                                               const int* __restrict__ wcount, RcpLds<C64, FAST>& R, int bid, int nblk) {
     using CT = typename std::conditional<C64, double, float>::type;
     constexpr int PARTS = 4 * (UNIT_RES / ZB) / INT_WG;  // workgroups per unit (INT_PARTS at the default ZB)
-    // one table per kernel: float64 reciprocals for the float64-colour kernel (its float32 ones are their roundings:
-    // (float)RN64(1/n) == RN32(1/n) for every n <= 2^20, no double-rounding case -- tools/markstein_check.cpp),
-    // float32 ones otherwise
-    __shared__ float s_r32[(FAST && !C64) ? RCP_N + 1 : 1];
-    __shared__ double s_r64[(FAST && C64) ? RCP_N + 1 : 1];
+    float* s_r32 = R.r32;
+    double* s_r64 = R.r64;
     // work item = (unit, part): the PARTS parts of a unit are items 8 apart, so they run on one XCD (blocks are dealt
     // round-robin over the 8 XCDs) at about the same time and share its L2's copy of the footprint.
     // The grid is sized for large batches (8x the resident workgroups): a workgroup without an item leaves before
@@ -775,7 +802,7 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : (ZB == 2 ? 4 : IN
     // more than the integrate itself (r05e: a 1/8 shard's 64-frame batch 165-200 us whatever its slicing)
     {
         const int n0 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(wcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if ((int)blockIdx.x >= (PARTS == 1 ? n0 : ((n0 + 7) / 8) * 8 * PARTS)) return;
+        if (bid >= (PARTS == 1 ? n0 : ((n0 + 7) / 8) * 8 * PARTS)) return;
     }
     if constexpr (FAST) {
         for (int r = threadIdx.x; r <= RCP_N; r += 64 * INT_WG) {
@@ -789,9 +816,9 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : (ZB == 2 ? 4 : IN
     const int npx = p.W * p.H;
     unsigned upd = 0;  // per lane: <= ZB voxels x 64 frames x units per workgroup, far below 2^32
     {
-        const int b = blockIdx.x;
+        const int b = bid;
         const int items = PARTS == 1 ? n : ((n + 7) / 8) * 8 * PARTS;
-        for (int it = b; it < items; it += gridDim.x) {
+        for (int it = b; it < items; it += nblk) {
             const int u = PARTS == 1 ? it : (it / (8 * PARTS)) * 8 + (it & 7);
             if (PARTS > 1 && u >= n) continue;
             const int part = PARTS == 1 ? 0 : (it >> 3) % PARTS;
@@ -1109,6 +1136,39 @@ __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : (ZB == 2 ? 4 : IN
     }
     const unsigned long long tot = wave_sum((unsigned long long)upd);
     if (lane == 0 && tot) atomicAdd(&d.stats[S_UPDATES], tot);
+}
+
+template <bool C64, bool FAST, int ZB = BZ, int KT = 1>
+__global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : (ZB == 2 ? 4 : INT_WAVES_PER_EU)) void k_batch_integrate(
+    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
+    const int* __restrict__ wcount) {
+    __shared__ RcpLds<C64, FAST> R;
+    integrate_body<C64, FAST, ZB, KT>(frames, p, d, work, wcount, R, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// The deferred integrate of a sharded volume's batch k and the touch of batch k + 1 in ONE launch (round 6): workgroups
+// [0, nint) integrate batch k (its set's staging and work list), the rest are batch k + 1's touch tiles (frame groups
+// along the grid).  A rank's integrate fills few of the CUs (a shard's batch is a few hundred units), so its latency-bound
+// touch runs in the gaps, with no second stream and no event between them (two streams' fork + join cost ~25 us of idle
+// GPU per batch: the double-buffered front end).  The touch writes only batch k + 1's state: its frame
+// masks / slot list / pair counter, hash inserts of its units, and the staged pixels of its samples in its own set --
+// nothing the integrate of batch k reads.  LDS: the touch's tables and the reciprocal table share one block.
+template <bool C64, bool FAST>
+__global__ __launch_bounds__(64 * INT_WG, INT_WAVES_PER_EU) void k_integrate_touch(
+    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
+    const int* __restrict__ wcount, int nint, const BatchFrame* __restrict__ tframes, BatchTouchParams tp, int tn) {
+    union Lds {
+        TouchLds t;
+        RcpLds<C64, FAST> r;
+    };
+    __shared__ Lds lds;
+    const int b = (int)blockIdx.x;
+    if (b < nint) {
+        integrate_body<C64, FAST, BZ, 1>(frames, p, d, work, wcount, lds.r, b, nint);
+    } else {
+        const int t = b - nint;
+        touch_body<false, false>(tframes, tp, d, tn, lds.t, t % tp.tiles, t / tp.tiles);
+    }
 }
 
 // export: units in sorted order, voxels transposed to Open3D IndexOf order (x*256 + y*16 + z); colour as CT
@@ -1533,6 +1593,7 @@ struct BatchCtx {
     IntegrateParams ip0;
     unsigned tiles;
     int n, pc, variant, set;
+    bool defer = false;         // deferred integrate (k_integrate_touch / the next flush launches it)
     bool split = false;         // split front end: a replay stages its units' tiles too (units the full hash dropped
     StageMaskParams sq{};       // were in no work list of the first pass, so their footprints were never staged)
     unsigned* smask = nullptr;  // the batch's tile masks (its parity)
@@ -1546,6 +1607,9 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
 static bool overlap_on(const ot_tsdf* vol) {
     return vol->overlap_mode > 0 || (vol->overlap_mode < 0 && vol->dev.shard_world > 1);
 }
+static bool split_on(const ot_tsdf* vol);
+static bool tmask_fits(int w, int h);
+static bool defer_on(const ot_tsdf* vol, bool split);
 // the split front end: sharded volumes.  Its tile masks are written and read on the caller's stream only (mask kernel,
 // then staging), so one buffer serves the double-buffered front end too: the integrate on istream never reads them.
 static int g_split = -1;  // test hook otx_split_frontend: -1 by the volume (default), 0 never, 1 always (unsharded too)
@@ -1573,6 +1637,15 @@ static ot_status ensure_tmask(ot_tsdf* vol, int w, int h, hipStream_t stream) {
     return OT_OK;
 }
 static void* set_work(ot_tsdf* vol, int s) { return s == 0 ? vol->dev.work : vol->bset[1].work; }
+// Deferred integrate (round 6): a sharded volume with the split front end launches batch k's integrate together with
+// batch k + 1's touch (k_integrate_touch, one stream, no events) -- the default from 4 ranks on (r06k, sector rank steps:
+// 0.919 vs 1.003 ms at 8, 1.301 vs 1.336 at 4, but 2.165 vs 2.075 at 2, where the rank's integrate fills the GPU and the
+// double-buffered front end stays the default) unless the double-buffered front end is asked for (overlap mode 1)
+static int g_defer = -1;  // test hook otx_defer_integrate: -1 by the volume (default), 0 never, 1 with any split batch
+static bool defer_on(const ot_tsdf* vol, bool split) {
+    if (!split || g_defer == 0 || vol->overlap_mode > 0) return false;
+    return g_defer > 0 || vol->dev.shard_world >= 4;
+}
 
 // order `stream` after the last batch's integrate when it ran on the volume's integrate stream
 static ot_status join_integrate(ot_tsdf* vol, hipStream_t stream) {
@@ -1598,17 +1671,69 @@ static ot_status ensure_overlap(ot_tsdf* vol) {
     return OT_OK;
 }
 
+// Launch the deferred batch's integrate on `stream`: with the touch of batch `next` in one launch (k_integrate_touch), or
+// alone (next == nullptr: a flush).  Coarse slices, the variant's colour precision and division form.
+static ot_status launch_deferred(ot_tsdf* vol, hipStream_t stream, const BatchCtx* next) {
+    if (!vol->dfr_on) return OT_OK;
+    BatchCtx D;
+    std::memcpy(&D, vol->dfr_ctx, sizeof(BatchCtx));
+    vol->dfr_on = false;
+    if (stream != vol->dfr_stream) {  // the batch's front end ran on another stream
+        if (!vol->ev_dfr) OT_HIP_TRY(hipEventCreateWithFlags(&vol->ev_dfr, hipEventDisableTiming));
+        OT_HIP_TRY(hipEventRecord(vol->ev_dfr, vol->dfr_stream));
+        OT_HIP_TRY(hipStreamWaitEvent(stream, vol->ev_dfr, 0));
+    }
+    const BatchFrame* bf = vol->bset[D.set].bframes;
+    const UnitWork* uw = (const UnitWork*)set_work(vol, D.set);
+    const int* wc = vol->wcount + D.set;
+    const int variant = D.variant & 3;  // coarse
+    const int nint = integrate_grid(variant);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (vol->profiling) {
+        OT_HIP_TRY(hipEventCreate(&e0));
+        OT_HIP_TRY(hipEventCreate(&e1));
+        OT_HIP_TRY(hipEventRecord(e0, stream));
+    }
+    if (next) {
+        const BatchFrame* tf = vol->bset[next->set].bframes;
+        BatchTouchParams tp = next->tp;
+        int tn = next->n;
+        int ni = nint;
+        void* args[] = {(void*)&bf, (void*)&D.ip0, (void*)&vol->dev, (void*)&uw, (void*)&wc, (void*)&ni,
+                        (void*)&tf, (void*)&tp, (void*)&tn};
+        static const void* const kt[4] = {(const void*)k_integrate_touch<false, false>,
+                                          (const void*)k_integrate_touch<false, true>,
+                                          (const void*)k_integrate_touch<true, false>,
+                                          (const void*)k_integrate_touch<true, true>};
+        const unsigned grid = (unsigned)nint + next->tiles * (unsigned)((tn + tp.tf - 1) / tp.tf);
+        OT_HIP_TRY(hipLaunchKernel(kt[variant], dim3(grid), dim3(64 * INT_WG), args, 0, stream));
+    } else {
+        void* args[] = {(void*)&bf, (void*)&D.ip0, (void*)&vol->dev, (void*)&uw, (void*)&wc};
+        OT_HIP_TRY(hipLaunchKernel(integrate_kernel(variant), dim3(nint), dim3(64 * INT_WG), args, 0, stream));
+    }
+    OT_LAUNCH_CHECK();
+    if (vol->profiling) {
+        OT_HIP_TRY(hipEventRecord(e1, stream));
+        vol->prof_events.emplace_back(e0, e1);
+    }
+    return OT_OK;
+}
+
 static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n, hipStream_t stream) {
     const ot_intrinsics& in = frames[0].intr;
     ot_status st = wait_normals(vol, stream);  // deferred vertex normals of the last mesh still read the volume
     if (st != OT_OK) return st;
     st = ensure_mult(vol, &in, stream);
     if (st != OT_OK) return st;
-    const bool ovl = overlap_on(vol);
-    if (ovl && (st = ensure_overlap(vol)) != OT_OK) return st;
-    const int set = ovl ? vol->bset_next : 0;
-    if (ovl) vol->bset_next ^= 1;
+    const bool split = split_on(vol) && tmask_fits(in.width, in.height);
+    const bool defer = defer_on(vol, split);
+    const bool ovl = !defer && overlap_on(vol);
+    if ((ovl || defer) && (st = ensure_overlap(vol)) != OT_OK) return st;
+    const int set = (ovl || defer) ? vol->bset_next : 0;
+    if (ovl || defer) vol->bset_next ^= 1;
     auto& bs = vol->bset[set];
+    // (deferred: the set's last batch was integrated inside the launch with the previous batch's touch, queued on
+    // this stream before that batch's units kernel -- done before anything below restages the set)
     // the set's previous batch (two batches ago) must have finished its integrate before its buffers are restaged
     // (an event never recorded counts as complete)
     if (ovl) OT_HIP_TRY(hipStreamWaitEvent(stream, bs.ev_done, 0));
@@ -1678,7 +1803,6 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     tp.stage_blocks = g_stage_blocks < 0 ? 2 * (int)bc.tiles : g_stage_blocks;
     tp.tf = g_touch_tf;
     // sharded volume: split front end (touch without staging -> units -> tile mask -> staging of the marked tiles)
-    const bool split = split_on(vol) && tmask_fits(in.width, in.height);
     tp.sample_stage = split ? 1 : 0;
     if (split) {
         tp.stage_blocks = -1;
@@ -1687,6 +1811,7 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
     bc.n = n;
     bc.pc = pc;
     bc.set = set;
+    bc.defer = defer;
     hipEvent_t f0 = nullptr, f1 = nullptr;  // front end (staging + touch + units): the part a sharded volume repeats
     if (vol->profiling) {
         OT_HIP_TRY(hipEventCreate(&f0));
@@ -1694,12 +1819,19 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         OT_HIP_TRY(hipEventRecord(f0, stream));
     }
     UnitWork* work = (UnitWork*)set_work(vol, set);
-    int* wcount = ovl ? vol->wcount + set : vol->dev.counters + pc;
-    hipLaunchKernelGGL(k_batch_touch<false>,
-                       dim3(bc.tiles + (unsigned)std::max(0, tp.stage_blocks), (unsigned)((n + tp.tf - 1) / tp.tf)),
-                       dim3(256), 0, stream, (const BatchFrame*)bs.bframes, tp, vol->dev, n);
+    int* wcount = (ovl || defer) ? vol->wcount + set : vol->dev.counters + pc;
+    if (defer && vol->dfr_on) {  // the last batch's integrate and this batch's touch in one launch
+        if ((st = launch_deferred(vol, stream, &bc)) != OT_OK) return st;
+    } else if (split) {
+        hipLaunchKernelGGL(k_batch_touch_split, dim3(bc.tiles, (unsigned)((n + tp.tf - 1) / tp.tf)), dim3(256), 0,
+                           stream, (const BatchFrame*)bs.bframes, tp, vol->dev, n);
+    } else {
+        hipLaunchKernelGGL(k_batch_touch<false>,
+                           dim3(bc.tiles + (unsigned)std::max(0, tp.stage_blocks), (unsigned)((n + tp.tf - 1) / tp.tf)),
+                           dim3(256), 0, stream, (const BatchFrame*)bs.bframes, tp, vol->dev, n);
+    }
     hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, work, pc,
-                       vol->hmail + OT_MAIL_WORDS, ovl ? wcount : (int*)nullptr, ++vol->units_seq);
+                       vol->hmail + OT_MAIL_WORDS, (ovl || defer) ? wcount : (int*)nullptr, ++vol->units_seq);
     if (split) {
         StageMaskParams q;
         q.W = in.width;
@@ -1741,8 +1873,23 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         const int64_t est = vol->dev.shard_world > 1 && vol->dev.shard_world < 16 ? (int64_t)1 << 30
                             : vol->last_batch_slots >= 0 ? vol->last_batch_slots
                                                          : (vol->dev.shard_world >= 16 ? 0 : (int64_t)1 << 30);
-        const bool fine = g_int_fine > 0 || (g_int_fine < 0 && est * INT_PARTS * 4 < (int64_t)resident * 3);
+        const bool fine = !defer && (g_int_fine > 0 || (g_int_fine < 0 && est * INT_PARTS * 4 < (int64_t)resident * 3));
         if (fine) bc.variant |= 4 | (((g_int_depth > 0 ? g_int_depth : INT_FINE_KT) - 1) << 3);
+    }
+    if (defer) {  // the integrate waits for the next batch's touch (or the next flush)
+        if (vol->profiling) {
+            OT_HIP_TRY(hipEventRecord(f1, stream));
+            vol->prof_fe_events.emplace_back(f0, f1);
+        }
+        static_assert(sizeof(BatchCtx) <= sizeof(vol->dfr_ctx), "deferred batch context");
+        std::memcpy(vol->dfr_ctx, &bc, sizeof(BatchCtx));
+        vol->dfr_on = true;
+        vol->dfr_stream = stream;
+        vol->batch_pc ^= 1;
+        vol->frame_id += n;
+        vol->sorted_frame = -1;
+        vol->early_frame = vol->frame_id;
+        return settle_batch(vol, bc, stream);
     }
     const int grid = integrate_grid(bc.variant);
     // overlap: the integrate on istream behind this set's units kernel (and the previous batch's integrate: same
@@ -1909,6 +2056,17 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
         UnitWork* work = (UnitWork*)set_work(vol, bc.set);
         hipLaunchKernelGGL(k_batch_touch<true>, dim3(bc.tiles, (unsigned)((bc.n + tp.tf - 1) / tp.tf)), dim3(256), 0, stream,
                            bf, tp, vol->dev, bc.n);
+        if (bc.defer) {  // nothing of the batch is integrated yet: rebuild its whole work list, restage, stay deferred
+            hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
+                               vol->hmail + OT_MAIL_WORDS, vol->wcount + bc.set, ++vol->units_seq);
+            hipLaunchKernelGGL(k_stage_mask, dim3((unsigned)bc.n), dim3(256), 0, stream, (const BatchFrame*)bf, bc.sq,
+                               (const UnitWork*)work, (const int*)(vol->wcount + bc.set), bc.smask);
+            hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)bc.sq.tiles_y, (unsigned)bc.n), dim3(256), 0, stream, bf,
+                               (const float*)vol->mult, (const unsigned*)bc.smask, bc.sq.W, bc.sq.H, bc.sq.tiles_x,
+                               bc.sq.tiles_y, bc.sq.wpr, (int64_t)bc.sq.W * bc.sq.H);
+            OT_LAUNCH_CHECK();
+            continue;
+        }
         hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
                            vol->hmail + OT_MAIL_WORDS, (int*)nullptr, ++vol->units_seq);
         if (bc.split) {  // the replayed units' tiles, from the caller's frames (valid until this flush returns)
@@ -1967,7 +2125,10 @@ ot_status tsdf_flush(ot_tsdf* vol, hipStream_t stream, bool join) {
         if (st != OT_OK) return st;
         i += n;
     }
-    return join ? join_integrate(vol, stream) : OT_OK;
+    if (!join) return OT_OK;
+    ot_status st = launch_deferred(vol, stream, nullptr);  // a reader needs the last batch integrated
+    if (st != OT_OK) return st;
+    return join_integrate(vol, stream);
 }
 
 static ot_status counter_errors(const int* c) {
@@ -2203,6 +2364,7 @@ ot_status ot_tsdf_destroy(ot_tsdf* v) {
     if (v->ev_join) (void)hipEventDestroy(v->ev_join);
     if (v->ev_normals) (void)hipEventDestroy(v->ev_normals);
     if (v->ev_made) (void)hipEventDestroy(v->ev_made);
+    if (v->ev_dfr) (void)hipEventDestroy(v->ev_dfr);
     if (v->side) (void)hipStreamDestroy(v->side);
     if (v->istream) (void)hipStreamDestroy(v->istream);
     for (auto& b : v->bset) {
@@ -2570,6 +2732,12 @@ ot_status ot_tsdf_set_shard_sector(ot_tsdf* vol, int32_t rank, int32_t world, do
 ot_status otx_integrate_depth(int32_t kt) {
     if (kt != -1 && (kt < 1 || kt > 3)) return fail(OT_ERR_INVALID_ARGUMENT, "integrate pipeline depth must be -1 or 1..3");
     g_int_depth = kt;
+    return OT_OK;
+}
+
+ot_status otx_defer_integrate(int32_t mode) {
+    if (mode < -1 || mode > 1) return fail(OT_ERR_INVALID_ARGUMENT, "deferred integrate mode must be -1, 0 or 1");
+    g_defer = mode;
     return OT_OK;
 }
 

@@ -203,13 +203,16 @@ def test_touch_staging_forms_bitexact(pkg, O, gpu, synth, blocks, tf):
         L.call("otx_touch_frames", 2)
 
 
-@pytest.mark.parametrize("batch", [16, 1])
-def test_split_frontend_bitexact(pkg, O, gpu, synth, seq16, batch):
+@pytest.mark.parametrize("batch,defer", [(16, 0), (1, 0), (16, 1), (1, 1)])
+def test_split_frontend_bitexact(pkg, O, gpu, synth, seq16, batch, defer):
     """The split front end (round 6: touch without staging, the batch units' footprint tiles marked, only those tiles
     staged) forced on an unsharded volume, where every visible tile must be marked: 40 frames at 5 mm, the odd
-    321x243 camera (partial 32x16 tiles, quads straddling rows) and the float-depth path, bitwise vs the oracle."""
+    321x243 camera (partial 32x16 tiles, quads straddling rows) and the float-depth path, bitwise vs the oracle;
+    with the deferred integrate too (each batch's integrate launched with the next batch's touch, k_integrate_touch,
+    the last one by the reader's flush)."""
     L = pkg._lib
     L.call("otx_split_frontend", 1)
+    L.call("otx_defer_integrate", defer)
     try:
         depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=80, frames=range(0, 80, 2))
         vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005, batch=batch)
@@ -223,6 +226,7 @@ def test_split_frontend_bitexact(pkg, O, gpu, synth, seq16, batch):
         _compare_volumes(vol, ref)
     finally:
         L.call("otx_split_frontend", -1)
+        L.call("otx_defer_integrate", -1)
 
 
 @pytest.mark.parametrize("batch", [1, None])

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--tf", default="2", help="frames per touch workgroup (otx_touch_frames)")
     ap.add_argument("--overlap", default="0", help="double-buffered front end (ot_tsdf_set_frontend_overlap)")
     ap.add_argument("--batch", default="64", help="frames per batch (ot_tsdf_set_batch)")
+    ap.add_argument("--defer", default="-1", help="deferred integrate (otx_defer_integrate)")
     ap.add_argument("--ranks", default="all")
     ap.add_argument("--steps", type=int, default=10)
     a = ap.parse_args()
@@ -49,9 +50,11 @@ def main():
     for N in [int(x) for x in a.worlds.split(",")]:
         for owner in (a.owners.split(",") if N > 1 else ["unsharded"]):
             for split in [int(x) for x in a.split.split(",")]:
-                for fine, depth, tf, ov, bt in [(int(x), int(y), int(t), int(o), int(b)) for x in a.fine.split(",")
+                for fine, depth, tf, ov, bt, df in [(int(x), int(y), int(t), int(o), int(b), int(df)) for x in a.fine.split(",")
                                                 for y in a.depth.split(",") for t in a.tf.split(",")
-                                                for o in a.overlap.split(",") for b in a.batch.split(",")]:
+                                                for o in a.overlap.split(",") for b in a.batch.split(",")
+                                                for df in a.defer.split(",")]:
+                    L.call("otx_defer_integrate", df)
                     L.call("otx_touch_frames", tf)
                     L.call("otx_split_frontend", split)
                     L.call("otx_integrate_fine", fine)
@@ -96,13 +99,14 @@ def main():
                         worst["fe"] = max(worst["fe"], fm.value / max(fb.value, 1) * 1e3)
                         worst["units"] = max(worst["units"], nu.value)
                         L.call("ot_tsdf_destroy", vol)
-                    print(f"N {N:2d} {owner:9s} split {split:2d} fine {fine:2d} depth {depth:2d} tf {tf} overlap {ov} batch {bt}: step {worst['step']:.3f} ms  "
+                    print(f"N {N:2d} {owner:9s} split {split:2d} fine {fine:2d} depth {depth:2d} tf {tf} overlap {ov} batch {bt} defer {df}: step {worst['step']:.3f} ms  "
                           f"units max {worst['units']:5d}  integrate {worst['int']:6.1f} us/batch  front end "
                           f"{worst['fe']:6.1f} us/batch", flush=True)
     L.call("otx_integrate_fine", -1)
     L.call("otx_integrate_depth", -1)
     L.call("otx_split_frontend", -1)
     L.call("otx_touch_frames", 2)
+    L.call("otx_defer_integrate", -1)
 
 
 if __name__ == "__main__":
