@@ -1138,12 +1138,360 @@ __device__ __forceinline__ void integrate_body(const BatchFrame* __restrict__ fr
     if (lane == 0 && tot) atomicAdd(&d.stats[S_UPDATES], tot);
 }
 
+// The product kernel keeps its own text (the same per-voxel code as integrate_body): compiled from the shared inlined
+// body, its frame loop gained five uniform branches and lost 1.3 % (0.726 vs 0.717 ms per launch, r06n vs r06j)
 template <bool C64, bool FAST, int ZB = BZ, int KT = 1>
 __global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : (ZB == 2 ? 4 : INT_WAVES_PER_EU)) void k_batch_integrate(
     const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
     const int* __restrict__ wcount) {
-    __shared__ RcpLds<C64, FAST> R;
-    integrate_body<C64, FAST, ZB, KT>(frames, p, d, work, wcount, R, (int)blockIdx.x, (int)gridDim.x);
+    using CT = typename std::conditional<C64, double, float>::type;
+    constexpr int PARTS = 4 * (UNIT_RES / ZB) / INT_WG;  // workgroups per unit (INT_PARTS at the default ZB)
+    // one table per kernel: float64 reciprocals for the float64-colour kernel (its float32 ones are their roundings:
+    // (float)RN64(1/n) == RN32(1/n) for every n <= 2^20, no double-rounding case -- tools/markstein_check.cpp),
+    // float32 ones otherwise
+    __shared__ float s_r32[(FAST && !C64) ? RCP_N + 1 : 1];
+    __shared__ double s_r64[(FAST && C64) ? RCP_N + 1 : 1];
+    // work item = (unit, part): the PARTS parts of a unit are items 8 apart, so they run on one XCD (blocks are dealt
+    // round-robin over the 8 XCDs) at about the same time and share its L2's copy of the footprint.
+    // The grid is sized for large batches (8x the resident workgroups): a workgroup without an item leaves before
+    // building the reciprocal table -- for a batch of few units (a spatial shard) the idle workgroups' tables had cost
+    // more than the integrate itself (r05e: a 1/8 shard's 64-frame batch 165-200 us whatever its slicing)
+    {
+        const int n0 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(wcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if ((int)blockIdx.x >= (PARTS == 1 ? n0 : ((n0 + 7) / 8) * 8 * PARTS)) return;
+    }
+    if constexpr (FAST) {
+        for (int r = threadIdx.x; r <= RCP_N; r += 64 * INT_WG) {
+            if constexpr (C64) s_r64[r] = 1.0 / (double)r;  // IEEE (correctly rounded) quotients
+            else s_r32[r] = 1.0f / (float)r;
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int n = *wcount;
+    const int npx = p.W * p.H;
+    unsigned upd = 0;  // per lane: <= ZB voxels x 64 frames x units per workgroup, far below 2^32
+    {
+        const int b = blockIdx.x;
+        const int items = PARTS == 1 ? n : ((n + 7) / 8) * 8 * PARTS;
+        for (int it = b; it < items; it += gridDim.x) {
+            const int u = PARTS == 1 ? it : (it / (8 * PARTS)) * 8 + (it & 7);
+            if (PARTS > 1 && u >= n) continue;
+            const int part = PARTS == 1 ? 0 : (it >> 3) % PARTS;
+            const int s = __builtin_amdgcn_readfirstlane(part * INT_WG + (int)(threadIdx.x >> 6));  // slice of this wave
+            const UnitWork& w = work[u];
+            const int ent = w.id;
+            const unsigned long long mask = w.mask;
+            if (ent != -1) {
+                const int id = ent & 0x7FFFFFFF;
+                const bool fresh = ent < 0;
+                // wave = 8 x 8 columns: a square patch of the unit's xy plane projects to fewer pixel rows
+                const int x = (s & 2) * 4 + (lane >> 3), y = (s & 1) * 8 + (lane & 7);
+                const int col = x * 16 + y;
+                const int z0 = (s >> 2) * ZB;
+                float* base = d.vox + (size_t)id * (C64 ? UNIT_FLOATS_C64 : UNIT_FLOATS);
+                // colour plane c of voxel vi: float32 planes addressed from base (one address register for the
+                // whole record: a separate colour pointer costs ~34 VGPRs in this kernel), float64 through a buffer
+                // resource over the record's float64 planes
+                const __amdgpu_buffer_rsrc_t col64 = make_rsrc(base + 2 * UNIT_VOX, 3 * UNIT_VOX * 8);
+                float ts[ZB], wt[ZB];
+                CT cr[ZB], cg[ZB], cb[ZB];
+#pragma unroll
+                for (int k = 0; k < ZB; ++k) {
+                    const int vi = (z0 + k) * 256 + col;
+                    if (fresh) {
+                        ts[k] = wt[k] = 0.0f;
+                        cr[k] = cg[k] = cb[k] = (CT)0;
+                    } else {
+                        ts[k] = base[vi];
+                        wt[k] = base[UNIT_VOX + vi];
+                        if constexpr (C64) {
+                            cr[k] = ld_f64(col64, vi);
+                            cg[k] = ld_f64(col64, UNIT_VOX + vi);
+                            cb[k] = ld_f64(col64, 2 * UNIT_VOX + vi);
+                        } else {
+                            cr[k] = base[2 * UNIT_VOX + vi];
+                            cg[k] = base[3 * UNIT_VOX + vi];
+                            cb[k] = base[4 * UNIT_VOX + vi];
+                        }
+                    }
+                }
+                const float ox = (float)((double)w.kx * p.unit_len);
+                const float oy = (float)((double)w.ky * p.unit_len);
+                const float oz = (float)((double)w.kz * p.unit_len);
+                const float px = (p.half + p.vl * (float)x) + ox;
+                const float py = (p.half + p.vl * (float)y) + oy;
+                const float pz = p.half + oz;
+                const unsigned upd0 = upd;
+                if constexpr (ZB == 2) {
+                    // Frame pipeline (the fine slices serve batches with few units, whose waves cannot hide a frame's
+                    // dependent gathers behind other waves: the wave's chain of frames IS the batch's time).  Every
+                    // load of a frame is state-independent -- the projections and depth gathers (tap), the depth test,
+                    // clamped tsdf term and colour gather (stage C) -- only the running means (stage D) read the
+                    // voxel state.  So frame f+KT's tap and frame f+KC's stage C are issued before frame f's update,
+                    // from KT + 1 register slots (the loop is unrolled over the slots so every slot is a fixed
+                    // register set: a rotating copy would wait for the loads in flight).  The updates still run in
+                    // frame order with the same arithmetic: the bits are the unpipelined loop's.  KT = 1, KC = 0 is the
+                    // round-5 one-frame skew.
+                    constexpr int KC = KT - 1, RS = KT + 1;
+                    unsigned long long mt = mask;  // frames not yet tapped
+                    int fs[RS];                     // frame of each slot (wave-uniform), -1: past the last frame
+                    int pixv[RS][ZB];
+                    float pcz[RS][ZB], dv[RS][ZB], mv[RS][ZB], tnv[RS][ZB];
+                    uint32_t cv[RS][ZB];
+                    bool dov[RS][ZB];
+                    auto tap = [&](auto J) __attribute__((always_inline)) {
+                        constexpr int j = decltype(J)::value;
+                        if (mt) {
+                            const int f = __ffsll((long long)mt) - 1;
+                            mt &= mt - 1;
+                            fs[j] = f;
+                            frame_tap<ZB>(frames[f], p, npx, px, py, pz, z0, pixv[j], pcz[j], dv[j], mv[j]);
+                        } else {
+                            fs[j] = -1;
+                        }
+                    };
+                    auto stage_c = [&](auto J) __attribute__((always_inline)) {
+                        constexpr int j = decltype(J)::value;
+                        if (fs[j] < 0) return;
+                        const BatchFrame& fr = frames[fs[j]];
+                        const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
+                        const bool use_color = fr.color != nullptr;
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            const float sdf = (dv[j][k] - pcz[j][k]) * mv[j][k];
+                            dov[j][k] = (pixv[j][k] >= 0) & (dv[j][k] > 0.0f) & (sdf > -p.trunc);
+                            const float sv = sdf * p.trunc_inv;
+                            tnv[j][k] = (sv < 1.0f) ? sv : 1.0f;
+                            cv[j][k] = 0u;
+                            if (use_color && dov[j][k])
+                                cv[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[j][k] * 4, 0, 0);
+                        }
+                    };
+                    auto stage_d = [&](auto J) __attribute__((always_inline)) -> bool {
+                        constexpr int j = decltype(J)::value;
+                        if (fs[j] < 0) return false;
+                        const bool use_color = frames[fs[j]].color != nullptr;
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            const bool doit = dov[j][k];
+                            const float tn = tnv[j][k];
+                            const float wv = wt[k];
+                            const float w1 = wv + 1.0f;
+                            const float ta = ts[k] * wv + tn;
+                            float tsn;
+                            const double y64 = (FAST && C64) ? s_r64[(int)w1] : 0.0;
+                            if constexpr (FAST) {
+                                const float y = C64 ? (float)y64 : s_r32[(int)w1];
+                                const float q0 = ta * y;
+                                tsn = __builtin_fmaf(__builtin_fmaf(-w1, q0, ta), y, q0);
+                            } else {
+                                tsn = ta / w1;
+                            }
+                            ts[k] = doit ? tsn : ts[k];
+                            if (use_color) {
+                                const uint32_t c = cv[j][k];
+                                if constexpr (C64) {
+                                    const double wd = (double)wv, w1d = (double)w1;
+                                    const double ar = cr[k] * wd + (double)(c & 0xFFu);
+                                    const double ag = cg[k] * wd + (double)((c >> 8) & 0xFFu);
+                                    const double ab = cb[k] * wd + (double)((c >> 16) & 0xFFu);
+                                    double nr, ng, nb;
+                                    if constexpr (FAST) {
+                                        const double y = y64;
+                                        const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
+                                        nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
+                                        ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
+                                        nb = __builtin_fma(__builtin_fma(-w1d, q0b, ab), y, q0b);
+                                    } else {
+                                        nr = ar / w1d;
+                                        ng = ag / w1d;
+                                        nb = ab / w1d;
+                                    }
+                                    cr[k] = doit ? nr : cr[k];
+                                    cg[k] = doit ? ng : cg[k];
+                                    cb[k] = doit ? nb : cb[k];
+                                } else {
+                                    const float rw = __builtin_amdgcn_rcpf(w1);
+                                    const float nr = ((float)cr[k] * wv + (float)(c & 0xFFu)) * rw;
+                                    const float ng = ((float)cg[k] * wv + (float)((c >> 8) & 0xFFu)) * rw;
+                                    const float nb = ((float)cb[k] * wv + (float)((c >> 16) & 0xFFu)) * rw;
+                                    cr[k] = doit ? nr : cr[k];
+                                    cg[k] = doit ? ng : cg[k];
+                                    cb[k] = doit ? nb : cb[k];
+                                }
+                            }
+                            wt[k] = doit ? w1 : wv;
+                            upd += doit ? 1u : 0u;
+                        }
+                        return true;
+                    };
+                    // one iteration = frame f in slot J: stage C of f + KC, the tap of f + KT (into the slot frame f - 1
+                    // left), the update of f
+                    auto iter = [&](auto J) __attribute__((always_inline)) -> bool {
+                        constexpr int j = decltype(J)::value;
+                        stage_c(std::integral_constant<int, (j + KC) % RS>{});
+                        tap(std::integral_constant<int, (j + KT) % RS>{});
+                        return stage_d(J);
+                    };
+                    // prologue: taps of the first KT frames, stage C of the first KC
+                    static_for<KT>(tap);
+                    static_for<KC>(stage_c);
+                    while (static_all<RS>(iter)) {
+                    }
+                } else {
+                    for (unsigned long long m = mask; m; m &= m - 1) {
+                        const int f = __ffsll((long long)m) - 1;
+                        const BatchFrame& fr = frames[f];
+                        const __amdgpu_buffer_rsrc_t dm_rsrc = make_rsrc(fr.dm, npx * 8);
+                        const __amdgpu_buffer_rsrc_t rgba_rsrc = make_rsrc(fr.rgba, npx * 4);
+                        const bool use_color = fr.color != nullptr;
+                        float pc[3];
+#pragma unroll
+                        for (int r = 0; r < 3; ++r) {
+                            const float a = fr.E[r * 4 + 0] * px;
+                            const float b = fr.E[r * 4 + 1] * py;
+                            const float c = fr.E[r * 4 + 2] * pz;
+                            pc[r] = ((a + b) + c) + fr.E[r * 4 + 3];
+                        }
+                        const float es0 = fr.es[0], es1 = fr.es[1], es2 = fr.es[2];
+                        for (int k = 0; k < z0; ++k) {  // wave-uniform: advance to this slice's first voxel
+                            pc[0] += es0;
+                            pc[1] += es1;
+                            pc[2] += es2;
+                        }
+                        // phase A: projections of the ZB voxels
+                        int pixv[ZB];
+                        float pcz[ZB];
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            const float nu = pc[0] * p.fx, nv = pc[1] * p.fy;
+                            // Certified fast projection.  Only floor(u), floor(v) and the bound tests are used, so
+                            // u = nu * rcp(z) decides them exactly unless u lies within proj_eps of an integer (the
+                            // bound tests 0.0001 and W - 0.0001 sit 1e-4 from integers); those rare waves redo the
+                            // IEEE quotients.
+                            const float rz = __builtin_amdgcn_rcpf(pc[2]);
+                            float u_f = (nu * rz + p.cx) + 0.5f;
+                            float v_f = (nv * rz + p.cy) + 0.5f;
+                            const bool sure = !(pc[2] > 0.0f) ||
+                                              ((int)(fabsf(u_f - __builtin_rintf(u_f)) > p.proj_eps) &
+                                               (int)(fabsf(v_f - __builtin_rintf(v_f)) > p.proj_eps));
+                            if (!sure) {
+                                u_f = ((nu / pc[2]) + p.cx) + 0.5f;
+                                v_f = ((nv / pc[2]) + p.cy) + 0.5f;
+                            }
+                            // non-short-circuit test keeps all ZB projections in one basic block
+                            const bool ok = (pc[2] > 0.0f) & (u_f >= 0.0001f) & (u_f < p.safe_w) & (v_f >= 0.0001f) &
+                                            (v_f < p.safe_h);
+                            pixv[k] = ok ? (int)__umul24((unsigned)(int)v_f, (unsigned)p.W) + (int)u_f : -1;
+                            pcz[k] = pc[2];
+                            pc[0] += es0;
+                            pc[1] += es1;
+                            pc[2] += es2;
+                        }
+                        // phase B: every depth gather issued before any use (buffer loads: wave-uniform resource +
+                        // 32-bit byte offset, no per-lane 64-bit address math)
+                        float dv[ZB], mv[ZB];
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            dv[k] = mv[k] = 0.0f;
+                            if (pixv[k] >= 0) {  // lanes projecting outside the image issue no gather
+                                const u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(dm_rsrc, pixv[k] * 8, 0, 0);
+                                dv[k] = __uint_as_float(raw.x);
+                                mv[k] = __uint_as_float(raw.y);
+                            }
+                        }
+                        // phase C: the depth test; colour gathered only by the lanes whose voxel updates
+                        bool doitv[ZB];
+                        float sdfv[ZB];
+                        uint32_t cv[ZB];
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            sdfv[k] = (dv[k] - pcz[k]) * mv[k];
+                            doitv[k] = (pixv[k] >= 0) & (dv[k] > 0.0f) & (sdfv[k] > -p.trunc);
+                            cv[k] = 0u;
+                            if (use_color && doitv[k]) cv[k] = __builtin_amdgcn_raw_buffer_load_b32(rgba_rsrc, pixv[k] * 4, 0, 0);
+                        }
+                        // phase D: updates in frame order (select form: identical values, no exec-mask branches)
+#pragma unroll
+                        for (int k = 0; k < ZB; ++k) {
+                            const bool doit = doitv[k];
+                            const float sv = sdfv[k] * p.trunc_inv;
+                            const float tn = (sv < 1.0f) ? sv : 1.0f;
+                            const float wv = wt[k];
+                            const float w1 = wv + 1.0f;
+                            const float ta = ts[k] * wv + tn;
+                            float tsn;  // (tsdf * w + t) / (w + 1): the IEEE quotient, tsdf bit-exact
+                            // one table read per voxel for the tsdf and the colour quotients (round 3: +0.8 %)
+                            const double y64 = (FAST && C64) ? s_r64[(int)w1] : 0.0;
+                            if constexpr (FAST) {
+                                const float y = C64 ? (float)y64 : s_r32[(int)w1];
+                                const float q0 = ta * y;
+                                tsn = __builtin_fmaf(__builtin_fmaf(-w1, q0, ta), y, q0);
+                            } else {
+                                tsn = ta / w1;
+                            }
+                            ts[k] = doit ? tsn : ts[k];
+                            if (use_color) {
+                                if constexpr (C64) {  // Open3D: color = (color * weight + rgb) / (weight + 1.0f) in float64
+                                    {  // every lane, in select form (skipping voxels without an updating lane: slower)
+                                        const double wd = (double)wv, w1d = (double)w1;
+                                        const double ar = cr[k] * wd + (double)(cv[k] & 0xFFu);
+                                        const double ag = cg[k] * wd + (double)((cv[k] >> 8) & 0xFFu);
+                                        const double ab = cb[k] * wd + (double)((cv[k] >> 16) & 0xFFu);
+                                        double nr, ng, nb;
+                                        if constexpr (FAST) {
+                                            const double y = y64;
+                                            const double q0r = ar * y, q0g = ag * y, q0b = ab * y;
+                                            nr = __builtin_fma(__builtin_fma(-w1d, q0r, ar), y, q0r);
+                                            ng = __builtin_fma(__builtin_fma(-w1d, q0g, ag), y, q0g);
+                                            nb = __builtin_fma(__builtin_fma(-w1d, q0b, ab), y, q0b);
+                                        } else {
+                                            nr = ar / w1d;
+                                            ng = ag / w1d;
+                                            nb = ab / w1d;
+                                        }
+                                        cr[k] = doit ? nr : cr[k];
+                                        cg[k] = doit ? ng : cg[k];
+                                        cb[k] = doit ? nb : cb[k];
+                                    }
+                                } else {  // float32 state, one reciprocal for the three channels (|rel| <= 1e-4)
+                                    const float rw = __builtin_amdgcn_rcpf(w1);
+                                    const float nr = ((float)cr[k] * wv + (float)(cv[k] & 0xFFu)) * rw;
+                                    const float ng = ((float)cg[k] * wv + (float)((cv[k] >> 8) & 0xFFu)) * rw;
+                                    const float nb = ((float)cb[k] * wv + (float)((cv[k] >> 16) & 0xFFu)) * rw;
+                                    cr[k] = doit ? nr : cr[k];
+                                    cg[k] = doit ? ng : cg[k];
+                                    cb[k] = doit ? nb : cb[k];
+                                }
+                            }
+                            wt[k] = doit ? w1 : wv;
+                            upd += doit ? 1u : 0u;
+                        }
+                    }
+                }
+                // a slice none of whose voxels updated in this batch still holds its HBM values (fresh ones: zeros)
+                if (!fresh && !__any(upd != upd0)) continue;
+#pragma unroll
+                for (int k = 0; k < ZB; ++k) {
+                    const int vi = (z0 + k) * 256 + col;
+                    base[vi] = ts[k];
+                    base[UNIT_VOX + vi] = wt[k];
+                    if constexpr (C64) {
+                        st_f64(col64, vi, cr[k]);
+                        st_f64(col64, UNIT_VOX + vi, cg[k]);
+                        st_f64(col64, 2 * UNIT_VOX + vi, cb[k]);
+                    } else {
+                        base[2 * UNIT_VOX + vi] = cr[k];
+                        base[3 * UNIT_VOX + vi] = cg[k];
+                        base[4 * UNIT_VOX + vi] = cb[k];
+                    }
+                }
+            }
+        }
+    }
+    const unsigned long long tot = wave_sum((unsigned long long)upd);
+    if (lane == 0 && tot) atomicAdd(&d.stats[S_UPDATES], tot);
 }
 
 // The deferred integrate of a sharded volume's batch k and the touch of batch k + 1 in ONE launch (round 6): workgroups
