@@ -290,24 +290,55 @@ __device__ inline void voxel_value(const TsdfDev& d, int id, int x, int y, int z
     }
 }
 
-// one unit's vertices (rank r): one lane per edge-bitmask word w.  The unit's +x / +y / +z neighbour ids are staged in
-// LDS with the words (not one dependent global load per vertex before its neighbour voxel's loads).  (A wave per unit,
-// each lane walking six words, measured 193 vs 109 us for the emission, r05t: fewer waves, longer chains.)
+// exclusive scan over an NT-thread workgroup (every thread of the workgroup must call it: two barriers)
+template <int NT>
+__device__ inline int block_excl_scan_n(int v, int& total) {
+    __shared__ int wsum[NT / 64];
+    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
+    const int inc = wave_incl_scan(v);
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        const int s = wsum[w];
+        if (w < wid) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return off + inc - v;
+}
+
+// one unit's vertices (rank r), EWORDS lanes.  Lane w reads edge-bitmask word w; one block scan of the words' popcounts
+// lists the unit's cut edges in LDS in edge-key order (list index = the vertex's id inside the unit: the word prefixes
+// count the same bits in the same order), and the lanes then take the listed vertices one each (round 6: a word's
+// vertices had been one lane's serial chain while most lanes held none).  The unit's +x / +y / +z neighbour ids are
+// staged in LDS (not one dependent global load per vertex before its neighbour voxel's loads).  (A wave per unit, each
+// lane walking six words, measured 193 vs 109 us for the emission, r05t: fewer waves, longer chains.)
+// lds: >= VLIST_BYTES
+constexpr int VLIST_BYTES = UNIT_VOX * 3 * 2;  // u16 edge bit per listed vertex (<= 3 per voxel)
 __device__ __forceinline__ void mc_vertices_unit(const TsdfDev& d, const McDev& m, double vl, double* V, double* VC,
-                                                 int r, int w) {
+                                                 int r, int w, unsigned char* lds) {
     __shared__ int s_vnbr[8];
+    unsigned short* s_vl = reinterpret_cast<unsigned short*>(lds);
     const int id = (int)m.sorted_ids[r];
     if (w < 8) s_vnbr[w] = m.nbr[id * 16 + w];
     unsigned bits = m.eflags[(size_t)id * EWORDS + w];
-    __syncthreads();
-    if (!bits) return;
-    long long vid = m.vert_base[r] + m.wprefix[(size_t)id * EWORDS + w];
-    const int kx = d.unit_keys[id * 3], ky = d.unit_keys[id * 3 + 1], kz = d.unit_keys[id * 3 + 2];
-    const double half = vl * 0.5;
+    int nv;
+    int slot = block_excl_scan_n<EWORDS>(__popc(bits), nv);  // (its barriers also publish s_vnbr)
     while (bits) {
         const int b = __ffs(bits) - 1;
         bits &= bits - 1;
-        const int gbit = w * 32 + b;
+        s_vl[slot++] = (unsigned short)(w * 32 + b);
+    }
+    __syncthreads();
+    const long long vbase = m.vert_base[r];
+    const int kx = d.unit_keys[id * 3], ky = d.unit_keys[id * 3 + 1], kz = d.unit_keys[id * 3 + 2];
+    const double half = vl * 0.5;
+    for (int i = w; i < nv; i += EWORDS) {
+        const int gbit = (int)s_vl[i];
+        const long long vid = vbase + i;
         const int local = gbit / 3, axis = gbit % 3;
         const int x = local >> 8, y = (local >> 4) & 15, z = local & 15;
         float f0f, f1f;
@@ -340,7 +371,6 @@ __device__ __forceinline__ void mc_vertices_unit(const TsdfDev& d, const McDev& 
                 }
             }
         }
-        ++vid;
     }
 }
 
@@ -353,35 +383,25 @@ __device__ __forceinline__ int pick12(const int (&v)[12], int e) {
     return (e & 8) ? q2 : ((e & 4) ? q1 : q0);
 }
 
-// exclusive scan over an NT-thread workgroup (every thread of the workgroup must call it: two barriers)
-template <int NT>
-__device__ inline int block_excl_scan_n(int v, int& total) {
-    __shared__ int wsum[NT / 64];
-    const int lane = (int)lane_id(), wid = threadIdx.x >> 6;
-    const int inc = wave_incl_scan(v);
-    if (lane == 63) wsum[wid] = inc;
-    __syncthreads();
-    int off = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w) {
-        const int s = wsum[w];
-        if (w < wid) off += s;
-        tot += s;
-    }
-    __syncthreads();
-    total = tot;
-    return off + inc - v;
-}
 
-// one unit's triangles (rank r): lanes [0, 256) one (x, y) column of 16 cubes each.  An NT-thread workgroup (k_mc_emit
-// runs the triangles in its 384-lane workgroups) keeps lanes >= 256 through the scan's barriers with no column, so every
-// thread of the workgroup reaches every barrier (no reliance on exited waves leaving the barrier count)
+// one unit's triangles (rank r).  Lanes [0, 256) own one (x, y) column of 16 cubes each for the counts: one block scan
+// gives every column its first triangle and its first non-empty cube, the per-cube offsets (ctri) are written, and the
+// non-empty cubes are listed in LDS in voxel order.  Then the workgroup's NT lanes take the LISTED cubes one each (round
+// 6: a unit's ~10-30 surface cubes were spread over a few columns, whose lanes walked their 16 z in series while the
+// rest idled; now each cube is one lane's single chain).  An NT-thread workgroup (k_mc_emit runs the triangles in its
+// 384-lane workgroups) keeps every lane through every barrier (no reliance on exited waves).
+// lds: >= TLIST_BYTES
+constexpr int TLIST_BYTES = UNIT_VOX * 5;  // per listed cube: u32 (first triangle inside the unit << 12 | local voxel)
+                                           // + its cube index byte
 template <int NT>
-__device__ __forceinline__ void mc_triangles_unit(const TsdfDev& d, const McDev& m, int32_t* T, int r, int t) {
+__device__ __forceinline__ void mc_triangles_unit(const TsdfDev& d, const McDev& m, int32_t* T, int r, int t,
+                                                  unsigned char* lds) {
     static_assert(NT >= 256 && NT % 64 == 0, "a unit's 256 columns need >= 256 lanes");
     const bool col = t < 256;
     __shared__ int snbr[8];
     __shared__ long long sbase[8];
+    unsigned* s_list = reinterpret_cast<unsigned*>(lds);
+    unsigned char* s_cube = lds + UNIT_VOX * 4;
     const int id = (int)m.sorted_ids[r];
     const int ukey[3] = {d.unit_keys[id * 3], d.unit_keys[id * 3 + 1], d.unit_keys[id * 3 + 2]};
     if (t < 8) {
@@ -392,35 +412,51 @@ __device__ __forceinline__ void mc_triangles_unit(const TsdfDev& d, const McDev&
     uint4 q = make_uint4(0u, 0u, 0u, 0u);
     if (col) q = *reinterpret_cast<const uint4*>(m.cubes + (size_t)id * UNIT_VOX + t * 16);
     const unsigned cw[4] = {q.x, q.y, q.z, q.w};
-    int cnt = 0;
+    int cnt = 0;  // non-empty cubes << 16 | triangles (a column's prefix of triangles < 256 * 80 < 2^16)
 #pragma unroll
-    for (int z = 0; z < UNIT_RES; ++z) cnt += c_ntri[(cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu];
+    for (int z = 0; z < UNIT_RES; ++z) {
+        const int nt = c_ntri[(cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu];
+        cnt += nt + (nt ? (1 << 16) : 0);
+    }
     int total;
     const int pre = block_excl_scan_n<NT>(cnt, total);  // contains __syncthreads (snbr visible after)
-    if (!col) return;  // no barrier below
-    long long out = m.tri_base[r] + pre;
-    {  // per cube its first triangle inside the unit (<= 5 * 4096 < 2^16): the vertex-normal walk's index
+    if (col) {
+        // per cube its first triangle inside the unit (<= 5 * 4096 < 2^16): the vertex-normal walk's index
         unsigned off[8];
-        int o = pre;
+        int o = pre & 0xFFFF, slot = pre >> 16;
 #pragma unroll
         for (int z = 0; z < UNIT_RES; z += 2) {
-            const int n0 = c_ntri[(cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu];
-            const int n1 = c_ntri[(cw[(z + 1) >> 2] >> (((z + 1) & 3) * 8)) & 0xFFu];
+            const int c0 = (int)((cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu);
+            const int c1 = (int)((cw[(z + 1) >> 2] >> (((z + 1) & 3) * 8)) & 0xFFu);
+            const int n0 = c_ntri[c0], n1 = c_ntri[c1];
             off[z >> 1] = (unsigned)o | ((unsigned)(o + n0) << 16);
+            if (n0) {
+                s_list[slot] = ((unsigned)o << 12) | (unsigned)(t * 16 + z);
+                s_cube[slot++] = (unsigned char)c0;
+            }
+            if (n1) {
+                s_list[slot] = ((unsigned)(o + n0) << 12) | (unsigned)(t * 16 + z + 1);
+                s_cube[slot++] = (unsigned char)c1;
+            }
             o += n0 + n1;
         }
         uint4* dst = reinterpret_cast<uint4*>(m.ctri + (size_t)id * UNIT_VOX + t * 16);
         dst[0] = make_uint4(off[0], off[1], off[2], off[3]);
         dst[1] = make_uint4(off[4], off[5], off[6], off[7]);
     }
-    // per non-empty cube two round trips: its table row and edge set, then the owner words and prefixes of every edge
-    // it uses (the 12 edges unrolled, each shift a constant), all issued before any is used; a corner's vertex id is
-    // sbase (the owner's first vertex) + the word's prefix + the set bits below its own -- the cut edges' ids are
-    // formed once per cube, not once per corner
-    const int x = t >> 4, y = t & 15;
-    for (int z = 0; z < UNIT_RES; ++z) {
-        const int cube = (int)((cw[z >> 2] >> ((z & 3) * 8)) & 0xFFu);
-        if (cube == 0) continue;
+    __syncthreads();
+    const int ncubes = total >> 16;
+    const long long tbase = m.tri_base[r];
+    // per listed cube two round trips: its table row and edge set, then the owner words and prefixes of every edge it
+    // uses (the 12 edges unrolled, each shift a constant), all issued before any is used; a corner's vertex id is sbase
+    // (the owner's first vertex) + the word's prefix + the set bits below its own -- the cut edges' ids are formed once
+    // per cube, not once per corner
+    for (int i = t; i < ncubes; i += NT) {
+        const unsigned ent = s_list[i];
+        const int cube = (int)s_cube[i];
+        const int lv = (int)(ent & 0xFFFu);
+        const int x = lv >> 8, y = (lv >> 4) & 15, z = lv & 15;
+        long long out = tbase + (long long)(ent >> 12);
         const int4 row = *reinterpret_cast<const int4*>(&c_tri[cube][0]);
         const unsigned info = c_cinfo[cube];
         unsigned wb[12];
@@ -471,22 +507,27 @@ __device__ __forceinline__ void mc_triangles_unit(const TsdfDev& d, const McDev&
     }
 }
 
+constexpr int EMIT_LDS = VLIST_BYTES > TLIST_BYTES ? VLIST_BYTES : TLIST_BYTES;
 __global__ __launch_bounds__(EWORDS) void k_mc_vertices(TsdfDev d, McDev m, double vl, double* V, double* VC) {
-    mc_vertices_unit(d, m, vl, V, VC, blockIdx.x, threadIdx.x);
+    __shared__ alignas(16) unsigned char lds[VLIST_BYTES];
+    mc_vertices_unit(d, m, vl, V, VC, blockIdx.x, threadIdx.x, lds);
 }
 __global__ __launch_bounds__(256) void k_mc_triangles(TsdfDev d, McDev m, int32_t* T) {
-    mc_triangles_unit<256>(d, m, T, blockIdx.x, threadIdx.x);
+    __shared__ alignas(16) unsigned char lds[TLIST_BYTES];
+    mc_triangles_unit<256>(d, m, T, blockIdx.x, threadIdx.x, lds);
 }
 // The emission in ONE launch: workgroups [0, U) the triangles (their upper 128 lanes take part in the scan's barriers
-// with no column, then leave), [U, 2U) the vertices.  Replaces the vertices on the side stream beside the triangles:
-// that fork and join cost the GPU ~25 us of idle queue time per extraction (tools/event_gap.hip, r05j)
+// and in the listed cubes), [U, 2U) the vertices; the two halves' cube / vertex lists share one LDS block.  Replaces the
+// vertices on the side stream beside the triangles: that fork and join cost the GPU ~25 us of idle queue time per
+// extraction (tools/event_gap.hip, r05j)
 __global__ __launch_bounds__(EWORDS) void k_mc_emit(TsdfDev d, McDev m, int U, double vl, double* V, double* VC,
                                                     int32_t* T) {
+    __shared__ alignas(16) unsigned char lds[EMIT_LDS];
     const int b = blockIdx.x;
     if (b < U) {
-        mc_triangles_unit<EWORDS>(d, m, T, b, threadIdx.x);
+        mc_triangles_unit<EWORDS>(d, m, T, b, threadIdx.x, lds);
     } else {
-        mc_vertices_unit(d, m, vl, V, VC, b - U, threadIdx.x);
+        mc_vertices_unit(d, m, vl, V, VC, b - U, threadIdx.x, lds);
     }
 }
 
