@@ -2740,6 +2740,7 @@ ot_status ot_tsdf_reset(ot_tsdf* v) {
     v->imported = false;
     v->early_frame = -1;
     v->pending.clear();
+    v->dfr_on = false;  // a deferred batch's integrate belongs to the old contents (its work list is stale now)
     v->stat_batches = v->stat_unit_batches = v->stat_fresh = v->stat_prev_units = 0;
     v->sorted_frame = -1;
     v->sorted_units = -1;

@@ -76,7 +76,8 @@ def unpack_units(rows):
 
     n = rows.shape[0]
     f = rows[:, 3:].contiguous().view(torch.float32)
-    c = rows[:, 3 + 8192:].contiguous()
+    # a fresh buffer: .contiguous() would keep a one-row (or empty) slice at its odd int32 offset / stride
+    c = rows[:, 3 + 8192:].clone(memory_format=torch.contiguous_format)
     c = c.view(torch.float64) if rows.shape[1] == UNIT_WORDS_C64 else c.view(torch.float32)
     return rows[:, :3].contiguous(), f[:, :4096].contiguous(), f[:, 4096:8192].contiguous(), c.view(n, 4096, 3)
 
@@ -107,7 +108,7 @@ def pack_border(keys, tsdf, weight, color):
     n = keys.shape[0]
     return torch.cat([keys.reshape(n, 3).to(torch.int32), tsdf.reshape(n, BORDER_VOX).view(torch.int32),
                       weight.reshape(n, BORDER_VOX).view(torch.int32),
-                      color.reshape(n, -1).contiguous().view(torch.int32)], 1)
+                      color.reshape(n, BORDER_VOX * 3).contiguous().view(torch.int32)], 1)
 
 
 def unpack_border(rows):
@@ -116,7 +117,8 @@ def unpack_border(rows):
 
     n = rows.shape[0]
     f = rows[:, 3:3 + 2 * BORDER_VOX].contiguous().view(torch.float32)
-    c = rows[:, 3 + 2 * BORDER_VOX:].contiguous()
+    # a fresh buffer: .contiguous() would keep a one-row (or empty) slice at its odd int32 offset / stride
+    c = rows[:, 3 + 2 * BORDER_VOX:].clone(memory_format=torch.contiguous_format)
     c = c.view(torch.float64) if rows.shape[1] == 3 + BORDER_VOX * 8 else c.view(torch.float32)
     return (rows[:, :3].contiguous(), f[:, :BORDER_VOX].contiguous(), f[:, BORDER_VOX:].contiguous(),
             c.reshape(n, BORDER_VOX, 3))

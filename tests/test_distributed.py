@@ -157,3 +157,26 @@ def test_merge_shard_meshes_cpu():
         parts.append((V[loc], VC[loc], lmap[Ts].to(torch.int32), vk[loc], units[tu[mine]].to(torch.int32)))
     Vm, VCm, Tm = D.merge_shard_meshes(parts)
     assert torch.equal(Vm, Vr) and torch.equal(VCm, VCr) and torch.equal(Tm, Tr)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2])
+@pytest.mark.parametrize("wide", [False, True])
+def test_pack_unpack_rows_small(n, wide):
+    """pack/unpack of unit and border rows with 0, 1 and 2 rows, float32 and float64 colours, arbitrary bit
+    patterns: a one-row slice counts as contiguous at its odd int32 column offset, so the float64 colours must be
+    copied out before the dtype view (round 6: a 4-rank halo exchange delivered exactly one row)."""
+    D = importlib.import_module(PKG + ".distributed")
+    rng = np.random.default_rng(n)
+    cdt = np.uint64 if wide else np.uint32
+
+    def bits(shape, dt):
+        return torch.from_numpy(rng.integers(0, 2 ** 63, shape, dtype=np.uint64).astype(dt).view(
+            np.float64 if dt == np.uint64 else np.float32).copy())
+
+    keys = torch.from_numpy(rng.integers(-500, 500, (n, 3)).astype(np.int32))
+    for vox, pack, unpack in ((4096, D.pack_units, D.unpack_units), (D.BORDER_VOX, D.pack_border, D.unpack_border)):
+        t, w, c = bits((n, vox), np.uint32), bits((n, vox), np.uint32), bits((n, vox, 3), cdt)
+        k2, t2, w2, c2 = unpack(pack(keys, t, w, c))
+        assert torch.equal(k2, keys) and c2.dtype == c.dtype and c2.shape == c.shape
+        for x, y in ((t2, t), (w2, w), (c2, c)):
+            assert np.array_equal(x.numpy().view(np.uint8), y.numpy().view(np.uint8))

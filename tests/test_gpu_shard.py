@@ -239,7 +239,7 @@ def test_assemble_after_halo_extraction_bitexact(pkg, seq16, gpu):
     assert_bitwise(np.asarray(m1.vertex_colors), np.asarray(m0.vertex_colors), "assembled mesh colours")
 
 
-def _halo_worker(rank, world, port, q):
+def _halo_worker(rank, world, port, q, sector=None):
     import os
     import sys
 
@@ -257,9 +257,12 @@ def _halo_worker(rank, world, port, q):
         synth = importlib.import_module(PKG + ".synth")
         D = importlib.import_module(PKG + ".distributed")
         seq = synth.make_sequence(n_frames=16, frames=[0, 3, 7, 12])
-        vol = _integrate_p(pkg, seq, 0.005, (rank, world), 64)
+        print(f"[halo rank {rank}] integrating", flush=True)
+        vol = _integrate_p(pkg, seq, 0.005, (rank, world) + tuple(sector or ()), 64)
         keys, _, _, _ = vol.export_border()
+        print(f"[halo rank {rank}] extracting", flush=True)
         mesh, got = D.extract_sharded_mesh(vol)
+        print(f"[halo rank {rank}] extracted", flush=True)
         n_rows = torch.tensor([[int(keys.shape[0])]], dtype=torch.int64)
         counts = D.all_gather_rows(n_rows).flatten().tolist()
         row_bytes = (3 + 721 * 8) * 4  # pack_border row, float64 colour
@@ -267,16 +270,21 @@ def _halo_worker(rank, world, port, q):
         q.put((rank, mesh._v.dev().cpu().numpy(), mesh._t.dev().cpu().numpy(), mesh._vc.dev().cpu().numpy(), got,
                allgather))
         dist.barrier()
+    except BaseException as e:  # report it: the parent fails at once instead of waiting out its queue timeout
+        q.put((rank, f"{type(e).__name__}: {e}"))
+        raise
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_halo_exchange_ranks_bitexact(pkg, seq16, gpu, world):
+@pytest.mark.parametrize("world,sector", [(2, None), (3, None), (4, (0.0, 0.0))])
+def test_halo_exchange_ranks_bitexact(pkg, seq16, gpu, world, sector):
     """`world` ranks (gloo, sharing this GPU) each integrate one object's frames into their shard
-    (ownership by blocks of units), exchange border rows only with the ranks owning a -x/-y/-z neighbour
-    (distributed.exchange_rows: all_to_all), extract and merge: every rank's mesh equals the unsharded mesh bit for
-    bit, and each rank receives at most half the border bytes an all-gather of every row delivers."""
+    (ownership by blocks of units; at 4 ranks by azimuth sectors, with the deferred integrate), exchange border rows
+    only with the ranks owning a -x/-y/-z neighbour (distributed.exchange_rows: all_to_all), extract and merge: every
+    rank's mesh equals the unsharded mesh bit for bit, and each rank receives at most half the border bytes an
+    all-gather of every row delivers.  At 4 sector ranks a rank can receive a single border row (round 6: its
+    float64 colours sat at an odd int32 offset, which unpack_border now copies out)."""
     import socket
 
     import torch.multiprocessing as mp
@@ -290,10 +298,14 @@ def test_halo_exchange_ranks_bitexact(pkg, seq16, gpu, world):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, q, sector)) for r in range(world)]
     for p in procs:
         p.start()
-    out = dict((r, rest) for r, *rest in (q.get(timeout=240) for _ in range(world)))
+    out = {}
+    for _ in range(world):
+        r, *rest = q.get(timeout=240)
+        assert len(rest) > 1, f"rank {r} failed: {rest[0]}"
+        out[r] = rest
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -303,3 +315,37 @@ def test_halo_exchange_ranks_bitexact(pkg, seq16, gpu, world):
         assert_bitwise(T, T0, f"rank {r} merged triangles")
         assert_bitwise(VC, C0, f"rank {r} merged colours")
         assert got <= 0.5 * allgather, f"rank {r}: {got} border bytes received vs {allgather} by all-gather"
+
+
+def test_deferred_integrate_sync_reset(pkg, gpu, synth):
+    """A sector shard of 4 ranks runs the deferred integrate (batch k's integrate launched with batch k + 1's touch):
+    ot_tsdf_reset (the synchronous C reset) with a batch still deferred drops it with the old contents, and the
+    volume then integrates a new scan exactly as a fresh volume does (keys, tsdf, weight, float64 colour bitwise)."""
+    integ = pkg.pipelines.integration
+    intr = pkg.camera.PinholeCameraIntrinsic(*ref_intr(synth))
+    depth, color, ext = synth.make_sequence(synth.Scene(seed=3), n_frames=80, frames=range(0, 80, 4))
+
+    def make():
+        v = integ.ScalableTSDFVolume(voxel_length=0.005, sdf_trunc=0.04, color_type=integ.TSDFVolumeColorType.RGB8,
+                                     batch_frames=4)
+        v.set_shard_sector(0, 4, (0.0, 0.0))
+        return v
+
+    def feed(v, ks):
+        for k in ks:
+            v.integrate(pkg.geometry.RGBDImage.create_from_color_and_depth(
+                pkg.geometry.Image(color[k]), pkg.geometry.Image(depth[k]), depth_scale=1000.0, depth_trunc=3.0,
+                convert_rgb_to_intensity=False), intr, ext[k])
+
+    a = make()
+    feed(a, range(12))  # three 4-frame batches: the third one's integrate is still deferred
+    import torch
+
+    torch.cuda.synchronize()
+    pkg._lib.call("ot_tsdf_reset", a._h)
+    a._keep.clear()
+    feed(a, range(12, 20))
+    b = make()
+    feed(b, range(12, 20))
+    for x, y, what in zip(a.export_units(), b.export_units(), ("keys", "tsdf", "weight", "colour")):
+        assert_bitwise(_host(x), _host(y), f"after a synchronous reset: {what}")
