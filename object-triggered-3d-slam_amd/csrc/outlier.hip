@@ -94,6 +94,11 @@ __device__ inline void query_cell(const GridDev& g, int64_t j, int& cx, int& cy,
     cx = (int)((key >> g.sx) & ((1ull << (g.sf - g.sx)) - 1));
 }
 __device__ inline int64_t sor_out(const GridDev& g, int64_t j) { return g.sidx ? (int64_t)g.sidx[j] : j; }
+// the frame of sorted point j: its cell key's frame field (one load, which query_cell makes anyway, instead of a
+// dependent binary search over the frame offsets at the head of every query's chain)
+__device__ inline int sorted_frame(const GridDev& g, int64_t j) {
+    return g.nframes > 1 ? (int)(g.pkey[j] >> g.sf) : 0;
+}
 
 template <typename KeyT>
 __global__ __launch_bounds__(256) void k_cell_keys(const double* __restrict__ xyz, int64_t n, GridDev g, KeyT* keys,
@@ -296,8 +301,6 @@ __device__ inline void topk_reset(double (&best)[KMAX], int kk) {
     for (int i = 0; i < KMAX; ++i) best[i] = (i < KMAX - kk) ? -INFINITY : INFINITY;
 }
 
-constexpr int SOR_RMAX = 8;  // beyond this ring a query falls back to an exact scan of its frame
-
 // distance from q to the faces of the (2R+1)^3 cell block around cell c, minus a rounding margin (f = q's position
 // inside c: in [0, 1) up to rounding; outside it the formula is still q's distance to the block's faces)
 __device__ inline double block_guard(const GridDev& g, const double q[3], const double* o, const int c[3], double R) {
@@ -311,36 +314,15 @@ __device__ inline double block_guard(const GridDev& g, const double q[3], const 
     return guard - 1e-6 * g.h;
 }
 
-// Continue an unsettled query through the Chebyshev rings r0 .. SOR_RMAX of its cell (rings < r0 are already in the
-// list) until the k-th distance lies inside the scanned cube, else scan the whole frame from scratch.
-template <int KMAX>
-__device__ inline void sor_rings(const GridDev& g, const double q[3], const double* o, int f, const int c[3], int r0,
-                                 int64_t fbeg, int64_t fend, int kk, long long have, double (&best)[KMAX]) {
-    const int cx = c[0], cy = c[1], cz = c[2];
-    for (int r = r0; r <= SOR_RMAX; ++r) {
-        for (int dx = -r; dx <= r; ++dx)
-            for (int dy = -r; dy <= r; ++dy) {
-                const bool face = (dx == -r || dx == r || dy == -r || dy == r);
-                for (int dz = -r; dz <= r; dz += (face || r == 0) ? 1 : 2 * r) {
-                    const int2 se = grid_find(g, f, cx + dx, cy + dy, cz + dz);
-                    scan_range<KMAX>(g.sxyz, q, se.x, se.y, best);
-                    have += se.y - se.x;
-                }
-            }
-        const double guard = block_guard(g, q, o, c, (double)r);
-        if (have >= fend - fbeg || (best[KMAX - 1] < INFINITY && best[KMAX - 1] <= guard * guard)) return;
-    }
-    topk_reset<KMAX>(best, kk);
-    scan_range<KMAX>(g.sxyz, q, (int)fbeg, (int)fend, best);
-}
-
 // column visiting order of a (2R+1)^2 block, nearest first (t = (dx + R) * (2R + 1) + dy + R)
 __constant__ unsigned char c_cols3[NBR3] = {4, 1, 3, 5, 7, 0, 2, 6, 8};
 __constant__ unsigned char c_cols5[NBR5] = {12, 7, 11, 13, 17, 6, 8, 16, 18, 2, 10, 14, 22,
                                             1, 3, 5, 9, 15, 19, 21, 23, 0, 4, 20, 24};
 
 // Queries stage 1 could not settle, deferred to a second launch so that its waves are full of them (a wave runs a
-// stage for all its lanes when one lane needs it): sorted position, candidates counted, the top-k list (SoA).
+// stage for all its lanes when one lane needs it): sorted position, candidates counted, the top-k list (SoA).  Stage 2
+// writes an unsettled query's count and list back into its slot and lists the slot for stage 3 (pd3: count and slots
+// only, capacity n, so no query ever falls back to a serial ring walk -- that path held stage 2 at 162 VGPRs).
 struct SorPend {
     int* count;
     int* j;
@@ -396,7 +378,7 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
     constexpr int W = 2 * R + 1;
     const int64_t j = xcd_block() * 256 + threadIdx.x;
     if (j >= n) return;
-    const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, j) : 0;
+    const int f = sorted_frame(g, j);
     const int64_t fbeg = g.foff[f], fend = g.foff[f + 1];
     const double* o = g.origin + 3 * f;
     const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
@@ -449,14 +431,15 @@ __global__ __launch_bounds__(256) void k_sor_knn(GridDev g, int64_t n, int k, do
 }
 
 // Stage 2 for the pending queries (grid-stride over the device count): R = 1 completes the 5x5x5 block (the inner
-// columns' cells at z-2 / z+2 and the 16 outer columns, each skipped when provably too far), then Chebyshev rings.
+// columns' cells at z-2 / z+2 and the 16 outer columns, each skipped when provably too far); what is still unsettled
+// goes to stage 3.
 template <int KMAX, int R>
 __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* avg, SorPend pd, SorPend pd3) {
     static_assert(R == 1 || R == 2, "stage 3 starts at ring 3");
     const int cnt = *pd.count;
     for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < cnt; s += (int64_t)gridDim.x * 256) {
         const int64_t j = pd.j[s];
-        const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, j) : 0;
+        const int f = sorted_frame(g, j);
         const int64_t fbeg = g.foff[f], fend = g.foff[f + 1];
         const double* o = g.origin + 3 * f;
         const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
@@ -466,7 +449,6 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
         for (int i = 0; i < KMAX; ++i) best[i] = pd.best[(int64_t)i * pd.cap + s];
         long long have = pd.have[s];
         bool settled = false;
-        int rnext = R + 1;
         int cc[3];
         query_cell(g, j, cc[0], cc[1], cc[2]);
         if (R == 1) {
@@ -474,9 +456,9 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
             const int cx = cc[0], cy = cc[1], cz = cc[2];
             double lo[3], hi[3];
             cell_fracs(g, q, o, cc, lo, hi);
-            const int2* r5 = g.nbr5 ? g.nbr5 + (int64_t)c * NBR5 : nullptr;
-            const int2* r3 = g.nbr3 + (int64_t)c * NBR3;
+            const int2* r3 = g.nbr3 + (int64_t)c * NBR3;  // the inner columns' z-1 .. z+1 ranges (stage 1's)
             bool counted_all = true;  // have counts every point of the 5x5x5 block
+#pragma nounroll
             for (int u = 0; u < NBR5; ++u) {
                 const int t = c_cols5[u];
                 const int dx = t / 5 - 2, dy = t % 5 - 2;
@@ -487,15 +469,8 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
                     counted_all = false;
                     continue;
                 }
-                int2 full, mid = make_int2(0, 0);
-                if (r5) {
-                    full = r5[t];
-                    if (inner) mid = r3[(dx + 1) * 3 + (dy + 1)];
-                } else {
-                    const int2 col = grid_column(g, f, cx + dx, cy + dy);
-                    full = column_range(g, col, cz - 2, cz + 2);
-                    if (inner) mid = column_range(g, col, cz - 1, cz + 1);
-                }
+                const int2 full = column_range(g, grid_column(g, f, cx + dx, cy + dy), cz - 2, cz + 2);
+                const int2 mid = inner ? r3[(dx + 1) * 3 + (dy + 1)] : make_int2(0, 0);
                 if (inner && mid.y > mid.x) {  // the column's cells at z-2 and z+2 only
                     const double ez = face_gap(lo[2], hi[2], 2, g.h);  // both are >= one cell plus q's gap away
                     const double ezl = face_gap(lo[2], hi[2], -2, g.h);
@@ -513,19 +488,17 @@ __global__ __launch_bounds__(256) void k_sor_knn_rest(GridDev g, int k, double* 
             settled = (counted_all && have >= fend - fbeg) ||
                       (best[KMAX - 1] < INFINITY && best[KMAX - 1] <= guard * guard);
             if (!counted_all) have = -1;  // only a full count may end the rings through the whole-frame test
-            rnext = 3;
         }
-        if (!settled) {
-            // stage 3 (one wave per query) unless its list is full; a query left here walks the rings serially
-            const int s3 = atomicAdd(pd3.count, 1);
-            if (s3 < pd3.cap) {
-                pd3.j[s3] = (int)j;
-                pd3.have[s3] = have;
+        if (!settled) {  // stage 3 (one wave per query): the pending slot listed, its count and list back in place
+            pd3.j[atomicAdd(pd3.count, 1)] = (int)s;  // capacity: every pending slot is listed at most once
+            pd.have[s] = have;
+            double* wp = pd.best + s;  // one running address (20 precomputed ones held stage 2 at 158 VGPRs)
 #pragma unroll
-                for (int i = 0; i < KMAX; ++i) pd3.best[(int64_t)i * pd3.cap + s3] = best[i];
-                continue;
+            for (int i = 0; i < KMAX; ++i) {
+                *wp = best[i];
+                wp += pd.cap;
             }
-            sor_rings<KMAX>(g, q, o, f, cc, rnext, fbeg, fend, kk, have, best);
+            continue;
         }
         avg[sor_out(g, j)] = sor_mean<KMAX>(best, kk);
     }
@@ -571,23 +544,24 @@ __device__ inline void wave_merge(double* lds, double* gl, const double (&L)[KMA
 }
 
 template <int KMAX>
-__global__ __launch_bounds__(64) void k_sor_knn_wave(GridDev g, int k, double* avg, SorPend pd3) {
+__global__ __launch_bounds__(64) void k_sor_knn_wave(GridDev g, int k, double* avg, SorPend pd, SorPend pd3) {
     __shared__ double lds[64 * KMAX];
     __shared__ double gl[KMAX];
-    const int cnt = (int)min((int64_t)*pd3.count, pd3.cap);
+    const int cnt = *pd3.count;
     const int l = (int)lane_id();
-    for (int64_t s = blockIdx.x; s < cnt; s += gridDim.x) {
-        const int64_t j = pd3.j[s];
-        const int f = g.nframes > 1 ? frame_of(g.foff, g.nframes, j) : 0;
+    for (int64_t s3 = blockIdx.x; s3 < cnt; s3 += gridDim.x) {
+        const int64_t s = pd3.j[s3];  // the stage-2 pending slot
+        const int64_t j = pd.j[s];
+        const int f = sorted_frame(g, j);
         const int64_t fbeg = g.foff[f], fend = g.foff[f + 1];
         const double* o = g.origin + 3 * f;
         const double q[3] = {g.sxyz[j * 3], g.sxyz[j * 3 + 1], g.sxyz[j * 3 + 2]};
         const int kk = (int)((int64_t)k < fend - fbeg ? k : fend - fbeg);
-        if (l < KMAX) gl[l] = pd3.best[(int64_t)l * pd3.cap + s];
+        if (l < KMAX) gl[l] = pd.best[(int64_t)l * pd.cap + s];
         if (KMAX > 64 && l == 0)
-            for (int i = 64; i < KMAX; ++i) gl[i] = pd3.best[(int64_t)i * pd3.cap + s];
+            for (int i = 64; i < KMAX; ++i) gl[i] = pd.best[(int64_t)i * pd.cap + s];
         __syncthreads();
-        long long have = pd3.have[s];  // < 0: not every point of the scanned cube was counted
+        long long have = pd.have[s];  // < 0: not every point of the scanned cube was counted
         int cc[3];
         query_cell(g, j, cc[0], cc[1], cc[2]);
         const int cx = cc[0], cy = cc[1], cz = cc[2];
@@ -1015,10 +989,9 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
     // pending list of stage-1 misses (device count; capacity n)
     const int km = kk <= 4 ? 4 : kk <= 8 ? 8 : kk <= 12 ? 12 : kk <= 16 ? 16 : kk <= 20 ? 20 : kk <= 24 ? 24
                  : kk <= 32 ? 32 : kk <= 48 ? 48 : 64;
-    // and of stage-2 misses (stage 3, one wave each; capacity n / 32 + 4096, overflow walks its rings serially)
-    const int64_t cap3 = std::min<int64_t>(n, n / 32 + 4096);
+    // and of stage-2 misses (stage 3, one wave each): their pending slots (capacity n; count and list stay in place)
     const size_t per = 4 + 8 + 8 * (size_t)km;
-    char* pw = (char*)scratch((size_t)(n + cap3) * per + 1024, slot0 + 1);
+    char* pw = (char*)scratch((size_t)n * (per + 4) + 1024, slot0 + 1);
     if (!pw) return fail(OT_ERR_HIP, "scratch allocation failed");
     SorPend pd, pd3;
     pd.count = (int*)pw;
@@ -1028,9 +1001,9 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
     pd.best = (double*)(pd.have + n);
     pd.cap = n;
     pd3.j = (int*)(((uintptr_t)(pd.best + (size_t)km * n) + 255) & ~(uintptr_t)255);
-    pd3.have = (long long*)(((uintptr_t)(pd3.j + cap3) + 15) & ~(uintptr_t)15);
-    pd3.best = (double*)(pd3.have + cap3);
-    pd3.cap = cap3;
+    pd3.have = nullptr;  // in the stage-2 slot (pd)
+    pd3.best = nullptr;
+    pd3.cap = n;
     OT_HIP_TRY(hipMemsetAsync(pd.count, 0, 2 * sizeof(int), stream));
     const unsigned rgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(grid / 4, 1), 2048);
 #define OT_SOR_LAUNCH(KM)                                                                                           \
@@ -1043,7 +1016,8 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
                                (int)nb_neighbors, avg, pd);                                                         \
         hipLaunchKernelGGL((k_sor_knn_rest<KM, SOR_BLOCK_R>), dim3(rgrid), dim3(256), 0, stream, gb.g,              \
                            (int)nb_neighbors, avg, pd, pd3);                                                        \
-        hipLaunchKernelGGL((k_sor_knn_wave<KM>), dim3(1024), dim3(64), 0, stream, gb.g, (int)nb_neighbors, avg, pd3); \
+        hipLaunchKernelGGL((k_sor_knn_wave<KM>), dim3(1024), dim3(64), 0, stream, gb.g, (int)nb_neighbors, avg, pd,   \
+                           pd3);                                                                                    \
     } while (0)
     if (kk <= 4) OT_SOR_LAUNCH(4);
     else if (kk <= 8) OT_SOR_LAUNCH(8);

@@ -19,6 +19,7 @@ ap.add_argument("--frames", type=int, default=64)
 ap.add_argument("--batches", default="8,16,32,64")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--ab-netfill", type=int, default=0, help="alternate otx_sor_netfill(1) / (0) over this many rounds")
+ap.add_argument("--ab-hook", default="otx_sor_netfill", help="the 0/1 test hook --ab-netfill alternates")
 a = ap.parse_args()
 synth = importlib.import_module(PKG + ".synth")
 from concurrent.futures import ProcessPoolExecutor
@@ -71,15 +72,15 @@ for B in [int(x) for x in a.batches.split(",")]:
           flush=True)
     for rnd in range(a.ab_netfill):  # A/B of the stage-1 list fill, alternating in one process
         for on in (1, 0):
-            L.call("otx_sor_netfill", on)
+            L.call(a.ab_hook, on)
             run_all()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             run_all()
             torch.cuda.synchronize()
-            print(f"netfill {on}: {(time.perf_counter() - t2) * 1e3 / a.frames:.4f} ms/frame (batch {B}, round {rnd})",
+            print(f"{a.ab_hook} {on}: {(time.perf_counter() - t2) * 1e3 / a.frames:.4f} ms/frame (batch {B}, round {rnd})",
                   flush=True)
-    L.call("otx_sor_netfill", 1)
+    L.call(a.ab_hook, 1)
     nb = (a.frames + B - 1) // B
     # per launch of the batch's kernels (one k_sor_knn per batch): SURVEY 8(d) algorithmic bytes of the SOR kNN =
     # 12 B per input point (the voxel centroids) + 12 B per kept point; read by tools/parse_pmc.py

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <unordered_map>
 #include <vector>
 
@@ -43,7 +44,14 @@ int main(int argc, char** argv) {
     // then inserted in ascending order while ANY lane of the wave still accepts its next one (a sorted batch's
     // acceptances are a prefix per lane, so a wave's insertion steps per batch = its largest prefix)
     const int batch = argc > 7 ? atoi(argv[7]) : 0;
-    long long batch_steps = 0, batch_ins_steps = 0;
+    // > 0: accepted candidates go to a per-lane queue of this many (tested against the k-th distance of the list as
+    // of the last drain); the wave drains (inserts every lane's queue, one entry per insertion step, as many steps as
+    // the longest queue) when any lane's queue is full, and at the end of the query.  Same final lists.
+    const int queue = argc > 8 ? atoi(argv[8]) : 0;
+    long long batch_steps = 0, batch_ins_steps = 0, drain_steps = 0, drains = 0, queued = 0;
+    std::vector<std::vector<double>> Q(64);
+    std::vector<std::pair<long long, std::vector<double>>> pend;  // stage-1 misses: sorted position, list
+    std::vector<long long> pend_wave;
     const double h = hm * 0.005;
     double mn[3] = {1e30, 1e30, 1e30};
     for (size_t i = 0; i < n; ++i)
@@ -198,6 +206,44 @@ int main(int argc, char** argv) {
                 }
                 continue;
             }
+            if (queue > 0) {
+                auto drain = [&]() {
+                    size_t mx = 0;
+                    for (int l = 0; l < nl; ++l) {
+                        mx = std::max(mx, Q[l].size());
+                        for (double d : Q[l]) {
+                            auto& b = best[l];
+                            if (!(d < b[K - 1])) continue;
+                            ++tot_ins;
+                            b[K - 1] = d;
+                            for (int i = K - 1; i > 0 && b[i] < b[i - 1]; --i) std::swap(b[i], b[i - 1]);
+                        }
+                        Q[l].clear();
+                    }
+                    drain_steps += mx;
+                    drains += mx > 0;
+                };
+                for (int s = 0; s < maxlen; ++s) {
+                    bool full = false;
+                    for (int l = 0; l < nl; ++l) {
+                        if (!act[l] || s >= plan[l][u].second - plan[l][u].first) continue;
+                        const size_t j = w0 + l, m = plan[l][u].first + s;
+                        const double d0 = S[j * 3] - S[m * 3], d1 = S[j * 3 + 1] - S[m * 3 + 1],
+                                     d2 = S[j * 3 + 2] - S[m * 3 + 2];
+                        const double d = (d0 * d0 + d1 * d1) + d2 * d2;
+                        ++tot_cand;
+                        if (d < best[l][K - 1]) {
+                            Q[l].push_back(d);
+                            ++queued;
+                            full |= (int)Q[l].size() >= queue;
+                        }
+                    }
+                    ++wave_steps;
+                    if (full) drain();
+                }
+                if (u == nslot - 1) drain();
+                continue;
+            }
             for (int s = 0; s < maxlen; ++s) {
                 bool any = false;
                 for (int l = 0; l < nl; ++l) {
@@ -229,6 +275,7 @@ int main(int argc, char** argv) {
             }
             const bool un = !(best[l][K - 1] <= g * g);
             unsettled += un;
+            if (un) pend.push_back({(long long)j, best[l]}), pend_wave.push_back((long long)(w0 / 64));
             if (un) {
                 long long x = (long long)std::floor((S[j * 3] - mn[0]) / h), y = (long long)std::floor((S[j * 3 + 1] - mn[1]) / h),
                           z = (long long)std::floor((S[j * 3 + 2] - mn[2]) / h);
@@ -259,6 +306,112 @@ int main(int argc, char** argv) {
                "(12/cand-slot x %d + %d/sort + 42/ins-step) per query %.1f\n", batch, batch_steps / nw,
                batch_ins_steps / nw, (double)batch_ins_steps / std::max<long long>(batch_steps, 1), batch, 2 * ce,
                ((12.0 * batch + 2.0 * ce) * batch_steps + 42.0 * batch_ins_steps) / nq);
+    }
+    if (queue > 0)
+        printf("   queue %d: per wave %.1f steps, %.1f drains, %.1f drain insertion steps; queued/query %.1f (exact "
+               "insertions %.1f) | VALU model (16/step + 42/drain step) per query %.1f\n", queue, wave_steps / nw,
+               drains / nw, drain_steps / nw, queued / nq, tot_ins / nq, (16.0 * wave_steps + 42.0 * drain_steps) / nq);
+    // Stage 2 (the 5x5x5 shell) in lockstep waves of 64 pending queries, in two list orders: "xcd" = the order stage 1's
+    // atomics give (8 XCDs each walking a contiguous eighth of the waves, their waves' misses interleaved round-robin),
+    // "sorted" = sorted query order (neighbouring misses share a wave)
+    if (R == 1 && !pend.empty()) {
+        const long long nwv = (long long)std::ceil(nq / 64);
+        std::vector<std::vector<size_t>> per_x(8);
+        for (size_t i = 0; i < pend.size(); ++i) per_x[std::min<long long>(7, pend_wave[i] * 8 / nwv)].push_back(i);
+        std::vector<size_t> xorder;
+        {
+            std::vector<size_t> at(8, 0);
+            bool more = true;
+            while (more) {
+                more = false;
+                for (int x = 0; x < 8; ++x) {  // one stage-1 wave's misses from each XCD in turn
+                    if (at[x] >= per_x[x].size()) continue;
+                    more = true;
+                    const long long w = pend_wave[per_x[x][at[x]]];
+                    while (at[x] < per_x[x].size() && pend_wave[per_x[x][at[x]]] == w) xorder.push_back(per_x[x][at[x]++]);
+                }
+            }
+        }
+        std::vector<size_t> sorder(pend.size());
+        for (size_t i = 0; i < pend.size(); ++i) sorder[i] = i;
+        static const int cols5[25] = {12, 7, 11, 13, 17, 6, 8, 16, 18, 2, 10, 14, 22, 1, 3, 5, 9, 15, 19, 21, 23, 0, 4, 20, 24};
+        for (int mode = 0; mode < 2; ++mode) {
+            const auto& ord2 = mode == 0 ? xorder : sorder;
+            long long st = 0, ins_st = 0, cand = 0, probes = 0;
+            std::set<long long> lines_w;  // distinct 64-B lines of candidates read per wave (L1-sharing proxy)
+            long long lines = 0;
+            for (size_t w0 = 0; w0 < ord2.size(); w0 += 64) {
+                const int nl = (int)std::min<size_t>(64, ord2.size() - w0);
+                std::vector<std::vector<double>> bl(nl);
+                std::vector<long long> qx(nl), qy(nl), qz(nl);
+                std::vector<double> flo(nl * 3), fhi(nl * 3);
+                lines_w.clear();
+                for (int l = 0; l < nl; ++l) {
+                    const auto& pe = pend[ord2[w0 + l]];
+                    bl[l] = pe.second;
+                    const size_t j = (size_t)pe.first;
+                    long long c3[3];
+                    for (int a = 0; a < 3; ++a) {
+                        const double uu = (S[j * 3 + a] - mn[a]) / h;
+                        c3[a] = (long long)std::floor(uu);
+                        const double fr = uu - std::floor(uu);
+                        flo[l * 3 + a] = fr * h, fhi[l * 3 + a] = (1 - fr) * h;
+                    }
+                    qx[l] = c3[0], qy[l] = c3[1], qz[l] = c3[2];
+                }
+                for (int u = 0; u < 25; ++u) {
+                    const int t = cols5[u], dx = t / 5 - 2, dy = t % 5 - 2;
+                    const bool inner = std::abs(dx) <= 1 && std::abs(dy) <= 1;
+                    for (int part = 0; part < (inner ? 2 : 1); ++part) {
+                        std::vector<std::pair<int, int>> rg(nl, {0, 0});
+                        int mx = 0;
+                        for (int l = 0; l < nl; ++l) {
+                            const double ex = dx < 0 ? flo[l * 3] + (-dx - 1) * h : (dx > 0 ? fhi[l * 3] + (dx - 1) * h : 0.0);
+                            const double ey = dy < 0 ? flo[l * 3 + 1] + (-dy - 1) * h : (dy > 0 ? fhi[l * 3 + 1] + (dy - 1) * h : 0.0);
+                            double e2 = ex * ex + ey * ey;
+                            if (inner) {
+                                const double ez = part == 0 ? flo[l * 3 + 2] + h : fhi[l * 3 + 2] + h;
+                                e2 += ez * ez;
+                            }
+                            if (e2 >= bl[l][K - 1]) continue;
+                            ++probes;
+                            int b = 1 << 30, e = 0;
+                            const int z0 = inner ? (part == 0 ? -2 : 2) : -2, z1 = inner ? z0 : 2;
+                            for (int dz = z0; dz <= z1; ++dz) {
+                                auto se = find(qx[l] + dx, qy[l] + dy, qz[l] + dz);
+                                if (se.second > se.first) b = std::min(b, se.first), e = std::max(e, se.second);
+                            }
+                            if (e > 0) rg[l] = {b, e}, mx = std::max(mx, e - b);
+                        }
+                        for (int s2 = 0; s2 < mx; ++s2) {
+                            bool any = false;
+                            for (int l = 0; l < nl; ++l) {
+                                if (s2 >= rg[l].second - rg[l].first) continue;
+                                const size_t j = (size_t)pend[ord2[w0 + l]].first, m = rg[l].first + s2;
+                                lines_w.insert((long long)(m * 24 / 64));
+                                const double d0 = S[j * 3] - S[m * 3], d1 = S[j * 3 + 1] - S[m * 3 + 1], d2 = S[j * 3 + 2] - S[m * 3 + 2];
+                                const double d = (d0 * d0 + d1 * d1) + d2 * d2;
+                                ++cand;
+                                auto& bb = bl[l];
+                                if (d < bb[K - 1]) {
+                                    any = true;
+                                    bb[K - 1] = d;
+                                    for (int i = K - 1; i > 0 && bb[i] < bb[i - 1]; --i) std::swap(bb[i], bb[i - 1]);
+                                }
+                            }
+                            ++st;
+                            ins_st += any;
+                        }
+                    }
+                }
+                lines += (long long)lines_w.size();
+            }
+            const double np2 = (double)pend.size(), nw2 = std::ceil(np2 / 64);
+            printf("   stage 2 %-6s: %zu pending, per wave %.1f steps, %.1f ins-steps, cand/query %.1f, distinct 64-B lines "
+                   "per wave %.0f, column parts probed per query %.1f | VALU model per pending query %.1f\n",
+                   mode == 0 ? "xcd" : "sorted", pend.size(), st / nw2, ins_st / nw2, cand / np2, lines / nw2,
+                   probes / np2, (12.0 * st + 42.0 * ins_st) / np2);
+        }
     }
     printf("   stage-2 wave steps per wave %.1f -> model incl. stage 2 (54/step) per query %.1f\n", stage2_steps / nw,
            (12.0 * wave_steps + 42.0 * wave_ins_steps + 54.0 * stage2_steps) / nq);
