@@ -1016,7 +1016,7 @@ ot_status sor_frames(const GridBuild& gb, int64_t n, const int* h_foff, int nb_n
                                (int)nb_neighbors, avg, pd);                                                         \
         hipLaunchKernelGGL((k_sor_knn_rest<KM, SOR_BLOCK_R>), dim3(rgrid), dim3(256), 0, stream, gb.g,              \
                            (int)nb_neighbors, avg, pd, pd3);                                                        \
-        hipLaunchKernelGGL((k_sor_knn_wave<KM>), dim3(1024), dim3(64), 0, stream, gb.g, (int)nb_neighbors, avg, pd,   \
+        hipLaunchKernelGGL((k_sor_knn_wave<KM>), dim3(4096), dim3(64), 0, stream, gb.g, (int)nb_neighbors, avg, pd,   \
                            pd3);                                                                                    \
     } while (0)
     if (kk <= 4) OT_SOR_LAUNCH(4);
