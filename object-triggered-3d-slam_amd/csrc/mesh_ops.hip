@@ -416,7 +416,9 @@ __device__ inline long long sat_add(long long a, long long b) {
 }
 
 constexpr int RUN_ITEMS = 4;  // consecutive chunks per thread: a 1024-thread tile covers 4096 chunks
-__global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict__ jobs) {
+// The runs of one chain by a whole 1024-thread workgroup: set_pre(b, inclusive run prefix), set_end(b, run end).
+template <class Head, class SetPre, class SetEnd>
+__device__ inline void chain_runs_block(const ChainJob& j, Head run_head, SetPre set_pre, SetEnd set_end) {
     __shared__ long long s_wv[16];
     __shared__ int s_wh[16];
     __shared__ long long s_cin[16];
@@ -424,7 +426,6 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
     __shared__ int s_nin[16];
     __shared__ long long s_carry;
     __shared__ int s_next;
-    const ChainJob j = jobs[blockIdx.x];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int64_t nb = (j.n + CH - 1) / CH;
     constexpr int TILE = 1024 * RUN_ITEMS;
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
         for (int k = 0; k < RUN_ITEMS; ++k) {
             const int64_t b = b0 + k;
             const bool in = b < nb;
-            const bool hd = !in || run_head(j, b);
+            const bool hd = !in || run_head(b);
             const long long x = in ? j.msum[b] : 0;
             v = hd ? x : sat_add(v, x);
             h |= hd ? 1 : 0;
@@ -483,7 +484,7 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
         const long long cin = eh ? ev : sat_add(s_cin[w], ev);  // the running value entering this thread's chunks
 #pragma unroll
         for (int k = 0; k < RUN_ITEMS; ++k)
-            if (b0 + k < nb) j.pre[b0 + k] = lh[k] ? lv[k] : sat_add(cin, lv[k]);
+            if (b0 + k < nb) set_pre(b0 + k, lh[k] ? lv[k] : sat_add(cin, lv[k]));
         __syncthreads();
     }
     // backward: every chunk's run end = (first head after it) - 1, tile by tile from the end (suffix minimum)
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
         for (int k = RUN_ITEMS - 1; k >= 0; --k) {
             ln[k] = nx;  // heads after chunk b0 + k inside this thread, excluding b0 + k + 1 (added next)
             const int64_t b1 = b0 + k + 1;
-            if (b1 < nb && run_head(j, b1)) ln[k] = (int)b1;
+            if (b1 < nb && run_head(b1)) ln[k] = (int)b1;
             nx = ln[k];
         }
         // nx = first head after chunk b0 within this thread; wave exclusive suffix minimum from later lanes
@@ -523,10 +524,16 @@ __global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict_
 #pragma unroll
         for (int k = 0; k < RUN_ITEMS; ++k) {
             const int nxt = ln[k] < after ? ln[k] : after;
-            if (b0 + k < nb) j.rend[b0 + k] = nxt - 1;
+            if (b0 + k < nb) set_end(b0 + k, nxt - 1);
         }
         __syncthreads();
     }
+}
+__global__ __launch_bounds__(1024) void k_chain_runs(const ChainJob* __restrict__ jobs) {
+    const ChainJob j = jobs[blockIdx.x];
+    chain_runs_block(
+        j, [&](int64_t b) { return run_head(j, b); }, [&](int64_t b, long long v) { j.pre[b] = v; },
+        [&](int64_t b, int e) { j.rend[b] = e; });
 }
 
 // The walk's per-chunk metadata (ex, run end, run prefix, kind), staged in LDS by the whole workgroup before the one
@@ -567,13 +574,27 @@ template <bool CDF, bool STAGED>
 __global__ __launch_bounds__(1024) void k_chain_walk(const ChainJob* __restrict__ jobs) {
     const ChainJob j = jobs[blockIdx.x];
     const int64_t nb = (j.n + CH - 1) / CH;
-    if constexpr (STAGED) {  // the whole workgroup stages the metadata, then one wave walks
+    if constexpr (STAGED) {  // the whole workgroup stages the metadata and forms the runs in LDS, then one wave walks
+        // (k_chain_runs folded in: its launch and the global round trip of the run prefixes and ends were on one
+        // object's critical path; the CDF chain's emission still reads the prefixes from global memory)
         signed char* s_kind = reinterpret_cast<signed char*>(s_walk_meta + nb);
         for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
-            const unsigned long long pv = (unsigned long long)j.pre[b];
-            s_walk_meta[b] = make_int4(j.ex[b], j.rend[b], (int)(unsigned)pv, (int)(unsigned)(pv >> 32));
+            s_walk_meta[b].x = j.ex[b];
             s_kind[b] = (signed char)j.kind[b];
         }
+        __syncthreads();
+        chain_runs_block(
+            j,
+            [&](int64_t b) {  // run_head() on the staged copies
+                return b == 0 || s_kind[b] != 0 || s_kind[b - 1] != 0 || s_walk_meta[b].x != s_walk_meta[b - 1].x;
+            },
+            [&](int64_t b, long long v) {
+                const unsigned long long pv = (unsigned long long)v;
+                s_walk_meta[b].z = (int)(unsigned)pv;
+                s_walk_meta[b].w = (int)(unsigned)(pv >> 32);
+                if (CDF) j.pre[b] = v;
+            },
+            [&](int64_t b, int e) { s_walk_meta[b].y = e; });
         __syncthreads();
     }
     if (threadIdx.x >= 64) return;
@@ -723,10 +744,11 @@ void launch_chains(const ChainJob* djobs, int n_jobs, int64_t max_n, hipStream_t
         hipLaunchKernelGGL(k_chain_guess, dim3(n_jobs), dim3(1024), 0, stream, djobs);
         hipLaunchKernelGGL(k_chain_chunk, grid, dim3(256), 0, stream, djobs);
     }
-    hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
+    // metadata staged in LDS (and the runs formed there) when every job's chunks fit (max_n bounds them all)
+    const bool staged = nb <= WALK_LDS_CHUNKS;
+    if (!staged) hipLaunchKernelGGL(k_chain_runs, dim3(n_jobs), dim3(1024), 0, stream, djobs);
     if (mark) (void)hipEventRecord(mark, stream);  // (a failure is the thread's last error: the caller's launch check)
-    // metadata staged in LDS when every job's chunks fit (max_n bounds them all)
-    if (nb <= WALK_LDS_CHUNKS) {
+    if (staged) {
         const size_t lds_bytes = (size_t)nb * 17 + 16;
         static std::atomic<bool> attr_set[2] = {false, false};
         if (!attr_set[CDF].load()) {  // above 64 KiB of dynamic LDS the kernel must opt in (once per process)

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 T=${TAG:?set TAG}
 timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_gpu_mesh.py tests/test_gpu_configs_full.py tests/test_gpu_e2e.py tests/test_gpu_golden.py tests/test_gpu_shard.py} \
-    -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 \
+    -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 \
     || { echo TESTS_FAILED; tail -60 gpurun_out/${T}_gpu_tests.log; exit 1; }
 tail -1 gpurun_out/${T}_gpu_tests.log
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
