@@ -30,6 +30,8 @@ constexpr int C_UNITS = 1;     // units allocated
 constexpr int C_OVERFLOW = 2;  // pool exhausted (units dropped)
 constexpr int C_HASHERR = 3;   // hash full or key out of range
 constexpr int C_BATCH_PAIRS = 4;  // (frame, unit) pairs of a batch: counters[4 + parity] (batches alternate, see k_batch_units)
+constexpr int C_ORDER_HEAVY = 6;  // k_batch_units: work-list entries placed from the front (units seen by >= half the
+constexpr int C_ORDER_LIGHT = 7;  // batch's frames) / from the back (the rest); the last workgroup zeroes both
 constexpr int C_KMAX = 8;   // [8, 11): max over allocated units of key_a + KEY_BIAS + 1 (0: no unit yet)
 constexpr int C_KNEG = 11;  // [11, 14): max over allocated units of KEY_BIAS - key_a + 1 (so min key_a = KEY_BIAS + 1 - it)
 constexpr int C_UNITS_DONE = 14;  // k_batch_units: workgroups finished (the last one mails the counters, then zeroes it)
