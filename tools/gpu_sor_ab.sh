@@ -1,12 +1,12 @@
 #!/bin/bash
 # A/B of a SOR test hook on one GPU box: the SOR / filter-chain parity tests, then the configs[2] chain under
 # rocprofv3 --kernel-trace --stats with the hook alternating 1 / 0 in one process (the two template variants show up
-# as separate kernels).  TAG names the outputs; HOOK (default otx_sor_rest_batched), ROUNDS.
+# as separate kernels).  TAG names the outputs; HOOK (default otx_sor_netfill), ROUNDS.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 TAG=${TAG:?set TAG}
-HOOK=${HOOK:-otx_sor_rest_batched}
+HOOK=${HOOK:-otx_sor_netfill}
 [ "${SKIP_TESTS:-0}" = 1 ] || timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_filters.py tests/test_gpu_filter_batch.py} -m gpu -x -v --timeout 120 \
     --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
 [ "${SKIP_TESTS:-0}" = 1 ] || tail -1 gpurun_out/${TAG}_tests.log
