@@ -52,6 +52,8 @@ int main(int argc, char** argv) {
     std::vector<std::vector<double>> Q(64);
     std::vector<std::pair<long long, std::vector<double>>> pend;  // stage-1 misses: sorted position, list
     std::vector<long long> pend_wave;
+    std::vector<double> un_ratio;  // unsettled queries: k-th distance / guard
+    std::vector<int> un_second;    // 1: the k-th sphere crosses only the nearest face, 2: two faces, 3: more
     const double h = hm * 0.005;
     double mn[3] = {1e30, 1e30, 1e30};
     for (size_t i = 0; i < n; ++i)
@@ -275,6 +277,19 @@ int main(int argc, char** argv) {
             }
             const bool un = !(best[l][K - 1] <= g * g);
             unsettled += un;
+            if (un) {  // how far past the guard: k-th distance / guard, and the second-nearest face's guard
+                double gs[6];
+                int q = 0;
+                for (int a = 0; a < 3; ++a) {
+                    const double uu = (S[j * 3 + a] - mn[a]) / h, fr = uu - std::floor(uu);
+                    gs[q++] = (R + fr) * h;
+                    gs[q++] = (R + 1 - fr) * h;
+                }
+                std::sort(gs, gs + 6);
+                const double kd = best[l][K - 1] < 1e30 ? std::sqrt(best[l][K - 1]) : 1e30;
+                un_ratio.push_back(kd / g);
+                un_second.push_back(kd <= gs[1] ? 1 : (kd <= gs[2] ? 2 : 3));
+            }
             if (un) pend.push_back({(long long)j, best[l]}), pend_wave.push_back((long long)(w0 / 64));
             if (un) {
                 long long x = (long long)std::floor((S[j * 3] - mn[0]) / h), y = (long long)std::floor((S[j * 3 + 1] - mn[1]) / h),
@@ -412,6 +427,15 @@ int main(int argc, char** argv) {
                    mode == 0 ? "xcd" : "sorted", pend.size(), st / nw2, ins_st / nw2, cand / np2, lines / nw2,
                    probes / np2, (12.0 * st + 42.0 * ins_st) / np2);
         }
+    }
+    if (!un_ratio.empty()) {
+        std::vector<double> r = un_ratio;
+        std::sort(r.begin(), r.end());
+        long long c1 = 0, c2 = 0;
+        for (int v : un_second) c1 += v == 1, c2 += v == 2;
+        printf("   unsettled: k-th / guard median %.3f p25 %.3f p75 %.3f p90 %.3f; sphere past one face only %.1f%%, two "
+               "faces %.1f%%\n", r[r.size() / 2], r[r.size() / 4], r[r.size() * 3 / 4], r[r.size() * 9 / 10],
+               100.0 * c1 / r.size(), 100.0 * c2 / r.size());
     }
     printf("   stage-2 wave steps per wave %.1f -> model incl. stage 2 (54/step) per query %.1f\n", stage2_steps / nw,
            (12.0 * wave_steps + 42.0 * wave_ins_steps + 54.0 * stage2_steps) / nq);
