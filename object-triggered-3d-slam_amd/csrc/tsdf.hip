@@ -586,6 +586,9 @@ __global__ __launch_bounds__(256) void k_batch_units(TsdfDev d, UnitWork* __rest
         if (threadIdx.x < N_COUNTERS) {
             const int v = __hip_atomic_load(&d.counters[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             early_mail[threadIdx.x] = threadIdx.x == C_UNITS_DONE ? 0u : (unsigned)v;
+            // the heavy units' count (the list's front; the light ones fill the back in reverse touch order, which
+            // integrate_body reads forward again) next to the length the integrate reads
+            if (threadIdx.x == C_ORDER_HEAVY && wcount) wcount[2] = d.shard_world > 1 ? v : n;
             if (threadIdx.x == C_UNITS_DONE || threadIdx.x == C_ORDER_HEAVY || threadIdx.x == C_ORDER_LIGHT)
                 d.counters[threadIdx.x] = 0;
         }
@@ -835,6 +838,7 @@ __device__ __forceinline__ void integrate_body(const BatchFrame* __restrict__ fr
     }
     const int lane = threadIdx.x & 63;
     const int n = *wcount;
+    const int nh = wcount[2];  // heavy units first; the rest are stored back to front (k_batch_units)
     const int npx = p.W * p.H;
     unsigned upd = 0;  // per lane: <= ZB voxels x 64 frames x units per workgroup, far below 2^32
     {
@@ -845,7 +849,7 @@ __device__ __forceinline__ void integrate_body(const BatchFrame* __restrict__ fr
             if (PARTS > 1 && u >= n) continue;
             const int part = PARTS == 1 ? 0 : (it >> 3) % PARTS;
             const int s = __builtin_amdgcn_readfirstlane(part * INT_WG + (int)(threadIdx.x >> 6));  // slice of this wave
-            const UnitWork& w = work[u];
+            const UnitWork& w = work[u < nh ? u : n - 1 - (u - nh)];
             const int ent = w.id;
             const unsigned long long mask = w.mask;
             if (ent != -1) {
@@ -2030,7 +2034,7 @@ static ot_status join_integrate(ot_tsdf* vol, hipStream_t stream) {
 static ot_status ensure_overlap(ot_tsdf* vol) {
     if (vol->istream) return OT_OK;
     OT_HIP_TRY(hipStreamCreateWithFlags(&vol->istream, hipStreamNonBlocking));
-    if (!vol->wcount) OT_HIP_TRY(hipMalloc(&vol->wcount, sizeof(int) * 2));
+    if (!vol->wcount) OT_HIP_TRY(hipMalloc(&vol->wcount, sizeof(int) * 4));  // [set]: length, [2 + set]: heavy units
     if (!vol->bset[1].bframes) OT_HIP_TRY(hipMalloc(&vol->bset[1].bframes, sizeof(BatchFrame) * MAX_BATCH));
     if (!vol->bset[1].work) OT_HIP_TRY(hipMalloc(&vol->bset[1].work, sizeof(UnitWork) * vol->hash_cap));
     for (auto& b : vol->bset) {
