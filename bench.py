@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="frames per fused launch (0 = library default)")
     ap.add_argument("--overlap", type=int, default=-1, choices=(-1, 0, 1),
                     help="headline volume's batch front end double-buffered beside the previous integrate "
-                         "(ot_tsdf_set_frontend_overlap; -1 = library default: on for sharded volumes only, 0 off, 1 on)")
+                         "(ot_tsdf_set_frontend_overlap; -1 = library default: "
+                         "sharded volumes double-buffer at 2-3 ranks and defer the integrate from 4, whole volumes "
+                         "neither; 0 off, 1 on)")
     ap.add_argument("--cpu-frames", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--sustain", type=float, default=12.0,
                     help="seconds of sustained headline steps after the timed ones (0 = skip): >= 12 s so a 5-s busy "

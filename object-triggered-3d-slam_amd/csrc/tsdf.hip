@@ -683,6 +683,7 @@ __global__ __launch_bounds__(256) void k_stage_mask(const BatchFrame* __restrict
 // spread over all 256 lanes (one wave per tile left 77 % of the waves idle: 23 us per batch, r06e).  A quad staged
 // twice writes the same bytes.
 constexpr int ST_MAX_TILES_X = 256;
+constexpr int ST_K = 4;  // quads per lane per step on the common path
 __global__ __launch_bounds__(256) void k_stage_tiles(const BatchFrame* __restrict__ frames, const float* __restrict__ mult,
                                                      const unsigned* __restrict__ mask, int W, int H, int tiles_x,
                                                      int tiles_y, int wpr, int64_t npx) {
@@ -701,6 +702,47 @@ __global__ __launch_bounds__(256) void k_stage_tiles(const BatchFrame* __restric
     const int slots = (W & 3) ? STX / 4 + 1 : STX / 4;
     const int per_tile = rows * slots;
     const BatchFrame& fr = frames[f];
+    const bool fast = fr.depth16 && fr.color && (npx & 3) == 0 && (W & 3) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(fr.depth16) & 7) == 0) &&
+                      ((reinterpret_cast<uintptr_t>(fr.color) & 3) == 0);
+    if (fast) {  // (u16 depth, RGB8, W % 4 == 0: every slot is a whole quad) a lane's ST_K quads' loads before any store
+        const int total = m * per_tile;
+        for (int i0 = threadIdx.x; i0 < total; i0 += 256 * ST_K) {
+            int64_t px[ST_K];
+            uint2 raw[ST_K];
+            float4 mv[ST_K];
+            uint32_t w[ST_K][3];
+#pragma unroll
+            for (int k = 0; k < ST_K; ++k) {
+                const int i = i0 + 256 * k;
+                px[k] = -1;
+                const int t = i / per_tile, rem = i - t * per_tile;
+                const int r = y0 + rem / slots, x = s_tx[min(t, m - 1)] * STX + (rem - (rem / slots) * slots) * 4;
+                if (i < total && x < W) {  // (the frame's last tile column may be narrower than STX)
+                    px[k] = (int64_t)r * W + x;
+                    raw[k] = *reinterpret_cast<const uint2*>(fr.depth16 + px[k]);
+                    mv[k] = *reinterpret_cast<const float4*>(mult + px[k]);
+                    const uint32_t* c = reinterpret_cast<const uint32_t*>(fr.color + px[k] * 3);
+                    w[k][0] = c[0], w[k][1] = c[1], w[k][2] = c[2];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < ST_K; ++k) {
+                if (px[k] < 0) continue;
+                const float d0 = prep_depth(fr, raw[k].x & 0xFFFFu), d1 = prep_depth(fr, raw[k].x >> 16);
+                const float d2 = prep_depth(fr, raw[k].y & 0xFFFFu), d3 = prep_depth(fr, raw[k].y >> 16);
+                float4* dm = reinterpret_cast<float4*>(fr.dm + px[k]);
+                dm[0] = make_float4(d0, mv[k].x, d1, mv[k].y);
+                dm[1] = make_float4(d2, mv[k].z, d3, mv[k].w);
+                const uint32_t p0 = w[k][0] & 0xFFFFFFu;
+                const uint32_t p1 = (w[k][0] >> 24) | ((w[k][1] & 0xFFFFu) << 8);
+                const uint32_t p2 = (w[k][1] >> 16) | ((w[k][2] & 0xFFu) << 16);
+                const uint32_t p3 = w[k][2] >> 8;
+                *reinterpret_cast<uint4*>(fr.rgba + px[k]) = make_uint4(p0, p1, p2, p3);
+            }
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < m * per_tile; i += 256) {
         const int t = i / per_tile, rem = i - t * per_tile;
         const int r = y0 + rem / slots, kq = rem - (rem / slots) * slots;

@@ -221,6 +221,11 @@ def test_split_frontend_bitexact(pkg, O, gpu, synth, seq16, batch, defer):
         depth, color, ext = synth.make_sequence(n_frames=12, frames=[0, 2, 5, 9], intr=intr_t)
         vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, batch=batch, intr_t=intr_t)
         assert _compare_volumes(vol, ref) > 100
+        # width a multiple of 4 but not of 32: the staging kernel's quad path with a narrower last tile column
+        intr_t = (324, 242, 283.1, 283.4, 161.7, 120.2)
+        depth, color, ext = synth.make_sequence(n_frames=12, frames=[0, 2, 5, 9], intr=intr_t)
+        vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, batch=batch, intr_t=intr_t)
+        assert _compare_volumes(vol, ref) > 100
         depth, color, ext = seq16
         vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.01, float_path=True)
         _compare_volumes(vol, ref)
