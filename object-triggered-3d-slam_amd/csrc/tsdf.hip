@@ -620,18 +620,21 @@ struct StageMaskParams {
 // One workgroup per FRAME: its threads walk the batch's work list, each unit whose frame mask has this frame's bit ORs
 // its footprint's tiles into the frame's map in LDS, and the map is stored whole -- no global atomics (one per (unit,
 // frame, tile row) had contended on the frames' few words: 8-18 us per batch, r06e), nothing to clear between batches.
+// SM_PARTS workgroups per frame, each over every SM_PARTS-th 256-unit chunk of the list into its own map (64 workgroups
+// for a 64-frame batch had left the mask kernel latency-bound: 5-8 us per batch, r06st); the staging kernel ORs them.
 constexpr int SM_WORDS = 2048;  // LDS map words: tile rows * words per row (8 KiB; 16K x 16K-pixel frames)
+constexpr int SM_PARTS = 4;
 __global__ __launch_bounds__(256) void k_stage_mask(const BatchFrame* __restrict__ frames, StageMaskParams q,
                                                     const UnitWork* __restrict__ work, const int* __restrict__ wcount,
                                                     unsigned* __restrict__ mask) {
     __shared__ unsigned s_map[SM_WORDS];
-    const int f = blockIdx.x;
+    const int f = blockIdx.x, part = blockIdx.y;
     const int words = q.tiles_y * q.wpr;
     for (int i = threadIdx.x; i < words; i += 256) s_map[i] = 0u;
     __syncthreads();
     const int n = *wcount;
     const BatchFrame& fr = frames[f];
-    for (int u = threadIdx.x; u < n; u += 256) {
+    for (int u = part * 256 + threadIdx.x; u < n; u += 256 * SM_PARTS) {
         const UnitWork& w = work[u];
         if (!((w.mask >> f) & 1ull)) continue;
         const float ox = (float)((double)w.kx * q.unit_len);
@@ -675,7 +678,7 @@ __global__ __launch_bounds__(256) void k_stage_mask(const BatchFrame* __restrict
             }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < words; i += 256) mask[(size_t)f * words + i] = s_map[i];
+    for (int i = threadIdx.x; i < words; i += 256) mask[((size_t)f * SM_PARTS + part) * words + i] = s_map[i];
 }
 
 // Stage the marked tiles: one workgroup per (tile row, frame); its lanes take the marked tiles' quads in turn (a row of
@@ -692,9 +695,14 @@ __global__ __launch_bounds__(256) void k_stage_tiles(const BatchFrame* __restric
     const int ty = blockIdx.x, f = blockIdx.y;
     if (threadIdx.x == 0) s_m = 0;
     __syncthreads();
-    const unsigned* row = mask + ((size_t)f * tiles_y + ty) * wpr;
-    for (int tx = threadIdx.x; tx < tiles_x; tx += 256)
-        if ((row[tx >> 5] >> (tx & 31)) & 1u) s_tx[atomicAdd(&s_m, 1)] = tx;
+    const size_t words = (size_t)tiles_y * wpr;
+    const unsigned* row = mask + (size_t)f * SM_PARTS * words + (size_t)ty * wpr;
+    for (int tx = threadIdx.x; tx < tiles_x; tx += 256) {
+        unsigned w = 0u;
+#pragma unroll
+        for (int part = 0; part < SM_PARTS; ++part) w |= row[part * words + (tx >> 5)];
+        if ((w >> (tx & 31)) & 1u) s_tx[atomicAdd(&s_m, 1)] = tx;
+    }
     __syncthreads();
     const int m = s_m;
     if (m == 0) return;
@@ -2040,7 +2048,7 @@ static bool tmask_fits(int w, int h) {
 }
 static ot_status ensure_tmask(ot_tsdf* vol, int w, int h, hipStream_t stream) {
     if (vol->tmask && vol->tmask_w == w && vol->tmask_h == h) return OT_OK;
-    const int64_t words = (int64_t)MAX_BATCH * ((h + STY - 1) / STY) * (((w + STX - 1) / STX + 31) / 32);
+    const int64_t words = (int64_t)MAX_BATCH * SM_PARTS * ((h + STY - 1) / STY) * (((w + STX - 1) / STX + 31) / 32);
     if (vol->tmask) {
         OT_HIP_TRY(hipStreamSynchronize(stream));
         OT_HIP_TRY(hipFree(vol->tmask));
@@ -2051,6 +2059,14 @@ static ot_status ensure_tmask(ot_tsdf* vol, int w, int h, hipStream_t stream) {
     vol->tmask_w = w, vol->tmask_h = h;
     note_alloc();
     return OT_OK;
+}
+// mark the tiles the units of the work list (`wcount` entries) project to, then stage those tiles
+static void launch_stage(const BatchFrame* bf, const StageMaskParams& q, const UnitWork* work, const int* wcount,
+                         unsigned* smask, const float* mult, hipStream_t stream) {
+    hipLaunchKernelGGL(k_stage_mask, dim3((unsigned)q.nframes, SM_PARTS), dim3(256), 0, stream, bf, q, work, wcount,
+                       smask);
+    hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)q.tiles_y, (unsigned)q.nframes), dim3(256), 0, stream, bf, mult,
+                       (const unsigned*)smask, q.W, q.H, q.tiles_x, q.tiles_y, q.wpr, (int64_t)q.W * q.H);
 }
 static void* set_work(ot_tsdf* vol, int s) { return s == 0 ? vol->dev.work : vol->bset[1].work; }
 // Deferred integrate (round 6): a sharded volume with the split front end launches batch k's integrate together with
@@ -2262,11 +2278,8 @@ static ot_status integrate_batch(ot_tsdf* vol, const PendingFrame* frames, int n
         bc.split = true;
         bc.sq = q;
         bc.smask = vol->tmask;
-        hipLaunchKernelGGL(k_stage_mask, dim3((unsigned)n), dim3(256), 0, stream, (const BatchFrame*)bs.bframes, q,
-                           (const UnitWork*)work, (const int*)wcount, vol->tmask);
-        hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)q.tiles_y, (unsigned)n), dim3(256), 0, stream,
-                           (const BatchFrame*)bs.bframes, (const float*)vol->mult, (const unsigned*)vol->tmask,
-                           in.width, in.height, q.tiles_x, q.tiles_y, q.wpr, npx);
+        launch_stage((const BatchFrame*)bs.bframes, q, (const UnitWork*)work, (const int*)wcount, vol->tmask,
+                     (const float*)vol->mult, stream);
     }
     // reciprocal-table kernel while every weight + 1 is an integer <= RCP_N: weights count updates, at most one
     // per frame since reset, unless units were imported (k_batch_integrate: Markstein's exact correction)
@@ -2475,22 +2488,16 @@ static ot_status settle_batch(ot_tsdf* vol, const BatchCtx& bc, hipStream_t stre
         if (bc.defer) {  // nothing of the batch is integrated yet: rebuild its whole work list, restage, stay deferred
             hipLaunchKernelGGL(k_batch_units<false>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
                                vol->hmail + OT_MAIL_WORDS, vol->wcount + bc.set, ++vol->units_seq);
-            hipLaunchKernelGGL(k_stage_mask, dim3((unsigned)bc.n), dim3(256), 0, stream, (const BatchFrame*)bf, bc.sq,
-                               (const UnitWork*)work, (const int*)(vol->wcount + bc.set), bc.smask);
-            hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)bc.sq.tiles_y, (unsigned)bc.n), dim3(256), 0, stream, bf,
-                               (const float*)vol->mult, (const unsigned*)bc.smask, bc.sq.W, bc.sq.H, bc.sq.tiles_x,
-                               bc.sq.tiles_y, bc.sq.wpr, (int64_t)bc.sq.W * bc.sq.H);
+            launch_stage(bf, bc.sq, (const UnitWork*)work, (const int*)(vol->wcount + bc.set), bc.smask,
+                         (const float*)vol->mult, stream);
             OT_LAUNCH_CHECK();
             continue;
         }
         hipLaunchKernelGGL(k_batch_units<true>, dim3(256), dim3(256), 0, stream, vol->dev, work, bc.pc,
                            vol->hmail + OT_MAIL_WORDS, (int*)nullptr, ++vol->units_seq);
         if (bc.split) {  // the replayed units' tiles, from the caller's frames (valid until this flush returns)
-            hipLaunchKernelGGL(k_stage_mask, dim3((unsigned)bc.n), dim3(256), 0, stream, (const BatchFrame*)bf, bc.sq,
-                               (const UnitWork*)work, (const int*)(vol->dev.counters + bc.pc), bc.smask);
-            hipLaunchKernelGGL(k_stage_tiles, dim3((unsigned)bc.sq.tiles_y, (unsigned)bc.n), dim3(256), 0, stream, bf,
-                               (const float*)vol->mult, (const unsigned*)bc.smask, bc.sq.W, bc.sq.H, bc.sq.tiles_x,
-                               bc.sq.tiles_y, bc.sq.wpr, (int64_t)bc.sq.W * bc.sq.H);
+            launch_stage(bf, bc.sq, (const UnitWork*)work, (const int*)(vol->dev.counters + bc.pc), bc.smask,
+                         (const float*)vol->mult, stream);
         }
         const UnitWork* uw = work;
         const int* wc = vol->dev.counters + bc.pc;
