@@ -1594,6 +1594,26 @@ __global__ __launch_bounds__(64 * INT_WG, INT_WAVES_PER_EU) void k_integrate_tou
         touch_body<false, false>(tframes, tp, d, tn, lds.t, t % tp.tiles, t / tp.tiles);
     }
 }
+// The same launch with the integrate in fine slices (2 voxels per lane along z, k_batch_integrate<.., 2, 1>'s per-voxel
+// code and occupancy): the deferred batch's unit count is known on the host by then (its units kernel mailed it), so a
+// batch of few units takes the fine slices without the guess the direct path makes from the previous batch
+template <bool C64, bool FAST>
+__global__ __launch_bounds__(64 * INT_WG, (C64 && !FAST) ? 5 : 4) void k_integrate_touch_fine(
+    const BatchFrame* __restrict__ frames, IntegrateParams p, TsdfDev d, const UnitWork* __restrict__ work,
+    const int* __restrict__ wcount, int nint, const BatchFrame* __restrict__ tframes, BatchTouchParams tp, int tn) {
+    union Lds {
+        TouchLds t;
+        RcpLds<C64, FAST> r;
+    };
+    __shared__ Lds lds;
+    const int b = (int)blockIdx.x;
+    if (b < nint) {
+        integrate_body<C64, FAST, 2, 1>(frames, p, d, work, wcount, lds.r, b, nint);
+    } else {
+        const int t = b - nint;
+        touch_body<false, false>(tframes, tp, d, tn, lds.t, t % tp.tiles, t / tp.tiles);
+    }
+}
 
 // export: units in sorted order, voxels transposed to Open3D IndexOf order (x*256 + y*16 + z); colour as CT
 // (float export of a float64 volume rounds to nearest)
@@ -1973,6 +1993,7 @@ constexpr int INT_GRID_MULT = 8;
 // the integrate instantiation of a batch: colour precision 64 (bit 1), reciprocal table (bit 0), fine slices (bit 2:
 // 2 voxels per lane along z, 32 waves per unit instead of 16 -- for batches with few units, below)
 static int g_int_fine = -1;  // test hook otx_integrate_fine: -1 by the batch's size (default), 0 coarse, 1 fine
+static int g_fine_units = -1;  // its threshold form (deferred integrate: fine below this many units; -1 the default)
 static int g_stage_blocks = -1;  // test hook otx_touch_stage_blocks: staging-only touch workgroups (-1: 2 per tile)
 // bits 3-4 of a fine variant: the frame pipeline's depth KT - 1 (k_batch_integrate's ZB == 2 loop)
 static int g_int_depth = -1;  // test hook otx_integrate_depth: -1 the default (INT_FINE_KT), else KT in 1..3
@@ -2118,7 +2139,18 @@ static ot_status launch_deferred(ot_tsdf* vol, hipStream_t stream, const BatchCt
     const BatchFrame* bf = vol->bset[D.set].bframes;
     const UnitWork* uw = (const UnitWork*)set_work(vol, D.set);
     const int* wc = vol->wcount + D.set;
-    const int variant = D.variant & 3;  // coarse
+    // coarse, or fine slices for a batch of few units: its count is known here (settle_batch read the mail of its
+    // units kernel; the direct path guesses it from the previous batch), the rule of integrate_batch
+    int variant = D.variant & 3;
+    {
+        const int64_t units = vol->last_batch_slots;
+        const int resident = integrate_grid(variant) / INT_GRID_MULT;
+        const bool small = g_fine_units >= 2 ? units >= 0 && units < g_fine_units
+                                             : units >= 0 && units * INT_PARTS * 4 < (int64_t)resident * 3;
+        if (g_int_fine > 0 || ((g_int_fine < 0 || g_fine_units >= 2) && small))
+            variant |= 4 | ((INT_FINE_KT - 1) << 3);
+    }
+    const bool fine = (variant & 4) != 0;
     const int nint = integrate_grid(variant);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (vol->profiling) {
@@ -2133,12 +2165,13 @@ static ot_status launch_deferred(ot_tsdf* vol, hipStream_t stream, const BatchCt
         int ni = nint;
         void* args[] = {(void*)&bf, (void*)&D.ip0, (void*)&vol->dev, (void*)&uw, (void*)&wc, (void*)&ni,
                         (void*)&tf, (void*)&tp, (void*)&tn};
-        static const void* const kt[4] = {(const void*)k_integrate_touch<false, false>,
-                                          (const void*)k_integrate_touch<false, true>,
-                                          (const void*)k_integrate_touch<true, false>,
-                                          (const void*)k_integrate_touch<true, true>};
+        static const void* const kt[8] = {
+            (const void*)k_integrate_touch<false, false>,      (const void*)k_integrate_touch<false, true>,
+            (const void*)k_integrate_touch<true, false>,       (const void*)k_integrate_touch<true, true>,
+            (const void*)k_integrate_touch_fine<false, false>, (const void*)k_integrate_touch_fine<false, true>,
+            (const void*)k_integrate_touch_fine<true, false>,  (const void*)k_integrate_touch_fine<true, true>};
         const unsigned grid = (unsigned)nint + next->tiles * (unsigned)((tn + tp.tf - 1) / tp.tf);
-        OT_HIP_TRY(hipLaunchKernel(kt[variant], dim3(grid), dim3(64 * INT_WG), args, 0, stream));
+        OT_HIP_TRY(hipLaunchKernel(kt[(variant & 3) + (fine ? 4 : 0)], dim3(grid), dim3(64 * INT_WG), args, 0, stream));
     } else {
         void* args[] = {(void*)&bf, (void*)&D.ip0, (void*)&vol->dev, (void*)&uw, (void*)&wc};
         OT_HIP_TRY(hipLaunchKernel(integrate_kernel(variant), dim3(nint), dim3(64 * INT_WG), args, 0, stream));
@@ -3096,9 +3129,11 @@ ot_status otx_tsdf_stats(ot_tsdf* vol, uint64_t* out4) {
 }
 
 // test hook: the integrate's slice granularity (-1 = by the batch's estimated unit count, 0 = 4 voxels per lane along z
-// always, 1 = 2 always): A/B timing and the parity of both instantiations
+// always, 1 = 2 always; >= 2: the deferred integrate takes the fine slices below that many units, a threshold sweep):
+// A/B timing and the parity of both instantiations
 ot_status otx_integrate_fine(int32_t mode) {
-    g_int_fine = mode < 0 ? -1 : (mode ? 1 : 0);
+    g_int_fine = mode < 0 ? -1 : (mode == 1 ? 1 : 0);
+    g_fine_units = mode >= 2 ? mode : -1;
     return OT_OK;
 }
 

@@ -203,16 +203,18 @@ def test_touch_staging_forms_bitexact(pkg, O, gpu, synth, blocks, tf):
         L.call("otx_touch_frames", 2)
 
 
-@pytest.mark.parametrize("batch,defer", [(16, 0), (1, 0), (16, 1), (1, 1)])
-def test_split_frontend_bitexact(pkg, O, gpu, synth, seq16, batch, defer):
+@pytest.mark.parametrize("batch,defer,fine", [(16, 0, -1), (1, 0, -1), (16, 1, -1), (1, 1, -1), (16, 1, 1), (16, 1, 0)])
+def test_split_frontend_bitexact(pkg, O, gpu, synth, seq16, batch, defer, fine):
     """The split front end (round 6: touch without staging, the batch units' footprint tiles marked, only those tiles
     staged) forced on an unsharded volume, where every visible tile must be marked: 40 frames at 5 mm, the odd
     321x243 camera (partial 32x16 tiles, quads straddling rows) and the float-depth path, bitwise vs the oracle;
     with the deferred integrate too (each batch's integrate launched with the next batch's touch, k_integrate_touch,
-    the last one by the reader's flush)."""
+    the last one by the reader's flush), its integrate in coarse or fine slices (by the batch's unit count, or forced:
+    k_integrate_touch_fine)."""
     L = pkg._lib
     L.call("otx_split_frontend", 1)
     L.call("otx_defer_integrate", defer)
+    L.call("otx_integrate_fine", fine)
     try:
         depth, color, ext = synth.make_sequence(synth.Scene(seed=5), n_frames=80, frames=range(0, 80, 2))
         vol, ref = _run_pair(pkg, O, synth, depth, color, ext, 0.005, batch=batch)
@@ -232,6 +234,7 @@ def test_split_frontend_bitexact(pkg, O, gpu, synth, seq16, batch, defer):
     finally:
         L.call("otx_split_frontend", -1)
         L.call("otx_defer_integrate", -1)
+        L.call("otx_integrate_fine", -1)
 
 
 @pytest.mark.parametrize("batch", [1, None])
