@@ -269,14 +269,14 @@ constexpr int TF = 2;
 static int g_touch_tf = TF;  // test hook otx_touch_frames: frames per touch workgroup (A/B timing)
 constexpr int LTAB = 1024;   // LDS table entries (16 B each + a 4-B slot in the list of used entries)
 
-__device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* masks, int* used, int* nused,
+__device__ inline bool lds_merge(unsigned long long* keys, unsigned long long* masks, unsigned short* used, int* nused,
                                  unsigned long long key, unsigned long long bit) {
     unsigned h = (unsigned)mix64(key) & (LTAB - 1);
     for (int probe = 0; probe < 64; ++probe) {
         unsigned long long k = keys[h];
         if (k == KEY_EMPTY) {
             const unsigned long long old = atomicCAS(&keys[h], KEY_EMPTY, key);
-            if (old == KEY_EMPTY) used[atomicAdd(nused, 1)] = (int)h;  // the inserting lane lists the entry
+            if (old == KEY_EMPTY) used[atomicAdd(nused, 1)] = (unsigned short)h;  // the inserting lane lists the entry
             k = (old == KEY_EMPTY) ? key : old;
         }
         if (k == key) {
@@ -314,7 +314,7 @@ __device__ inline void stage_share(const BatchFrame* __restrict__ frames, const 
 struct TouchLds {
     unsigned long long keys[LTAB];
     unsigned long long masks[LTAB];
-    int used[LTAB];
+    unsigned short used[LTAB];  // 16-bit entry indices: 18 KiB in all, so 8 workgroups fit a CU's 160 KiB
     int nused;
 };
 // STAGE: the staging code paths (stage_blocks >= 0) are compiled in; the split front end's touch has none (the touch half
@@ -324,7 +324,7 @@ __device__ __forceinline__ void touch_body(const BatchFrame* __restrict__ frames
                                            const TsdfDev& d, int nframes, TouchLds& L, int tile, int grp) {
     unsigned long long* s_keys = L.keys;
     unsigned long long* s_masks = L.masks;
-    int* s_used = L.used;
+    unsigned short* s_used = L.used;
     int& s_nused = L.nused;
     const int tid = threadIdx.x;
     if constexpr (STAGE) {
