@@ -1993,6 +1993,7 @@ constexpr int INT_GRID_MULT = 8;
 // the integrate instantiation of a batch: colour precision 64 (bit 1), reciprocal table (bit 0), fine slices (bit 2:
 // 2 voxels per lane along z, 32 waves per unit instead of 16 -- for batches with few units, below)
 static int g_int_fine = -1;  // test hook otx_integrate_fine: -1 by the batch's size (default), 0 coarse, 1 fine
+constexpr int DEFER_FINE_NUM = 21, DEFER_FINE_DEN = 8;  // units * 16 < 21/8 of the resident workgroups: 336 units
 static int g_fine_units = -1;  // its threshold form (deferred integrate: fine below this many units; -1 the default)
 static int g_stage_blocks = -1;  // test hook otx_touch_stage_blocks: staging-only touch workgroups (-1: 2 per tile)
 // bits 3-4 of a fine variant: the frame pipeline's depth KT - 1 (k_batch_integrate's ZB == 2 loop)
@@ -2145,8 +2146,12 @@ static ot_status launch_deferred(ot_tsdf* vol, hipStream_t stream, const BatchCt
     {
         const int64_t units = vol->last_batch_slots;
         const int resident = integrate_grid(variant) / INT_GRID_MULT;
+        // below DEFER_FINE_UNITS: 8 sector ranks' batches of 135 / 161 / 317 units ran fine in 112 / 126 / 131 us
+        // against 146 / 146 / 142 coarse, one of 367 units 167 against 148 (r06fn); a fraction of the resident
+        // workgroups, as the direct path's rule
         const bool small = g_fine_units >= 2 ? units >= 0 && units < g_fine_units
-                                             : units >= 0 && units * INT_PARTS * 4 < (int64_t)resident * 3;
+                                             : units >= 0 && units * INT_PARTS * 4 * DEFER_FINE_DEN <
+                                                                 (int64_t)resident * DEFER_FINE_NUM;
         if (g_int_fine > 0 || ((g_int_fine < 0 || g_fine_units >= 2) && small))
             variant |= 4 | ((INT_FINE_KT - 1) << 3);
     }
